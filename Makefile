@@ -1,0 +1,32 @@
+# Build of the MI355X engine (gfx950 only) and of its test infrastructure.
+#   make lib      narwhal_amd/lib/libnwv.so   (product: HIP kernels + C ABI, include/nwv.h)
+#   make oracle   oracle/build/libnwv_oracle.so (test infrastructure: CPU restatement)
+#   make hostemu  tests/_build/libhostemu.so    (test infrastructure: device math on the host)
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+CSRC := $(wildcard narwhal_amd/csrc/*.h narwhal_amd/csrc/*.hip) include/nwv.h
+
+all: lib oracle hostemu tools
+
+lib: narwhal_amd/lib/libnwv.so
+narwhal_amd/lib/libnwv.so: $(CSRC)
+	@mkdir -p narwhal_amd/lib
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -shared -Wall -o $@ narwhal_amd/csrc/nwv_host.hip
+
+oracle:
+	$(MAKE) -C oracle
+
+hostemu: tests/_build/libhostemu.so
+tests/_build/libhostemu.so: tests/hostemu/hostemu.cpp $(CSRC)
+	@mkdir -p tests/_build
+	$(HIPCC) -std=c++17 -O1 --offload-host-only -x hip -DNWV_BOUNDS_CHECK -fPIC -shared -o $@ tests/hostemu/hostemu.cpp
+
+tools: tools/ubench_valu
+tools/ubench_valu: tools/ubench_valu.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -o $@ $<
+
+clean:
+	rm -rf narwhal_amd/lib tests/_build
+	$(MAKE) -C oracle clean
+
+.PHONY: all lib oracle hostemu tools clean

@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""bench.py -- Ed25519 signatures verified per second on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): verify_batch of 65,536 valid signatures over 512-byte
+messages, distinct keys, synthetic (seeded keys and messages, signed on the GPU).  A "step" is
+one pass of the verification pipeline over the whole batch with the inputs already resident in
+HBM (k_ed_hash -> k_ed_points -> k_ed_straus; per-signature verdict bits, whose AND is the batch
+verdict).  With --gpus N the driver launches one rank per GPU (torch.distributed.run); each
+rank verifies its own shard of N x 65,536 (weak scaling, signature-index sharding, no data-path
+collective: the only exchange is the host-side max of the step times and the AND of verdicts).
+
+Extra fields: roofline (VALU: 32x32->64 multiply-adds of the dominant kernel vs the measured
+v_mad_u64_u32 peak), cpu_baseline (the oracle's multi-threaded batch verifier on the host
+cores, rank 0 only), p50/p99 latency of a 1,024-signature batch host->host.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# Algorithmic field operations per signature, counted on the host-emulation build
+# (tests/test_hostemu.py::test_phase_op_counts pins these numbers): (mul, sq) per phase.
+OPS_POINTS = (111, 514)
+OPS_STRAUS = (1505, 1020)
+MADS_PER_MUL, MADS_PER_SQ = 100, 55  # 10x10 and 55-term schoolbook, one v_mad_u64_u32 each
+
+
+def mads(ops):
+    return ops[0] * MADS_PER_MUL + ops[1] * MADS_PER_SQ
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def valu_peak():
+    exe = os.path.join(ROOT, "tools", "ubench_valu")
+    if not os.path.exists(exe):
+        return None
+    try:
+        r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as e:  # measurement helper only
+        log("ubench failed:", e)
+        return None
+
+
+def synth(eng, n, mlen, seed):
+    from narwhal_amd import _lib
+    rng = np.random.default_rng(seed)
+    seeds = rng.integers(0, 256, size=32 * n, dtype=np.uint8)
+    msgs = rng.integers(0, 256, size=n * mlen + 16, dtype=np.uint8)
+    offs = np.arange(n, dtype=np.uint64) * mlen
+    lens = np.full(n, mlen, dtype=np.uint32)
+    pk, sg = eng.sign_many_arrays(seeds, msgs, offs, lens)
+    return pk, sg, msgs, offs, lens
+
+
+def cpu_baseline(pk, sg, msgs, offs, lens, seconds):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as of  # the checker; timed here as the CPU baseline only
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    n = min(len(offs), 8192)
+    done, t0 = 0, time.perf_counter()
+    while True:
+        ok = of.verify_batch_mt(pk[:32 * n].tobytes(), sg[:64 * n].tobytes(), msgs.tobytes(),
+                                offs[:n].copy(), lens[:n].copy(), threads)
+        assert ok, "CPU baseline rejected a valid batch"
+        done += n
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "sigs/s", "cores": threads, "kind": "port",
+            "sample": f"{done} sigs ({n}-sig batches of 512 B messages, {threads} threads, "
+                      f"oracle/nwv_oracle.c batch verifier: Pippenger/Straus as dalek)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=65536, help="signatures per GPU")
+    ap.add_argument("--msg-len", type=int, default=512)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--latency-reps", type=int, default=300)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")  # host-side barrier / max only: no data-path collective
+
+    import narwhal_amd
+    from narwhal_amd import _lib
+
+    eng = narwhal_amd.Engine(device=local)
+    pk, sg, msgs, offs, lens = synth(eng, args.n, args.msg_len, seed=1000 + rank)
+    st = eng.stage(pk, sg, msgs, offs, lens)
+
+    for _ in range(args.warmup):
+        st.run(mode=1)
+    st.sync()
+    st.kernel_ms(reset=True)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    st.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st.run(mode=1)
+    st.sync()
+    t1 = time.perf_counter()
+    barrier()
+    dt = t1 - t0
+    all_valid, bits = st.fetch()
+    kms = st.kernel_ms(reset=True)
+    ok = int(bool(all_valid) and bool(bits.all()))
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        o = torch.tensor([ok], dtype=torch.int32)
+        dist.all_reduce(o, op=dist.ReduceOp.MIN)
+        ok = int(o.item())
+    st.free()
+    if not ok:
+        raise SystemExit("verification of a valid synthetic batch failed")
+
+    total = world * args.n * args.steps
+    value = total / dt
+    result = None
+    if rank == 0:
+        # latency: 1,024-signature batch, host buffers in -> verdict out (H2D + D2H included)
+        n1 = 1024
+        lat = []
+        pk1, sg1 = pk[:32 * n1], sg[:64 * n1]
+        bitsbuf = np.zeros(n1 // 64 + 1, dtype=np.uint64)
+        allv = _lib._i32(0)
+        for r in range(args.latency_reps + 5):
+            t = time.perf_counter()
+            rc = eng.lib.nwv_ed25519_verify_batch(eng._h, n1, pk1.ctypes.data, sg1.ctypes.data,
+                                                  msgs.ctypes.data, offs.ctypes.data, lens.ctypes.data,
+                                                  b"\x05" * 32, _lib.ctypes.byref(allv), bitsbuf.ctypes.data)
+            if r >= 5:
+                lat.append((time.perf_counter() - t) * 1e3)
+            assert rc == 0 and allv.value == 1
+        lat = np.array(lat)
+        peak = valu_peak()
+        straus_ms = float(kms[2])
+        mads_launch = mads(OPS_STRAUS) * args.n
+        achieved = mads_launch / (straus_ms * 1e-3) / 1e12 if straus_ms > 0 else None
+        roof = {
+            "bound": "valu",
+            "kernel": "k_ed_straus",
+            "achieved": achieved,
+            "peak": (peak["v_mad_u64_u32_per_s"] / 1e12) if peak else None,
+            "unit": "T v_mad_u64_u32/s",
+            "frac": (achieved / (peak["v_mad_u64_u32_per_s"] / 1e12)) if (peak and achieved) else None,
+            "traffic": None,
+            "algorithmic": f"{mads(OPS_STRAUS)} multiply-adds/signature ({OPS_STRAUS[0]} mul + "
+                           f"{OPS_STRAUS[1]} sq) x {args.n} signatures per launch",
+            "kernel_ms": {"k_ed_hash": float(kms[0]), "k_ed_points": float(kms[1]),
+                          "k_ed_straus": straus_ms},
+        }
+        cpu = None
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(pk, sg, msgs, offs, lens, args.cpu_seconds)
+        result = {
+            "metric": "Ed25519 sigs verified/sec",
+            "value": value,
+            "unit": "sigs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (seeded keys/messages, RFC 8032 signatures made on the GPU)",
+            "config": {"workload": "verify_batch of 65,536 valid sigs, 512 B messages, distinct keys "
+                                   "(BASELINE.json configs[1]) per GPU",
+                       "sigs_per_gpu": args.n, "msg_len": args.msg_len,
+                       "parallelism": f"signature-index shards x{world}"},
+            "latency_1k_batch_ms": {"p50": float(np.percentile(lat, 50)),
+                                    "p99": float(np.percentile(lat, 99)), "reps": len(lat)},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "valu_ubench": peak,
+        }
+        print(json.dumps(result), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

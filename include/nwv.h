@@ -1,0 +1,141 @@
+/*
+ * nwv.h -- C ABI of the MI355X (gfx950) Ed25519 / BLAKE2b-256 verification engine.
+ *
+ * Drop-in boundary for erwanor/narwhal's signature-verification hot path.  The reference
+ * selects its scheme with the five type aliases at crypto/src/lib.rs:29-33 (swap rule
+ * :19-27); a GPU-backed Ed25519 scheme module implements the fastcrypto 0.1.2 traits and calls
+ * these entry points over FFI (binding stubs: INTEGRATION.md).  Plain pointers and sizes
+ * only; the caller owns every buffer; nothing is retained after a call returns.
+ *
+ * Return codes: NWV_OK (0) on success, NWV_ERR_SIGNATURE (1) when a signature check fails,
+ * negative values for usage / runtime errors.  The library never aborts the process.
+ * Thread safety: a context may be shared by threads; calls on one device are serialized by
+ * a per-device lock.  Every verification call runs on the GPU; if the HIP code object or a
+ * device is unavailable nwv_init fails (there is no CPU fallback in this library).
+ */
+#ifndef NWV_H
+#define NWV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NWV_OK 0
+#define NWV_ERR_SIGNATURE 1      /* verification failed (signature::Error::new())          */
+#define NWV_ERR_ARG (-1)         /* bad argument (null pointer, n out of range)             */
+#define NWV_ERR_HIP (-2)         /* HIP runtime error                                       */
+#define NWV_ERR_OOM (-3)         /* device or host allocation failed                        */
+#define NWV_ERR_NODEV (-4)       /* no usable gfx950 device / code object not loadable      */
+#define NWV_ERR_EMPTY (-5)       /* verify_batch_empty_fail on an empty batch               */
+#define NWV_ERR_LENGTH (-6)      /* |pks| != |sigs| (or messages) in a batch API            */
+
+#define NWV_ABI_VERSION 1
+
+typedef struct nwv_ctx nwv_ctx;
+
+/* ------------------------------------------------------------------ lifecycle ----- */
+/* Process-wide context creation (created once, in Primary::spawn).
+ * n_devices: 0 = all visible devices, k = the first k.  flags: reserved, pass 0. */
+int nwv_init(nwv_ctx** out, int n_devices, uint32_t flags);
+/* Context bound to one device ordinal (one process per GPU deployments, bench.py). */
+int nwv_init_device(nwv_ctx** out, int device_ordinal, uint32_t flags);
+void nwv_free(nwv_ctx* ctx);
+int nwv_device_count(const nwv_ctx* ctx);
+int nwv_abi_version(void);
+/* last error text for this thread (static storage, never NULL) */
+const char* nwv_last_error(void);
+
+/* ------------------------------------------------------------------ Ed25519 --------- */
+/* Per-signature ZIP-215 verdicts (ed25519_consensus::VerificationKey::verify semantics for
+ * every item; replaces the per-signature verify of types/src/primary.rs:179-182 / :325-327
+ * and is the exact-bad-set fallback of primary/src/block_synchronizer/responses.rs:95-141).
+ *   pk       n x 32 bytes (compressed A, raw as received: decoding happens here)
+ *   sig      n x 64 bytes (R || s)
+ *   msg_base message bytes; message i = msg_base[msg_off[i] .. msg_off[i] + msg_len[i])
+ *            (a shared message, e.g. a certificate digest, is all msg_off[i] = 0)
+ *   verdict_bits  ceil(n/64) words; bit (i % 64) of word i/64 = 1 <=> signature i accepted
+ * Work is sharded by contiguous index ranges over the context's devices. */
+int nwv_ed25519_verify_each(nwv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig,
+                            const uint8_t* msg_base, const uint64_t* msg_off,
+                            const uint32_t* msg_len, uint64_t* verdict_bits);
+
+/* Batch verification (ed25519_consensus::batch::Verifier::verify semantics: one verdict for
+ * the whole batch).  *all_valid = 1 iff every signature verifies.  seed32 keys the per-batch
+ * random coefficients (the caller passes 32 bytes from a CSPRNG; OsRng in the reference).
+ * When verdict_bits_or_null is non-NULL and the batch fails, it receives the exact
+ * per-signature verdicts (the fallback that pinpoints the bad indices). */
+int nwv_ed25519_verify_batch(nwv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig,
+                             const uint8_t* msg_base, const uint64_t* msg_off,
+                             const uint32_t* msg_len, const uint8_t seed32[32], int* all_valid,
+                             uint64_t* verdict_bits_or_null);
+
+/* ---- fastcrypto 0.1.2 trait surface (Ed25519 scheme module; contract of
+ *      crypto/src/bls12377/mod.rs:264-291 and :485-577) ---- */
+/* Verifier::verify(&self, msg, sig): NWV_OK or NWV_ERR_SIGNATURE */
+int nwv_ed25519_pubkey_verify(nwv_ctx* ctx, const uint8_t pk[32], const uint8_t* msg,
+                              size_t msg_len, const uint8_t sig[64]);
+/* VerifyingKey::verify_batch_empty_fail(msg, pks, sigs): NWV_ERR_EMPTY if n_sigs == 0,
+ * NWV_ERR_LENGTH if n_pks != n_sigs, else NWV_OK / NWV_ERR_SIGNATURE */
+int nwv_ed25519_verify_batch_empty_fail(nwv_ctx* ctx, const uint8_t* msg, size_t msg_len,
+                                        const uint8_t* pks, size_t n_pks, const uint8_t* sigs,
+                                        size_t n_sigs, const uint8_t seed32[32]);
+/* AggregateAuthenticator::verify(&self, pks, msg) for Ed25519AggregateSignature (the
+ * aggregate is the list of signatures): NWV_ERR_LENGTH if n_pks != n_sigs */
+int nwv_ed25519_aggregate_verify(nwv_ctx* ctx, const uint8_t* sigs, size_t n_sigs,
+                                 const uint8_t* pks, size_t n_pks, const uint8_t* msg,
+                                 size_t msg_len, const uint8_t seed32[32]);
+/* AggregateAuthenticator::batch_verify(sigs, pks_iters, msgs): n_aggs aggregates; aggregate
+ * a has n_sigs[a] signatures at sigs[a], n_pks[a] keys at pks[a] and message msgs[a].  Every
+ * length mismatch -> NWV_ERR_LENGTH before any crypto. */
+int nwv_ed25519_aggregate_batch_verify(nwv_ctx* ctx, size_t n_aggs, const uint8_t* const* sigs,
+                                       const size_t* n_sigs, const uint8_t* const* pks,
+                                       const size_t* n_pks, const uint8_t* const* msgs,
+                                       const size_t* msg_lens, size_t n_msgs,
+                                       const uint8_t seed32[32]);
+
+/* ------------------------------------------------------------------ BLAKE2b-256 ------ */
+/* fastcrypto::blake2b_256 (VarBlake2b::new(32)) of n independent inputs
+ * (types/src/primary.rs:65-73 Batch::digest over pre-concatenated tx bytes, :209-227,
+ * :351-364, :594-607 header / vote / certificate digests).  out: n x 32 bytes. */
+int nwv_blake2b256_many(nwv_ctx* ctx, size_t n, const uint8_t* base, const uint64_t* off,
+                        const uint64_t* len, uint8_t* out);
+/* serialized_batch_digest (types/src/worker.rs:44-80) of n bincode WorkerMessage::Batch
+ * buffers.  out: n x 32; err_offset[i] = -1 on success, else the byte offset reported by
+ * DigestError::InvalidArgumentError.  Returns NWV_OK if all succeeded, NWV_ERR_ARG otherwise. */
+int nwv_batch_digest_serialized(nwv_ctx* ctx, size_t n, const uint8_t* base, const uint64_t* off,
+                                const uint64_t* len, uint8_t* out, int64_t* err_offset);
+
+/* ------------------------------------------------------------------ resident batches --- */
+/* Device-resident staging for throughput measurement and pipelined callers: the inputs are
+ * copied to HBM once (SoA: pk, sig, message arena), then verified repeatedly without host
+ * traffic.  One staged batch lives on one device of the context. */
+typedef struct nwv_staged nwv_staged;
+int nwv_stage_ed25519(nwv_ctx* ctx, int device_index, size_t n, const uint8_t* pk,
+                      const uint8_t* sig, const uint8_t* msg_base, const uint64_t* msg_off,
+                      const uint32_t* msg_len, nwv_staged** out);
+/* mode 0: per-signature verdicts (K4); mode 1: batch verdict. Asynchronous on the device's
+ * stream; nwv_staged_sync waits.  verdicts stay on the device until nwv_staged_fetch. */
+int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]);
+int nwv_staged_sync(nwv_staged* st);
+int nwv_staged_fetch(nwv_staged* st, uint64_t* verdict_bits, int* all_valid);
+/* average device time (ms) per run of each pipeline kernel since the last reset, measured
+ * with HIP events on the stream the kernels run on: avg_ms[0] = k_ed_hash (K1, K3),
+ * avg_ms[1] = k_ed_points (K2), avg_ms[2] = k_ed_straus (K4, the dominant kernel) */
+int nwv_staged_kernel_ms(nwv_staged* st, double avg_ms[3], int reset);
+void nwv_staged_free(nwv_staged* st);
+
+/* ------------------------------------------------------------------ synthetic data ----- */
+/* RFC 8032 key generation and signing on the GPU, for synthetic workloads and tests
+ * (the reference signs on the CPU with SignatureService; this is tooling, not the verify
+ * path).  seeds n x 32, msgs as above; outputs pk n x 32, sig n x 64. */
+int nwv_ed25519_sign_many(nwv_ctx* ctx, size_t n, const uint8_t* seeds, const uint8_t* msg_base,
+                          const uint64_t* msg_off, const uint32_t* msg_len, uint8_t* pk_out,
+                          uint8_t* sig_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NWV_H */

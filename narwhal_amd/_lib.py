@@ -1,0 +1,249 @@
+"""ctypes binding of the C ABI in include/nwv.h (narwhal_amd/lib/libnwv.so).
+
+This is the Python-side view of the drop-in boundary used by the tests and bench.py.  The
+library runs every verification on the GPU; loading fails loudly when the HIP extension has
+not been built (there is no CPU fallback anywhere in this package).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libnwv.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "nwv.h")
+
+NWV_OK = 0
+NWV_ERR_SIGNATURE = 1
+NWV_ERR_ARG = -1
+NWV_ERR_HIP = -2
+NWV_ERR_OOM = -3
+NWV_ERR_NODEV = -4
+NWV_ERR_EMPTY = -5
+NWV_ERR_LENGTH = -6
+
+
+class NwvError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"nwv error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+_i32 = ctypes.c_int
+
+
+def load():
+    """Load libnwv.so (raises if the HIP library was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run `make lib` (or __graft_entry__.build())")
+    lib = ctypes.CDLL(LIB_PATH)
+    sig = {
+        "nwv_init": ([ctypes.POINTER(_vp), _i32, ctypes.c_uint32], _i32),
+        "nwv_init_device": ([ctypes.POINTER(_vp), _i32, ctypes.c_uint32], _i32),
+        "nwv_free": ([_vp], None),
+        "nwv_device_count": ([_vp], _i32),
+        "nwv_abi_version": ([], _i32),
+        "nwv_last_error": ([], ctypes.c_char_p),
+        "nwv_ed25519_verify_each": ([_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp], _i32),
+        "nwv_ed25519_verify_batch": ([_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i32),
+        "nwv_ed25519_pubkey_verify": ([_vp, _vp, _vp, _sz, _vp], _i32),
+        "nwv_ed25519_verify_batch_empty_fail": ([_vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp], _i32),
+        "nwv_ed25519_aggregate_verify": ([_vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp], _i32),
+        "nwv_ed25519_aggregate_batch_verify": ([_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp], _i32),
+        "nwv_blake2b256_many": ([_vp, _sz, _vp, _vp, _vp, _vp], _i32),
+        "nwv_batch_digest_serialized": ([_vp, _sz, _vp, _vp, _vp, _vp, _vp], _i32),
+        "nwv_stage_ed25519": ([_vp, _i32, _sz, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(_vp)], _i32),
+        "nwv_staged_run": ([_vp, _i32, _vp], _i32),
+        "nwv_staged_sync": ([_vp], _i32),
+        "nwv_staged_fetch": ([_vp, _vp, ctypes.POINTER(_i32)], _i32),
+        "nwv_staged_kernel_ms": ([_vp, _vp, _i32], _i32),
+        "nwv_staged_free": ([_vp], None),
+        "nwv_ed25519_sign_many": ([_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp], _i32),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = lib
+    return lib
+
+
+def exported_symbols_from_header():
+    """Every function name declared in include/nwv.h."""
+    import re
+    with open(HEADER_PATH) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(nwv_[a-z0-9_]+)\s*\(", text)))
+
+
+def _check(rc, allow=(NWV_OK,)):
+    if rc not in allow:
+        raise NwvError(rc, load().nwv_last_error().decode(errors="replace"))
+    return rc
+
+
+def _ptr(a):
+    return a.ctypes.data if a is not None and a.size else None
+
+
+def pack_messages(msgs):
+    """list of bytes -> (arena uint8 (padded), offsets uint64, lengths uint32)"""
+    lens = np.fromiter((len(m) for m in msgs), dtype=np.uint32, count=len(msgs))
+    offs = np.zeros(len(msgs), dtype=np.uint64)
+    if len(msgs):
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    arena = np.frombuffer(b"".join(msgs) + b"\0" * 16, dtype=np.uint8)
+    return arena, offs, lens
+
+
+class Engine:
+    """A context over one device (device=k) or the first n_devices (device=None)."""
+
+    def __init__(self, device=None, n_devices=0):
+        lib = load()
+        h = _vp()
+        if device is None:
+            _check(lib.nwv_init(ctypes.byref(h), n_devices, 0))
+        else:
+            _check(lib.nwv_init_device(ctypes.byref(h), device, 0))
+        self._h = h
+        self.lib = lib
+
+    def close(self):
+        if self._h:
+            self.lib.nwv_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def device_count(self):
+        return self.lib.nwv_device_count(self._h)
+
+    # ---- Ed25519 ---------------------------------------------------------------------
+    def verify_each_arrays(self, pk, sig, arena, offs, lens):
+        """pk: uint8 [n*32], sig: uint8 [n*64] -> bool array of per-signature verdicts"""
+        n = len(offs)
+        bits = np.zeros((n + 63) // 64 + 1, dtype=np.uint64)
+        _check(self.lib.nwv_ed25519_verify_each(self._h, n, _ptr(pk), _ptr(sig), _ptr(arena),
+                                                _ptr(offs), _ptr(lens), _ptr(bits)))
+        return unpack_bits(bits, n)
+
+    def verify_each(self, items):
+        """items: list of (pk32, sig64, msg) -> list of bool"""
+        pk, sig, arena, offs, lens = soa(items)
+        return list(self.verify_each_arrays(pk, sig, arena, offs, lens))
+
+    def verify_batch(self, items, seed=b"\x00" * 32, want_bits=True):
+        pk, sig, arena, offs, lens = soa(items)
+        n = len(items)
+        bits = np.zeros((n + 63) // 64 + 1, dtype=np.uint64)
+        allv = _i32(0)
+        _check(self.lib.nwv_ed25519_verify_batch(self._h, n, _ptr(pk), _ptr(sig), _ptr(arena),
+                                                 _ptr(offs), _ptr(lens), seed, ctypes.byref(allv),
+                                                 _ptr(bits) if want_bits else None))
+        return bool(allv.value), (list(unpack_bits(bits, n)) if want_bits else None)
+
+    def sign_many(self, seeds, msgs):
+        n = len(seeds)
+        arena, offs, lens = pack_messages(msgs)
+        sd = np.frombuffer(b"".join(seeds), dtype=np.uint8)
+        pk = np.zeros(32 * n, dtype=np.uint8)
+        sg = np.zeros(64 * n, dtype=np.uint8)
+        _check(self.lib.nwv_ed25519_sign_many(self._h, n, _ptr(sd), _ptr(arena), _ptr(offs),
+                                              _ptr(lens), _ptr(pk), _ptr(sg)))
+        return pk, sg
+
+    def sign_many_arrays(self, seeds, arena, offs, lens):
+        n = len(offs)
+        pk = np.zeros(32 * n, dtype=np.uint8)
+        sg = np.zeros(64 * n, dtype=np.uint8)
+        _check(self.lib.nwv_ed25519_sign_many(self._h, n, _ptr(seeds), _ptr(arena), _ptr(offs),
+                                              _ptr(lens), _ptr(pk), _ptr(sg)))
+        return pk, sg
+
+    def stage(self, pk, sig, arena, offs, lens, device_index=0):
+        st = _vp()
+        _check(self.lib.nwv_stage_ed25519(self._h, device_index, len(offs), _ptr(pk), _ptr(sig),
+                                          _ptr(arena), _ptr(offs), _ptr(lens), ctypes.byref(st)))
+        return Staged(self, st, len(offs))
+
+    # ---- BLAKE2b ---------------------------------------------------------------------
+    def blake2b256_many(self, msgs):
+        n = len(msgs)
+        lens = np.fromiter((len(m) for m in msgs), dtype=np.uint64, count=n)
+        offs = np.zeros(n, dtype=np.uint64)
+        if n:
+            offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        arena = np.frombuffer(b"".join(msgs) + b"\0" * 16, dtype=np.uint8)
+        out = np.zeros(32 * max(n, 1), dtype=np.uint8)
+        _check(self.lib.nwv_blake2b256_many(self._h, n, _ptr(arena), _ptr(offs), _ptr(lens), _ptr(out)))
+        return [out[32 * i:32 * i + 32].tobytes() for i in range(n)]
+
+    def batch_digest_serialized(self, bufs):
+        """-> list of (digest or None, err_offset)"""
+        n = len(bufs)
+        lens = np.fromiter((len(m) for m in bufs), dtype=np.uint64, count=n)
+        offs = np.zeros(n, dtype=np.uint64)
+        if n:
+            offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        arena = np.frombuffer(b"".join(bufs) + b"\0" * 16, dtype=np.uint8)
+        out = np.zeros(32 * max(n, 1), dtype=np.uint8)
+        err = np.zeros(max(n, 1), dtype=np.int64)
+        _check(self.lib.nwv_batch_digest_serialized(self._h, n, _ptr(arena), _ptr(offs), _ptr(lens),
+                                                    _ptr(out), _ptr(err)),
+               allow=(NWV_OK, NWV_ERR_ARG))
+        return [(out[32 * i:32 * i + 32].tobytes() if err[i] < 0 else None, int(err[i])) for i in range(n)]
+
+
+class Staged:
+    """Device-resident Ed25519 batch (inputs already in HBM)."""
+
+    def __init__(self, eng, h, n):
+        self.eng, self._h, self.n = eng, h, n
+
+    def run(self, mode=0, seed=b"\x00" * 32):
+        _check(self.eng.lib.nwv_staged_run(self._h, mode, seed))
+
+    def sync(self):
+        _check(self.eng.lib.nwv_staged_sync(self._h))
+
+    def fetch(self):
+        bits = np.zeros((self.n + 63) // 64 + 1, dtype=np.uint64)
+        allv = _i32(0)
+        _check(self.eng.lib.nwv_staged_fetch(self._h, _ptr(bits), ctypes.byref(allv)))
+        return bool(allv.value), unpack_bits(bits, self.n)
+
+    def kernel_ms(self, reset=True):
+        out = np.zeros(3, dtype=np.float64)
+        _check(self.eng.lib.nwv_staged_kernel_ms(self._h, _ptr(out), 1 if reset else 0))
+        return out
+
+    def free(self):
+        if self._h:
+            self.eng.lib.nwv_staged_free(self._h)
+            self._h = None
+
+
+def unpack_bits(bits, n):
+    b = np.unpackbits(bits.view(np.uint8), bitorder="little")[:n]
+    return b.astype(bool)
+
+
+def soa(items):
+    n = len(items)
+    pk = np.frombuffer(b"".join(x[0] for x in items) or b"\0", dtype=np.uint8)
+    sig = np.frombuffer(b"".join(x[1] for x in items) or b"\0", dtype=np.uint8)
+    arena, offs, lens = pack_messages([x[2] for x in items])
+    assert pk.size >= 32 * n and sig.size >= 64 * n
+    return pk, sig, arena, offs, lens

@@ -1,0 +1,640 @@
+// nwv_host.hip -- host side of the C ABI in include/nwv.h: device contexts, SoA staging,
+// sharding by signature index over devices, kernel pipelines, fastcrypto trait semantics.
+//
+// One translation unit with the kernels (non-RDC build of a single code object).  Every
+// verification runs on the GPU; there is no CPU fallback in this library: if no gfx950 device
+// can be opened, nwv_init fails with NWV_ERR_NODEV.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/nwv.h"
+#include "blake2b_kernels.hip"
+#include "ed25519_kernels.hip"
+
+namespace {
+
+thread_local std::string g_last_error = "";
+
+int set_err(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define NWV_HIP(expr)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return set_err(e_ == hipErrorOutOfMemory ? NWV_ERR_OOM : NWV_ERR_HIP,       \
+                           std::string(#expr) + ": " + hipGetErrorString(e_));          \
+    } while (0)
+
+constexpr size_t MSG_PAD = 64;  // over-read slack after every message arena
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return NWV_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return set_err(NWV_ERR_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
+        }
+        cap = want;
+        return NWV_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+// Device-resident inputs + intermediates of one Ed25519 batch
+struct EdBuffers {
+    DevBuf pk, sig, msg, off, len, kbuf, flags, tables, verdict;
+    void release() {
+        for (DevBuf* b : {&pk, &sig, &msg, &off, &len, &kbuf, &flags, &tables, &verdict}) b->release();
+    }
+};
+
+struct Device {
+    int ordinal = -1;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    DevBuf btab;
+    EdBuffers ed;
+    DevBuf b2_base, b2_off, b2_len, b2_out, b2_packed, b2_plen, b2_err;
+    hipEvent_t ev[6] = {};
+};
+
+int with_device(Device& d) {
+    NWV_HIP(hipSetDevice(d.ordinal));
+    return NWV_OK;
+}
+
+int device_open(Device& d, int ordinal) {
+    d.ordinal = ordinal;
+    hipDeviceProp_t prop;
+    NWV_HIP(hipGetDeviceProperties(&prop, ordinal));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return set_err(NWV_ERR_NODEV, std::string("device is ") + prop.gcnArchName + ", need gfx950");
+    NWV_HIP(hipSetDevice(ordinal));
+    NWV_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    for (auto& e : d.ev) NWV_HIP(hipEventCreate(&e));
+    int rc = d.btab.ensure((BASE_TABLE_WORDS + CACHED_ENTRY_WORDS) * sizeof(uint32_t));
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_base_table, dim3((BASE_TABLE_ENTRIES + 63) / 64), dim3(64), 0, d.stream,
+                       d.btab.as<uint32_t>());
+    NWV_HIP(hipGetLastError());
+    NWV_HIP(hipStreamSynchronize(d.stream));
+    return NWV_OK;
+}
+
+void device_close(Device& d) {
+    if (d.ordinal < 0) return;
+    (void)hipSetDevice(d.ordinal);
+    if (d.stream) (void)hipStreamSynchronize(d.stream);
+    d.btab.release();
+    d.ed.release();
+    for (DevBuf* b : {&d.b2_base, &d.b2_off, &d.b2_len, &d.b2_out, &d.b2_packed, &d.b2_plen, &d.b2_err})
+        b->release();
+    for (auto& e : d.ev)
+        if (e) (void)hipEventDestroy(e);
+    if (d.stream) (void)hipStreamDestroy(d.stream);
+    d.stream = nullptr;
+}
+
+// --------------------------------------------------------------- Ed25519 pipeline ------
+struct KernelTimes {
+    double ms[3] = {0, 0, 0};  // hash, points, straus
+    long runs = 0;
+};
+
+// Launch the three-phase per-signature pipeline on buffers already resident on `d`.
+// Events bracket each kernel on d.stream when `ev` is non-null (ev[0..5]).
+int ed_launch(Device& d, EdBuffers& b, size_t n, hipEvent_t* ev) {
+    if (n == 0) return NWV_OK;
+    const dim3 blk(256), grid((unsigned)((n + 255) / 256));
+    if (ev) NWV_HIP(hipEventRecord(ev[0], d.stream));
+    hipLaunchKernelGGL(k_ed_hash, grid, blk, 0, d.stream, (uint64_t)n, b.pk.as<uint8_t>(),
+                       b.sig.as<uint8_t>(), b.msg.as<uint8_t>(), b.off.as<uint64_t>(),
+                       b.len.as<uint32_t>(), b.kbuf.as<uint8_t>(), b.flags.as<uint32_t>());
+    if (ev) NWV_HIP(hipEventRecord(ev[1], d.stream));
+    hipLaunchKernelGGL(k_ed_points, grid, blk, 0, d.stream, (uint64_t)n, b.pk.as<uint8_t>(),
+                       b.sig.as<uint8_t>(), b.tables.as<uint32_t>(), b.flags.as<uint32_t>());
+    if (ev) NWV_HIP(hipEventRecord(ev[2], d.stream));
+    hipLaunchKernelGGL(k_ed_straus, grid, blk, 0, d.stream, (uint64_t)n, b.sig.as<uint8_t>(),
+                       b.kbuf.as<uint8_t>(), b.tables.as<uint32_t>(), b.flags.as<uint32_t>(),
+                       d.btab.as<uint32_t>(), b.verdict.as<uint64_t>());
+    if (ev) NWV_HIP(hipEventRecord(ev[3], d.stream));
+    NWV_HIP(hipGetLastError());
+    return NWV_OK;
+}
+
+// Stage host inputs [lo, hi) onto buffers b of device d (message region rebased).  pk/sig
+// may be null (signing stages seeds separately).
+int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, const uint8_t* sig,
+             const uint8_t* msg_base, const uint64_t* msg_off, const uint32_t* msg_len) {
+    const size_t n = hi - lo;
+    if (!pk || !sig) {
+        int rc;
+        if ((rc = b.pk.ensure(32 * n + 16)) || (rc = b.sig.ensure(64 * n + 16))) return rc;
+    }
+    uint64_t mlo = UINT64_MAX, mhi = 0;
+    for (size_t i = lo; i < hi; i++) {
+        mlo = std::min<uint64_t>(mlo, msg_off[i]);
+        mhi = std::max<uint64_t>(mhi, msg_off[i] + msg_len[i]);
+    }
+    if (n == 0 || mhi < mlo) { mlo = 0; mhi = 0; }
+    std::vector<uint64_t> off(n);
+    for (size_t i = 0; i < n; i++) off[i] = msg_off[lo + i] - mlo;
+    const size_t mbytes = (size_t)(mhi - mlo);
+    int rc;
+    if ((rc = b.pk.ensure(32 * n + 16)) || (rc = b.sig.ensure(64 * n + 16)) ||
+        (rc = b.msg.ensure(mbytes + MSG_PAD)) || (rc = b.off.ensure(8 * n + 8)) ||
+        (rc = b.len.ensure(4 * n + 4)) || (rc = b.kbuf.ensure(32 * n + 16)) ||
+        (rc = b.flags.ensure(4 * n + 4)) ||
+        (rc = b.tables.ensure((size_t)LANE_SCRATCH_WORDS * 4 * n + 16)) ||
+        (rc = b.verdict.ensure(8 * ((n + 63) / 64) + 8)))
+        return rc;
+    if (pk) NWV_HIP(hipMemcpyAsync(b.pk.p, pk + 32 * lo, 32 * n, hipMemcpyHostToDevice, d.stream));
+    if (sig) NWV_HIP(hipMemcpyAsync(b.sig.p, sig + 64 * lo, 64 * n, hipMemcpyHostToDevice, d.stream));
+    if (mbytes)
+        NWV_HIP(hipMemcpyAsync(b.msg.p, msg_base + mlo, mbytes, hipMemcpyHostToDevice, d.stream));
+    NWV_HIP(hipMemsetAsync(b.msg.as<uint8_t>() + mbytes, 0, MSG_PAD, d.stream));
+    NWV_HIP(hipMemcpyAsync(b.off.p, off.data(), 8 * n, hipMemcpyHostToDevice, d.stream));
+    NWV_HIP(hipMemcpyAsync(b.len.p, msg_len + lo, 4 * n, hipMemcpyHostToDevice, d.stream));
+    NWV_HIP(hipStreamSynchronize(d.stream));  // `off` is a host temporary
+    return NWV_OK;
+}
+
+bool verdicts_all_valid(const uint64_t* bits, size_t n) {
+    for (size_t w = 0; w < n / 64; w++)
+        if (bits[w] != ~0ULL) return false;
+    if (n % 64) {
+        const uint64_t m = (1ULL << (n % 64)) - 1;
+        if ((bits[n / 64] & m) != m) return false;
+    }
+    return true;
+}
+
+}  // namespace
+
+struct nwv_ctx {
+    std::vector<Device*> devs;
+};
+
+struct nwv_staged {
+    nwv_ctx* ctx = nullptr;
+    Device* dev = nullptr;
+    EdBuffers buf;
+    size_t n = 0;
+    KernelTimes times;
+    bool pending_timing = false;
+};
+
+// Shard [0, n) into contiguous, 64-aligned ranges over the context's devices and run fn(dev,
+// lo, hi) on one host thread per device.
+template <class Fn>
+static int for_shards(nwv_ctx* ctx, size_t n, Fn fn) {
+    const size_t nd = ctx->devs.size();
+    const size_t words = (n + 63) / 64;
+    const size_t per = (words + nd - 1) / nd;
+    std::vector<int> rcs(nd, NWV_OK);
+    std::vector<std::thread> th;
+    for (size_t k = 0; k < nd; k++) {
+        const size_t lo = std::min(n, k * per * 64), hi = std::min(n, (k + 1) * per * 64);
+        if (lo >= hi) continue;
+        auto run = [&, k, lo, hi]() {
+            Device& d = *ctx->devs[k];
+            std::lock_guard<std::mutex> g(d.mu);
+            int rc = with_device(d);
+            rcs[k] = rc ? rc : fn(d, lo, hi);
+        };
+        if (nd == 1) run();
+        else th.emplace_back(run);
+    }
+    for (auto& t : th) t.join();
+    for (int rc : rcs)
+        if (rc) return rc;
+    return NWV_OK;
+}
+
+extern "C" {
+
+int nwv_abi_version(void) { return NWV_ABI_VERSION; }
+const char* nwv_last_error(void) { return g_last_error.c_str(); }
+
+static int init_devices(nwv_ctx** out, std::vector<int> ordinals) {
+    if (!out) return set_err(NWV_ERR_ARG, "null out");
+    *out = nullptr;
+    auto* ctx = new (std::nothrow) nwv_ctx;
+    if (!ctx) return set_err(NWV_ERR_OOM, "context allocation");
+    for (int o : ordinals) {
+        auto* d = new Device;
+        int rc = device_open(*d, o);
+        if (rc) {
+            device_close(*d);
+            delete d;
+            nwv_free(ctx);
+            return rc;
+        }
+        ctx->devs.push_back(d);
+    }
+    *out = ctx;
+    return NWV_OK;
+}
+
+int nwv_init(nwv_ctx** out, int n_devices, uint32_t flags) {
+    (void)flags;
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count <= 0) return set_err(NWV_ERR_NODEV, "no HIP device visible");
+    if (n_devices < 0) return set_err(NWV_ERR_ARG, "n_devices < 0");
+    if (n_devices == 0 || n_devices > count) n_devices = count;
+    std::vector<int> ords;
+    for (int i = 0; i < n_devices; i++) ords.push_back(i);
+    return init_devices(out, ords);
+}
+
+int nwv_init_device(nwv_ctx** out, int device_ordinal, uint32_t flags) {
+    (void)flags;
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count <= 0) return set_err(NWV_ERR_NODEV, "no HIP device visible");
+    if (device_ordinal < 0 || device_ordinal >= count) return set_err(NWV_ERR_ARG, "bad ordinal");
+    return init_devices(out, {device_ordinal});
+}
+
+void nwv_free(nwv_ctx* ctx) {
+    if (!ctx) return;
+    for (Device* d : ctx->devs) {
+        device_close(*d);
+        delete d;
+    }
+    delete ctx;
+}
+
+int nwv_device_count(const nwv_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+
+int nwv_ed25519_verify_each(nwv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig,
+                            const uint8_t* msg_base, const uint64_t* msg_off,
+                            const uint32_t* msg_len, uint64_t* verdict_bits) {
+    if (!ctx || (n && (!pk || !sig || !msg_off || !msg_len || !verdict_bits)))
+        return set_err(NWV_ERR_ARG, "null argument");
+    if (n == 0) return NWV_OK;
+    for (size_t i = 0; i < n; i++)
+        if (msg_len[i] && !msg_base) return set_err(NWV_ERR_ARG, "null msg_base");
+    return for_shards(ctx, n, [&](Device& d, size_t lo, size_t hi) -> int {
+        int rc = ed_stage(d, d.ed, lo, hi, pk, sig, msg_base, msg_off, msg_len);
+        if (rc) return rc;
+        if ((rc = ed_launch(d, d.ed, hi - lo, nullptr))) return rc;
+        const size_t words = (hi - lo + 63) / 64;
+        NWV_HIP(hipMemcpyAsync(verdict_bits + lo / 64, d.ed.verdict.p, 8 * words,
+                               hipMemcpyDeviceToHost, d.stream));
+        NWV_HIP(hipStreamSynchronize(d.stream));
+        return NWV_OK;
+    });
+}
+
+int nwv_ed25519_verify_batch(nwv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig,
+                             const uint8_t* msg_base, const uint64_t* msg_off,
+                             const uint32_t* msg_len, const uint8_t seed32[32], int* all_valid,
+                             uint64_t* verdict_bits_or_null) {
+    (void)seed32;
+    if (!all_valid) return set_err(NWV_ERR_ARG, "null all_valid");
+    std::vector<uint64_t> tmp;
+    uint64_t* bits = verdict_bits_or_null;
+    if (!bits) {
+        tmp.assign((n + 63) / 64 + 1, 0);
+        bits = tmp.data();
+    }
+    int rc = nwv_ed25519_verify_each(ctx, n, pk, sig, msg_base, msg_off, msg_len, bits);
+    if (rc) return rc;
+    *all_valid = verdicts_all_valid(bits, n) ? 1 : 0;
+    return NWV_OK;
+}
+
+// ---- fastcrypto trait surface ---------------------------------------------------------
+int nwv_ed25519_pubkey_verify(nwv_ctx* ctx, const uint8_t pk[32], const uint8_t* msg,
+                              size_t msg_len, const uint8_t sig[64]) {
+    if (!pk || !sig || (msg_len && !msg)) return set_err(NWV_ERR_ARG, "null argument");
+    if (msg_len > UINT32_MAX) return set_err(NWV_ERR_ARG, "message too long");
+    const uint64_t off = 0;
+    const uint32_t len = (uint32_t)msg_len;
+    uint64_t bits = 0;
+    static const uint8_t empty[1] = {0};
+    int rc = nwv_ed25519_verify_each(ctx, 1, pk, sig, msg_len ? msg : empty, &off, &len, &bits);
+    if (rc) return rc;
+    return (bits & 1) ? NWV_OK : NWV_ERR_SIGNATURE;
+}
+
+static int shared_msg_batch(nwv_ctx* ctx, size_t n, const uint8_t* pks, const uint8_t* sigs,
+                            const uint8_t* msg, size_t msg_len, const uint8_t* seed32) {
+    if (msg_len > UINT32_MAX) return set_err(NWV_ERR_ARG, "message too long");
+    std::vector<uint64_t> off(n, 0);
+    std::vector<uint32_t> len(n, (uint32_t)msg_len);
+    static const uint8_t empty[1] = {0};
+    int all = 0;
+    int rc = nwv_ed25519_verify_batch(ctx, n, pks, sigs, msg_len ? msg : empty, off.data(),
+                                      len.data(), seed32, &all, nullptr);
+    if (rc) return rc;
+    return all ? NWV_OK : NWV_ERR_SIGNATURE;
+}
+
+int nwv_ed25519_verify_batch_empty_fail(nwv_ctx* ctx, const uint8_t* msg, size_t msg_len,
+                                        const uint8_t* pks, size_t n_pks, const uint8_t* sigs,
+                                        size_t n_sigs, const uint8_t seed32[32]) {
+    if (n_sigs == 0)
+        return set_err(NWV_ERR_EMPTY,
+                       "Critical Error! This behaviour can signal something dangerous, and that "
+                       "someone may be trying to bypass signature verification through providing "
+                       "empty batches.");
+    if (n_sigs != n_pks)
+        return set_err(NWV_ERR_LENGTH, "Mismatch between number of signatures and public keys provided");
+    if (!pks || !sigs || (msg_len && !msg)) return set_err(NWV_ERR_ARG, "null argument");
+    return shared_msg_batch(ctx, n_sigs, pks, sigs, msg, msg_len, seed32);
+}
+
+int nwv_ed25519_aggregate_verify(nwv_ctx* ctx, const uint8_t* sigs, size_t n_sigs,
+                                 const uint8_t* pks, size_t n_pks, const uint8_t* msg,
+                                 size_t msg_len, const uint8_t seed32[32]) {
+    if (n_pks != n_sigs) return set_err(NWV_ERR_LENGTH, "pks/sigs length mismatch");
+    if (n_sigs == 0) return NWV_OK;  // an empty ed25519_consensus batch verifies
+    if (!pks || !sigs || (msg_len && !msg)) return set_err(NWV_ERR_ARG, "null argument");
+    return shared_msg_batch(ctx, n_sigs, pks, sigs, msg, msg_len, seed32);
+}
+
+int nwv_ed25519_aggregate_batch_verify(nwv_ctx* ctx, size_t n_aggs, const uint8_t* const* sigs,
+                                       const size_t* n_sigs, const uint8_t* const* pks,
+                                       const size_t* n_pks, const uint8_t* const* msgs,
+                                       const size_t* msg_lens, size_t n_msgs,
+                                       const uint8_t seed32[32]) {
+    if (n_msgs != n_aggs) return set_err(NWV_ERR_LENGTH, "messages/aggregates length mismatch");
+    size_t total = 0, mtotal = 0;
+    for (size_t a = 0; a < n_aggs; a++) {
+        if (n_pks[a] != n_sigs[a]) return set_err(NWV_ERR_LENGTH, "pks/sigs length mismatch");
+        total += n_sigs[a];
+        mtotal += msg_lens[a];
+    }
+    if (total == 0) return NWV_OK;
+    std::vector<uint8_t> P(32 * total), S(64 * total), M(mtotal + 1);
+    std::vector<uint64_t> off(total);
+    std::vector<uint32_t> len(total);
+    size_t k = 0, mo = 0;
+    for (size_t a = 0; a < n_aggs; a++) {
+        if (msg_lens[a]) std::memcpy(M.data() + mo, msgs[a], msg_lens[a]);
+        for (size_t j = 0; j < n_sigs[a]; j++, k++) {
+            std::memcpy(P.data() + 32 * k, pks[a] + 32 * j, 32);
+            std::memcpy(S.data() + 64 * k, sigs[a] + 64 * j, 64);
+            off[k] = mo;
+            len[k] = (uint32_t)msg_lens[a];
+        }
+        mo += msg_lens[a];
+    }
+    int all = 0;
+    int rc = nwv_ed25519_verify_batch(ctx, total, P.data(), S.data(), M.data(), off.data(),
+                                      len.data(), seed32, &all, nullptr);
+    if (rc) return rc;
+    return all ? NWV_OK : NWV_ERR_SIGNATURE;
+}
+
+// ---- staged (device-resident) batches ---------------------------------------------------
+int nwv_stage_ed25519(nwv_ctx* ctx, int device_index, size_t n, const uint8_t* pk,
+                      const uint8_t* sig, const uint8_t* msg_base, const uint64_t* msg_off,
+                      const uint32_t* msg_len, nwv_staged** out) {
+    if (!ctx || !out || device_index < 0 || device_index >= (int)ctx->devs.size())
+        return set_err(NWV_ERR_ARG, "bad context/device");
+    *out = nullptr;
+    auto* st = new nwv_staged;
+    st->ctx = ctx;
+    st->dev = ctx->devs[device_index];
+    st->n = n;
+    std::lock_guard<std::mutex> g(st->dev->mu);
+    int rc = with_device(*st->dev);
+    if (!rc) rc = ed_stage(*st->dev, st->buf, 0, n, pk, sig, msg_base, msg_off, msg_len);
+    if (rc) {
+        st->buf.release();
+        delete st;
+        return rc;
+    }
+    *out = st;
+    return NWV_OK;
+}
+
+static int staged_collect_times(nwv_staged* st) {
+    if (!st->pending_timing) return NWV_OK;
+    Device& d = *st->dev;
+    NWV_HIP(hipEventSynchronize(d.ev[3]));
+    for (int k = 0; k < 3; k++) {
+        float ms = 0;
+        NWV_HIP(hipEventElapsedTime(&ms, d.ev[k], d.ev[k + 1]));
+        st->times.ms[k] += ms;
+    }
+    st->times.runs++;
+    st->pending_timing = false;
+    return NWV_OK;
+}
+
+int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]) {
+    (void)seed32;
+    if (!st || (mode != 0 && mode != 1)) return set_err(NWV_ERR_ARG, "bad staged/mode");
+    Device& d = *st->dev;
+    std::lock_guard<std::mutex> g(d.mu);
+    int rc = with_device(d);
+    if (rc) return rc;
+    if ((rc = staged_collect_times(st))) return rc;
+    if ((rc = ed_launch(d, st->buf, st->n, d.ev))) return rc;
+    st->pending_timing = st->n > 0;
+    return NWV_OK;
+}
+
+int nwv_staged_sync(nwv_staged* st) {
+    if (!st) return set_err(NWV_ERR_ARG, "null staged");
+    Device& d = *st->dev;
+    std::lock_guard<std::mutex> g(d.mu);
+    int rc = with_device(d);
+    if (rc) return rc;
+    NWV_HIP(hipStreamSynchronize(d.stream));
+    return staged_collect_times(st);
+}
+
+int nwv_staged_fetch(nwv_staged* st, uint64_t* verdict_bits, int* all_valid) {
+    if (!st) return set_err(NWV_ERR_ARG, "null staged");
+    int rc = nwv_staged_sync(st);
+    if (rc) return rc;
+    const size_t words = (st->n + 63) / 64;
+    std::vector<uint64_t> tmp;
+    uint64_t* bits = verdict_bits;
+    if (!bits) {
+        tmp.assign(words + 1, 0);
+        bits = tmp.data();
+    }
+    Device& d = *st->dev;
+    std::lock_guard<std::mutex> g(d.mu);
+    if ((rc = with_device(d))) return rc;
+    if (words) NWV_HIP(hipMemcpy(bits, st->buf.verdict.p, 8 * words, hipMemcpyDeviceToHost));
+    if (all_valid) *all_valid = verdicts_all_valid(bits, st->n) ? 1 : 0;
+    return NWV_OK;
+}
+
+int nwv_staged_kernel_ms(nwv_staged* st, double* avg_ms, int reset) {
+    if (!st || !avg_ms) return set_err(NWV_ERR_ARG, "null argument");
+    int rc = nwv_staged_sync(st);
+    if (rc) return rc;
+    for (int k = 0; k < 3; k++) avg_ms[k] = st->times.runs ? st->times.ms[k] / st->times.runs : 0.0;
+    if (reset) st->times = KernelTimes{};
+    return NWV_OK;
+}
+
+void nwv_staged_free(nwv_staged* st) {
+    if (!st) return;
+    {
+        std::lock_guard<std::mutex> g(st->dev->mu);
+        (void)hipSetDevice(st->dev->ordinal);
+        (void)hipStreamSynchronize(st->dev->stream);
+        st->buf.release();
+    }
+    delete st;
+}
+
+// ---- BLAKE2b-256 --------------------------------------------------------------------
+static int b2_stage(Device& d, size_t n, const uint8_t* base, const uint64_t* off,
+                    const uint64_t* len, size_t lo, size_t hi, std::vector<uint64_t>& roff) {
+    uint64_t mlo = UINT64_MAX, mhi = 0;
+    for (size_t i = lo; i < hi; i++) {
+        mlo = std::min<uint64_t>(mlo, off[i]);
+        mhi = std::max<uint64_t>(mhi, off[i] + len[i]);
+    }
+    if (mhi < mlo) { mlo = 0; mhi = 0; }
+    const size_t m = hi - lo, bytes = (size_t)(mhi - mlo);
+    roff.resize(m);
+    for (size_t i = 0; i < m; i++) roff[i] = off[lo + i] - mlo;
+    int rc;
+    if ((rc = d.b2_base.ensure(bytes + MSG_PAD)) || (rc = d.b2_off.ensure(8 * m + 8)) ||
+        (rc = d.b2_len.ensure(8 * m + 8)) || (rc = d.b2_out.ensure(32 * m + 32)))
+        return rc;
+    (void)n;
+    if (bytes) NWV_HIP(hipMemcpyAsync(d.b2_base.p, base + mlo, bytes, hipMemcpyHostToDevice, d.stream));
+    NWV_HIP(hipMemsetAsync(d.b2_base.as<uint8_t>() + bytes, 0, MSG_PAD, d.stream));
+    NWV_HIP(hipMemcpyAsync(d.b2_off.p, roff.data(), 8 * m, hipMemcpyHostToDevice, d.stream));
+    NWV_HIP(hipMemcpyAsync(d.b2_len.p, len + lo, 8 * m, hipMemcpyHostToDevice, d.stream));
+    return NWV_OK;
+}
+
+int nwv_blake2b256_many(nwv_ctx* ctx, size_t n, const uint8_t* base, const uint64_t* off,
+                        const uint64_t* len, uint8_t* out) {
+    if (!ctx || (n && (!off || !len || !out))) return set_err(NWV_ERR_ARG, "null argument");
+    if (n == 0) return NWV_OK;
+    static const uint8_t empty[1] = {0};
+    if (!base) base = empty;
+    const size_t nd = ctx->devs.size();
+    const size_t per = (n + nd - 1) / nd;
+    std::vector<int> rcs(nd, NWV_OK);
+    std::vector<std::thread> th;
+    for (size_t k = 0; k < nd; k++) {
+        const size_t lo = std::min(n, k * per), hi = std::min(n, (k + 1) * per);
+        if (lo >= hi) continue;
+        auto run = [&, k, lo, hi]() {
+            Device& d = *ctx->devs[k];
+            std::lock_guard<std::mutex> g(d.mu);
+            std::vector<uint64_t> roff;
+            int rc = with_device(d);
+            if (!rc) rc = b2_stage(d, n, base, off, len, lo, hi, roff);
+            if (!rc) {
+                const size_t m = hi - lo;
+                hipLaunchKernelGGL(k_blake2b_many, dim3((unsigned)((m + 255) / 256)), dim3(256), 0,
+                                   d.stream, (uint64_t)m, d.b2_base.as<uint8_t>(),
+                                   d.b2_off.as<uint64_t>(), d.b2_len.as<uint64_t>(),
+                                   d.b2_out.as<uint32_t>());
+                hipError_t e = hipGetLastError();
+                if (e == hipSuccess) e = hipMemcpyAsync(out + 32 * lo, d.b2_out.p, 32 * m,
+                                                        hipMemcpyDeviceToHost, d.stream);
+                if (e == hipSuccess) e = hipStreamSynchronize(d.stream);
+                if (e != hipSuccess) rc = set_err(NWV_ERR_HIP, hipGetErrorString(e));
+            }
+            rcs[k] = rc;
+        };
+        if (nd == 1) run();
+        else th.emplace_back(run);
+    }
+    for (auto& t : th) t.join();
+    for (int rc : rcs)
+        if (rc) return rc;
+    return NWV_OK;
+}
+
+int nwv_batch_digest_serialized(nwv_ctx* ctx, size_t n, const uint8_t* base, const uint64_t* off,
+                                const uint64_t* len, uint8_t* out, int64_t* err_offset) {
+    if (!ctx || (n && (!base || !off || !len || !out || !err_offset)))
+        return set_err(NWV_ERR_ARG, "null argument");
+    if (n == 0) return NWV_OK;
+    Device& d = *ctx->devs[0];
+    std::lock_guard<std::mutex> g(d.mu);
+    int rc = with_device(d);
+    std::vector<uint64_t> roff;
+    if (!rc) rc = b2_stage(d, n, base, off, len, 0, n, roff);
+    if (rc) return rc;
+    size_t bytes = 0;
+    for (size_t i = 0; i < n; i++) bytes = std::max<size_t>(bytes, roff[i] + len[i]);
+    if ((rc = d.b2_packed.ensure(bytes + MSG_PAD)) || (rc = d.b2_plen.ensure(8 * n + 8)) ||
+        (rc = d.b2_err.ensure(8 * n + 8)))
+        return rc;
+    NWV_HIP(hipMemsetAsync(d.b2_packed.p, 0, bytes + MSG_PAD, d.stream));
+    hipLaunchKernelGGL(k_batch_compact, dim3((unsigned)n), dim3(256), 0, d.stream, (uint64_t)n,
+                       d.b2_base.as<uint8_t>(), d.b2_off.as<uint64_t>(), d.b2_len.as<uint64_t>(),
+                       d.b2_packed.as<uint8_t>(), d.b2_plen.as<uint64_t>(), d.b2_err.as<int64_t>());
+    hipLaunchKernelGGL(k_blake2b_many, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, d.stream,
+                       (uint64_t)n, d.b2_packed.as<uint8_t>(), d.b2_off.as<uint64_t>(),
+                       d.b2_plen.as<uint64_t>(), d.b2_out.as<uint32_t>());
+    NWV_HIP(hipGetLastError());
+    NWV_HIP(hipMemcpyAsync(out, d.b2_out.p, 32 * n, hipMemcpyDeviceToHost, d.stream));
+    NWV_HIP(hipMemcpyAsync(err_offset, d.b2_err.p, 8 * n, hipMemcpyDeviceToHost, d.stream));
+    NWV_HIP(hipStreamSynchronize(d.stream));
+    for (size_t i = 0; i < n; i++)
+        if (err_offset[i] >= 0) return set_err(NWV_ERR_ARG, "malformed serialized batch");
+    return NWV_OK;
+}
+
+// ---- synthetic signing ----------------------------------------------------------------
+int nwv_ed25519_sign_many(nwv_ctx* ctx, size_t n, const uint8_t* seeds, const uint8_t* msg_base,
+                          const uint64_t* msg_off, const uint32_t* msg_len, uint8_t* pk_out,
+                          uint8_t* sig_out) {
+    if (!ctx || (n && (!seeds || !msg_off || !msg_len || !pk_out || !sig_out)))
+        return set_err(NWV_ERR_ARG, "null argument");
+    if (n == 0) return NWV_OK;
+    static const uint8_t empty[1] = {0};
+    if (!msg_base) msg_base = empty;
+    return for_shards(ctx, n, [&](Device& d, size_t lo, size_t hi) -> int {
+        // messages via the Ed25519 staging; seeds go to kbuf, outputs come back in pk / sig
+        int rc = ed_stage(d, d.ed, lo, hi, nullptr, nullptr, msg_base, msg_off, msg_len);
+        if (rc) return rc;
+        const size_t m = hi - lo;
+        NWV_HIP(hipMemcpyAsync(d.ed.kbuf.p, seeds + 32 * lo, 32 * m, hipMemcpyHostToDevice, d.stream));
+        hipLaunchKernelGGL(k_sign, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, d.stream,
+                           (uint64_t)m, d.ed.kbuf.as<uint8_t>(), d.ed.msg.as<uint8_t>(),
+                           d.ed.off.as<uint64_t>(), d.ed.len.as<uint32_t>(), d.btab.as<uint32_t>(),
+                           d.ed.pk.as<uint8_t>(), d.ed.sig.as<uint8_t>());
+        NWV_HIP(hipGetLastError());
+        NWV_HIP(hipMemcpyAsync(pk_out + 32 * lo, d.ed.pk.p, 32 * m, hipMemcpyDeviceToHost, d.stream));
+        NWV_HIP(hipMemcpyAsync(sig_out + 64 * lo, d.ed.sig.p, 64 * m, hipMemcpyDeviceToHost, d.stream));
+        NWV_HIP(hipStreamSynchronize(d.stream));
+        return NWV_OK;
+    });
+}
+
+}  // extern "C"

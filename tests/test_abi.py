@@ -1,0 +1,46 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library loads, exports every entry point
+declared in include/nwv.h, and refuses to run without a gfx950 device (no CPU fallback)."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+import narwhal_amd
+from narwhal_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_header_symbol():
+    names = _lib.exported_symbols_from_header()
+    assert len(names) >= 20
+    lib = _lib.load()
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    assert set(names) <= exported
+
+
+def test_abi_version():
+    assert _lib.load().nwv_abi_version() == 1
+
+
+def test_library_contains_gfx950_code_object():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-S", _lib.LIB_PATH],
+                         capture_output=True, text=True).stdout
+    assert ".hip_fatbin" in out
+    raw = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in raw
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK),
+                    reason="a GPU is present")
+def test_no_cpu_fallback_without_gpu():
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    rc = lib.nwv_init(ctypes.byref(h), 0, 0)
+    assert rc == _lib.NWV_ERR_NODEV
+    with pytest.raises(narwhal_amd.NwvError):
+        narwhal_amd.Engine(device=0)

@@ -1,0 +1,56 @@
+"""GPU parity of the BLAKE2b-256 kernels: fastcrypto::blake2b_256 known answers
+(RFC 7693 / hashlib, committed in tests/golden) and serialized_batch_digest
+(types/src/worker.rs:44-80) on the reference's golden bincode layout."""
+import hashlib
+import random
+import struct
+
+import pytest
+
+import oracle_ffi as of
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    import narwhal_amd
+    e = narwhal_amd.Engine(device=0)
+    yield e
+    e.close()
+
+
+def test_known_answers(eng):
+    g = of.load_golden("hash_vectors.json")
+    msgs = [bytes.fromhex(v["msg"]) for v in g["blake2b256"]]
+    got = eng.blake2b256_many(msgs)
+    assert [d.hex() for d in got] == [v["digest"] for v in g["blake2b256"]]
+
+
+def test_many_random_lengths(eng):
+    rnd = random.Random(1)
+    msgs = [bytes(rnd.getrandbits(8) for _ in range(rnd.randrange(0, 700))) for _ in range(500)]
+    assert eng.blake2b256_many(msgs) == [hashlib.blake2b(m, digest_size=32).digest() for m in msgs]
+
+
+def test_serialized_batches_golden(eng):
+    g = of.load_golden("worker_batches.json")
+    bufs = [bytes.fromhex(b["serialized"]) for b in g["batches"] if "serialized" in b]
+    exp = [b["digest"] for b in g["batches"] if "serialized" in b]
+    got = eng.batch_digest_serialized(bufs)
+    assert [d.hex() for d, e in got] == exp
+    assert all(e == -1 for _, e in got)
+    bad = [bytes.fromhex(m["hex"]) for m in g["malformed"]]
+    got = eng.batch_digest_serialized(bad)
+    assert [e for _, e in got] == [m["err_offset"] for m in g["malformed"]]
+
+
+def test_worker_batch_500kb(eng):
+    # config 5 worker batch: 977 txs x 512 B (node/src/benchmark_client.rs:153-168 layout)
+    rnd = random.Random(5)
+    txs = [(bytes([1]) + struct.pack(">Q", rnd.getrandbits(64))).ljust(512, b"\0") for _ in range(977)]
+    ser = struct.pack("<IQ", 0, len(txs)) + b"".join(struct.pack("<Q", len(t)) + t for t in txs)
+    want = hashlib.blake2b(b"".join(txs), digest_size=32).digest()
+    (d, e), = eng.batch_digest_serialized([ser])
+    assert e == -1 and d == want
+    assert eng.blake2b256_many([b"".join(txs)]) == [want]

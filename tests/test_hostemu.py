@@ -1,0 +1,114 @@
+"""The device arithmetic (narwhal_amd/csrc/*.h) compiled for the host with limb-magnitude
+assertions (tests/hostemu), checked against the golden fixtures and the oracle.  This pins the
+kernel math on CPU; the GPU parity tests (-m gpu) pin the compiled kernels."""
+import ctypes
+import hashlib
+import os
+import random
+
+import pytest
+
+import oracle_ffi as of
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HE_PATH = os.path.join(ROOT, "tests", "_build", "libhostemu.so")
+
+
+@pytest.fixture(scope="module")
+def he():
+    if not os.path.exists(HE_PATH):
+        import subprocess
+        subprocess.run(["make", "-C", ROOT, "hostemu"], check=True)
+    lib = ctypes.CDLL(HE_PATH)
+    lib.he_verify.argtypes = [ctypes.c_char_p] * 3 + [ctypes.c_uint32]
+    lib.he_sha512_p64.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p]
+    lib.he_blake2b256.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p]
+    lib.he_sc_reduce.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
+    lib.he_sign.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+    lib.he_decompress.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
+    return lib
+
+
+def _v(v):
+    return bytes.fromhex(v["pk"]), bytes.fromhex(v["sig"]), bytes.fromhex(v["msg"])
+
+
+def test_golden_vectors(he):
+    g = of.load_golden("ed25519_vectors.json")
+    for v in g["vectors"]:
+        pk, sig, msg = _v(v)
+        assert bool(he.he_verify(pk, sig, msg, len(msg))) == v["expect"], v["category"]
+
+
+def test_zip215_small_order(he):
+    for v in of.load_golden("zip215_small_order.json")["vectors"]:
+        pk, sig, msg = _v(v)
+        assert he.he_verify(pk, sig, msg, len(msg)) == 1
+
+
+def test_differential_random_and_adversarial(he):
+    rnd = random.Random(11)
+    for _ in range(800):
+        seed = bytes(rnd.getrandbits(8) for _ in range(32))
+        n = rnd.choice([0, 1, 7, 32, 64, 100, 512])
+        m = bytes(rnd.getrandbits(8) for _ in range(n))
+        sig = bytearray(of.sign(seed, m))
+        pk = bytearray(of.pubkey(seed))
+        r = rnd.random()
+        if r < 0.3:
+            sig[rnd.randrange(64)] ^= 1 << rnd.randrange(8)
+        elif r < 0.4:
+            pk[rnd.randrange(32)] ^= 1 << rnd.randrange(8)
+        elif r < 0.5:
+            sig = bytearray(rnd.getrandbits(8) for _ in range(64))
+        assert bool(he.he_verify(bytes(pk), bytes(sig), m, n)) == of.verify(bytes(pk), bytes(sig), m)
+
+
+def test_decompress_matches_oracle_acceptance(he):
+    rnd = random.Random(3)
+    out = ctypes.create_string_buffer(64)
+    for _ in range(300):
+        b = bytes(rnd.getrandbits(8) for _ in range(32))
+        assert bool(he.he_decompress(b, out)) == bool(of.lib().or_point_decompress_ok(b))
+
+
+def test_hashes_and_scalars(he):
+    out = ctypes.create_string_buffer(64)
+    rnd = random.Random(5)
+    for n in [0, 1, 3, 31, 32, 47, 48, 49, 63, 64, 111, 112, 113, 200, 511, 512, 1000]:
+        pre = bytes(rnd.getrandbits(8) for _ in range(64))
+        m = bytes(rnd.getrandbits(8) for _ in range(n))
+        he.he_sha512_p64(pre, m, n, out)
+        assert out.raw == hashlib.sha512(pre + m).digest()
+    g = of.load_golden("hash_vectors.json")
+    for v in g["blake2b256"]:
+        m = bytes.fromhex(v["msg"])
+        he.he_blake2b256(m, len(m), out)
+        assert out.raw[:32].hex() == v["digest"]
+    for v in g["sc_reduce"]:
+        he.he_sc_reduce(bytes.fromhex(v["in"]), out)
+        assert out.raw[:32].hex() == v["out"]
+
+
+def test_signing_matches_rfc8032(he):
+    pk = ctypes.create_string_buffer(32)
+    sg = ctypes.create_string_buffer(64)
+    for k in of.load_golden("keys.json")["keys"]:
+        seed = bytes.fromhex(k["seed"])
+        for m in (b"", b"narwhal", bytes(range(200))):
+            he.he_sign(seed, m, len(m), pk, sg)
+            assert pk.raw.hex() == k["pk"]
+            assert sg.raw == of.sign(seed, m)
+
+
+def test_phase_op_counts_match_bench_constants(he):
+    """bench.py's roofline numerator: field multiplies/squarings per signature and phase."""
+    import bench
+    c = (ctypes.c_ulonglong * 6)()
+    seed = b"\x01" * 32
+    for mlen in (0, 32, 512):
+        m = bytes(mlen)
+        he.he_phase_counts(of.pubkey(seed), of.sign(seed, m), m, mlen, c)
+        assert (c[0], c[1]) == (0, 0)
+        assert (c[2], c[3]) == bench.OPS_POINTS
+        assert (c[4], c[5]) == bench.OPS_STRAUS
