@@ -92,6 +92,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-reps", type=int, default=300)
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="resident batches in flight on separate streams (step s runs batch s %% K)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -108,29 +110,37 @@ def main():
 
     eng = narwhal_amd.Engine(device=local)
     pk, sg, msgs, offs, lens = synth(eng, args.n, args.msg_len, seed=1000 + rank)
-    st = eng.stage(pk, sg, msgs, offs, lens)
+    stages = [eng.stage(pk, sg, msgs, offs, lens) for _ in range(max(1, args.inflight))]
+    st = stages[0]
 
-    for _ in range(args.warmup):
-        st.run(mode=1)
-    st.sync()
-    st.kernel_ms(reset=True)
+    def sync_all():
+        for s_ in stages:
+            s_.sync()
+
+    for w in range(args.warmup):
+        stages[w % len(stages)].run(mode=1)
+    sync_all()
+    for s_ in stages:
+        s_.kernel_ms(reset=True)
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
     barrier()
-    st.sync()
+    sync_all()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        st.run(mode=1)
-    st.sync()
+    for s in range(args.steps):
+        stages[s % len(stages)].run(mode=1)
+    sync_all()
     t1 = time.perf_counter()
     barrier()
     dt = t1 - t0
-    all_valid, bits = st.fetch()
+    ok = 1
+    for s_ in stages:
+        all_valid, bits = s_.fetch()
+        ok &= int(bool(all_valid) and bool(bits.all()))
     kms = st.kernel_ms(reset=True)
-    ok = int(bool(all_valid) and bool(bits.all()))
     if dist is not None:
         import torch
         t = torch.tensor([dt], dtype=torch.float64)
@@ -139,7 +149,8 @@ def main():
         o = torch.tensor([ok], dtype=torch.int32)
         dist.all_reduce(o, op=dist.ReduceOp.MIN)
         ok = int(o.item())
-    st.free()
+    for s_ in stages:
+        s_.free()
     if not ok:
         raise SystemExit("verification of a valid synthetic batch failed")
 
@@ -198,7 +209,8 @@ def main():
             "config": {"workload": "verify_batch of 65,536 valid sigs, 512 B messages, distinct keys "
                                    "(BASELINE.json configs[1]) per GPU",
                        "sigs_per_gpu": args.n, "msg_len": args.msg_len,
-                       "parallelism": f"signature-index shards x{world}"},
+                       "parallelism": f"signature-index shards x{world}",
+                       "inflight_batches": len(stages)},
             "latency_1k_batch_ms": {"p50": float(np.percentile(lat, 50)),
                                     "p99": float(np.percentile(lat, 99)), "reps": len(lat)},
             "roofline": roof,

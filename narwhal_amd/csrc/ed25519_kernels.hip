@@ -55,15 +55,28 @@ extern "C" __global__ void __launch_bounds__(256) k_ed_hash(
     store_words8(kbuf + 32 * i, k);
 }
 
+// Two lanes per signature, in different waves: even waves decompress R (table entry
+// R_ENTRY) for 64 signatures, odd waves decompress A and build entries 0..8 for the same 64.
+// The role is wave-uniform (no divergence); the wave count doubles and each lane's chain
+// halves.  Flags are combined with an atomic OR.
 extern "C" __global__ void __launch_bounds__(256) k_ed_points(
     uint64_t n, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
     uint32_t* __restrict__ tables, uint32_t* __restrict__ flags) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t wv = t >> 6;
+    const uint64_t i = (wv >> 1) * 64 + (t & 63);
     if (i >= n) return;
-    uint32_t Aw[8], Rw[8];
-    load_words8(pk + 32 * i, Aw);
-    load_words8(sig + 64 * i, Rw);
-    flags[i] |= lane_points(Aw, Rw, tables + i * LANE_SCRATCH_WORDS);
+    uint32_t w[8];
+    uint32_t* tbl = tables + i * LANE_SCRATCH_WORDS;
+    uint32_t f;
+    if ((wv & 1) == 0) {
+        load_words8(sig + 64 * i, w);
+        f = lane_point_R(w, tbl);
+    } else {
+        load_words8(pk + 32 * i, w);
+        f = lane_point_A(w, tbl);
+    }
+    atomicOr(flags + i, f);
 }
 
 extern "C" __global__ void __launch_bounds__(256) k_ed_straus(

@@ -115,18 +115,22 @@ NWV_HD uint32_t lane_hash(const uint32_t Aw[8], const uint32_t Rw[8], const uint
     challenge_scalar(Rw, Aw, msg, mlen, k);
     return sc_is_canonical(Sw) ? FLAG_S_OK : 0u;
 }
-// phase 2: decompress R (entry R_ENTRY) and A (entries 0..8 = j A)
-NWV_HD uint32_t lane_points(const uint32_t Aw[8], const uint32_t Rw[8], uint32_t* tbl) {
-    uint32_t f = 0;
-    {
-        ge_p3 R;
-        f |= ge_decompress(Rw, R) ? FLAG_R_OK : 0u;
-        store_cached_entry(tbl + R_ENTRY * CACHED_ENTRY_WORDS, ge_p3_to_cached(R));
-    }
+// phase 2: decompress R (entry R_ENTRY) and A (entries 0..8 = j A); on the GPU the two halves
+// run in two lanes
+NWV_HD uint32_t lane_point_R(const uint32_t Rw[8], uint32_t* tbl) {
+    ge_p3 R;
+    const uint32_t f = ge_decompress(Rw, R) ? FLAG_R_OK : 0u;
+    store_cached_entry(tbl + R_ENTRY * CACHED_ENTRY_WORDS, ge_p3_to_cached(R));
+    return f;
+}
+NWV_HD uint32_t lane_point_A(const uint32_t Aw[8], uint32_t* tbl) {
     ge_p3 A;
-    f |= ge_decompress(Aw, A) ? FLAG_A_OK : 0u;
+    const uint32_t f = ge_decompress(Aw, A) ? FLAG_A_OK : 0u;
     build_a_table(A, tbl);
     return f;
+}
+NWV_HD uint32_t lane_points(const uint32_t Aw[8], const uint32_t Rw[8], uint32_t* tbl) {
+    return lane_point_R(Rw, tbl) | lane_point_A(Aw, tbl);
 }
 // phase 3: [8]([s]B - [k]A - R) == identity
 NWV_HD bool lane_straus_check(const uint32_t k[8], const uint32_t Sw[8], const uint32_t* tbl,

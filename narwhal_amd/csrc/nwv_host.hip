@@ -78,7 +78,6 @@ struct Device {
     DevBuf btab;
     EdBuffers ed;
     DevBuf b2_base, b2_off, b2_len, b2_out, b2_packed, b2_plen, b2_err;
-    hipEvent_t ev[6] = {};
 };
 
 int with_device(Device& d) {
@@ -94,7 +93,6 @@ int device_open(Device& d, int ordinal) {
         return set_err(NWV_ERR_NODEV, std::string("device is ") + prop.gcnArchName + ", need gfx950");
     NWV_HIP(hipSetDevice(ordinal));
     NWV_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-    for (auto& e : d.ev) NWV_HIP(hipEventCreate(&e));
     int rc = d.btab.ensure((BASE_TABLE_WORDS + CACHED_ENTRY_WORDS) * sizeof(uint32_t));
     if (rc) return rc;
     hipLaunchKernelGGL(k_base_table, dim3((BASE_TABLE_ENTRIES + 63) / 64), dim3(64), 0, d.stream,
@@ -112,8 +110,6 @@ void device_close(Device& d) {
     d.ed.release();
     for (DevBuf* b : {&d.b2_base, &d.b2_off, &d.b2_len, &d.b2_out, &d.b2_packed, &d.b2_plen, &d.b2_err})
         b->release();
-    for (auto& e : d.ev)
-        if (e) (void)hipEventDestroy(e);
     if (d.stream) (void)hipStreamDestroy(d.stream);
     d.stream = nullptr;
 }
@@ -126,21 +122,22 @@ struct KernelTimes {
 
 // Launch the three-phase per-signature pipeline on buffers already resident on `d`.
 // Events bracket each kernel on d.stream when `ev` is non-null (ev[0..5]).
-int ed_launch(Device& d, EdBuffers& b, size_t n, hipEvent_t* ev) {
+int ed_launch(Device& d, EdBuffers& b, size_t n, hipStream_t stream, hipEvent_t* ev) {
     if (n == 0) return NWV_OK;
-    const dim3 blk(256), grid((unsigned)((n + 255) / 256));
-    if (ev) NWV_HIP(hipEventRecord(ev[0], d.stream));
-    hipLaunchKernelGGL(k_ed_hash, grid, blk, 0, d.stream, (uint64_t)n, b.pk.as<uint8_t>(),
+    const size_t waves = (n + 63) / 64;
+    const dim3 blk(256), grid((unsigned)((n + 255) / 256)), grid2((unsigned)((2 * 64 * waves + 255) / 256));
+    if (ev) NWV_HIP(hipEventRecord(ev[0], stream));
+    hipLaunchKernelGGL(k_ed_hash, grid, blk, 0, stream, (uint64_t)n, b.pk.as<uint8_t>(),
                        b.sig.as<uint8_t>(), b.msg.as<uint8_t>(), b.off.as<uint64_t>(),
                        b.len.as<uint32_t>(), b.kbuf.as<uint8_t>(), b.flags.as<uint32_t>());
-    if (ev) NWV_HIP(hipEventRecord(ev[1], d.stream));
-    hipLaunchKernelGGL(k_ed_points, grid, blk, 0, d.stream, (uint64_t)n, b.pk.as<uint8_t>(),
+    if (ev) NWV_HIP(hipEventRecord(ev[1], stream));
+    hipLaunchKernelGGL(k_ed_points, grid2, blk, 0, stream, (uint64_t)n, b.pk.as<uint8_t>(),
                        b.sig.as<uint8_t>(), b.tables.as<uint32_t>(), b.flags.as<uint32_t>());
-    if (ev) NWV_HIP(hipEventRecord(ev[2], d.stream));
-    hipLaunchKernelGGL(k_ed_straus, grid, blk, 0, d.stream, (uint64_t)n, b.sig.as<uint8_t>(),
+    if (ev) NWV_HIP(hipEventRecord(ev[2], stream));
+    hipLaunchKernelGGL(k_ed_straus, grid, blk, 0, stream, (uint64_t)n, b.sig.as<uint8_t>(),
                        b.kbuf.as<uint8_t>(), b.tables.as<uint32_t>(), b.flags.as<uint32_t>(),
                        d.btab.as<uint32_t>(), b.verdict.as<uint64_t>());
-    if (ev) NWV_HIP(hipEventRecord(ev[3], d.stream));
+    if (ev) NWV_HIP(hipEventRecord(ev[3], stream));
     NWV_HIP(hipGetLastError());
     return NWV_OK;
 }
@@ -203,6 +200,8 @@ struct nwv_staged {
     Device* dev = nullptr;
     EdBuffers buf;
     size_t n = 0;
+    hipStream_t stream = nullptr;  // each resident batch runs on its own stream, so several
+    hipEvent_t ev[4] = {};         // staged batches on one device overlap
     KernelTimes times;
     bool pending_timing = false;
 };
@@ -302,7 +301,7 @@ int nwv_ed25519_verify_each(nwv_ctx* ctx, size_t n, const uint8_t* pk, const uin
     return for_shards(ctx, n, [&](Device& d, size_t lo, size_t hi) -> int {
         int rc = ed_stage(d, d.ed, lo, hi, pk, sig, msg_base, msg_off, msg_len);
         if (rc) return rc;
-        if ((rc = ed_launch(d, d.ed, hi - lo, nullptr))) return rc;
+        if ((rc = ed_launch(d, d.ed, hi - lo, d.stream, nullptr))) return rc;
         const size_t words = (hi - lo + 63) / 64;
         NWV_HIP(hipMemcpyAsync(verdict_bits + lo / 64, d.ed.verdict.p, 8 * words,
                                hipMemcpyDeviceToHost, d.stream));
@@ -427,6 +426,10 @@ int nwv_stage_ed25519(nwv_ctx* ctx, int device_index, size_t n, const uint8_t* p
     std::lock_guard<std::mutex> g(st->dev->mu);
     int rc = with_device(*st->dev);
     if (!rc) rc = ed_stage(*st->dev, st->buf, 0, n, pk, sig, msg_base, msg_off, msg_len);
+    if (!rc && hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking) != hipSuccess)
+        rc = set_err(NWV_ERR_HIP, "hipStreamCreate");
+    for (auto& e : st->ev)
+        if (!rc && hipEventCreate(&e) != hipSuccess) rc = set_err(NWV_ERR_HIP, "hipEventCreate");
     if (rc) {
         st->buf.release();
         delete st;
@@ -438,11 +441,10 @@ int nwv_stage_ed25519(nwv_ctx* ctx, int device_index, size_t n, const uint8_t* p
 
 static int staged_collect_times(nwv_staged* st) {
     if (!st->pending_timing) return NWV_OK;
-    Device& d = *st->dev;
-    NWV_HIP(hipEventSynchronize(d.ev[3]));
+    NWV_HIP(hipEventSynchronize(st->ev[3]));
     for (int k = 0; k < 3; k++) {
         float ms = 0;
-        NWV_HIP(hipEventElapsedTime(&ms, d.ev[k], d.ev[k + 1]));
+        NWV_HIP(hipEventElapsedTime(&ms, st->ev[k], st->ev[k + 1]));
         st->times.ms[k] += ms;
     }
     st->times.runs++;
@@ -458,7 +460,7 @@ int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]) {
     int rc = with_device(d);
     if (rc) return rc;
     if ((rc = staged_collect_times(st))) return rc;
-    if ((rc = ed_launch(d, st->buf, st->n, d.ev))) return rc;
+    if ((rc = ed_launch(d, st->buf, st->n, st->stream, st->ev))) return rc;
     st->pending_timing = st->n > 0;
     return NWV_OK;
 }
@@ -469,7 +471,7 @@ int nwv_staged_sync(nwv_staged* st) {
     std::lock_guard<std::mutex> g(d.mu);
     int rc = with_device(d);
     if (rc) return rc;
-    NWV_HIP(hipStreamSynchronize(d.stream));
+    NWV_HIP(hipStreamSynchronize(st->stream));
     return staged_collect_times(st);
 }
 
@@ -506,8 +508,11 @@ void nwv_staged_free(nwv_staged* st) {
     {
         std::lock_guard<std::mutex> g(st->dev->mu);
         (void)hipSetDevice(st->dev->ordinal);
-        (void)hipStreamSynchronize(st->dev->stream);
+        if (st->stream) (void)hipStreamSynchronize(st->stream);
         st->buf.release();
+        for (auto& e : st->ev)
+            if (e) (void)hipEventDestroy(e);
+        if (st->stream) (void)hipStreamDestroy(st->stream);
     }
     delete st;
 }

@@ -1,0 +1,37 @@
+#!/usr/bin/env python3
+"""Minimal driver for rocprofv3 passes (kernel trace / PMC counters): stages one synthetic
+batch of --n signatures and runs the verification pipeline --reps times.  No CPU baseline,
+no latency loop, so every k_ed_* dispatch in the profile has the same size."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402  (synthetic data generator)
+import narwhal_amd  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--msg-len", type=int, default=512)
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    eng = narwhal_amd.Engine(device=0)
+    pk, sg, msgs, offs, lens = bench.synth(eng, args.n, args.msg_len, seed=7)
+    st = eng.stage(pk, sg, msgs, offs, lens)
+    for _ in range(args.reps):
+        st.run(mode=1)
+    allv, bits = st.fetch()
+    ms = st.kernel_ms()
+    st.free()
+    eng.close()
+    assert allv
+    print(json.dumps({"n": args.n, "reps": args.reps, "kernel_ms": list(map(float, ms))}))
+
+
+if __name__ == "__main__":
+    main()
