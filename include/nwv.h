@@ -36,9 +36,15 @@ extern "C" {
 
 typedef struct nwv_ctx nwv_ctx;
 
+/* nwv_init flags.  Batch verification (nwv_ed25519_verify_batch and the trait entry points built
+ * on it) runs one Pippenger MSM per device shard when the shard has >= 4096 signatures (env
+ * NWV_MSM_MIN_N overrides), else the per-signature pipeline; these force one or the other. */
+#define NWV_FLAG_MSM_ALWAYS 1u
+#define NWV_FLAG_MSM_NEVER 2u
+
 /* ------------------------------------------------------------------ lifecycle ----- */
 /* Process-wide context creation (created once, in Primary::spawn).
- * n_devices: 0 = all visible devices, k = the first k.  flags: reserved, pass 0. */
+ * n_devices: 0 = all visible devices, k = the first k.  flags: NWV_FLAG_* or 0. */
 int nwv_init(nwv_ctx** out, int n_devices, uint32_t flags);
 /* Context bound to one device ordinal (one process per GPU deployments, bench.py). */
 int nwv_init_device(nwv_ctx** out, int device_ordinal, uint32_t flags);
@@ -116,8 +122,10 @@ typedef struct nwv_staged nwv_staged;
 int nwv_stage_ed25519(nwv_ctx* ctx, int device_index, size_t n, const uint8_t* pk,
                       const uint8_t* sig, const uint8_t* msg_base, const uint64_t* msg_off,
                       const uint32_t* msg_len, nwv_staged** out);
-/* mode 0: per-signature verdicts (K4); mode 1: batch verdict. Asynchronous on the device's
- * stream; nwv_staged_sync waits.  verdicts stay on the device until nwv_staged_fetch. */
+/* mode 0: per-signature verdicts (K1-K4); mode 1: batch verdict through one Pippenger MSM (K5),
+ * coefficients keyed by seed32 (NULL: OS entropy).  Asynchronous on the batch's own stream;
+ * nwv_staged_sync waits.  Verdicts stay on the device until nwv_staged_fetch, which after a
+ * rejected mode-1 run also runs the per-signature fallback (exact bad indices). */
 int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]);
 int nwv_staged_sync(nwv_staged* st);
 int nwv_staged_fetch(nwv_staged* st, uint64_t* verdict_bits, int* all_valid);
@@ -125,6 +133,13 @@ int nwv_staged_fetch(nwv_staged* st, uint64_t* verdict_bits, int* all_valid);
  * with HIP events on the stream the kernels run on: avg_ms[0] = k_ed_hash (K1, K3),
  * avg_ms[1] = k_ed_points (K2), avg_ms[2] = k_ed_straus (K4, the dominant kernel) */
 int nwv_staged_kernel_ms(nwv_staged* st, double avg_ms[3], int reset);
+/* per-kernel average device time (ms) of mode `mode` runs since the last reset: fills up to
+ * cap (name, ms) pairs in launch order (names point to static strings) and returns the number
+ * of kernels in that pipeline (< 0 on error).  mode 1 (batch MSM, K5) kernels:
+ * k_msm_scalars, k_msm_bscalar, k_msm_points, k_msm_recode, k_msm_hist, k_scan,
+ * k_msm_scatter, k_msm_bucket, k_msm_window, k_msm_final */
+int nwv_staged_kernel_times(nwv_staged* st, int mode, int cap, const char** names, double* avg_ms,
+                            int reset);
 void nwv_staged_free(nwv_staged* st);
 
 /* ------------------------------------------------------------------ synthetic data ----- */

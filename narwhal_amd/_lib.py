@@ -21,6 +21,8 @@ NWV_ERR_OOM = -3
 NWV_ERR_NODEV = -4
 NWV_ERR_EMPTY = -5
 NWV_ERR_LENGTH = -6
+NWV_FLAG_MSM_ALWAYS = 1
+NWV_FLAG_MSM_NEVER = 2
 
 
 class NwvError(RuntimeError):
@@ -63,6 +65,7 @@ def load():
         "nwv_staged_sync": ([_vp], _i32),
         "nwv_staged_fetch": ([_vp, _vp, ctypes.POINTER(_i32)], _i32),
         "nwv_staged_kernel_ms": ([_vp, _vp, _i32], _i32),
+        "nwv_staged_kernel_times": ([_vp, _i32, _i32, _vp, _vp, _i32], _i32),
         "nwv_staged_free": ([_vp], None),
         "nwv_ed25519_sign_many": ([_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp], _i32),
     }
@@ -105,13 +108,13 @@ def pack_messages(msgs):
 class Engine:
     """A context over one device (device=k) or the first n_devices (device=None)."""
 
-    def __init__(self, device=None, n_devices=0):
+    def __init__(self, device=None, n_devices=0, flags=0):
         lib = load()
         h = _vp()
         if device is None:
-            _check(lib.nwv_init(ctypes.byref(h), n_devices, 0))
+            _check(lib.nwv_init(ctypes.byref(h), n_devices, flags))
         else:
-            _check(lib.nwv_init_device(ctypes.byref(h), device, 0))
+            _check(lib.nwv_init_device(ctypes.byref(h), device, flags))
         self._h = h
         self.lib = lib
 
@@ -228,6 +231,16 @@ class Staged:
         out = np.zeros(3, dtype=np.float64)
         _check(self.eng.lib.nwv_staged_kernel_ms(self._h, _ptr(out), 1 if reset else 0))
         return out
+
+    def kernel_times(self, mode, reset=True):
+        """{kernel name: average device ms} of the mode-`mode` pipeline since the last reset"""
+        cap = 32
+        names = (ctypes.c_char_p * cap)()
+        ms = np.zeros(cap, dtype=np.float64)
+        k = self.eng.lib.nwv_staged_kernel_times(self._h, mode, cap, names, _ptr(ms), 1 if reset else 0)
+        if k < 0:
+            _check(k)
+        return {names[i].decode(): float(ms[i]) for i in range(min(k, cap))}
 
     def free(self):
         if self._h:

@@ -1,0 +1,185 @@
+// msm.h -- lane-level pieces of the batch-verification multi-scalar multiplication (K5).
+//
+// Restates ed25519_consensus 2.0.1 batch::Verifier::verify (SURVEY.md Appendix A "Batch
+// verify"; called through fastcrypto's Ed25519 verify_batch_empty_fail / AggregateSignature
+// ::verify from Certificate::verify, types/src/primary.rs:531-534): for n signatures with
+// random 128-bit z_i the batch is accepted iff
+//     [8]( -(sum z_i s_i) B  +  sum z_i R_i  +  sum (z_i k_i) A_i ) == identity.
+// Any undecodable R/A or non-canonical s rejects the whole batch, exactly as the reference.
+// A single invalid signature makes the check fail deterministically (its error term has a
+// nonzero prime-order component and 0 < z_i < l); several can cancel with probability
+// ~2^-128, the same bound as the reference's.
+//
+// The MSM is Pippenger's bucket method over 2n + 1 points laid out as
+//     j in [0, n)        A_i   scalar z_i k_i mod l   (253 bits)
+//     j = n              B     scalar -sum z_i s_i mod l
+//     j in [n+1, 2n+1)   R_i   scalar z_i             (128 bits)
+// so that the windows above bit 128 only visit the prefix [0, n]. Scalars are recoded to signed
+// digits over the windows of an MsmLayout; bucket |d| - 1 of window w collects sign(d) P_j.
+// Everything here is __host__ __device__ so tests/hostemu can run the same arithmetic on the
+// CPU with limb-bound assertions.
+#pragma once
+#include "ge25519.h"
+#include "sc25519.h"
+#include "sha512.h"
+
+namespace nwv {
+
+static constexpr int P3_WORDS = 40;  // X | Y | Z | T, ten carried limbs each
+
+NWV_HD void store_p3(uint32_t* d, const ge_p3& p) {
+    store_fe(d, p.X);
+    store_fe(d + 10, p.Y);
+    store_fe(d + 20, p.Z);
+    store_fe(d + 30, p.T);
+}
+NWV_HD ge_p3 load_p3(const uint32_t* s) {
+    return ge_p3{load_fe(s), load_fe(s + 10), load_fe(s + 20), load_fe(s + 30)};
+}
+NWV_HD ge_p3 p3_add(const ge_p3& a, const ge_p3& b) {
+    return ge_p1p1_to_p3(ge_add(a, ge_p3_to_cached(b)));
+}
+// [2^k] p, k >= 1, through the projective doubling chain
+NWV_HD ge_p3 p3_dbl_n(const ge_p3& p, int k) {
+    ge_p2 r = ge_p3_to_p2(p);
+    ge_p1p1 t = ge_p2_dbl(r);
+#pragma unroll 1
+    for (int i = 1; i < k; i++) {
+        r = ge_p1p1_to_p2(t);
+        t = ge_p2_dbl(r);
+    }
+    return ge_p1p1_to_p3(t);
+}
+// [8] p == identity (the cofactored acceptance test)
+NWV_HD bool p3_mul8_is_identity(const ge_p3& p) {
+    ge_p2 q = ge_p3_to_p2(p);
+    ge_p1p1 t = ge_p2_dbl(q);
+    q = ge_p1p1_to_p2(t);
+    t = ge_p2_dbl(q);
+    q = ge_p1p1_to_p2(t);
+    t = ge_p2_dbl(q);
+    return ge_p1p1_is_identity(t);
+}
+
+// Per-signature random coefficient z_i in [0, 2^128): the first 16 bytes of
+// SHA-512(seed32 || le64(i) || "nwv-z128"). The reference draws z_i from OsRng; here the
+// caller's 32-byte CSPRNG seed keys a PRF so the kernels need no device RNG state.
+NWV_HD void msm_z(const uint32_t seed[8], uint64_t i, uint32_t z[8]) {
+    uint32_t pre[12];
+#pragma unroll
+    for (int k = 0; k < 8; k++) pre[k] = seed[k];
+    pre[8] = (uint32_t)i;
+    pre[9] = (uint32_t)(i >> 32);
+    pre[10] = 0x2d76776eu;  // "nwv-"
+    pre[11] = 0x3832317au;  // "z128" (little-endian words)
+    sha512_state st;
+    sha512_prefixed(st, pre, 0, [](uint32_t) -> uint32_t { return 0u; });
+    uint32_t h[16];
+    sha512_digest_words(st, h);
+#pragma unroll
+    for (int k = 0; k < 8; k++) z[k] = k < 4 ? h[k] : 0u;
+}
+
+// Window layout.  Windows have near-equal widths <= c chosen so that every window's bucket range
+// is fully used (no skewed top window):  widths 0..nw_z-1 sum to 129 = 128 bits of z plus the
+// signed-digit headroom, and all nw windows sum to 254 = 253 bits of a scalar mod l plus headroom.
+// The top window of each range holds width-1 raw bits plus the incoming carry, i.e. digits in
+// [0, 2^(width-1)], exactly the bucket range of the window; every lower window holds signed
+// digits in [-2^(width-1), 2^(width-1)).  Bucket key of digit d in window w: kbase[w] + |d| - 1.
+static constexpr int MSM_MAX_WINDOWS = 48;
+static constexpr int MSM_BITS_FULL = 253;  // scalars mod l
+static constexpr int MSM_BITS_Z = 128;     // z_i
+
+struct MsmLayout {
+    int32_t nw, nw_z, cmax, pad;
+    uint8_t width[MSM_MAX_WINDOWS];
+    uint16_t pos[MSM_MAX_WINDOWS];
+    uint32_t kbase[MSM_MAX_WINDOWS + 1];  // kbase[nw] = number of bucket keys
+};
+
+NWV_HD void msm_split(MsmLayout& L, int first, int count, int total_bits) {
+    for (int k = 0; k < count; k++) {
+        const int lo = total_bits * k / count, hi = total_bits * (k + 1) / count;
+        L.width[first + k] = (uint8_t)(hi - lo);
+    }
+}
+
+// base width c (6..16) -> layout; false if it does not fit MSM_MAX_WINDOWS
+NWV_HD bool msm_make_layout(int c, MsmLayout& L) {
+    const int lo_bits = MSM_BITS_Z + 1, hi_bits = MSM_BITS_FULL + 1 - lo_bits;
+    const int nz = (lo_bits + c - 1) / c, nh = (hi_bits + c - 1) / c;
+    if (nz + nh > MSM_MAX_WINDOWS) return false;
+    L.nw = nz + nh;
+    L.nw_z = nz;
+    msm_split(L, 0, nz, lo_bits);
+    msm_split(L, nz, nh, hi_bits);
+    int pos = 0, cm = 0;
+    uint32_t kb = 0;
+    for (int w = 0; w < L.nw; w++) {
+        L.pos[w] = (uint16_t)pos;
+        L.kbase[w] = kb;
+        pos += L.width[w];
+        kb += 1u << (L.width[w] - 1);
+        cm = L.width[w] > cm ? L.width[w] : cm;
+    }
+    L.kbase[L.nw] = kb;
+    L.cmax = cm;
+    L.pad = 0;
+    return true;
+}
+
+// raw bits [pos, pos + width) of a 256-bit little-endian scalar (width <= 16)
+NWV_HD uint32_t msm_window_bits(const uint32_t s[8], int pos, int width) {
+    uint64_t v = 0;
+    const int word = pos >> 5, sh = pos & 31;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        if (k == word) v |= (uint64_t)s[k];
+        if (k == word + 1) v |= (uint64_t)s[k] << 32;
+    }
+    return (uint32_t)(v >> sh) & ((1u << width) - 1u);
+}
+
+// Signed recoding of a scalar over windows [0, nw) of layout L (nw = L.nw for scalars mod l,
+// L.nw_z for z); emit(w, d) for every window.
+template <class Emit>
+NWV_HD void msm_recode(const uint32_t s[8], const MsmLayout& L, int nw, Emit emit) {
+    uint32_t carry = 0;
+#pragma unroll 1
+    for (int w = 0; w < nw; w++) {
+        const int c = L.width[w];
+        int d = (int)(msm_window_bits(s, L.pos[w], c) + carry);
+        carry = 0;
+        if (w + 1 < nw && d >= (1 << (c - 1))) {
+            d -= 1 << c;
+            carry = 1;
+        }
+        emit(w, d);
+    }
+}
+
+// Bucket entry encoding: point index | sign bit
+static constexpr uint32_t MSM_NEG = 0x80000000u;
+
+// affine Niels entry (y+x | y-x | 2dxy | -2dxy) of a decompressed point (Z = 1, T = xy)
+NWV_HD void store_affine_entry(uint32_t* e, const ge_p3& p) {
+    ge_precomp q{fe_carry(fe_add(p.Y, p.X)), fe_carry(fe_sub(p.Y, p.X)), fe_mul(p.T, fe_d2())};
+    store_precomp_entry(e, q);
+}
+
+// Weighted bucket sums.  For one window with buckets S_1..S_NB (bucket b has weight b), a lane
+// g owns the L consecutive buckets b = gL+1 .. gL+L and returns, scanning down,
+//     run = sum S_b           acc = sum (b - gL) S_b
+// so that  sum_b b S_b = sum_g acc_g + L * sum_{g >= 1} suffix_g,  suffix_g = sum_{g' >= g} run_g'.
+template <class LoadBucket>
+NWV_HD void msm_segment_sums(int L, LoadBucket load_bucket, ge_p3& run, ge_p3& acc) {
+    run = ge_p3_identity();
+    acc = ge_p3_identity();
+#pragma unroll 1
+    for (int k = L - 1; k >= 0; k--) {
+        run = p3_add(run, load_bucket(k));
+        acc = p3_add(acc, run);
+    }
+}
+
+}  // namespace nwv

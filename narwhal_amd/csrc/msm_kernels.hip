@@ -1,0 +1,424 @@
+// msm_kernels.hip -- K5: batch verification as one Pippenger MSM per batch (gfx950).
+//
+// Pipeline (one batch resident on one device; layout of the 2n+1 points in msm.h):
+//   k_msm_scalars   lane i: k_i = SHA-512(R||A||M) mod l, s_i < l, z_i = PRF(seed, i),
+//                   scalars z_i k_i and z_i; per-workgroup partial sums of z_i s_i
+//   k_msm_bscalar   one workgroup: b = -sum z_i s_i mod l (the basepoint's scalar), B entry
+//   k_msm_points    2 lanes per signature (wave-uniform R / A roles): decompress, store the
+//                   affine Niels entry of each point
+//   k_msm_recode    lane j: signed radix-2^C digits of point j's scalar -> digits[w][j] (i16)
+//   k_msm_hist      workgroup (chunk, window): LDS histogram of the window's bucket ids
+//   k_scan_*        exclusive scan of the (window, bucket, chunk)-ordered counts
+//   k_msm_scatter   workgroup (chunk, window): LDS cursors place j|sign into bucket order
+//   k_msm_bucket    lane per fixed-size chunk of the sorted entries: key-segment sums (mixed
+//                   additions, affine Niels), balanced whatever the bucket sizes
+//   k_msm_fixup     lane per bucket: joins the pieces of buckets that span chunks
+//   k_msm_window    workgroup per window: sum_b b S_b (segment running sums + LDS suffix scan
+//                   + LDS tree), 256 lanes
+//   k_msm_final     Horner over windows, [8], identity test -> batch verdict word
+// The counting sort keeps every histogram / cursor atomic in LDS; the only global atomics are
+// the (rare) failure flags.  Entry order inside a bucket depends on LDS atomic order, which
+// changes the projective representation of a bucket sum but never the group element, so the
+// verdict is deterministic.
+#include "msm.h"
+
+using namespace nwv;
+
+struct MsmSeed {
+    uint32_t w[8];
+};
+
+namespace {
+
+__device__ __forceinline__ void msm_load8(const uint8_t* p, uint32_t w[8]) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    const uint4 a = q[0], b = q[1];
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+    w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+__device__ __forceinline__ void msm_store8(uint32_t* p, const uint32_t w[8]) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+    q[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    q[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+}  // namespace
+
+// scal: (2n+1) x 8 words; partial: gridDim.x x 9 words (sum of z_i s_i over the workgroup, as a
+// plain 288-bit integer); fail: bit 0 set when any s_i >= l
+extern "C" __global__ void __launch_bounds__(256) k_msm_scalars(
+    uint64_t n, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
+    const uint8_t* __restrict__ msg, const uint64_t* __restrict__ msg_off,
+    const uint32_t* __restrict__ msg_len, MsmSeed seed, uint32_t* __restrict__ scal,
+    uint32_t* __restrict__ partial, uint32_t* __restrict__ fail) {
+    __shared__ uint32_t zs_lds[256 * 9];
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t zs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (i < n) {
+        uint32_t Aw[8], Rw[8], Sw[8], k[8], z[8], a[8];
+        msm_load8(pk + 32 * i, Aw);
+        msm_load8(sig + 64 * i, Rw);
+        msm_load8(sig + 64 * i + 32, Sw);
+        const uint32_t f = lane_hash(Aw, Rw, Sw, msg + msg_off[i], msg_len[i], k);
+        if (f != FLAG_S_OK) atomicOr(fail, 1u);
+        msm_z(seed.w, i, z);
+        sc_mul(z, k, a);
+        msm_store8(scal + 8 * i, a);
+        msm_store8(scal + 8 * (n + 1 + i), z);
+        sc_mul(z, Sw, zs);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) zs_lds[threadIdx.x * 9 + k] = zs[k];
+    __syncthreads();
+    // column sums: thread t < 8 adds word t of the 256 values (< 2^40), then thread 0 carries
+    __shared__ unsigned long long col[8];
+    if (threadIdx.x < 8) {
+        unsigned long long s = 0;
+        for (int r = 0; r < 256; r++) s += zs_lds[r * 9 + threadIdx.x];
+        col[threadIdx.x] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long c = 0;
+        uint32_t* out = partial + 9 * blockIdx.x;
+        for (int k = 0; k < 8; k++) {
+            c += col[k];
+            out[k] = (uint32_t)c;
+            c >>= 32;
+        }
+        out[8] = (uint32_t)c;
+    }
+}
+
+// One workgroup of 256: b = -(sum of the partials) mod l -> scal[n]; B's affine entry -> pts[n]
+extern "C" __global__ void __launch_bounds__(256) k_msm_bscalar(
+    uint64_t n, uint32_t nparts, const uint32_t* __restrict__ partial, const uint32_t* __restrict__ btab,
+    uint32_t* __restrict__ scal, uint32_t* __restrict__ pts) {
+    __shared__ unsigned long long col[256 * 9];
+    unsigned long long s[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t p = threadIdx.x; p < nparts; p += 256)
+#pragma unroll
+        for (int k = 0; k < 9; k++) s[k] += partial[9 * p + k];
+#pragma unroll
+    for (int k = 0; k < 9; k++) col[threadIdx.x * 9 + k] = s[k];
+    __syncthreads();
+    if (threadIdx.x < 9) {
+        unsigned long long t = 0;
+        for (int r = 0; r < 256; r++) t += col[r * 9 + threadIdx.x];  // < 2^(32+13+8)
+        col[threadIdx.x] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t x[16];
+        unsigned long long c = 0;
+        for (int k = 0; k < 16; k++) {
+            if (k < 9) c += col[k];
+            x[k] = (uint32_t)c;
+            c >>= 32;
+        }
+        uint32_t r[8], b[8];
+        sc_reduce512(x, r);
+        // b = l - r (mod l)
+        uint32_t nz = 0;
+        for (int k = 0; k < 8; k++) nz |= r[k];
+        long long br = 0;
+        for (int k = 0; k < 8; k++) {
+            long long d = (long long)sc_l(k) - r[k] + br;
+            b[k] = nz ? (uint32_t)d : 0u;
+            br = d >> 32;
+        }
+        for (int k = 0; k < 8; k++) scal[8 * n + k] = b[k];
+    }
+    if (threadIdx.x < PRECOMP_ENTRY_WORDS)
+        pts[(size_t)PRECOMP_ENTRY_WORDS * n + threadIdx.x] = btab[PRECOMP_ENTRY_WORDS + threadIdx.x];  // 1*B
+}
+
+// Two lanes per signature in different waves (as k_ed_points): even waves decompress R_i into
+// point n+1+i, odd waves A_i into point i.
+extern "C" __global__ void __launch_bounds__(256) k_msm_points(
+    uint64_t n, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
+    uint32_t* __restrict__ pts, uint32_t* __restrict__ fail) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t wv = t >> 6;
+    const uint64_t i = (wv >> 1) * 64 + (t & 63);
+    if (i >= n) return;
+    uint32_t w[8];
+    const bool is_r = (wv & 1) == 0;
+    msm_load8(is_r ? sig + 64 * i : pk + 32 * i, w);
+    ge_p3 P;
+    const bool ok = ge_decompress(w, P);
+    store_affine_entry(pts + (size_t)PRECOMP_ENTRY_WORDS * (is_r ? n + 1 + i : i), P);
+    if (!ok) atomicOr(fail, 2u);
+}
+
+// digits[w * np + j] for w < windows(j); np = 2n + 1
+extern "C" __global__ void __launch_bounds__(256) k_msm_recode(uint64_t n, MsmLayout lay,
+                                                               const uint32_t* __restrict__ scal,
+                                                               int16_t* __restrict__ digits) {
+    const uint64_t np = 2 * n + 1;
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= np) return;
+    uint32_t s[8];
+    msm_load8(reinterpret_cast<const uint8_t*>(scal + 8 * j), s);
+    const int nw = j <= n ? lay.nw : lay.nw_z;
+    msm_recode(s, lay, nw, [&](int w, int d) { digits[(uint64_t)w * np + j] = (int16_t)d; });
+}
+
+// points of window w: all 2n+1 below nw_z, else the prefix [0, n]
+__device__ __forceinline__ uint64_t msm_window_points(uint64_t n, int w, int nw_z) {
+    return w < nw_z ? 2 * n + 1 : n + 1;
+}
+
+// grid (chunks, windows); counts laid out [(kbase[w] + b) * chunks + chunk]
+extern "C" __global__ void __launch_bounds__(256) k_msm_hist(
+    uint64_t n, MsmLayout lay, uint32_t chunk_pts, const int16_t* __restrict__ digits,
+    uint32_t* __restrict__ cnt) {
+    extern __shared__ uint32_t hist[];
+    const int w = blockIdx.y, nw_z = lay.nw_z, nb = 1 << (lay.width[w] - 1);
+    const uint32_t chunks = gridDim.x, chunk = blockIdx.x;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) hist[b] = 0;
+    __syncthreads();
+    const uint64_t np = 2 * n + 1, cnt_w = msm_window_points(n, w, nw_z);
+    const uint64_t lo = (uint64_t)chunk * chunk_pts;
+    const uint64_t hi = lo + chunk_pts < cnt_w ? lo + chunk_pts : cnt_w;
+    const int16_t* dw = digits + (uint64_t)w * np;
+    for (uint64_t j = lo + threadIdx.x; j < hi; j += blockDim.x) {
+        const int d = dw[j];
+        if (d) atomicAdd(&hist[(d < 0 ? -d : d) - 1], 1u);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < nb; b += blockDim.x)
+        cnt[((uint64_t)lay.kbase[w] + b) * chunks + chunk] = hist[b];
+}
+
+extern "C" __global__ void __launch_bounds__(256) k_msm_scatter(
+    uint64_t n, MsmLayout lay, uint32_t chunk_pts, const int16_t* __restrict__ digits,
+    const uint32_t* __restrict__ off, uint32_t* __restrict__ entries) {
+    extern __shared__ uint32_t cur[];
+    const int w = blockIdx.y, nw_z = lay.nw_z, nb = 1 << (lay.width[w] - 1);
+    const uint32_t chunks = gridDim.x, chunk = blockIdx.x;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x)
+        cur[b] = off[((uint64_t)lay.kbase[w] + b) * chunks + chunk];
+    __syncthreads();
+    const uint64_t np = 2 * n + 1, cnt_w = msm_window_points(n, w, nw_z);
+    const uint64_t lo = (uint64_t)chunk * chunk_pts;
+    const uint64_t hi = lo + chunk_pts < cnt_w ? lo + chunk_pts : cnt_w;
+    const int16_t* dw = digits + (uint64_t)w * np;
+    for (uint64_t j = lo + threadIdx.x; j < hi; j += blockDim.x) {
+        const int d = dw[j];
+        if (d) {
+            const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
+            const uint32_t slot = atomicAdd(&cur[b], 1u);
+            entries[slot] = (uint32_t)j | (d < 0 ? MSM_NEG : 0u);
+        }
+    }
+}
+
+// ---- exclusive scan of u32 counts (tiles of 4096: 256 threads x 16) ----------------------
+extern "C" __global__ void __launch_bounds__(256) k_scan_tile(uint64_t len, uint32_t* __restrict__ a,
+                                                              uint32_t* __restrict__ tile_sum) {
+    __shared__ uint32_t sh[256];
+    const uint64_t base = (uint64_t)blockIdx.x * 4096 + threadIdx.x * 16;
+    uint32_t v[16], s = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        v[k] = base + k < len ? a[base + k] : 0u;
+        s += v[k];
+    }
+    sh[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+        const uint32_t x = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0u;
+        __syncthreads();
+        sh[threadIdx.x] += x;
+        __syncthreads();
+    }
+    uint32_t run = sh[threadIdx.x] - s;  // exclusive prefix of this thread
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        if (base + k < len) a[base + k] = run;
+        run += v[k];
+    }
+    if (threadIdx.x == 255) tile_sum[blockIdx.x] = sh[255];
+}
+
+// one workgroup: exclusive scan of the tile sums in place; tile_sum[ntiles] = total
+extern "C" __global__ void __launch_bounds__(1024) k_scan_tiles(uint32_t ntiles, uint32_t* __restrict__ t) {
+    __shared__ uint32_t sh[1024];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < ntiles; b0 += 1024) {
+        const uint32_t idx = b0 + threadIdx.x;
+        const uint32_t v = idx < ntiles ? t[idx] : 0u;
+        sh[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            const uint32_t x = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0u;
+            __syncthreads();
+            sh[threadIdx.x] += x;
+            __syncthreads();
+        }
+        if (idx < ntiles) t[idx] = carry + sh[threadIdx.x] - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry += sh[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) t[ntiles] = carry;
+}
+
+// adds the tile offsets; also gathers kstart[key] = a[key * chunks] (first entry of each key)
+extern "C" __global__ void __launch_bounds__(256) k_scan_add(uint64_t len, uint32_t* __restrict__ a,
+                                                             const uint32_t* __restrict__ tile_sum,
+                                                             uint32_t chunks, uint32_t* __restrict__ kstart) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < len) {
+        const uint32_t v = a[i] + tile_sum[i >> 12];
+        a[i] = v;
+        if (i % chunks == 0) kstart[i / chunks] = v;
+    }
+}
+
+// ---- bucket sums: fixed-size chunks of the sorted entries ---------------------------------
+// Lane q adds the entries [qT, qT + T) (mixed additions of affine Niels points, the next point's
+// words loaded while the current one is added).  Each key segment that ends inside the chunk is
+// written out: to bsum[key] if the key starts in this chunk (complete, or the key's first piece),
+// else to hpart[q] (a continuation from earlier chunks, completed by k_msm_fixup).  Every lane
+// does the same number of additions whatever the bucket sizes.
+__device__ __forceinline__ void msm_load_entry(const uint32_t* __restrict__ pts, uint32_t v, ge_precomp& q) {
+    const uint32_t* e = pts + (size_t)PRECOMP_ENTRY_WORDS * (v & ~MSM_NEG);
+    const bool neg = (v & MSM_NEG) != 0;
+    q.ypx = load_fe(e + (neg ? 10 : 0));
+    q.ymx = load_fe(e + (neg ? 0 : 10));
+    q.xy2d = load_fe(e + (neg ? 30 : 20));
+}
+
+extern "C" __global__ void __launch_bounds__(256) k_msm_bucket(
+    uint32_t T, uint32_t nkeys, const uint32_t* __restrict__ total, const uint32_t* __restrict__ entries,
+    const uint32_t* __restrict__ kstart, const uint32_t* __restrict__ pts, uint32_t* __restrict__ bsum,
+    uint32_t* __restrict__ hpart) {
+    const uint32_t E = *total;
+    const uint64_t k0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * T;
+    if (k0 >= E) return;
+    const uint32_t k1 = (uint32_t)(k0 + T < E ? k0 + T : E);
+    // key = the largest key with kstart[key] <= k0 (non-empty, contains entry k0)
+    uint32_t lo = 0, hi = nkeys;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (kstart[mid] <= k0) lo = mid;
+        else hi = mid;
+    }
+    uint32_t key = lo;
+    uint32_t kend = key + 1 < nkeys ? kstart[key + 1] : E;
+    bool head = kstart[key] < k0;
+    ge_p3 acc = ge_p3_identity();
+    ge_precomp nxt;
+    msm_load_entry(pts, entries[k0], nxt);
+#pragma unroll 1
+    for (uint32_t k = (uint32_t)k0; k < k1; k++) {
+        const ge_precomp cur = nxt;
+        if (k + 1 < k1) msm_load_entry(pts, entries[k + 1], nxt);
+        acc = ge_p1p1_to_p3(ge_madd(acc, cur));
+        if (k + 1 == k1 || k + 1 == kend) {
+            store_p3(head ? hpart + (size_t)P3_WORDS * (k0 / T) : bsum + (size_t)P3_WORDS * key, acc);
+            acc = ge_p3_identity();
+            head = false;
+            if (k + 1 < k1) {
+                do {  // next non-empty key
+                    key++;
+                    kend = key + 1 < nkeys ? kstart[key + 1] : E;
+                } while (kend <= k + 1);
+            }
+        }
+    }
+}
+
+// One lane per key: empty buckets become the identity; a key spanning chunks i0..i1 adds the
+// continuation pieces hpart[i0+1 .. i1] to its first piece.
+extern "C" __global__ void __launch_bounds__(256) k_msm_fixup(
+    uint32_t nkeys, uint32_t chunks, uint32_t T, const uint32_t* __restrict__ off,
+    const uint32_t* __restrict__ total, const uint32_t* __restrict__ hpart, uint32_t* __restrict__ bsum) {
+    const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
+    if (key >= nkeys) return;
+    const uint32_t s = off[(uint64_t)key * chunks];
+    const uint32_t e = key + 1 < nkeys ? off[(uint64_t)(key + 1) * chunks] : *total;
+    uint32_t* out = bsum + (size_t)P3_WORDS * key;
+    if (s == e) {
+        store_p3(out, ge_p3_identity());
+        return;
+    }
+    const uint32_t i0 = s / T, i1 = (e - 1) / T;
+    if (i1 == i0) return;
+    ge_p3 acc = load_p3(out);
+#pragma unroll 1
+    for (uint32_t i = i0 + 1; i <= i1; i++) acc = p3_add(acc, load_p3(hpart + (size_t)P3_WORDS * i));
+    store_p3(out, acc);
+}
+
+// ---- per-window weighted sum W_w = sum_b b S_{w,b}: one workgroup per window -------------
+// The window's nb buckets are split over Gw = min(blockDim, nb) lanes (L = nb / Gw each); lanes
+// beyond Gw hold empty groups.  lds: blockDim points (40 KiB at 256), reused by scan and tree.
+extern "C" __global__ void __launch_bounds__(256) k_msm_window(MsmLayout lay, const uint32_t* __restrict__ bsum,
+                                                               uint32_t* __restrict__ wsum) {
+    extern __shared__ uint32_t lds[];
+    const int G = blockDim.x, g = threadIdx.x, w = blockIdx.x;
+    const int nb = 1 << (lay.width[w] - 1);
+    const int Gw = nb < G ? nb : G;
+    const int L = nb / Gw;
+    const uint32_t* bw = bsum + (size_t)P3_WORDS * ((size_t)lay.kbase[w] + (size_t)g * L);
+    ge_p3 run, acc;
+    msm_segment_sums(g < Gw ? L : 0, [&](int k) { return load_p3(bw + (size_t)P3_WORDS * k); }, run, acc);
+    // suffix_g = sum_{g' >= g} run_g' (Hillis-Steele: read, barrier, write, barrier)
+    uint32_t* mine = lds + P3_WORDS * g;
+    store_p3(mine, run);
+    __syncthreads();
+    ge_p3 suf = run;
+    for (int o = 1; o < G; o <<= 1) {
+        const bool take = g + o < G;
+        ge_p3 other = ge_p3_identity();
+        if (take) other = load_p3(lds + P3_WORDS * (g + o));
+        __syncthreads();
+        if (take) {
+            suf = p3_add(suf, other);
+            store_p3(mine, suf);
+        }
+        __syncthreads();
+    }
+    // x_g = acc_g + L * suffix_g (g >= 1), then a tree sum of x_g over the workgroup
+    ge_p3 x = acc;
+    if (g >= 1) {
+        int lg = 0;
+        while ((1 << lg) < L) lg++;
+        x = p3_add(x, lg ? p3_dbl_n(suf, lg) : suf);
+    }
+    store_p3(mine, x);
+    __syncthreads();
+    for (int o = G / 2; o >= 1; o >>= 1) {
+        if (g < o) {
+            x = p3_add(x, load_p3(lds + P3_WORDS * (g + o)));
+            store_p3(mine, x);
+        }
+        __syncthreads();
+    }
+    if (g == 0) store_p3(wsum + (size_t)P3_WORDS * w, x);
+}
+
+// Horner over windows, [8], identity: *verdict = 1 iff accepted and nothing failed.  All 64
+// lanes run the same chain on a VGPR-laundered index so the compiler keeps it on the VALU
+// (a lone lane's uniform chain is otherwise scalarised onto the SALU with SGPR spills).
+extern "C" __global__ void __launch_bounds__(64) k_msm_final(MsmLayout lay, const uint32_t* __restrict__ wsum,
+                                                             const uint32_t* __restrict__ fail,
+                                                             uint32_t* __restrict__ verdict) {
+    uint32_t zero = 0;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
+    const uint32_t* ws = wsum + zero;
+    const int nw = lay.nw;
+    ge_p3 d = load_p3(ws + (size_t)P3_WORDS * (nw - 1));
+#pragma unroll 1
+    for (int w = nw - 2; w >= 0; w--) {
+        d = p3_dbl_n(d, lay.width[w]);
+        d = p3_add(d, load_p3(ws + (size_t)P3_WORDS * w));
+    }
+    const bool ok = p3_mul8_is_identity(d) && *fail == 0;
+    if (threadIdx.x == 0) *verdict = ok ? 1u : 0u;
+}

@@ -17,6 +17,9 @@
 #include "../../include/nwv.h"
 #include "blake2b_kernels.hip"
 #include "ed25519_kernels.hip"
+#include "msm_kernels.hip"
+
+#include <random>
 
 namespace {
 
@@ -63,16 +66,23 @@ struct DevBuf {
     T* as() const { return static_cast<T*>(p); }
 };
 
-// Device-resident inputs + intermediates of one Ed25519 batch
+// Device-resident inputs + intermediates of one Ed25519 batch: the per-signature pipeline
+// (kbuf, flags, tables, verdict) and the batch MSM (m_*)
 struct EdBuffers {
     DevBuf pk, sig, msg, off, len, kbuf, flags, tables, verdict;
+    DevBuf m_scal, m_partial, m_state, m_pts, m_digits, m_cnt, m_tiles, m_entries, m_kstart, m_hpart,
+        m_bsum, m_wsum;
     void release() {
-        for (DevBuf* b : {&pk, &sig, &msg, &off, &len, &kbuf, &flags, &tables, &verdict}) b->release();
+        for (DevBuf* b : {&pk, &sig, &msg, &off, &len, &kbuf, &flags, &tables, &verdict, &m_scal,
+                          &m_partial, &m_state, &m_pts, &m_digits, &m_cnt, &m_tiles, &m_entries,
+                          &m_kstart, &m_hpart, &m_bsum, &m_wsum})
+            b->release();
     }
 };
 
 struct Device {
     int ordinal = -1;
+    uint32_t flags = 0;  // nwv_init flags (NWV_FLAG_*)
     hipStream_t stream = nullptr;
     std::mutex mu;
     DevBuf btab;
@@ -142,6 +152,135 @@ int ed_launch(Device& d, EdBuffers& b, size_t n, hipStream_t stream, hipEvent_t*
     return NWV_OK;
 }
 
+// ------------------------------------------------------------------ batch MSM (K5) ------
+// Window layout and work decomposition of one batch MSM over np = 2n + 1 points.
+struct MsmPlan {
+    MsmLayout lay{};
+    uint32_t chunk_pts = 0, chunks = 0, nkeys = 0, ntiles = 0, wg_window = 0;
+    uint32_t seg = 0;  // entries per k_msm_bucket lane
+    uint64_t np = 0, cnt_len = 0, max_entries = 0, nseg = 0;
+};
+
+// Base width c minimises  7 Fmul x entries + 18 Fmul x buckets  (SURVEY.md §8d K5 cost model:
+// one mixed addition per nonzero digit, two full additions per bucket in the running-sum
+// reduction).
+MsmPlan msm_plan(size_t n) {
+    MsmPlan p;
+    p.np = 2 * (uint64_t)n + 1;
+    double best = 1e300;
+    for (int c = 6; c <= 15; c++) {
+        MsmLayout L;
+        if (!msm_make_layout(c, L)) continue;
+        const double entries = (double)(n + 1) * L.nw + (double)n * L.nw_z;
+        const double cost = 7.0 * entries + 18.0 * L.kbase[L.nw];
+        if (cost < best) {
+            best = cost;
+            p.lay = L;
+        }
+    }
+    p.chunk_pts = (uint32_t)std::max<uint64_t>(8192, (p.np + 63) / 64);
+    p.chunks = (uint32_t)((p.np + p.chunk_pts - 1) / p.chunk_pts);
+    p.nkeys = p.lay.kbase[p.lay.nw];
+    p.cnt_len = (uint64_t)p.nkeys * p.chunks;
+    p.ntiles = (uint32_t)((p.cnt_len + 4095) / 4096);
+    p.wg_window = (uint32_t)std::min(256, 1 << (p.lay.cmax - 1));
+    p.max_entries = (uint64_t)(n + 1) * p.lay.nw + (uint64_t)n * p.lay.nw_z;
+    // ~4 waves per SIMD of bucket lanes (256 CUs x 4 SIMDs x 4 x 64), 8..64 entries each
+    p.seg = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, p.max_entries / (256 * 4 * 4 * 64)));
+    p.nseg = (p.max_entries + p.seg - 1) / p.seg;
+    return p;
+}
+
+int msm_alloc(EdBuffers& b, const MsmPlan& p, size_t n) {
+    const size_t nblk = (n + 255) / 256;
+    int rc;
+    if ((rc = b.m_scal.ensure(32 * p.np + 32)) || (rc = b.m_partial.ensure(36 * nblk + 36)) ||
+        (rc = b.m_state.ensure(64)) ||
+        (rc = b.m_pts.ensure((size_t)4 * PRECOMP_ENTRY_WORDS * p.np + 64)) ||
+        (rc = b.m_digits.ensure((size_t)2 * p.lay.nw * p.np + 64)) ||
+        (rc = b.m_cnt.ensure((size_t)4 * p.cnt_len + 64)) ||
+        (rc = b.m_tiles.ensure((size_t)4 * (p.ntiles + 1) + 64)) ||
+        (rc = b.m_entries.ensure((size_t)4 * p.max_entries + 64)) ||
+        (rc = b.m_kstart.ensure((size_t)4 * p.nkeys + 64)) ||
+        (rc = b.m_hpart.ensure((size_t)4 * P3_WORDS * p.nseg + 64)) ||
+        (rc = b.m_bsum.ensure((size_t)4 * P3_WORDS * p.nkeys + 64)) ||
+        (rc = b.m_wsum.ensure((size_t)4 * P3_WORDS * p.lay.nw + 64)))
+        return rc;
+    return NWV_OK;
+}
+
+static const char* const MSM_KERNEL_NAMES[] = {
+    "k_msm_scalars", "k_msm_bscalar", "k_msm_points", "k_msm_recode", "k_msm_hist", "k_scan",
+    "k_msm_scatter", "k_msm_bucket+fixup", "k_msm_window", "k_msm_final"};
+constexpr int MSM_NKERNELS = 10;
+
+// Launch the batch MSM on resident buffers; the verdict word (1 = batch accepted) is
+// m_state[1] (m_state[0] = failure flags).  ev: MSM_NKERNELS + 1 events or null.
+int msm_launch(Device& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStream_t stream,
+               hipEvent_t* ev) {
+    if (n == 0) return NWV_OK;
+    const MsmPlan p = msm_plan(n);
+    int rc = msm_alloc(b, p, n);
+    if (rc) return rc;
+    MsmSeed seed;
+    std::memcpy(seed.w, seed32, 32);
+    uint32_t* state = b.m_state.as<uint32_t>();
+    const unsigned nblk = (unsigned)((n + 255) / 256);
+    auto mark = [&](int k) -> int {
+        if (ev) NWV_HIP(hipEventRecord(ev[k], stream));
+        return NWV_OK;
+    };
+    NWV_HIP(hipMemsetAsync(state, 0, 8, stream));
+    if ((rc = mark(0))) return rc;
+    hipLaunchKernelGGL(k_msm_scalars, dim3(nblk), dim3(256), 0, stream, (uint64_t)n, b.pk.as<uint8_t>(),
+                       b.sig.as<uint8_t>(), b.msg.as<uint8_t>(), b.off.as<uint64_t>(), b.len.as<uint32_t>(),
+                       seed, b.m_scal.as<uint32_t>(), b.m_partial.as<uint32_t>(), state);
+    if ((rc = mark(1))) return rc;
+    hipLaunchKernelGGL(k_msm_bscalar, dim3(1), dim3(256), 0, stream, (uint64_t)n, (uint32_t)nblk,
+                       b.m_partial.as<uint32_t>(), d.btab.as<uint32_t>(), b.m_scal.as<uint32_t>(),
+                       b.m_pts.as<uint32_t>());
+    if ((rc = mark(2))) return rc;
+    const size_t waves = (n + 63) / 64;
+    hipLaunchKernelGGL(k_msm_points, dim3((unsigned)((2 * 64 * waves + 255) / 256)), dim3(256), 0, stream,
+                       (uint64_t)n, b.pk.as<uint8_t>(), b.sig.as<uint8_t>(), b.m_pts.as<uint32_t>(), state);
+    if ((rc = mark(3))) return rc;
+    const dim3 gnp((unsigned)((p.np + 255) / 256));
+    int16_t* digits = b.m_digits.as<int16_t>();
+    const uint32_t* scal = b.m_scal.as<uint32_t>();
+    hipLaunchKernelGGL(k_msm_recode, gnp, dim3(256), 0, stream, (uint64_t)n, p.lay, scal, digits);
+    if ((rc = mark(4))) return rc;
+    const dim3 gsort(p.chunks, (unsigned)p.lay.nw);
+    const size_t lds_nb = (size_t)4 << (p.lay.cmax - 1);
+    uint32_t* cnt = b.m_cnt.as<uint32_t>();
+    uint32_t* tiles = b.m_tiles.as<uint32_t>();
+    hipLaunchKernelGGL(k_msm_hist, gsort, dim3(256), lds_nb, stream, (uint64_t)n, p.lay, p.chunk_pts,
+                       digits, cnt);
+    if ((rc = mark(5))) return rc;
+    hipLaunchKernelGGL(k_scan_tile, dim3(p.ntiles), dim3(256), 0, stream, p.cnt_len, cnt, tiles);
+    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, stream, p.ntiles, tiles);
+    hipLaunchKernelGGL(k_scan_add, dim3((unsigned)((p.cnt_len + 255) / 256)), dim3(256), 0, stream,
+                       p.cnt_len, cnt, tiles, p.chunks, b.m_kstart.as<uint32_t>());
+    if ((rc = mark(6))) return rc;
+    hipLaunchKernelGGL(k_msm_scatter, gsort, dim3(256), lds_nb, stream, (uint64_t)n, p.lay,
+                       p.chunk_pts, digits, cnt, b.m_entries.as<uint32_t>());
+    if ((rc = mark(7))) return rc;
+    hipLaunchKernelGGL(k_msm_bucket, dim3((unsigned)((p.nseg + 255) / 256)), dim3(256), 0, stream, p.seg,
+                       p.nkeys, tiles + p.ntiles, b.m_entries.as<uint32_t>(), b.m_kstart.as<uint32_t>(),
+                       b.m_pts.as<uint32_t>(), b.m_bsum.as<uint32_t>(), b.m_hpart.as<uint32_t>());
+    hipLaunchKernelGGL(k_msm_fixup, dim3((p.nkeys + 255) / 256), dim3(256), 0, stream, p.nkeys, p.chunks,
+                       p.seg, cnt, tiles + p.ntiles, b.m_hpart.as<uint32_t>(), b.m_bsum.as<uint32_t>());
+    if ((rc = mark(8))) return rc;
+    hipLaunchKernelGGL(k_msm_window, dim3((unsigned)p.lay.nw), dim3(p.wg_window),
+                       (size_t)4 * P3_WORDS * p.wg_window, stream, p.lay, b.m_bsum.as<uint32_t>(),
+                       b.m_wsum.as<uint32_t>());
+    if ((rc = mark(9))) return rc;
+    hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, stream, p.lay, b.m_wsum.as<uint32_t>(),
+                       state, state + 1);
+    if ((rc = mark(10))) return rc;
+    NWV_HIP(hipGetLastError());
+    return NWV_OK;
+}
+
 // Stage host inputs [lo, hi) onto buffers b of device d (message region rebased).  pk/sig
 // may be null (signing stages seeds separately).
 int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, const uint8_t* sig,
@@ -195,14 +334,31 @@ struct nwv_ctx {
     std::vector<Device*> devs;
 };
 
+// Per-kernel device time of the staged pipelines (HIP events on the batch's own stream).
+struct KernelLog {
+    std::vector<std::string> names;
+    std::vector<double> ms;
+    long runs = 0;
+    void add(const char* const* nm, const float* t, int k) {
+        if (names.empty())
+            for (int i = 0; i < k; i++) {
+                names.emplace_back(nm[i]);
+                ms.push_back(0.0);
+            }
+        for (int i = 0; i < k; i++) ms[i] += t[i];
+        runs++;
+    }
+};
+
 struct nwv_staged {
     nwv_ctx* ctx = nullptr;
     Device* dev = nullptr;
     EdBuffers buf;
     size_t n = 0;
     hipStream_t stream = nullptr;  // each resident batch runs on its own stream, so several
-    hipEvent_t ev[4] = {};         // staged batches on one device overlap
-    KernelTimes times;
+    hipEvent_t ev[MSM_NKERNELS + 1] = {};  // staged batches on one device overlap
+    KernelLog log[2];              // [0] per-signature pipeline, [1] batch MSM
+    int last_mode = -1;
     bool pending_timing = false;
 };
 
@@ -238,13 +394,14 @@ extern "C" {
 int nwv_abi_version(void) { return NWV_ABI_VERSION; }
 const char* nwv_last_error(void) { return g_last_error.c_str(); }
 
-static int init_devices(nwv_ctx** out, std::vector<int> ordinals) {
+static int init_devices(nwv_ctx** out, std::vector<int> ordinals, uint32_t flags) {
     if (!out) return set_err(NWV_ERR_ARG, "null out");
     *out = nullptr;
     auto* ctx = new (std::nothrow) nwv_ctx;
     if (!ctx) return set_err(NWV_ERR_OOM, "context allocation");
     for (int o : ordinals) {
         auto* d = new Device;
+        d->flags = flags;
         int rc = device_open(*d, o);
         if (rc) {
             device_close(*d);
@@ -259,7 +416,6 @@ static int init_devices(nwv_ctx** out, std::vector<int> ordinals) {
 }
 
 int nwv_init(nwv_ctx** out, int n_devices, uint32_t flags) {
-    (void)flags;
     int count = 0;
     hipError_t e = hipGetDeviceCount(&count);
     if (e != hipSuccess || count <= 0) return set_err(NWV_ERR_NODEV, "no HIP device visible");
@@ -267,16 +423,15 @@ int nwv_init(nwv_ctx** out, int n_devices, uint32_t flags) {
     if (n_devices == 0 || n_devices > count) n_devices = count;
     std::vector<int> ords;
     for (int i = 0; i < n_devices; i++) ords.push_back(i);
-    return init_devices(out, ords);
+    return init_devices(out, ords, flags);
 }
 
 int nwv_init_device(nwv_ctx** out, int device_ordinal, uint32_t flags) {
-    (void)flags;
     int count = 0;
     hipError_t e = hipGetDeviceCount(&count);
     if (e != hipSuccess || count <= 0) return set_err(NWV_ERR_NODEV, "no HIP device visible");
     if (device_ordinal < 0 || device_ordinal >= count) return set_err(NWV_ERR_ARG, "bad ordinal");
-    return init_devices(out, {device_ordinal});
+    return init_devices(out, {device_ordinal}, flags);
 }
 
 void nwv_free(nwv_ctx* ctx) {
@@ -310,22 +465,96 @@ int nwv_ed25519_verify_each(nwv_ctx* ctx, size_t n, const uint8_t* pk, const uin
     });
 }
 
+// Batches of at least this many signatures go through the MSM (K5); smaller ones through the
+// per-signature pipeline, whose single-lane chain is shorter than the MSM's window Horner.
+static size_t msm_min_n() {
+    static const size_t v = [] {
+        const char* e = std::getenv("NWV_MSM_MIN_N");
+        return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)4096;
+    }();
+    return v;
+}
+
+static void fill_seed(const uint8_t* seed32, uint8_t out[32]) {
+    if (seed32) {
+        std::memcpy(out, seed32, 32);
+        return;
+    }
+    std::random_device rd;  // OS entropy, as the reference's OsRng
+    for (int i = 0; i < 32; i += 4) {
+        const uint32_t v = rd();
+        std::memcpy(out + i, &v, 4);
+    }
+}
+
+static void set_ones(uint64_t* bits, size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; i++) bits[i >> 6] |= 1ULL << (i & 63);
+}
+
+// Batch verdict of resident buffers: MSM, then (only if it rejects) the per-signature fallback
+// for the exact bad set.  bits: the shard's verdict words (may be null).
+static int batch_on_device(Device& d, EdBuffers& b, size_t n, const uint8_t seed[32], hipStream_t stream,
+                           int* ok, uint64_t* bits) {
+    int rc;
+    const bool use_msm = (d.flags & NWV_FLAG_MSM_ALWAYS) ||
+                         (!(d.flags & NWV_FLAG_MSM_NEVER) && n >= msm_min_n());
+    if (use_msm) {
+        if ((rc = msm_launch(d, b, n, seed, stream, nullptr))) return rc;
+        uint32_t st[2] = {0, 0};
+        NWV_HIP(hipMemcpyAsync(st, b.m_state.p, 8, hipMemcpyDeviceToHost, stream));
+        NWV_HIP(hipStreamSynchronize(stream));
+        if (st[1] == 1) {
+            *ok = 1;
+            if (bits) {
+                std::memset(bits, 0, 8 * ((n + 63) / 64));
+                set_ones(bits, 0, n);
+            }
+            return NWV_OK;
+        }
+    }
+    if ((rc = ed_launch(d, b, n, stream, nullptr))) return rc;
+    std::vector<uint64_t> tmp;
+    uint64_t* out = bits;
+    if (!out) {
+        tmp.assign((n + 63) / 64, 0);
+        out = tmp.data();
+    }
+    NWV_HIP(hipMemcpyAsync(out, b.verdict.p, 8 * ((n + 63) / 64), hipMemcpyDeviceToHost, stream));
+    NWV_HIP(hipStreamSynchronize(stream));
+    *ok = verdicts_all_valid(out, n) ? 1 : 0;
+    return NWV_OK;
+}
+
 int nwv_ed25519_verify_batch(nwv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig,
                              const uint8_t* msg_base, const uint64_t* msg_off,
                              const uint32_t* msg_len, const uint8_t seed32[32], int* all_valid,
                              uint64_t* verdict_bits_or_null) {
-    (void)seed32;
-    if (!all_valid) return set_err(NWV_ERR_ARG, "null all_valid");
-    std::vector<uint64_t> tmp;
-    uint64_t* bits = verdict_bits_or_null;
-    if (!bits) {
-        tmp.assign((n + 63) / 64 + 1, 0);
-        bits = tmp.data();
-    }
-    int rc = nwv_ed25519_verify_each(ctx, n, pk, sig, msg_base, msg_off, msg_len, bits);
-    if (rc) return rc;
-    *all_valid = verdicts_all_valid(bits, n) ? 1 : 0;
-    return NWV_OK;
+    if (!ctx || !all_valid || (n && (!pk || !sig || !msg_off || !msg_len)))
+        return set_err(NWV_ERR_ARG, "null argument");
+    *all_valid = 1;
+    if (n == 0) return NWV_OK;
+    for (size_t i = 0; i < n; i++)
+        if (msg_len[i] && !msg_base) return set_err(NWV_ERR_ARG, "null msg_base");
+    uint8_t seed[32];
+    fill_seed(seed32, seed);
+    std::vector<int> oks(ctx->devs.size(), 1);
+    std::mutex omu;
+    int rc = for_shards(ctx, n, [&](Device& d, size_t lo, size_t hi) -> int {
+        int r = ed_stage(d, d.ed, lo, hi, pk, sig, msg_base, msg_off, msg_len);
+        if (r) return r;
+        // each shard gets its own coefficient stream: seed' = seed with the shard start mixed in
+        uint8_t s2[32];
+        std::memcpy(s2, seed, 32);
+        for (int k = 0; k < 8; k++) s2[24 + k] ^= (uint8_t)((uint64_t)lo >> (8 * k));
+        int ok = 1;
+        r = batch_on_device(d, d.ed, hi - lo, s2, d.stream, &ok,
+                            verdict_bits_or_null ? verdict_bits_or_null + lo / 64 : nullptr);
+        if (r) return r;
+        std::lock_guard<std::mutex> g(omu);
+        if (!ok) *all_valid = 0;
+        return NWV_OK;
+    });
+    return rc;
 }
 
 // ---- fastcrypto trait surface ---------------------------------------------------------
@@ -439,28 +668,35 @@ int nwv_stage_ed25519(nwv_ctx* ctx, int device_index, size_t n, const uint8_t* p
     return NWV_OK;
 }
 
+static const char* const ED_KERNEL_NAMES[] = {"k_ed_hash", "k_ed_points", "k_ed_straus"};
+
 static int staged_collect_times(nwv_staged* st) {
     if (!st->pending_timing) return NWV_OK;
-    NWV_HIP(hipEventSynchronize(st->ev[3]));
-    for (int k = 0; k < 3; k++) {
-        float ms = 0;
-        NWV_HIP(hipEventElapsedTime(&ms, st->ev[k], st->ev[k + 1]));
-        st->times.ms[k] += ms;
-    }
-    st->times.runs++;
+    const int k = st->last_mode == 1 ? MSM_NKERNELS : 3;
+    NWV_HIP(hipEventSynchronize(st->ev[k]));
+    float t[MSM_NKERNELS];
+    for (int i = 0; i < k; i++) NWV_HIP(hipEventElapsedTime(&t[i], st->ev[i], st->ev[i + 1]));
+    st->log[st->last_mode].add(st->last_mode == 1 ? MSM_KERNEL_NAMES : ED_KERNEL_NAMES, t, k);
     st->pending_timing = false;
     return NWV_OK;
 }
 
 int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]) {
-    (void)seed32;
     if (!st || (mode != 0 && mode != 1)) return set_err(NWV_ERR_ARG, "bad staged/mode");
     Device& d = *st->dev;
     std::lock_guard<std::mutex> g(d.mu);
     int rc = with_device(d);
     if (rc) return rc;
     if ((rc = staged_collect_times(st))) return rc;
-    if ((rc = ed_launch(d, st->buf, st->n, st->stream, st->ev))) return rc;
+    if (mode == 1) {
+        uint8_t seed[32];
+        fill_seed(seed32, seed);
+        rc = msm_launch(d, st->buf, st->n, seed, st->stream, st->ev);
+    } else {
+        rc = ed_launch(d, st->buf, st->n, st->stream, st->ev);
+    }
+    if (rc) return rc;
+    st->last_mode = mode;
     st->pending_timing = st->n > 0;
     return NWV_OK;
 }
@@ -475,6 +711,8 @@ int nwv_staged_sync(nwv_staged* st) {
     return staged_collect_times(st);
 }
 
+// Verdicts of the last run.  After a batch run (mode 1) that rejected, the per-signature
+// pipeline runs here to pinpoint the bad indices.
 int nwv_staged_fetch(nwv_staged* st, uint64_t* verdict_bits, int* all_valid) {
     if (!st) return set_err(NWV_ERR_ARG, "null staged");
     int rc = nwv_staged_sync(st);
@@ -489,6 +727,18 @@ int nwv_staged_fetch(nwv_staged* st, uint64_t* verdict_bits, int* all_valid) {
     Device& d = *st->dev;
     std::lock_guard<std::mutex> g(d.mu);
     if ((rc = with_device(d))) return rc;
+    if (st->last_mode == 1 && st->n) {
+        uint32_t state[2] = {0, 0};
+        NWV_HIP(hipMemcpy(state, st->buf.m_state.p, 8, hipMemcpyDeviceToHost));
+        if (state[1] == 1) {
+            std::memset(bits, 0, 8 * words);
+            set_ones(bits, 0, st->n);
+            if (all_valid) *all_valid = 1;
+            return NWV_OK;
+        }
+        if ((rc = ed_launch(d, st->buf, st->n, st->stream, nullptr))) return rc;
+        NWV_HIP(hipStreamSynchronize(st->stream));
+    }
     if (words) NWV_HIP(hipMemcpy(bits, st->buf.verdict.p, 8 * words, hipMemcpyDeviceToHost));
     if (all_valid) *all_valid = verdicts_all_valid(bits, st->n) ? 1 : 0;
     return NWV_OK;
@@ -498,9 +748,26 @@ int nwv_staged_kernel_ms(nwv_staged* st, double* avg_ms, int reset) {
     if (!st || !avg_ms) return set_err(NWV_ERR_ARG, "null argument");
     int rc = nwv_staged_sync(st);
     if (rc) return rc;
-    for (int k = 0; k < 3; k++) avg_ms[k] = st->times.runs ? st->times.ms[k] / st->times.runs : 0.0;
-    if (reset) st->times = KernelTimes{};
+    const KernelLog& l = st->log[0];
+    for (int k = 0; k < 3; k++) avg_ms[k] = l.runs ? l.ms[k] / l.runs : 0.0;
+    if (reset) st->log[0] = KernelLog{};
     return NWV_OK;
+}
+
+int nwv_staged_kernel_times(nwv_staged* st, int mode, int cap, const char** names, double* avg_ms,
+                            int reset) {
+    if (!st || (mode != 0 && mode != 1) || cap < 0) return set_err(NWV_ERR_ARG, "bad argument");
+    int rc = nwv_staged_sync(st);
+    if (rc) return rc;
+    KernelLog& l = st->log[mode];
+    const int k = std::min<int>(cap, (int)l.names.size());
+    for (int i = 0; i < k; i++) {
+        if (names) names[i] = (mode == 1 ? MSM_KERNEL_NAMES : ED_KERNEL_NAMES)[i];
+        if (avg_ms) avg_ms[i] = l.runs ? l.ms[i] / l.runs : 0.0;
+    }
+    const int total = (int)l.names.size();
+    if (reset) l = KernelLog{};
+    return total;
 }
 
 void nwv_staged_free(nwv_staged* st) {

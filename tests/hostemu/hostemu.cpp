@@ -10,6 +10,7 @@ unsigned long long nwv_count_mul = 0, nwv_count_sq = 0;
 
 #include "../../narwhal_amd/csrc/blake2b.h"
 #include "../../narwhal_amd/csrc/ed25519_lane.h"
+#include "../../narwhal_amd/csrc/msm.h"
 
 using namespace nwv;
 
@@ -155,6 +156,141 @@ void he_sign(const uint8_t* seed, const uint8_t* msg, uint32_t len, uint8_t* pk_
     std::memcpy(pk_out, Aw, 32);
     std::memcpy(sig_out, Rw, 32);
     std::memcpy(sig_out + 32, S, 32);
+}
+
+// Batch verification through the K5 MSM, sequentially on the host with the device arithmetic
+// (msm.h): same point layout, window layout, recoding, bucket rule, G-lane window reduction and
+// Horner as narwhal_amd/csrc/msm_kernels.hip, without the parallel sort.  Returns the verdict.
+int he_msm_batch(size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
+                 const uint32_t* len, const uint8_t* seed32, int c, int G, unsigned long long* counts) {
+    ensure_btab();
+    MsmLayout lay;
+    if (!msm_make_layout(c, lay)) return -1;
+    uint32_t seed[8];
+    std::memcpy(seed, seed32, 32);
+    const size_t np = 2 * n + 1;
+    std::vector<uint32_t> scal(8 * np, 0), pts(PRECOMP_ENTRY_WORDS * np);
+    bool ok = true;
+    unsigned long long col[9] = {0};
+    for (size_t i = 0; i < n; i++) {
+        uint32_t Aw[8], Rw[8], Sw[8], k[8], z[8], a[8], zs[8];
+        words(pk + 32 * i, Aw);
+        words(sig + 64 * i, Rw);
+        words(sig + 64 * i + 32, Sw);
+        std::vector<uint8_t> m(len[i] + 64, 0);
+        if (len[i]) std::memcpy(m.data(), msg + off[i], len[i]);
+        if (lane_hash(Aw, Rw, Sw, m.data(), len[i], k) != FLAG_S_OK) ok = false;
+        msm_z(seed, i, z);
+        sc_mul(z, k, a);
+        sc_mul(z, Sw, zs);
+        for (int t = 0; t < 8; t++) {
+            scal[8 * i + t] = a[t];
+            scal[8 * (n + 1 + i) + t] = z[t];
+            col[t] += zs[t];
+        }
+        ge_p3 P;
+        ok &= ge_decompress(Aw, P);
+        store_affine_entry(pts.data() + PRECOMP_ENTRY_WORDS * i, P);
+        ok &= ge_decompress(Rw, P);
+        store_affine_entry(pts.data() + PRECOMP_ENTRY_WORDS * (n + 1 + i), P);
+    }
+    {
+        uint32_t x[16];
+        unsigned long long cc = 0;
+        for (int t = 0; t < 16; t++) {
+            if (t < 9) cc += col[t];
+            x[t] = (uint32_t)cc;
+            cc >>= 32;
+        }
+        uint32_t r[8];
+        sc_reduce512(x, r);
+        uint32_t nz = 0;
+        for (int t = 0; t < 8; t++) nz |= r[t];
+        long long br = 0;
+        for (int t = 0; t < 8; t++) {
+            long long d = (long long)sc_l(t) - r[t] + br;
+            scal[8 * n + t] = nz ? (uint32_t)d : 0u;
+            br = d >> 32;
+        }
+        std::memcpy(pts.data() + PRECOMP_ENTRY_WORDS * n, g_btab.data() + PRECOMP_ENTRY_WORDS,
+                    4 * PRECOMP_ENTRY_WORDS);
+    }
+    nwv_count_mul = nwv_count_sq = 0;
+    const uint32_t nkeys = lay.kbase[lay.nw];
+    std::vector<std::vector<uint32_t>> buckets(nkeys);
+    for (size_t j = 0; j < np; j++) {
+        msm_recode(&scal[8 * j], lay, j <= n ? lay.nw : lay.nw_z, [&](int w, int d) {
+            if (d) buckets[lay.kbase[w] + (d < 0 ? -d : d) - 1].push_back((uint32_t)j | (d < 0 ? MSM_NEG : 0u));
+        });
+    }
+    std::vector<uint32_t> bs((size_t)P3_WORDS * nkeys), ws((size_t)P3_WORDS * lay.nw);
+    for (size_t key = 0; key < nkeys; key++) {
+        ge_p3 acc = ge_p3_identity();
+        for (uint32_t v : buckets[key])
+            acc = ge_p1p1_to_p3(ge_madd_entry(acc, pts.data() + PRECOMP_ENTRY_WORDS * (v & ~MSM_NEG), (v & MSM_NEG) != 0));
+        store_p3(bs.data() + P3_WORDS * key, acc);
+    }
+    for (int w = 0; w < lay.nw; w++) {
+        const int nb = 1 << (lay.width[w] - 1);
+        const int Gw = nb < G ? nb : G;
+        const int L = nb / Gw;
+        std::vector<ge_p3> run(Gw), acc(Gw);
+        for (int g = 0; g < Gw; g++) {
+            const uint32_t* bw = bs.data() + (size_t)P3_WORDS * ((size_t)lay.kbase[w] + (size_t)g * L);
+            msm_segment_sums(L, [&](int k) { return load_p3(bw + (size_t)P3_WORDS * k); }, run[g], acc[g]);
+        }
+        int lg = 0;
+        while ((1 << lg) < L) lg++;
+        ge_p3 suf = ge_p3_identity(), tot = acc[0];
+        for (int g = Gw - 1; g >= 1; g--) {
+            suf = p3_add(suf, run[g]);
+            tot = p3_add(tot, p3_add(acc[g], lg ? p3_dbl_n(suf, lg) : suf));
+        }
+        store_p3(ws.data() + P3_WORDS * w, tot);
+    }
+    ge_p3 d = load_p3(ws.data() + (size_t)P3_WORDS * (lay.nw - 1));
+    for (int w = lay.nw - 2; w >= 0; w--) {
+        d = p3_dbl_n(d, lay.width[w]);
+        d = p3_add(d, load_p3(ws.data() + (size_t)P3_WORDS * w));
+    }
+    const bool eq = p3_mul8_is_identity(d);
+    if (counts) {
+        counts[0] = nwv_count_mul;
+        counts[1] = nwv_count_sq;
+    }
+    return (ok && eq) ? 1 : 0;
+}
+
+// signed digits of a 256-bit scalar over layout(c): z range (bits = 128) or full range (253);
+// out: nw, then (pos, digit) pairs
+int he_msm_recode(const uint8_t* s32, int c, int bits, int* out) {
+    uint32_t s[8];
+    words(s32, s);
+    MsmLayout lay;
+    if (!msm_make_layout(c, lay)) return -1;
+    const int nw = bits == MSM_BITS_Z ? lay.nw_z : lay.nw;
+    msm_recode(s, lay, nw, [&](int w, int d) {
+        out[2 * w] = lay.pos[w];
+        out[2 * w + 1] = d;
+    });
+    return nw;
+}
+
+// layout(c): nw, nw_z, then widths
+int he_msm_layout(int c, int* out) {
+    MsmLayout lay;
+    if (!msm_make_layout(c, lay)) return -1;
+    out[0] = lay.nw;
+    out[1] = lay.nw_z;
+    for (int w = 0; w < lay.nw; w++) out[2 + w] = lay.width[w];
+    return lay.nw;
+}
+
+void he_msm_z(const uint8_t* seed32, uint64_t i, uint8_t* z32) {
+    uint32_t seed[8], z[8];
+    words(seed32, seed);
+    msm_z(seed, i, z);
+    std::memcpy(z32, z, 32);
 }
 
 }  // extern "C"

@@ -1,0 +1,113 @@
+"""GPU parity of batch verification through the Pippenger MSM (K5, msm_kernels.hip) via the C
+ABI: the batch verdict equals the AND of the oracle's per-signature ZIP-215 verdicts on valid,
+invalid and adversarial batches of every size class (window widths 6..15 are chosen from n),
+and a rejected batch's fallback pinpoints exactly the oracle's bad indices (config 4)."""
+import random
+
+import numpy as np
+import pytest
+
+import oracle_ffi as of
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    import narwhal_amd
+    from narwhal_amd import _lib
+    e = narwhal_amd.Engine(device=0, flags=_lib.NWV_FLAG_MSM_ALWAYS)
+    yield e
+    e.close()
+
+
+def _v(v):
+    return bytes.fromhex(v["pk"]), bytes.fromhex(v["sig"]), bytes.fromhex(v["msg"])
+
+
+def _synthetic(eng, n, mlen, seed=1):
+    rnd = np.random.default_rng(seed)
+    seeds = [rnd.bytes(32) for _ in range(n)]
+    msgs = [rnd.bytes(mlen) for _ in range(n)]
+    pk, sg = eng.sign_many(seeds, msgs)
+    items = [(pk[32 * i:32 * i + 32].tobytes(), sg[64 * i:64 * i + 64].tobytes(), msgs[i]) for i in range(n)]
+    return items
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 300, 1024, 5000, 40000])
+def test_valid_batches_accept(eng, n):
+    items = _synthetic(eng, n, 32 if n > 1000 else 77, seed=n)
+    ok, bits = eng.verify_batch(items, seed=bytes([n % 251]) * 32)
+    assert ok and all(bits)
+
+
+@pytest.mark.parametrize("n", [1, 64, 1000, 5000])
+def test_one_bad_signature_rejects_and_is_pinpointed(eng, n):
+    items = _synthetic(eng, n, 32, seed=100 + n)
+    rnd = random.Random(n)
+    i = rnd.randrange(n)
+    pk, sg, m = items[i]
+    sg = bytearray(sg)
+    sg[rnd.randrange(64)] ^= 1 << rnd.randrange(8)
+    items[i] = (pk, bytes(sg), m)
+    ok, bits = eng.verify_batch(items)
+    want = [of.verify(*it) for it in items] if n <= 1000 else None
+    assert not ok
+    assert [k for k in range(n) if not bits[k]] == [i]
+    if want is not None:
+        assert bits == want
+
+
+def test_golden_and_zip215_vectors_in_batches(eng):
+    g = of.load_golden("ed25519_vectors.json")["vectors"]
+    z = of.load_golden("zip215_small_order.json")["vectors"]
+    honest = _synthetic(eng, 40, 32, seed=3)
+    for k, v in enumerate(g + z):
+        items = honest[: k % 7] + [_v(v)] + honest[k % 7:]
+        want = [of.verify(*it) for it in items]
+        ok, bits = eng.verify_batch(items, seed=bytes([k % 256]) * 32)
+        assert ok == all(want), (k, v.get("category"))
+        assert bits == want
+
+
+def test_all_small_order_vectors_one_batch(eng):
+    z = [_v(v) for v in of.load_golden("zip215_small_order.json")["vectors"]]
+    ok, bits = eng.verify_batch(z)
+    assert ok and all(bits)
+
+
+def test_adversarial_mix_config4(eng):
+    """config 4 shape: 1% invalid / non-canonical / small-order, batch false, exact bad set"""
+    n = 20000
+    items = _synthetic(eng, n, 32, seed=4)
+    rnd = random.Random(4)
+    bad = sorted(rnd.sample(range(n), n // 100))
+    adv = [_v(v) for v in of.load_golden("ed25519_vectors.json")["vectors"] if v["category"] != "honest"]
+    for j, i in enumerate(bad):
+        if j % 2 == 0:
+            pk, sg, m = items[i]
+            sg = bytearray(sg)
+            sg[rnd.randrange(64)] ^= 1 << rnd.randrange(8)
+            items[i] = (pk, bytes(sg), m)
+        else:
+            items[i] = adv[j % len(adv)]
+    want = [True] * n
+    for i in bad:
+        want[i] = of.verify(*items[i])
+    ok, bits = eng.verify_batch(items)
+    assert not ok
+    assert bits == want
+
+
+def test_staged_msm_runs_and_times(eng):
+    from narwhal_amd import _lib
+    items = _synthetic(eng, 8192, 512, seed=9)
+    pk, sg, arena, offs, lens = _lib.soa(items)
+    st = eng.stage(pk, sg, arena, offs, lens)
+    for r in range(3):
+        st.run(mode=1, seed=bytes([r]) * 32)
+    allv, bits = st.fetch()
+    t = st.kernel_times(1)
+    st.free()
+    assert allv and bits.all()
+    assert len(t) == 10 and all(v > 0 for v in t.values())

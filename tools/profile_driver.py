@@ -19,18 +19,20 @@ def main():
     ap.add_argument("--n", type=int, default=65536)
     ap.add_argument("--msg-len", type=int, default=512)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--mode", type=int, default=0, help="0 per-signature pipeline, 1 batch MSM")
     args = ap.parse_args()
     eng = narwhal_amd.Engine(device=0)
     pk, sg, msgs, offs, lens = bench.synth(eng, args.n, args.msg_len, seed=7)
     st = eng.stage(pk, sg, msgs, offs, lens)
-    for _ in range(args.reps):
-        st.run(mode=1)
+    for r in range(args.reps):
+        st.run(mode=args.mode, seed=bytes([r + 1]) * 32)
     allv, bits = st.fetch()
-    ms = st.kernel_ms()
+    ms = st.kernel_times(args.mode)
     st.free()
     eng.close()
     assert allv
-    print(json.dumps({"n": args.n, "reps": args.reps, "kernel_ms": list(map(float, ms))}))
+    print(json.dumps({"n": args.n, "reps": args.reps, "mode": args.mode, "kernel_ms": ms,
+                      "total_ms": sum(ms.values())}))
 
 
 if __name__ == "__main__":
