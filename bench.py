@@ -3,15 +3,19 @@
 
 Workload (BASELINE.json configs[1]): verify_batch of 65,536 valid signatures over 512-byte
 messages, distinct keys, synthetic (seeded keys and messages, signed on the GPU).  A "step" is
-one pass of the verification pipeline over the whole batch with the inputs already resident in
-HBM (k_ed_hash -> k_ed_points -> k_ed_straus; per-signature verdict bits, whose AND is the batch
-verdict).  With --gpus N the driver launches one rank per GPU (torch.distributed.run); each
-rank verifies its own shard of N x 65,536 (weak scaling, signature-index sharding, no data-path
-collective: the only exchange is the host-side max of the step times and the AND of verdicts).
+one batch verdict over one whole resident batch (inputs already in HBM): by default the batch
+MSM (K5: k_msm_scalars -> k_msm_points -> counting sort -> buckets -> window sums -> Horner,
+ed25519_consensus batch::Verifier semantics); --mode 0 runs the per-signature pipeline instead
+(K1-K4, per-signature verdict bits whose AND is the batch verdict).  --inflight K keeps K
+resident batches on K streams and issues the steps round-robin (a verification firehose: each
+step still verifies one full 65,536-signature batch); the single-stream step time is reported
+beside it.  With --gpus N the driver launches one rank per GPU (torch.distributed.run); each rank
+verifies its own batches (weak scaling, signature-index sharding, no data-path collective: the
+only exchange is the host-side max of the step times and the AND of verdicts over gloo).
 
-Extra fields: roofline (VALU: 32x32->64 multiply-adds of the dominant kernel vs the measured
+Extra fields: roofline (VALU: 32x32->64 multiply-adds of the dominant bulk kernel vs the measured
 v_mad_u64_u32 peak), cpu_baseline (the oracle's multi-threaded batch verifier on the host
-cores, rank 0 only), p50/p99 latency of a 1,024-signature batch host->host.
+cores, rank 0 only), p50/p99 latency of a 1,024-signature batch host->host, per-kernel times.
 """
 import argparse
 import json
@@ -26,9 +30,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 # Algorithmic field operations per signature, counted on the host-emulation build
-# (tests/test_hostemu.py::test_phase_op_counts pins these numbers): (mul, sq) per phase.
+# (tests/test_hostemu.py::test_phase_op_counts and tests/test_msm_hostemu.py pin these
+# numbers): (mul, sq) per phase.
 OPS_POINTS = (111, 514)
 OPS_STRAUS = (1505, 1020)
+OPS_MSM_POINTS = (48, 514)  # k_msm_points: decompress R and A + affine Niels entries
 MADS_PER_MUL, MADS_PER_SQ = 100, 55  # 10x10 and 55-term schoolbook, one v_mad_u64_u32 each
 
 
@@ -82,18 +88,39 @@ def cpu_baseline(pk, sg, msgs, offs, lens, seconds):
                       f"oracle/nwv_oracle.c batch verifier: Pippenger/Straus as dalek)"}
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc pass (FETCH_SIZE
+    doubled for gfx950's half-counted wide reads + WRITE_SIZE, MI355X_MICROARCH.md HBM section),
+    or None when no profile for it is committed."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+            k = d.get("kernels", {}).get(kernel)
+            if k and "FETCH_SIZE" in k and "WRITE_SIZE" in k:
+                return {"bytes": 2 * k["FETCH_SIZE"] * 1024 + k["WRITE_SIZE"] * 1024,
+                        "source": os.path.relpath(f, ROOT), "n": d.get("n")}
+        except (OSError, ValueError):
+            continue
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=65536, help="signatures per GPU")
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=6)
+    ap.add_argument("--n", type=int, default=65536, help="signatures per batch (per GPU)")
     ap.add_argument("--msg-len", type=int, default=512)
+    ap.add_argument("--mode", type=int, default=1, help="1 batch MSM (K5), 0 per-signature pipeline")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-reps", type=int, default=300)
-    ap.add_argument("--inflight", type=int, default=1,
+    ap.add_argument("--inflight", type=int, default=3,
                     help="resident batches in flight on separate streams (step s runs batch s %% K)")
+    ap.add_argument("--single-steps", type=int, default=8,
+                    help="single-stream steps timed after the run (step latency, per-kernel times)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -111,17 +138,15 @@ def main():
     eng = narwhal_amd.Engine(device=local)
     pk, sg, msgs, offs, lens = synth(eng, args.n, args.msg_len, seed=1000 + rank)
     stages = [eng.stage(pk, sg, msgs, offs, lens) for _ in range(max(1, args.inflight))]
-    st = stages[0]
+    seed = lambda s_: (bytes([(s_ * 7 + rank) % 256]) * 32)
 
     def sync_all():
         for s_ in stages:
             s_.sync()
 
     for w in range(args.warmup):
-        stages[w % len(stages)].run(mode=1)
+        stages[w % len(stages)].run(mode=args.mode, seed=seed(w))
     sync_all()
-    for s_ in stages:
-        s_.kernel_ms(reset=True)
 
     def barrier():
         if dist is not None:
@@ -131,7 +156,7 @@ def main():
     sync_all()
     t0 = time.perf_counter()
     for s in range(args.steps):
-        stages[s % len(stages)].run(mode=1)
+        stages[s % len(stages)].run(mode=args.mode, seed=seed(s))
     sync_all()
     t1 = time.perf_counter()
     barrier()
@@ -140,7 +165,17 @@ def main():
     for s_ in stages:
         all_valid, bits = s_.fetch()
         ok &= int(bool(all_valid) and bool(bits.all()))
-    kms = st.kernel_ms(reset=True)
+    # single-stream pass: step latency and per-kernel device times without overlap
+    st = stages[0]
+    st.kernel_times(args.mode, reset=True)
+    single = []
+    for s in range(args.single_steps):
+        ts = time.perf_counter()
+        st.run(mode=args.mode, seed=seed(1000 + s))
+        st.sync()
+        single.append((time.perf_counter() - ts) * 1e3)
+    kt = st.kernel_times(args.mode, reset=True)
+    ok &= int(st.fetch()[0])
     if dist is not None:
         import torch
         t = torch.tensor([dt], dtype=torch.float64)
@@ -174,21 +209,27 @@ def main():
             assert rc == 0 and allv.value == 1
         lat = np.array(lat)
         peak = valu_peak()
-        straus_ms = float(kms[2])
-        mads_launch = mads(OPS_STRAUS) * args.n
-        achieved = mads_launch / (straus_ms * 1e-3) / 1e12 if straus_ms > 0 else None
+        peak_t = (peak["v_mad_u64_u32_per_s"] / 1e12) if peak else None
+        if args.mode == 1:
+            kname, ops = "k_msm_points", OPS_MSM_POINTS
+        else:
+            kname, ops = "k_ed_straus", OPS_STRAUS
+        kms = float(kt.get(kname, 0.0))
+        mads_launch = mads(ops) * args.n
+        achieved = mads_launch / (kms * 1e-3) / 1e12 if kms > 0 else None
+        traffic = pmc_traffic(kname)
         roof = {
             "bound": "valu",
-            "kernel": "k_ed_straus",
+            "kernel": kname,
             "achieved": achieved,
-            "peak": (peak["v_mad_u64_u32_per_s"] / 1e12) if peak else None,
+            "peak": peak_t,
             "unit": "T v_mad_u64_u32/s",
-            "frac": (achieved / (peak["v_mad_u64_u32_per_s"] / 1e12)) if (peak and achieved) else None,
-            "traffic": None,
-            "algorithmic": f"{mads(OPS_STRAUS)} multiply-adds/signature ({OPS_STRAUS[0]} mul + "
-                           f"{OPS_STRAUS[1]} sq) x {args.n} signatures per launch",
-            "kernel_ms": {"k_ed_hash": float(kms[0]), "k_ed_points": float(kms[1]),
-                          "k_ed_straus": straus_ms},
+            "frac": (achieved / peak_t) if (peak_t and achieved) else None,
+            "traffic": traffic["bytes"] if traffic else None,
+            "traffic_source": traffic,
+            "algorithmic": f"{mads(ops)} multiply-adds/signature ({ops[0]} mul x 100 + {ops[1]} sq x 55) "
+                           f"x {args.n} signatures per launch",
+            "kernel_ms": kt,
         }
         cpu = None
         if not args.no_cpu_baseline:
@@ -208,9 +249,12 @@ def main():
             "data": "synthetic (seeded keys/messages, RFC 8032 signatures made on the GPU)",
             "config": {"workload": "verify_batch of 65,536 valid sigs, 512 B messages, distinct keys "
                                    "(BASELINE.json configs[1]) per GPU",
-                       "sigs_per_gpu": args.n, "msg_len": args.msg_len,
+                       "sigs_per_batch": args.n, "msg_len": args.msg_len,
+                       "path": "batch MSM (K5)" if args.mode == 1 else "per-signature (K1-K4)",
                        "parallelism": f"signature-index shards x{world}",
                        "inflight_batches": len(stages)},
+            "single_stream": {"ms_per_step": float(np.median(single)),
+                              "sigs_per_s": args.n / (float(np.median(single)) * 1e-3) * world},
             "latency_1k_batch_ms": {"p50": float(np.percentile(lat, 50)),
                                     "p99": float(np.percentile(lat, 99)), "reps": len(lat)},
             "roofline": roof,

@@ -293,4 +293,19 @@ void he_msm_z(const uint8_t* seed32, uint64_t i, uint8_t* z32) {
     std::memcpy(z32, z, 32);
 }
 
+// field multiplies / squarings of k_msm_points per signature (decompress R and A, affine entry)
+void he_msm_point_counts(const uint8_t* pk, const uint8_t* sig, unsigned long long counts[2]) {
+    uint32_t Aw[8], Rw[8], e[PRECOMP_ENTRY_WORDS];
+    words(pk, Aw);
+    words(sig, Rw);
+    nwv_count_mul = nwv_count_sq = 0;
+    ge_p3 P;
+    ge_decompress(Rw, P);
+    store_affine_entry(e, P);
+    ge_decompress(Aw, P);
+    store_affine_entry(e, P);
+    counts[0] = nwv_count_mul;
+    counts[1] = nwv_count_sq;
+}
+
 }  // extern "C"

@@ -151,3 +151,13 @@ def test_all_small_order_batch_accepts(he):
     z = of.load_golden("zip215_small_order.json")["vectors"]
     items = [(bytes.fromhex(v["pk"]), bytes.fromhex(v["sig"]), bytes.fromhex(v["msg"])) for v in z]
     assert msm_batch(he, items, 7, 64)
+
+
+def test_point_kernel_op_count_matches_bench(he):
+    """bench.py's roofline numerator for k_msm_points: field multiplies/squarings per signature."""
+    import bench
+    he.he_msm_point_counts.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p]
+    c = (ctypes.c_ulonglong * 2)()
+    for seed in (b"\x01" * 32, b"\x77" * 32):
+        he.he_msm_point_counts(of.pubkey(seed), of.sign(seed, b"m"), c)
+        assert (c[0], c[1]) == bench.OPS_MSM_POINTS
