@@ -4,14 +4,19 @@
 #   make hostemu  tests/_build/libhostemu.so    (test infrastructure: device math on the host)
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
-CSRC := $(wildcard narwhal_amd/csrc/*.h narwhal_amd/csrc/*.hip) include/nwv.h
+CSRC := $(wildcard narwhal_amd/csrc/*.h narwhal_amd/csrc/*.hip narwhal_amd/csrc/*.cpp) include/nwv.h include/nwv_types.h
 
 all: lib oracle hostemu tools
 
 lib: narwhal_amd/lib/libnwv.so
-narwhal_amd/lib/libnwv.so: $(CSRC)
+# nwv_types.cpp is plain host C++ (no kernels): built by g++ on its own, because mixing `-x c++`
+# into the hipcc line makes hipcc drop --offload-arch (the code object silently falls back to gfx906)
+narwhal_amd/lib/nwv_types.o: narwhal_amd/csrc/nwv_types.cpp include/nwv.h include/nwv_types.h
 	@mkdir -p narwhal_amd/lib
-	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -shared -Wall -o $@ narwhal_amd/csrc/nwv_host.hip
+	g++ -O2 -std=c++17 -fPIC -Wall -c -o $@ $<
+narwhal_amd/lib/libnwv.so: $(CSRC) narwhal_amd/lib/nwv_types.o
+	@mkdir -p narwhal_amd/lib
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -shared -Wall -o $@ narwhal_amd/lib/nwv_types.o narwhal_amd/csrc/nwv_host.hip
 
 oracle:
 	$(MAKE) -C oracle

@@ -78,11 +78,14 @@ def load():
 
 
 def exported_symbols_from_header():
-    """Every function name declared in include/nwv.h."""
+    """Every function name declared in include/*.h (nwv.h and nwv_types.h)."""
+    import glob
     import re
-    with open(HEADER_PATH) as f:
-        text = f.read()
-    return sorted(set(re.findall(r"\b(nwv_[a-z0-9_]+)\s*\(", text)))
+    names = set()
+    for h in glob.glob(os.path.join(os.path.dirname(HEADER_PATH), "*.h")):
+        with open(h) as f:
+            names |= set(re.findall(r"\b(nwv_[a-z0-9_]+)\s*\(", f.read()))
+    return sorted(names)
 
 
 def _check(rc, allow=(NWV_OK,)):

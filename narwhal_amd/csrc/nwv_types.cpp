@@ -1,0 +1,435 @@
+// nwv_types.cpp -- Narwhal Header / Vote / Certificate verification over the GPU engine
+// (include/nwv_types.h).  Host-side control flow mirrors types/src/primary.rs check by check;
+// every digest and every signature goes to the device through the C ABI of include/nwv.h, with
+// the *_many forms batching a whole call into one BLAKE2b launch and one batch MSM.
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/nwv_types.h"
+
+namespace {
+
+void put_le64(std::vector<uint8_t>& b, uint64_t v) {
+    for (int i = 0; i < 8; i++) b.push_back((uint8_t)(v >> (8 * i)));
+}
+void put_le32(std::vector<uint8_t>& b, uint32_t v) {
+    for (int i = 0; i < 4; i++) b.push_back((uint8_t)(v >> (8 * i)));
+}
+void put(std::vector<uint8_t>& b, const uint8_t* p, size_t n) { b.insert(b.end(), p, p + n); }
+
+// Header::digest preimage (types/src/primary.rs:209-227): author || round_le || epoch_le ||
+// (batch digest || worker id_le)* in payload order || parent digests in BTreeSet order
+void header_preimage(const nwv_header& h, std::vector<uint8_t>& b) {
+    put(b, h.author, 32);
+    put_le64(b, h.round);
+    put_le64(b, h.epoch);
+    for (size_t i = 0; i < h.n_payload; i++) {
+        put(b, h.payload_digests + 32 * i, 32);
+        put_le32(b, h.payload_workers[i]);
+    }
+    for (size_t i = 0; i < h.n_parents; i++) put(b, h.parents + 32 * i, 32);
+}
+// Vote::digest (:351-364) and Certificate::digest (:594-607): id || round_le || epoch_le || origin
+void id_round_epoch_origin(const uint8_t* id, uint64_t round, uint64_t epoch, const uint8_t* origin,
+                           std::vector<uint8_t>& b) {
+    put(b, id, 32);
+    put_le64(b, round);
+    put_le64(b, epoch);
+    put(b, origin, 32);
+}
+
+// Preimages appended to one arena, hashed in one nwv_blake2b256_many launch
+struct DigestBatch {
+    std::vector<uint8_t> arena;
+    std::vector<uint64_t> off, len;
+    size_t add_begin() {
+        off.push_back(arena.size());
+        return off.size() - 1;
+    }
+    void add_end() { len.push_back(arena.size() - off.back()); }
+    int run(nwv_ctx* ctx, std::vector<uint8_t>& out) {
+        out.assign(32 * off.size(), 0);
+        if (off.empty()) return NWV_OK;
+        arena.resize(arena.size() + 16);
+        return nwv_blake2b256_many(ctx, off.size(), arena.data(), off.data(), len.data(), out.data());
+    }
+};
+
+// Signatures of one call, verified as one batch (MSM; per-signature fallback when it rejects)
+struct SigBatch {
+    std::vector<uint8_t> pk, sig, msgs;
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> len;
+    size_t add(const uint8_t* p, const uint8_t* s, const uint8_t* m, size_t mlen) {
+        put(pk, p, 32);
+        put(sig, s, 64);
+        off.push_back(msgs.size());
+        len.push_back((uint32_t)mlen);
+        put(msgs, m, mlen);
+        return off.size() - 1;
+    }
+    size_t size() const { return off.size(); }
+    int run(nwv_ctx* ctx, std::vector<uint8_t>& ok) {
+        const size_t n = size();
+        ok.assign(n, 1);
+        if (n == 0) return NWV_OK;
+        msgs.resize(msgs.size() + 16);
+        std::vector<uint64_t> bits((n + 63) / 64 + 1, 0);
+        int all = 0;
+        int rc = nwv_ed25519_verify_batch(ctx, n, pk.data(), sig.data(), msgs.data(), off.data(),
+                                          len.data(), nullptr, &all, bits.data());
+        if (rc) return rc;
+        for (size_t i = 0; i < n; i++) ok[i] = (uint8_t)((bits[i >> 6] >> (i & 63)) & 1);
+        return NWV_OK;
+    }
+};
+
+// Committee lookups (keys sorted by bytes, as the BTreeMap)
+long committee_index(const nwv_committee& c, const uint8_t* pk) {
+    size_t lo = 0, hi = c.n;
+    while (lo < hi) {
+        const size_t mid = (lo + hi) / 2;
+        const int r = std::memcmp(c.keys + 32 * mid, pk, 32);
+        if (r == 0) return (long)mid;
+        if (r < 0) lo = mid + 1;
+        else hi = mid;
+    }
+    return -1;
+}
+uint64_t committee_stake(const nwv_committee& c, const uint8_t* pk) {
+    const long i = committee_index(c, pk);
+    return i < 0 ? 0 : c.stakes[i];
+}
+// WorkerCache::worker(author, id) succeeds
+bool worker_known(const nwv_committee& c, const uint8_t* author, uint32_t id) {
+    const long i = committee_index(c, author);
+    if (i < 0 || !c.n_workers) return false;
+    for (uint32_t k = 0; k < c.n_workers[i]; k++)
+        if (c.worker_ids[i][k] == id) return true;
+    return false;
+}
+uint64_t quorum_threshold(const nwv_committee& c) {
+    uint64_t total = 0;
+    for (size_t i = 0; i < c.n; i++) total += c.stakes[i];
+    return 2 * total / 3 + 1;
+}
+bool is_zero32(const uint8_t* p) {
+    for (int i = 0; i < 32; i++)
+        if (p[i]) return false;
+    return true;
+}
+// Certificate::genesis(committee).contains(self): PartialEq (:615-623) compares header id,
+// round, epoch and origin against the genesis certificates (default header of every authority)
+bool is_genesis(const nwv_committee& c, const nwv_certificate& cert) {
+    return is_zero32(cert.header.id) && cert.header.round == 0 && cert.header.epoch == c.epoch &&
+           committee_index(c, cert.header.author) >= 0;
+}
+
+// Host-side checks of Header::verify before its digest and signature (:150-176); the digest
+// comparison and worker ids are evaluated in reference order by the caller.
+struct HeaderPlan {
+    int pre = NWV_DAG_OK;   // epoch
+    long digest = -1;       // index in the digest batch
+    long sig = -1;          // index in the signature batch
+    int post = NWV_DAG_OK;  // authority / worker checks (after the id check)
+};
+
+void plan_header(const nwv_committee& c, const nwv_header& h, DigestBatch& db, HeaderPlan& p) {
+    if (h.epoch != c.epoch) {
+        p.pre = NWV_DAG_INVALID_EPOCH;
+        return;
+    }
+    p.digest = (long)db.add_begin();
+    header_preimage(h, db.arena);
+    db.add_end();
+    if (committee_stake(c, h.author) == 0) {
+        p.post = NWV_DAG_UNKNOWN_AUTHORITY;
+        return;
+    }
+    for (size_t i = 0; i < h.n_payload; i++)
+        if (!worker_known(c, h.author, h.payload_workers[i])) {
+            p.post = NWV_DAG_MALFORMED_HEADER;
+            return;
+        }
+}
+
+// verdict of Header::verify once digests are known; queues the signature when reached
+int header_after_digest(const nwv_header& h, const HeaderPlan& p, const std::vector<uint8_t>& dig,
+                        SigBatch* sb, HeaderPlan& pw) {
+    if (p.pre) return p.pre;
+    if (std::memcmp(dig.data() + 32 * p.digest, h.id, 32) != 0) return NWV_DAG_INVALID_HEADER_ID;
+    if (p.post) return p.post;
+    if (sb) pw.sig = (long)sb->add(h.author, h.signature, h.id, 32);
+    return NWV_DAG_OK;
+}
+
+bool valid_args(const nwv_committee* c) {
+    return c && (c->n == 0 || (c->keys && c->stakes));
+}
+
+}  // namespace
+
+extern "C" {
+
+uint64_t nwv_committee_quorum_threshold(const nwv_committee* committee) {
+    return committee ? quorum_threshold(*committee) : 0;
+}
+
+// ------------------------------------------------------------------ digests ------------
+int nwv_header_digest_many(nwv_ctx* ctx, size_t n, const nwv_header* h, uint8_t* out) {
+    if (!ctx || (n && (!h || !out))) return NWV_ERR_ARG;
+    DigestBatch db;
+    for (size_t i = 0; i < n; i++) {
+        db.add_begin();
+        header_preimage(h[i], db.arena);
+        db.add_end();
+    }
+    std::vector<uint8_t> d;
+    int rc = db.run(ctx, d);
+    if (rc) return rc;
+    if (n) std::memcpy(out, d.data(), 32 * n);
+    return NWV_OK;
+}
+int nwv_vote_digest_many(nwv_ctx* ctx, size_t n, const nwv_vote* v, uint8_t* out) {
+    if (!ctx || (n && (!v || !out))) return NWV_ERR_ARG;
+    DigestBatch db;
+    for (size_t i = 0; i < n; i++) {
+        db.add_begin();
+        id_round_epoch_origin(v[i].id, v[i].round, v[i].epoch, v[i].origin, db.arena);
+        db.add_end();
+    }
+    std::vector<uint8_t> d;
+    int rc = db.run(ctx, d);
+    if (rc) return rc;
+    if (n) std::memcpy(out, d.data(), 32 * n);
+    return NWV_OK;
+}
+int nwv_certificate_digest_many(nwv_ctx* ctx, size_t n, const nwv_certificate* c, uint8_t* out) {
+    if (!ctx || (n && (!c || !out))) return NWV_ERR_ARG;
+    DigestBatch db;
+    for (size_t i = 0; i < n; i++) {
+        db.add_begin();
+        id_round_epoch_origin(c[i].header.id, c[i].header.round, c[i].header.epoch, c[i].header.author,
+                              db.arena);
+        db.add_end();
+    }
+    std::vector<uint8_t> d;
+    int rc = db.run(ctx, d);
+    if (rc) return rc;
+    if (n) std::memcpy(out, d.data(), 32 * n);
+    return NWV_OK;
+}
+int nwv_header_digest(nwv_ctx* ctx, const nwv_header* h, uint8_t out[32]) {
+    return nwv_header_digest_many(ctx, 1, h, out);
+}
+int nwv_vote_digest(nwv_ctx* ctx, const nwv_vote* v, uint8_t out[32]) { return nwv_vote_digest_many(ctx, 1, v, out); }
+int nwv_certificate_digest(nwv_ctx* ctx, const nwv_certificate* c, uint8_t out[32]) {
+    return nwv_certificate_digest_many(ctx, 1, c, out);
+}
+
+// ------------------------------------------------------------------ Header::verify -----
+int nwv_header_verify_many(nwv_ctx* ctx, const nwv_committee* committee, size_t n, const nwv_header* h,
+                           int32_t* results) {
+    if (!ctx || !valid_args(committee) || (n && (!h || !results))) return NWV_ERR_ARG;
+    const nwv_committee& c = *committee;
+    DigestBatch db;
+    std::vector<HeaderPlan> plan(n);
+    for (size_t i = 0; i < n; i++) plan_header(c, h[i], db, plan[i]);
+    std::vector<uint8_t> dig;
+    int rc = db.run(ctx, dig);
+    if (rc) return rc;
+    SigBatch sb;
+    for (size_t i = 0; i < n; i++) results[i] = header_after_digest(h[i], plan[i], dig, &sb, plan[i]);
+    std::vector<uint8_t> ok;
+    if ((rc = sb.run(ctx, ok))) return rc;
+    for (size_t i = 0; i < n; i++)
+        if (results[i] == NWV_DAG_OK && plan[i].sig >= 0 && !ok[plan[i].sig]) results[i] = NWV_DAG_INVALID_SIGNATURE;
+    return NWV_OK;
+}
+int nwv_header_verify(nwv_ctx* ctx, const nwv_committee* committee, const nwv_header* h) {
+    int32_t r = 0;
+    int rc = nwv_header_verify_many(ctx, committee, 1, h, &r);
+    return rc ? rc : r;
+}
+
+// ------------------------------------------------------------------ Vote::verify -------
+int nwv_vote_verify_many(nwv_ctx* ctx, const nwv_committee* committee, size_t n, const nwv_vote* v,
+                         int32_t* results) {
+    if (!ctx || !valid_args(committee) || (n && (!v || !results))) return NWV_ERR_ARG;
+    const nwv_committee& c = *committee;
+    std::vector<uint8_t> dig(32 * n);
+    int rc = n ? nwv_vote_digest_many(ctx, n, v, dig.data()) : NWV_OK;
+    if (rc) return rc;
+    SigBatch sb;
+    std::vector<long> sig(n, -1);
+    for (size_t i = 0; i < n; i++) {
+        if (v[i].epoch != c.epoch) results[i] = NWV_DAG_INVALID_EPOCH;
+        else if (committee_stake(c, v[i].author) == 0) results[i] = NWV_DAG_UNKNOWN_AUTHORITY;
+        else {
+            results[i] = NWV_DAG_OK;
+            sig[i] = (long)sb.add(v[i].author, v[i].signature, dig.data() + 32 * i, 32);
+        }
+    }
+    std::vector<uint8_t> ok;
+    if ((rc = sb.run(ctx, ok))) return rc;
+    for (size_t i = 0; i < n; i++)
+        if (sig[i] >= 0 && !ok[sig[i]]) results[i] = NWV_DAG_INVALID_SIGNATURE;
+    return NWV_OK;
+}
+int nwv_vote_verify(nwv_ctx* ctx, const nwv_committee* committee, const nwv_vote* v) {
+    int32_t r = 0;
+    int rc = nwv_vote_verify_many(ctx, committee, 1, v, &r);
+    return rc ? rc : r;
+}
+
+// ------------------------------------------------------------------ Certificate::verify -
+int nwv_certificate_verify_many(nwv_ctx* ctx, const nwv_committee* committee, size_t n,
+                                const nwv_certificate* cs, int32_t* results) {
+    if (!ctx || !valid_args(committee) || (n && (!cs || !results))) return NWV_ERR_ARG;
+    const nwv_committee& c = *committee;
+    const uint64_t quorum = quorum_threshold(c);
+    // phase 1: host checks and every digest (header ids to re-derive, certificate digests)
+    DigestBatch db;
+    std::vector<HeaderPlan> plan(n);
+    std::vector<long> cdig(n, -1);
+    std::vector<uint8_t> done(n, 0);
+    for (size_t i = 0; i < n; i++) {
+        const nwv_certificate& x = cs[i];
+        results[i] = NWV_DAG_OK;
+        if (x.header.epoch != c.epoch) {  // Certificate::verify's own epoch check
+            results[i] = NWV_DAG_INVALID_EPOCH;
+            done[i] = 1;
+            continue;
+        }
+        if (is_genesis(c, x)) {  // genesis certificates are always valid
+            done[i] = 1;
+            continue;
+        }
+        plan_header(c, x.header, db, plan[i]);
+        cdig[i] = (long)db.add_begin();
+        id_round_epoch_origin(x.header.id, x.header.round, x.header.epoch, x.header.author, db.arena);
+        db.add_end();
+    }
+    std::vector<uint8_t> dig;
+    int rc = db.run(ctx, dig);
+    if (rc) return rc;
+    // phase 2: header verdicts, quorum, and the signature batch (header + aggregated)
+    SigBatch sb;
+    std::vector<long> agg_first(n, -1), agg_count(n, 0);
+    std::vector<int32_t> after_header(n, NWV_DAG_OK);
+    for (size_t i = 0; i < n; i++) {
+        if (done[i]) continue;
+        const nwv_certificate& x = cs[i];
+        const int hr = header_after_digest(x.header, plan[i], dig, &sb, plan[i]);
+        if (hr) {
+            results[i] = hr;
+            done[i] = 1;
+            continue;
+        }
+        // bitmap -> pks in committee order, as the filter at :505-520
+        uint64_t weight = 0;
+        size_t it = 0;
+        std::vector<size_t> pks;
+        for (size_t a = 0; a < c.n; a++) {
+            if (it < x.n_signed && x.signed_authorities[it] == (uint32_t)a) {
+                weight += c.stakes[a];
+                it++;
+                pks.push_back(a);
+            }
+        }
+        if (weight < quorum) {
+            after_header[i] = NWV_DAG_CERTIFICATE_REQUIRES_QUORUM;
+            continue;
+        }
+        // Ed25519AggregateSignature::verify: |pks| != |sigs| -> Err before any crypto
+        if (pks.size() != x.n_sigs) {
+            after_header[i] = NWV_DAG_INVALID_SIGNATURE;
+            continue;
+        }
+        const uint8_t* d = dig.data() + 32 * cdig[i];
+        for (size_t k = 0; k < pks.size(); k++) {
+            const long idx = (long)sb.add(c.keys + 32 * pks[k], x.aggregated_signature + 64 * k, d, 32);
+            if (k == 0) agg_first[i] = idx;
+        }
+        agg_count[i] = (long)pks.size();
+    }
+    std::vector<uint8_t> ok;
+    if ((rc = sb.run(ctx, ok))) return rc;
+    for (size_t i = 0; i < n; i++) {
+        if (done[i]) continue;
+        if (plan[i].sig >= 0 && !ok[plan[i].sig]) {  // Header::verify's signature comes first
+            results[i] = NWV_DAG_INVALID_SIGNATURE;
+            continue;
+        }
+        if (after_header[i]) {
+            results[i] = after_header[i];
+            continue;
+        }
+        for (long k = 0; k < agg_count[i]; k++)
+            if (!ok[agg_first[i] + k]) {
+                results[i] = NWV_DAG_INVALID_SIGNATURE;
+                break;
+            }
+    }
+    return NWV_OK;
+}
+int nwv_certificate_verify(nwv_ctx* ctx, const nwv_committee* committee, const nwv_certificate* c) {
+    int32_t r = 0;
+    int rc = nwv_certificate_verify_many(ctx, committee, 1, c, &r);
+    return rc ? rc : r;
+}
+
+int nwv_validate_certificates(nwv_ctx* ctx, const nwv_committee* committee, size_t n,
+                              const nwv_certificate* c, size_t* n_invalid, size_t* invalid_idx) {
+    if (!n_invalid || (n && !invalid_idx)) return NWV_ERR_ARG;
+    *n_invalid = 0;
+    if (n == 0) return NWV_OK;  // "No certificates are able to be served": Ok(vec![])
+    std::vector<int32_t> r(n);
+    int rc = nwv_certificate_verify_many(ctx, committee, n, c, r.data());
+    if (rc) return rc;
+    for (size_t i = 0; i < n; i++)
+        if (r[i] != NWV_DAG_OK) invalid_idx[(*n_invalid)++] = i;
+    return *n_invalid ? NWV_ERR_SIGNATURE : NWV_OK;
+}
+
+// ------------------------------------------------------------------ Certificate::new ----
+int nwv_certificate_new(const nwv_committee* committee, size_t n_votes, const uint8_t* vote_pks,
+                        const uint8_t* vote_sigs, int check_stake, uint32_t* signed_out,
+                        size_t* n_signed, uint8_t* sigs_out, size_t* n_sigs) {
+    if (!valid_args(committee) || !n_signed || !n_sigs || (n_votes && (!vote_pks || !vote_sigs)))
+        return NWV_ERR_ARG;
+    const nwv_committee& c = *committee;
+    // votes.sort_by_key(pk) (stable), then walk the committee keys in order
+    std::vector<size_t> order(n_votes);
+    for (size_t i = 0; i < n_votes; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+        return std::memcmp(vote_pks + 32 * a, vote_pks + 32 * b, 32) < 0;
+    });
+    auto same_vote = [&](size_t a, size_t b) {
+        return std::memcmp(vote_pks + 32 * a, vote_pks + 32 * b, 32) == 0 &&
+               std::memcmp(vote_sigs + 64 * a, vote_sigs + 64 * b, 64) == 0;
+    };
+    size_t front = 0, ns = 0;
+    uint64_t weight = 0;
+    std::vector<size_t> taken;
+    for (size_t k = 0; k < c.n; k++) {
+        if (front < n_votes && std::memcmp(c.keys + 32 * k, vote_pks + 32 * order[front], 32) == 0) {
+            taken.push_back(order[front++]);
+            weight += c.stakes[k];
+            while (front < n_votes && same_vote(order[front], taken.back())) front++;  // repeats
+            if (signed_out) signed_out[ns] = (uint32_t)k;
+            ns++;
+        }
+    }
+    if (front < n_votes) return NWV_DAG_UNKNOWN_AUTHORITY;
+    if (check_stake && weight < quorum_threshold(c)) return NWV_DAG_CERTIFICATE_REQUIRES_QUORUM;
+    *n_signed = ns;
+    *n_sigs = taken.size();
+    if (sigs_out)
+        for (size_t k = 0; k < taken.size(); k++) std::memcpy(sigs_out + 64 * k, vote_sigs + 64 * taken[k], 64);
+    return NWV_DAG_OK;
+}
+
+}  // extern "C"

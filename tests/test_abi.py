@@ -32,7 +32,9 @@ def test_library_contains_gfx950_code_object():
                          capture_output=True, text=True).stdout
     assert ".hip_fatbin" in out
     raw = open(_lib.LIB_PATH, "rb").read()
-    assert b"gfx950" in raw
+    import re
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", raw))
+    assert targets == {b"gfx950"}, targets  # gfx950 code objects only
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK),
