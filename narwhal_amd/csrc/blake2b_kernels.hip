@@ -41,6 +41,132 @@ extern "C" __global__ void __launch_bounds__(256) k_blake2b_many(
     o[1] = make_uint4(d[4], d[5], d[6], d[7]);
 }
 
+// ---- long messages: 4 lanes per message --------------------------------------------------
+// BLAKE2b is sequential over blocks, so a worker batch (types/src/primary.rs:65-73, ~500 KB =
+// 3,909 compressions) is latency-bound on one lane.  Here the 4 lanes of a quad hold the 4
+// columns of the 4x4 state (lane q: v[q], v[q+4], v[q+8], v[q+12]) and run the column step's
+// and the diagonal step's G functions in parallel; between the two steps rows 1-3 rotate
+// across the quad with DPP quad_perm moves.  The 128-byte block is staged in LDS (each lane
+// loads 32 bytes) and every G reads its two sigma-selected words from there.
+namespace {
+// quad_perm controls: lane q reads lane (q+1)%4, (q+2)%4, (q+3)%4
+constexpr int QP_NEXT1 = 0x39, QP_NEXT2 = 0x4E, QP_NEXT3 = 0x93;
+template <int CTRL>
+__device__ __forceinline__ uint64_t quad_rot(uint64_t x) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)x, CTRL, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, false);
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ __forceinline__ uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// G on native 64-bit words: the adds become single v_lshl_add_u64 (gfx950), which shortens the
+// dependent chain that bounds a long message's latency
+__device__ __forceinline__ void b2_g(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d, uint64_t x, uint64_t y) {
+    a = a + b + x;
+    d = rotr64(d ^ a, 32);
+    c = c + d;
+    b = rotr64(b ^ c, 24);
+    a = a + b + y;
+    d = rotr64(d ^ a, 16);
+    c = c + d;
+    b = rotr64(b ^ c, 63);
+}
+// nibble q of the packed sigma entries for lane q
+constexpr uint32_t sigma_pack(int r, int first) {
+    uint32_t v = 0;
+    for (int q = 0; q < 4; q++) v |= (uint32_t)BLAKE2B_SIGMA[r][first + 2 * q] << (4 * q);
+    return v;
+}
+__device__ __forceinline__ uint64_t iv64(int k) {
+    return (uint64_t)BLAKE2B_IV32[2 * k] | ((uint64_t)BLAKE2B_IV32[2 * k + 1] << 32);
+}
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(64) k_blake2b_quad(
+    uint64_t n, const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+    const uint64_t* __restrict__ len, uint32_t* __restrict__ out) {
+    __shared__ uint64_t blk[16][16];
+    const int lane = threadIdx.x, q = lane & 3, slot = lane >> 2;
+    const uint64_t i = (uint64_t)blockIdx.x * 16 + slot;
+    const bool active = i < n;
+    const uint8_t* p = active ? base + off[i] : base;
+    const uint64_t L = active ? len[i] : 0;
+    const uint64_t nb = active ? (L == 0 ? 1 : (L + 127) / 128) : 0;
+    uint64_t nmax = nb;  // blocks of the longest message of the wave
+    for (int o = 4; o < 64; o <<= 1) {
+        const uint64_t t = __shfl_xor(nmax, o);
+        nmax = t > nmax ? t : nmax;
+    }
+    const uint64_t iv0 = iv64(q), iv1 = iv64(q + 4);
+    uint64_t h0 = iv0, h1 = iv1;
+    if (q == 0) h0 ^= 0x01010000u ^ 32u;
+    const int sh = 4 * q;
+    // the next block's 32 bytes for this lane are fetched one block ahead (9 aligned dwords
+    // cover an unaligned 32-byte window), so the global-load latency overlaps a compression
+    uint32_t raw[9];
+    auto fetch = [&](uint64_t blk_idx) {
+        const uintptr_t a = (uintptr_t)(p + 128 * blk_idx + 32 * q);
+        const uint32_t* wp = (const uint32_t*)(a & ~(uintptr_t)3);
+#pragma unroll
+        for (int t = 0; t < 9; t++) raw[t] = wp[t];
+    };
+    if (nb > 0) fetch(0);
+#pragma unroll 1
+    for (uint64_t b = 0; b < nmax; b++) {
+        const bool live = b < nb;
+        const uint64_t pos = 128 * b + 32 * q;
+        const uint32_t ash = (uint32_t)(((uintptr_t)(p + pos)) & 3) * 8;
+        uint32_t w[8];
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            const uint64_t two = ((uint64_t)raw[t + 1] << 32) | raw[t];
+            uint32_t v = (uint32_t)(two >> ash);
+            const uint64_t bp = pos + 4 * t;  // trim to the message length (zero past the end)
+            if (!live || bp >= L) v = 0u;
+            else if (bp + 4 > L) v &= 0xffffffffu >> (8 * (uint32_t)(bp + 4 - L));
+            w[t] = v;
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++) blk[slot][4 * q + t] = (uint64_t)w[2 * t] | ((uint64_t)w[2 * t + 1] << 32);
+        if (b + 1 < nb) fetch(b + 1);
+        __syncthreads();
+        // every sigma-selected word this lane needs for the 12 rounds, before the chain starts
+        const uint64_t* m = blk[slot];
+        uint64_t mw[12][4];
+#pragma unroll
+        for (int r = 0; r < 12; r++) {
+            mw[r][0] = m[(sigma_pack(r, 0) >> sh) & 15];
+            mw[r][1] = m[(sigma_pack(r, 1) >> sh) & 15];
+            mw[r][2] = m[(sigma_pack(r, 8) >> sh) & 15];
+            mw[r][3] = m[(sigma_pack(r, 9) >> sh) & 15];
+        }
+        const bool last = b + 1 == nb;
+        const uint64_t tb = last ? L : 128 * (b + 1);  // bytes compressed so far
+        uint64_t va = h0, vb = h1, vc = iv0, vd = iv1;
+        if (q == 0) vd ^= tb;
+        if (q == 2 && last) vd = ~vd;
+#pragma unroll
+        for (int r = 0; r < 12; r++) {
+            b2_g(va, vb, vc, vd, mw[r][0], mw[r][1]);
+            vb = quad_rot<QP_NEXT1>(vb);
+            vc = quad_rot<QP_NEXT2>(vc);
+            vd = quad_rot<QP_NEXT3>(vd);
+            b2_g(va, vb, vc, vd, mw[r][2], mw[r][3]);
+            vb = quad_rot<QP_NEXT3>(vb);
+            vc = quad_rot<QP_NEXT2>(vc);
+            vd = quad_rot<QP_NEXT1>(vd);
+        }
+        if (live) {
+            h0 ^= va ^ vc;
+            h1 ^= vb ^ vd;
+        }
+        __syncthreads();
+    }
+    if (active) {
+        out[8 * i + 2 * q] = (uint32_t)h0;
+        out[8 * i + 2 * q + 1] = (uint32_t)(h0 >> 32);
+    }
+}
+
 namespace {
 __device__ __forceinline__ uint64_t ld_u64_unaligned(const uint8_t* p) {
     return (uint64_t)ld_u32_unaligned(p) | ((uint64_t)ld_u32_unaligned(p + 4) << 32);

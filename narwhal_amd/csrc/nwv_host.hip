@@ -785,6 +785,24 @@ void nwv_staged_free(nwv_staged* st) {
 }
 
 // ---- BLAKE2b-256 --------------------------------------------------------------------
+// Messages of at least this many bytes (the longest of the call) go 4 lanes per message
+static uint64_t b2_quad_min() {
+    static const uint64_t v = [] {
+        const char* e = std::getenv("NWV_B2_QUAD_MIN");
+        return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)1024;
+    }();
+    return v;
+}
+static void b2_launch(Device& d, size_t m, uint64_t maxlen, const uint8_t* base, const uint64_t* off,
+                      const uint64_t* len, uint32_t* out) {
+    if (maxlen >= b2_quad_min())
+        hipLaunchKernelGGL(k_blake2b_quad, dim3((unsigned)((m + 15) / 16)), dim3(64), 0, d.stream,
+                           (uint64_t)m, base, off, len, out);
+    else
+        hipLaunchKernelGGL(k_blake2b_many, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, d.stream,
+                           (uint64_t)m, base, off, len, out);
+}
+
 static int b2_stage(Device& d, size_t n, const uint8_t* base, const uint64_t* off,
                     const uint64_t* len, size_t lo, size_t hi, std::vector<uint64_t>& roff) {
     uint64_t mlo = UINT64_MAX, mhi = 0;
@@ -829,10 +847,10 @@ int nwv_blake2b256_many(nwv_ctx* ctx, size_t n, const uint8_t* base, const uint6
             if (!rc) rc = b2_stage(d, n, base, off, len, lo, hi, roff);
             if (!rc) {
                 const size_t m = hi - lo;
-                hipLaunchKernelGGL(k_blake2b_many, dim3((unsigned)((m + 255) / 256)), dim3(256), 0,
-                                   d.stream, (uint64_t)m, d.b2_base.as<uint8_t>(),
-                                   d.b2_off.as<uint64_t>(), d.b2_len.as<uint64_t>(),
-                                   d.b2_out.as<uint32_t>());
+                uint64_t maxlen = 0;
+                for (size_t k2 = lo; k2 < hi; k2++) maxlen = std::max<uint64_t>(maxlen, len[k2]);
+                b2_launch(d, m, maxlen, d.b2_base.as<uint8_t>(), d.b2_off.as<uint64_t>(),
+                          d.b2_len.as<uint64_t>(), d.b2_out.as<uint32_t>());
                 hipError_t e = hipGetLastError();
                 if (e == hipSuccess) e = hipMemcpyAsync(out + 32 * lo, d.b2_out.p, 32 * m,
                                                         hipMemcpyDeviceToHost, d.stream);
@@ -870,9 +888,10 @@ int nwv_batch_digest_serialized(nwv_ctx* ctx, size_t n, const uint8_t* base, con
     hipLaunchKernelGGL(k_batch_compact, dim3((unsigned)n), dim3(256), 0, d.stream, (uint64_t)n,
                        d.b2_base.as<uint8_t>(), d.b2_off.as<uint64_t>(), d.b2_len.as<uint64_t>(),
                        d.b2_packed.as<uint8_t>(), d.b2_plen.as<uint64_t>(), d.b2_err.as<int64_t>());
-    hipLaunchKernelGGL(k_blake2b_many, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, d.stream,
-                       (uint64_t)n, d.b2_packed.as<uint8_t>(), d.b2_off.as<uint64_t>(),
-                       d.b2_plen.as<uint64_t>(), d.b2_out.as<uint32_t>());
+    uint64_t maxlen = 0;
+    for (size_t k2 = 0; k2 < n; k2++) maxlen = std::max<uint64_t>(maxlen, len[k2]);
+    b2_launch(d, n, maxlen, d.b2_packed.as<uint8_t>(), d.b2_off.as<uint64_t>(), d.b2_plen.as<uint64_t>(),
+              d.b2_out.as<uint32_t>());
     NWV_HIP(hipGetLastError());
     NWV_HIP(hipMemcpyAsync(out, d.b2_out.p, 32 * n, hipMemcpyDeviceToHost, d.stream));
     NWV_HIP(hipMemcpyAsync(err_offset, d.b2_err.p, 8 * n, hipMemcpyDeviceToHost, d.stream));

@@ -54,3 +54,25 @@ def test_worker_batch_500kb(eng):
     (d, e), = eng.batch_digest_serialized([ser])
     assert e == -1 and d == want
     assert eng.blake2b256_many([b"".join(txs)]) == [want]
+
+
+def test_quad_kernel_mixed_lengths(eng):
+    """a call whose longest message is >= 1 KiB runs 4 lanes per message (k_blake2b_quad):
+    block-boundary lengths, empty, unaligned offsets inside the arena, and ~500 KB batches"""
+    rnd = random.Random(9)
+    lens = [0, 1, 111, 127, 128, 129, 255, 256, 257, 1023, 1024, 1025, 4096, 65537, 500224]
+    lens += [rnd.randrange(0, 3000) for _ in range(40)]
+    msgs = [rnd.randbytes(n) for n in lens]
+    assert eng.blake2b256_many(msgs) == [hashlib.blake2b(m, digest_size=32).digest() for m in msgs]
+
+
+def test_hundred_worker_batches_dag_round(eng):
+    """configs[4]: 100 worker batches of 977 x 512 B serialized, digested in one call"""
+    rnd = random.Random(55)
+    bufs, want = [], []
+    for b in range(100):
+        txs = [(bytes([b % 2]) + struct.pack(">Q", rnd.getrandbits(64))).ljust(512, b"\0") for _ in range(977)]
+        bufs.append(struct.pack("<IQ", 0, len(txs)) + b"".join(struct.pack("<Q", len(t)) + t for t in txs))
+        want.append(hashlib.blake2b(b"".join(txs), digest_size=32).digest())
+    got = eng.batch_digest_serialized(bufs)
+    assert [d for d, _ in got] == want
