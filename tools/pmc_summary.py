@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""Average rocprofv3 --pmc counter values per kernel over the dispatches of one or more passes
+(csv output dirs) -> JSON.  Usage: pmc_summary.py --n N --out FILE DIR [DIR ...]"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dirs", nargs="+")
+    ap.add_argument("--n", type=int, default=0)
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--note", default="")
+    a = ap.parse_args()
+    sums = collections.defaultdict(lambda: collections.defaultdict(float))
+    cnt = collections.defaultdict(lambda: collections.defaultdict(set))
+    for d in a.dirs:
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    k = row.get("Kernel_Name", "").split("(")[0]
+                    c = row.get("Counter_Name")
+                    v = float(row.get("Counter_Value", 0) or 0)
+                    did = row.get("Dispatch_Id") or row.get("Correlation_Id")
+                    sums[k][c] += v
+                    cnt[k][c].add(did)
+    out = {"n": a.n, "note": a.note, "kernels": {}}
+    for k, cs in sums.items():
+        out["kernels"][k] = {c: v / max(1, len(cnt[k][c])) for c, v in cs.items()}
+    with open(a.out, "w") as fh:
+        json.dump(out, fh, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
