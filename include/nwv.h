@@ -37,8 +37,8 @@ extern "C" {
 typedef struct nwv_ctx nwv_ctx;
 
 /* nwv_init flags.  Batch verification (nwv_ed25519_verify_batch and the trait entry points built
- * on it) runs one Pippenger MSM per device shard when the shard has >= 4096 signatures (env
- * NWV_MSM_MIN_N overrides), else the per-signature pipeline; these force one or the other. */
+ * on it) runs one Pippenger MSM per device shard (env NWV_MSM_MIN_N sets a minimum shard size,
+ * below which the per-signature pipeline runs); these force one or the other. */
 #define NWV_FLAG_MSM_ALWAYS 1u
 #define NWV_FLAG_MSM_NEVER 2u
 

@@ -161,10 +161,30 @@ NWV_HD void msm_recode(const uint32_t s[8], const MsmLayout& L, int nw, Emit emi
 // Bucket entry encoding: point index | sign bit
 static constexpr uint32_t MSM_NEG = 0x80000000u;
 
-// affine Niels entry (y+x | y-x | 2dxy | -2dxy) of a decompressed point (Z = 1, T = xy)
-NWV_HD void store_affine_entry(uint32_t* e, const ge_p3& p) {
-    ge_precomp q{fe_carry(fe_add(p.Y, p.X)), fe_carry(fe_sub(p.Y, p.X)), fe_mul(p.T, fe_d2())};
-    store_precomp_entry(e, q);
+// MSM point record: affine Niels (y+x | y-x | 2dxy) of a decompressed point (Z = 1, T = xy),
+// padded to 32 words = 128 bytes so a bucket lane's random gather touches one cache line; a
+// negative digit swaps y+x / y-x and negates 2dxy on the fly.
+static constexpr int MSM_PT_WORDS = 32;
+
+NWV_HD void msm_store_point(uint32_t* e, const ge_p3& p) {
+    store_fe(e, fe_carry(fe_add(p.Y, p.X)));
+    store_fe(e + 10, fe_carry(fe_sub(p.Y, p.X)));
+    store_fe(e + 20, fe_mul(p.T, fe_d2()));
+    e[30] = 0u;
+    e[31] = 0u;
+}
+// record from a basepoint-table precomp entry (y+x | y-x | 2dxy | -2dxy)
+NWV_HD void msm_point_from_precomp(uint32_t* e, const uint32_t* pre) {
+    for (int k = 0; k < 30; k++) e[k] = pre[k];
+    e[30] = 0u;
+    e[31] = 0u;
+}
+NWV_HD ge_precomp msm_point_select(const fe& ypx, const fe& ymx, const fe& xy2d, bool neg) {
+    const fe nxy = fe_neg(xy2d);  // 2p - 2dxy: limbs < 2^27, a valid multiply input
+    return ge_precomp{fe_select(ypx, ymx, neg), fe_select(ymx, ypx, neg), fe_select(xy2d, nxy, neg)};
+}
+NWV_HD ge_precomp msm_load_point(const uint32_t* e, bool neg) {
+    return msm_point_select(load_fe(e), load_fe(e + 10), load_fe(e + 20), neg);
 }
 
 // Weighted bucket sums.  For one window with buckets S_1..S_NB (bucket b has weight b), a lane

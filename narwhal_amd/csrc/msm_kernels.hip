@@ -2,11 +2,12 @@
 //
 // Pipeline (one batch resident on one device; layout of the 2n+1 points in msm.h):
 //   k_msm_scalars   lane i: k_i = SHA-512(R||A||M) mod l, s_i < l, z_i = PRF(seed, i),
-//                   scalars z_i k_i and z_i; per-workgroup partial sums of z_i s_i
-//   k_msm_bscalar   one workgroup: b = -sum z_i s_i mod l (the basepoint's scalar), B entry
+//                   scalars z_i k_i and z_i recoded to signed digits -> digits[w][.] (i16);
+//                   per-workgroup partial sums of z_i s_i
+//   k_msm_bscalar   one workgroup: b = -sum z_i s_i mod l (the basepoint's scalar), its digits,
+//                   B's point record
 //   k_msm_points    2 lanes per signature (wave-uniform R / A roles): decompress, store the
-//                   affine Niels entry of each point
-//   k_msm_recode    lane j: signed radix-2^C digits of point j's scalar -> digits[w][j] (i16)
+//                   128-byte affine Niels record of each point
 //   k_msm_hist      workgroup (chunk, window): LDS histogram of the window's bucket ids
 //   k_scan_*        exclusive scan of the (window, bucket, chunk)-ordered counts
 //   k_msm_scatter   workgroup (chunk, window): LDS cursors place j|sign into bucket order
@@ -44,13 +45,14 @@ __device__ __forceinline__ void msm_store8(uint32_t* p, const uint32_t w[8]) {
 
 }  // namespace
 
-// scal: (2n+1) x 8 words; partial: gridDim.x x 9 words (sum of z_i s_i over the workgroup, as a
+// digits: [window][2n+1] signed digits of every point's scalar (A_i at i, R_i at n+1+i; B's row
+// entry n is written by k_msm_bscalar); partial: gridDim.x x 9 words (sum of z_i s_i over the workgroup, as a
 // plain 288-bit integer); fail: bit 0 set when any s_i >= l
 extern "C" __global__ void __launch_bounds__(256) k_msm_scalars(
     uint64_t n, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, const uint64_t* __restrict__ msg_off,
-    const uint32_t* __restrict__ msg_len, MsmSeed seed, uint32_t* __restrict__ scal,
-    uint32_t* __restrict__ partial, uint32_t* __restrict__ fail) {
+    const uint32_t* __restrict__ msg_len, MsmSeed seed, MsmLayout lay, uint32_t* __restrict__ scal,
+    int16_t* __restrict__ digits, uint32_t* __restrict__ partial, uint32_t* __restrict__ fail) {
     __shared__ uint32_t zs_lds[256 * 9];
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t zs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -63,9 +65,11 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_scalars(
         if (f != FLAG_S_OK) atomicOr(fail, 1u);
         msm_z(seed.w, i, z);
         sc_mul(z, k, a);
-        msm_store8(scal + 8 * i, a);
-        msm_store8(scal + 8 * (n + 1 + i), z);
         sc_mul(z, Sw, zs);
+        // signed digits of A_i's and R_i's scalars straight from registers (window-major rows)
+        const uint64_t np = 2 * n + 1;
+        msm_recode(a, lay, lay.nw, [&](int w, int d) { digits[(uint64_t)w * np + i] = (int16_t)d; });
+        msm_recode(z, lay, lay.nw_z, [&](int w, int d) { digits[(uint64_t)w * np + n + 1 + i] = (int16_t)d; });
     }
 #pragma unroll
     for (int k = 0; k < 8; k++) zs_lds[threadIdx.x * 9 + k] = zs[k];
@@ -92,8 +96,9 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_scalars(
 
 // One workgroup of 256: b = -(sum of the partials) mod l -> scal[n]; B's affine entry -> pts[n]
 extern "C" __global__ void __launch_bounds__(256) k_msm_bscalar(
-    uint64_t n, uint32_t nparts, const uint32_t* __restrict__ partial, const uint32_t* __restrict__ btab,
-    uint32_t* __restrict__ scal, uint32_t* __restrict__ pts) {
+    uint64_t n, uint32_t nparts, MsmLayout lay, const uint32_t* __restrict__ partial,
+    const uint32_t* __restrict__ btab, uint32_t* __restrict__ scal, int16_t* __restrict__ digits,
+    uint32_t* __restrict__ pts) {
     __shared__ unsigned long long col[256 * 9];
     unsigned long long s[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (uint32_t p = threadIdx.x; p < nparts; p += 256)
@@ -128,9 +133,12 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_bscalar(
             br = d >> 32;
         }
         for (int k = 0; k < 8; k++) scal[8 * n + k] = b[k];
+        const uint64_t np = 2 * n + 1;
+        msm_recode(b, lay, lay.nw, [&](int w, int d) { digits[(uint64_t)w * np + n] = (int16_t)d; });
     }
-    if (threadIdx.x < PRECOMP_ENTRY_WORDS)
-        pts[(size_t)PRECOMP_ENTRY_WORDS * n + threadIdx.x] = btab[PRECOMP_ENTRY_WORDS + threadIdx.x];  // 1*B
+    if (threadIdx.x < MSM_PT_WORDS)  // B's record from the basepoint table's entry 1 (= 1*B)
+        pts[(size_t)MSM_PT_WORDS * n + threadIdx.x] =
+            threadIdx.x < 30 ? btab[PRECOMP_ENTRY_WORDS + threadIdx.x] : 0u;
 }
 
 // Two lanes per signature in different waves (as k_ed_points): even waves decompress R_i into
@@ -147,21 +155,8 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_points(
     msm_load8(is_r ? sig + 64 * i : pk + 32 * i, w);
     ge_p3 P;
     const bool ok = ge_decompress(w, P);
-    store_affine_entry(pts + (size_t)PRECOMP_ENTRY_WORDS * (is_r ? n + 1 + i : i), P);
+    msm_store_point(pts + (size_t)MSM_PT_WORDS * (is_r ? n + 1 + i : i), P);
     if (!ok) atomicOr(fail, 2u);
-}
-
-// digits[w * np + j] for w < windows(j); np = 2n + 1
-extern "C" __global__ void __launch_bounds__(256) k_msm_recode(uint64_t n, MsmLayout lay,
-                                                               const uint32_t* __restrict__ scal,
-                                                               int16_t* __restrict__ digits) {
-    const uint64_t np = 2 * n + 1;
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= np) return;
-    uint32_t s[8];
-    msm_load8(reinterpret_cast<const uint8_t*>(scal + 8 * j), s);
-    const int nw = j <= n ? lay.nw : lay.nw_z;
-    msm_recode(s, lay, nw, [&](int w, int d) { digits[(uint64_t)w * np + j] = (int16_t)d; });
 }
 
 // points of window w: all 2n+1 below nw_z, else the prefix [0, n]
@@ -285,12 +280,17 @@ extern "C" __global__ void __launch_bounds__(256) k_scan_add(uint64_t len, uint3
 // written out: to bsum[key] if the key starts in this chunk (complete, or the key's first piece),
 // else to hpart[q] (a continuation from earlier chunks, completed by k_msm_fixup).  Every lane
 // does the same number of additions whatever the bucket sizes.
-__device__ __forceinline__ void msm_load_entry(const uint32_t* __restrict__ pts, uint32_t v, ge_precomp& q) {
-    const uint32_t* e = pts + (size_t)PRECOMP_ENTRY_WORDS * (v & ~MSM_NEG);
-    const bool neg = (v & MSM_NEG) != 0;
-    q.ypx = load_fe(e + (neg ? 10 : 0));
-    q.ymx = load_fe(e + (neg ? 0 : 10));
-    q.xy2d = load_fe(e + (neg ? 30 : 20));
+// one 128-byte record as eight 16-byte loads (affine Niels words 0..29)
+__device__ __forceinline__ void msm_load_raw(const uint32_t* __restrict__ pts, uint32_t v, uint32_t w[32]) {
+    const uint4* e = reinterpret_cast<const uint4*>(pts + (size_t)MSM_PT_WORDS * (v & ~MSM_NEG));
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint4 t = e[k];
+        w[4 * k] = t.x; w[4 * k + 1] = t.y; w[4 * k + 2] = t.z; w[4 * k + 3] = t.w;
+    }
+}
+__device__ __forceinline__ ge_precomp msm_point_of(const uint32_t w[32], uint32_t v) {
+    return msm_point_select(load_fe(w), load_fe(w + 10), load_fe(w + 20), (v & MSM_NEG) != 0);
 }
 
 extern "C" __global__ void __launch_bounds__(256) k_msm_bucket(
@@ -312,12 +312,15 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_bucket(
     uint32_t kend = key + 1 < nkeys ? kstart[key + 1] : E;
     bool head = kstart[key] < k0;
     ge_p3 acc = ge_p3_identity();
-    ge_precomp nxt;
-    msm_load_entry(pts, entries[k0], nxt);
+    uint32_t nv = entries[k0], nw[32];
+    msm_load_raw(pts, nv, nw);
 #pragma unroll 1
     for (uint32_t k = (uint32_t)k0; k < k1; k++) {
-        const ge_precomp cur = nxt;
-        if (k + 1 < k1) msm_load_entry(pts, entries[k + 1], nxt);
+        const ge_precomp cur = msm_point_of(nw, nv);
+        if (k + 1 < k1) {
+            nv = entries[k + 1];
+            msm_load_raw(pts, nv, nw);
+        }
         acc = ge_p1p1_to_p3(ge_madd(acc, cur));
         if (k + 1 == k1 || k + 1 == kend) {
             store_p3(head ? hpart + (size_t)P3_WORDS * (k0 / T) : bsum + (size_t)P3_WORDS * key, acc);
@@ -403,21 +406,74 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_window(MsmLayout lay, co
     if (g == 0) store_p3(wsum + (size_t)P3_WORDS * w, x);
 }
 
-// Horner over windows, [8], identity: *verdict = 1 iff accepted and nothing failed.  All 64
-// lanes run the same chain on a VGPR-laundered index so the compiler keeps it on the VALU
-// (a lone lane's uniform chain is otherwise scalarised onto the SALU with SGPR spills).
+// ---- the window Horner on a lane quad ----------------------------------------------------
+// The Horner over windows is one chain of ~241 doublings.  Each doubling's four squarings
+// (X^2, Y^2, Z^2, (X+Y)^2) and the three multiplies of its completed->projective step are
+// independent, so lane q of a quad computes the q-th one and the results are broadcast back with
+// DPP quad_perm moves: the chain issues 1 squaring + 1 multiply per doubling instead of 4 + 3.
+namespace {
+template <int SRC>
+__device__ __forceinline__ fe quad_bcast(const fe& a) {
+    constexpr int ctrl = SRC | (SRC << 2) | (SRC << 4) | (SRC << 6);
+    fe r;
+#pragma unroll
+    for (int i = 0; i < 10; i++) r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.v[i], ctrl, 0xF, 0xF, false);
+    return r;
+}
+__device__ __forceinline__ fe pick4(int q, const fe& a, const fe& b, const fe& c, const fe& d) {
+    return fe_select(fe_select(a, b, q == 1), fe_select(c, d, q == 3), q >= 2);
+}
+// r <- [2^k] r, every lane of the quad holding the whole point
+__device__ __forceinline__ ge_p2 quad_dbl_n(ge_p2 r, int k, int q) {
+#pragma unroll 1
+    for (int i = 0; i < k; i++) {
+        const fe sq = fe_sq(pick4(q, r.X, r.Y, r.Z, fe_add(r.X, r.Y)));
+        const fe XX = quad_bcast<0>(sq), YY = quad_bcast<1>(sq), ZZ = quad_bcast<2>(sq), S = quad_bcast<3>(sq);
+        const fe Y1 = fe_carry(fe_add(YY, XX));
+        const fe Z1 = fe_carry(fe_sub(YY, XX));
+        const fe X1 = fe_sub(S, Y1);
+        const fe T1 = fe_sub(fe_carry(fe_add(ZZ, ZZ)), Z1);
+        const fe m = fe_mul(pick4(q, X1, Y1, Z1, Z1), pick4(q, T1, Z1, T1, T1));
+        r.X = quad_bcast<0>(m);
+        r.Y = quad_bcast<1>(m);
+        r.Z = quad_bcast<2>(m);
+    }
+    return r;
+}
+// p (projective, Z != 0 representation of an extended point) + q (extended), result extended
+__device__ __forceinline__ ge_p3 quad_add(const ge_p3& p, const ge_p3& o, int q) {
+    const ge_cached c = ge_p3_to_cached(o);
+    // PP = (Y+X)(Y'+X'), MM = (Y-X)(Y'-X'), TT2d = T * 2dT', ZZ2 = Z * 2Z'
+    const fe m1 = fe_mul(pick4(q, fe_add(p.Y, p.X), fe_sub(p.Y, p.X), p.T, p.Z),
+                         pick4(q, c.YpX, c.YmX, c.T2d, c.Z2));
+    const fe PP = quad_bcast<0>(m1), MM = quad_bcast<1>(m1), TT = quad_bcast<2>(m1), ZZ = quad_bcast<3>(m1);
+    const fe X1 = fe_sub(PP, MM), Y1 = fe_add(PP, MM), Z1 = fe_add(ZZ, TT), T1 = fe_sub(ZZ, TT);
+    const fe m2 = fe_mul(pick4(q, X1, Y1, Z1, X1), pick4(q, T1, Z1, T1, Y1));
+    return ge_p3{quad_bcast<0>(m2), quad_bcast<1>(m2), quad_bcast<2>(m2), quad_bcast<3>(m2)};
+}
+}  // namespace
+
+// Horner over windows, [8], identity: *verdict = 1 iff accepted and nothing failed.  One wave;
+// every quad runs the same chain (lane 0 writes the verdict).
 extern "C" __global__ void __launch_bounds__(64) k_msm_final(MsmLayout lay, const uint32_t* __restrict__ wsum,
                                                              const uint32_t* __restrict__ fail,
                                                              uint32_t* __restrict__ verdict) {
-    uint32_t zero = 0;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
-    const uint32_t* ws = wsum + zero;
+    const int q = threadIdx.x & 3;
     const int nw = lay.nw;
-    ge_p3 d = load_p3(ws + (size_t)P3_WORDS * (nw - 1));
+    ge_p3 d = load_p3(wsum + (size_t)P3_WORDS * (nw - 1));
 #pragma unroll 1
     for (int w = nw - 2; w >= 0; w--) {
-        d = p3_dbl_n(d, lay.width[w]);
-        d = p3_add(d, load_p3(ws + (size_t)P3_WORDS * w));
+        ge_p2 r = quad_dbl_n(ge_p3_to_p2(d), lay.width[w] - 1, q);
+        // last doubling left completed, then -> extended (4 multiplies on the quad)
+        const fe sq = fe_sq(pick4(q, r.X, r.Y, r.Z, fe_add(r.X, r.Y)));
+        const fe XX = quad_bcast<0>(sq), YY = quad_bcast<1>(sq), ZZ = quad_bcast<2>(sq), S = quad_bcast<3>(sq);
+        const fe Y1 = fe_carry(fe_add(YY, XX));
+        const fe Z1 = fe_carry(fe_sub(YY, XX));
+        const fe X1 = fe_sub(S, Y1);
+        const fe T1 = fe_sub(fe_carry(fe_add(ZZ, ZZ)), Z1);
+        const fe m = fe_mul(pick4(q, X1, Y1, Z1, X1), pick4(q, T1, Z1, T1, Y1));
+        d = ge_p3{quad_bcast<0>(m), quad_bcast<1>(m), quad_bcast<2>(m), quad_bcast<3>(m)};
+        d = quad_add(d, load_p3(wsum + (size_t)P3_WORDS * w), q);
     }
     const bool ok = p3_mul8_is_identity(d) && *fail == 0;
     if (threadIdx.x == 0) *verdict = ok ? 1u : 0u;

@@ -186,7 +186,8 @@ MsmPlan msm_plan(size_t n) {
     p.wg_window = (uint32_t)std::min(256, 1 << (p.lay.cmax - 1));
     p.max_entries = (uint64_t)(n + 1) * p.lay.nw + (uint64_t)n * p.lay.nw_z;
     // ~4 waves per SIMD of bucket lanes (256 CUs x 4 SIMDs x 4 x 64), 8..64 entries each
-    p.seg = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, p.max_entries / (256 * 4 * 4 * 64)));
+    p.seg = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(16, p.max_entries / (256 * 4 * 4 * 64)));
+    if (const char* e = std::getenv("NWV_MSM_SEG")) p.seg = (uint32_t)std::max(1L, std::strtol(e, nullptr, 10));
     p.nseg = (p.max_entries + p.seg - 1) / p.seg;
     return p;
 }
@@ -196,7 +197,7 @@ int msm_alloc(EdBuffers& b, const MsmPlan& p, size_t n) {
     int rc;
     if ((rc = b.m_scal.ensure(32 * p.np + 32)) || (rc = b.m_partial.ensure(36 * nblk + 36)) ||
         (rc = b.m_state.ensure(64)) ||
-        (rc = b.m_pts.ensure((size_t)4 * PRECOMP_ENTRY_WORDS * p.np + 64)) ||
+        (rc = b.m_pts.ensure((size_t)4 * MSM_PT_WORDS * p.np + 64)) ||
         (rc = b.m_digits.ensure((size_t)2 * p.lay.nw * p.np + 64)) ||
         (rc = b.m_cnt.ensure((size_t)4 * p.cnt_len + 64)) ||
         (rc = b.m_tiles.ensure((size_t)4 * (p.ntiles + 1) + 64)) ||
@@ -209,13 +210,15 @@ int msm_alloc(EdBuffers& b, const MsmPlan& p, size_t n) {
     return NWV_OK;
 }
 
+static const char* const ED_KERNEL_NAMES[] = {"k_ed_hash", "k_ed_points", "k_ed_straus"};
 static const char* const MSM_KERNEL_NAMES[] = {
-    "k_msm_scalars", "k_msm_bscalar", "k_msm_points", "k_msm_recode", "k_msm_hist", "k_scan",
+    "k_msm_scalars", "k_msm_bscalar", "k_msm_points", "k_msm_hist", "k_scan",
     "k_msm_scatter", "k_msm_bucket+fixup", "k_msm_window", "k_msm_final"};
-constexpr int MSM_NKERNELS = 10;
+constexpr int MSM_NKERNELS = 9;
+constexpr int MSM_NEVENTS = MSM_NKERNELS + 1;  // one event before each kernel, one after the last
 
 // Launch the batch MSM on resident buffers; the verdict word (1 = batch accepted) is
-// m_state[1] (m_state[0] = failure flags).  ev: MSM_NKERNELS + 1 events or null.
+// m_state[1] (m_state[0] = failure flags).  ev: MSM_NEVENTS events or null.
 int msm_launch(Device& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStream_t stream,
                hipEvent_t* ev) {
     if (n == 0) return NWV_OK;
@@ -232,51 +235,47 @@ int msm_launch(Device& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipS
     };
     NWV_HIP(hipMemsetAsync(state, 0, 8, stream));
     if ((rc = mark(0))) return rc;
+    int16_t* digits = b.m_digits.as<int16_t>();
     hipLaunchKernelGGL(k_msm_scalars, dim3(nblk), dim3(256), 0, stream, (uint64_t)n, b.pk.as<uint8_t>(),
                        b.sig.as<uint8_t>(), b.msg.as<uint8_t>(), b.off.as<uint64_t>(), b.len.as<uint32_t>(),
-                       seed, b.m_scal.as<uint32_t>(), b.m_partial.as<uint32_t>(), state);
+                       seed, p.lay, b.m_scal.as<uint32_t>(), digits, b.m_partial.as<uint32_t>(), state);
     if ((rc = mark(1))) return rc;
-    hipLaunchKernelGGL(k_msm_bscalar, dim3(1), dim3(256), 0, stream, (uint64_t)n, (uint32_t)nblk,
-                       b.m_partial.as<uint32_t>(), d.btab.as<uint32_t>(), b.m_scal.as<uint32_t>(),
+    hipLaunchKernelGGL(k_msm_bscalar, dim3(1), dim3(256), 0, stream, (uint64_t)n, (uint32_t)nblk, p.lay,
+                       b.m_partial.as<uint32_t>(), d.btab.as<uint32_t>(), b.m_scal.as<uint32_t>(), digits,
                        b.m_pts.as<uint32_t>());
     if ((rc = mark(2))) return rc;
     const size_t waves = (n + 63) / 64;
     hipLaunchKernelGGL(k_msm_points, dim3((unsigned)((2 * 64 * waves + 255) / 256)), dim3(256), 0, stream,
                        (uint64_t)n, b.pk.as<uint8_t>(), b.sig.as<uint8_t>(), b.m_pts.as<uint32_t>(), state);
     if ((rc = mark(3))) return rc;
-    const dim3 gnp((unsigned)((p.np + 255) / 256));
-    int16_t* digits = b.m_digits.as<int16_t>();
-    const uint32_t* scal = b.m_scal.as<uint32_t>();
-    hipLaunchKernelGGL(k_msm_recode, gnp, dim3(256), 0, stream, (uint64_t)n, p.lay, scal, digits);
-    if ((rc = mark(4))) return rc;
     const dim3 gsort(p.chunks, (unsigned)p.lay.nw);
     const size_t lds_nb = (size_t)4 << (p.lay.cmax - 1);
     uint32_t* cnt = b.m_cnt.as<uint32_t>();
     uint32_t* tiles = b.m_tiles.as<uint32_t>();
     hipLaunchKernelGGL(k_msm_hist, gsort, dim3(256), lds_nb, stream, (uint64_t)n, p.lay, p.chunk_pts,
                        digits, cnt);
-    if ((rc = mark(5))) return rc;
+    if ((rc = mark(4))) return rc;
     hipLaunchKernelGGL(k_scan_tile, dim3(p.ntiles), dim3(256), 0, stream, p.cnt_len, cnt, tiles);
     hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, stream, p.ntiles, tiles);
     hipLaunchKernelGGL(k_scan_add, dim3((unsigned)((p.cnt_len + 255) / 256)), dim3(256), 0, stream,
                        p.cnt_len, cnt, tiles, p.chunks, b.m_kstart.as<uint32_t>());
-    if ((rc = mark(6))) return rc;
+    if ((rc = mark(5))) return rc;
     hipLaunchKernelGGL(k_msm_scatter, gsort, dim3(256), lds_nb, stream, (uint64_t)n, p.lay,
                        p.chunk_pts, digits, cnt, b.m_entries.as<uint32_t>());
-    if ((rc = mark(7))) return rc;
+    if ((rc = mark(6))) return rc;
     hipLaunchKernelGGL(k_msm_bucket, dim3((unsigned)((p.nseg + 255) / 256)), dim3(256), 0, stream, p.seg,
                        p.nkeys, tiles + p.ntiles, b.m_entries.as<uint32_t>(), b.m_kstart.as<uint32_t>(),
                        b.m_pts.as<uint32_t>(), b.m_bsum.as<uint32_t>(), b.m_hpart.as<uint32_t>());
     hipLaunchKernelGGL(k_msm_fixup, dim3((p.nkeys + 255) / 256), dim3(256), 0, stream, p.nkeys, p.chunks,
                        p.seg, cnt, tiles + p.ntiles, b.m_hpart.as<uint32_t>(), b.m_bsum.as<uint32_t>());
-    if ((rc = mark(8))) return rc;
+    if ((rc = mark(7))) return rc;
     hipLaunchKernelGGL(k_msm_window, dim3((unsigned)p.lay.nw), dim3(p.wg_window),
                        (size_t)4 * P3_WORDS * p.wg_window, stream, p.lay, b.m_bsum.as<uint32_t>(),
                        b.m_wsum.as<uint32_t>());
-    if ((rc = mark(9))) return rc;
+    if ((rc = mark(8))) return rc;
     hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, stream, p.lay, b.m_wsum.as<uint32_t>(),
                        state, state + 1);
-    if ((rc = mark(10))) return rc;
+    if ((rc = mark(9))) return rc;
     NWV_HIP(hipGetLastError());
     return NWV_OK;
 }
@@ -356,7 +355,7 @@ struct nwv_staged {
     EdBuffers buf;
     size_t n = 0;
     hipStream_t stream = nullptr;  // each resident batch runs on its own stream, so several
-    hipEvent_t ev[MSM_NKERNELS + 1] = {};  // staged batches on one device overlap
+    hipEvent_t ev[MSM_NEVENTS] = {};  // staged batches on one device overlap
     KernelLog log[2];              // [0] per-signature pipeline, [1] batch MSM
     int last_mode = -1;
     bool pending_timing = false;
@@ -466,11 +465,15 @@ int nwv_ed25519_verify_each(nwv_ctx* ctx, size_t n, const uint8_t* pk, const uin
 }
 
 // Batches of at least this many signatures go through the MSM (K5); smaller ones through the
-// per-signature pipeline, whose single-lane chain is shorter than the MSM's window Horner.
+// per-signature pipeline (tools/latency_sweep.py measures the crossover: the MSM's quad-lane
+// window Horner is shorter than the per-signature Straus chain already at small n).
+#ifndef NWV_MSM_MIN_N_DEFAULT
+#define NWV_MSM_MIN_N_DEFAULT 1
+#endif
 static size_t msm_min_n() {
     static const size_t v = [] {
         const char* e = std::getenv("NWV_MSM_MIN_N");
-        return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)4096;
+        return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)NWV_MSM_MIN_N_DEFAULT;
     }();
     return v;
 }
@@ -668,15 +671,18 @@ int nwv_stage_ed25519(nwv_ctx* ctx, int device_index, size_t n, const uint8_t* p
     return NWV_OK;
 }
 
-static const char* const ED_KERNEL_NAMES[] = {"k_ed_hash", "k_ed_points", "k_ed_straus"};
-
 static int staged_collect_times(nwv_staged* st) {
     if (!st->pending_timing) return NWV_OK;
-    const int k = st->last_mode == 1 ? MSM_NKERNELS : 3;
-    NWV_HIP(hipEventSynchronize(st->ev[k]));
     float t[MSM_NKERNELS];
-    for (int i = 0; i < k; i++) NWV_HIP(hipEventElapsedTime(&t[i], st->ev[i], st->ev[i + 1]));
-    st->log[st->last_mode].add(st->last_mode == 1 ? MSM_KERNEL_NAMES : ED_KERNEL_NAMES, t, k);
+    if (st->last_mode == 1) {
+        NWV_HIP(hipEventSynchronize(st->ev[MSM_NKERNELS]));
+        for (int i = 0; i < MSM_NKERNELS; i++) NWV_HIP(hipEventElapsedTime(&t[i], st->ev[i], st->ev[i + 1]));
+        st->log[1].add(MSM_KERNEL_NAMES, t, MSM_NKERNELS);
+    } else {
+        NWV_HIP(hipEventSynchronize(st->ev[3]));
+        for (int i = 0; i < 3; i++) NWV_HIP(hipEventElapsedTime(&t[i], st->ev[i], st->ev[i + 1]));
+        st->log[0].add(ED_KERNEL_NAMES, t, 3);
+    }
     st->pending_timing = false;
     return NWV_OK;
 }

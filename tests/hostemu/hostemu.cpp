@@ -169,7 +169,7 @@ int he_msm_batch(size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t*
     uint32_t seed[8];
     std::memcpy(seed, seed32, 32);
     const size_t np = 2 * n + 1;
-    std::vector<uint32_t> scal(8 * np, 0), pts(PRECOMP_ENTRY_WORDS * np);
+    std::vector<uint32_t> scal(8 * np, 0), pts(MSM_PT_WORDS * np);
     bool ok = true;
     unsigned long long col[9] = {0};
     for (size_t i = 0; i < n; i++) {
@@ -190,9 +190,9 @@ int he_msm_batch(size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t*
         }
         ge_p3 P;
         ok &= ge_decompress(Aw, P);
-        store_affine_entry(pts.data() + PRECOMP_ENTRY_WORDS * i, P);
+        msm_store_point(pts.data() + MSM_PT_WORDS * i, P);
         ok &= ge_decompress(Rw, P);
-        store_affine_entry(pts.data() + PRECOMP_ENTRY_WORDS * (n + 1 + i), P);
+        msm_store_point(pts.data() + MSM_PT_WORDS * (n + 1 + i), P);
     }
     {
         uint32_t x[16];
@@ -212,8 +212,7 @@ int he_msm_batch(size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t*
             scal[8 * n + t] = nz ? (uint32_t)d : 0u;
             br = d >> 32;
         }
-        std::memcpy(pts.data() + PRECOMP_ENTRY_WORDS * n, g_btab.data() + PRECOMP_ENTRY_WORDS,
-                    4 * PRECOMP_ENTRY_WORDS);
+        msm_point_from_precomp(pts.data() + MSM_PT_WORDS * n, g_btab.data() + PRECOMP_ENTRY_WORDS);
     }
     nwv_count_mul = nwv_count_sq = 0;
     const uint32_t nkeys = lay.kbase[lay.nw];
@@ -227,7 +226,7 @@ int he_msm_batch(size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t*
     for (size_t key = 0; key < nkeys; key++) {
         ge_p3 acc = ge_p3_identity();
         for (uint32_t v : buckets[key])
-            acc = ge_p1p1_to_p3(ge_madd_entry(acc, pts.data() + PRECOMP_ENTRY_WORDS * (v & ~MSM_NEG), (v & MSM_NEG) != 0));
+            acc = ge_p1p1_to_p3(ge_madd(acc, msm_load_point(pts.data() + MSM_PT_WORDS * (v & ~MSM_NEG), (v & MSM_NEG) != 0)));
         store_p3(bs.data() + P3_WORDS * key, acc);
     }
     for (int w = 0; w < lay.nw; w++) {
@@ -295,15 +294,15 @@ void he_msm_z(const uint8_t* seed32, uint64_t i, uint8_t* z32) {
 
 // field multiplies / squarings of k_msm_points per signature (decompress R and A, affine entry)
 void he_msm_point_counts(const uint8_t* pk, const uint8_t* sig, unsigned long long counts[2]) {
-    uint32_t Aw[8], Rw[8], e[PRECOMP_ENTRY_WORDS];
+    uint32_t Aw[8], Rw[8], e[MSM_PT_WORDS];
     words(pk, Aw);
     words(sig, Rw);
     nwv_count_mul = nwv_count_sq = 0;
     ge_p3 P;
     ge_decompress(Rw, P);
-    store_affine_entry(e, P);
+    msm_store_point(e, P);
     ge_decompress(Aw, P);
-    store_affine_entry(e, P);
+    msm_store_point(e, P);
     counts[0] = nwv_count_mul;
     counts[1] = nwv_count_sq;
 }

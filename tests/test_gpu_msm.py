@@ -110,4 +110,4 @@ def test_staged_msm_runs_and_times(eng):
     t = st.kernel_times(1)
     st.free()
     assert allv and bits.all()
-    assert len(t) == 10 and all(v > 0 for v in t.values())
+    assert len(t) == 9 and all(v > 0 for v in t.values())
