@@ -58,10 +58,13 @@ def valu_peak():
         return None
 
 
-def synth(eng, n, mlen, seed):
-    from narwhal_amd import _lib
+def synth(eng, n, mlen, seed, keys=0):
+    """n signatures over seeded random messages; keys > 0: signed by `keys` seeded keys in turn
+    (signature i by key i % keys), else every signature by its own key"""
     rng = np.random.default_rng(seed)
     seeds = rng.integers(0, 256, size=32 * n, dtype=np.uint8)
+    if keys:
+        seeds = np.tile(seeds[:32 * keys], (n + keys - 1) // keys)[:32 * n].copy()
     msgs = rng.integers(0, 256, size=n * mlen + 16, dtype=np.uint8)
     offs = np.arange(n, dtype=np.uint64) * mlen
     lens = np.full(n, mlen, dtype=np.uint32)
@@ -119,6 +122,9 @@ def main():
     ap.add_argument("--latency-reps", type=int, default=300)
     ap.add_argument("--inflight", type=int, default=3,
                     help="resident batches in flight on separate streams (step s runs batch s %% K)")
+    ap.add_argument("--keys", type=int, default=0,
+                    help="distinct verifying keys (0: one per signature, the configs[1] worst case; "
+                         "100: its committee variant, keyed batch MSM)")
     ap.add_argument("--single-steps", type=int, default=8,
                     help="single-stream steps timed after the run (step latency, per-kernel times)")
     args = ap.parse_args()
@@ -136,8 +142,13 @@ def main():
     from narwhal_amd import _lib
 
     eng = narwhal_amd.Engine(device=local)
-    pk, sg, msgs, offs, lens = synth(eng, args.n, args.msg_len, seed=1000 + rank)
-    stages = [eng.stage(pk, sg, msgs, offs, lens) for _ in range(max(1, args.inflight))]
+    pk, sg, msgs, offs, lens = synth(eng, args.n, args.msg_len, seed=1000 + rank, keys=args.keys)
+    if args.keys:
+        kidx = np.arange(args.n, dtype=np.uint32) % np.uint32(args.keys)
+        stages = [eng.stage_keyed(pk[:32 * args.keys].copy(), kidx, sg, msgs, offs, lens)
+                  for _ in range(max(1, args.inflight))]
+    else:
+        stages = [eng.stage(pk, sg, msgs, offs, lens) for _ in range(max(1, args.inflight))]
     seed = lambda s_: (bytes([(s_ * 7 + rank) % 256]) * 32)
 
     def sync_all():
@@ -251,6 +262,7 @@ def main():
                                    "(BASELINE.json configs[1]) per GPU",
                        "sigs_per_batch": args.n, "msg_len": args.msg_len,
                        "path": "batch MSM (K5)" if args.mode == 1 else "per-signature (K1-K4)",
+                       "distinct_keys": args.keys or args.n,
                        "parallelism": f"signature-index shards x{world}",
                        "inflight_batches": len(stages)},
             "single_stream": {"ms_per_step": float(np.median(single)),

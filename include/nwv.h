@@ -78,6 +78,17 @@ int nwv_ed25519_verify_batch(nwv_ctx* ctx, size_t n, const uint8_t* pk, const ui
                              const uint32_t* msg_len, const uint8_t seed32[32], int* all_valid,
                              uint64_t* verdict_bits_or_null);
 
+/* Batch verification with each verifying key given once: keys (n_keys x 32) and key_idx[n]
+ * (signature i is by keys[key_idx[i]]).  ed25519_consensus's batch verifier groups its entries
+ * by key the same way (one MSM point per distinct key with coefficient sum z_i k_i), so the
+ * device decompresses each distinct key once and carries one point per key instead of one per
+ * signature -- the committee case of Certificate::verify / validate_certificates.  Same verdict
+ * semantics and outputs as nwv_ed25519_verify_batch. */
+int nwv_ed25519_verify_batch_keyed(nwv_ctx* ctx, size_t n_keys, const uint8_t* keys, size_t n,
+                                   const uint32_t* key_idx, const uint8_t* sig, const uint8_t* msg_base,
+                                   const uint64_t* msg_off, const uint32_t* msg_len,
+                                   const uint8_t seed32[32], int* all_valid, uint64_t* verdict_bits_or_null);
+
 /* ---- fastcrypto 0.1.2 trait surface (Ed25519 scheme module; contract of
  *      crypto/src/bls12377/mod.rs:264-291 and :485-577) ---- */
 /* Verifier::verify(&self, msg, sig): NWV_OK or NWV_ERR_SIGNATURE */
@@ -122,6 +133,10 @@ typedef struct nwv_staged nwv_staged;
 int nwv_stage_ed25519(nwv_ctx* ctx, int device_index, size_t n, const uint8_t* pk,
                       const uint8_t* sig, const uint8_t* msg_base, const uint64_t* msg_off,
                       const uint32_t* msg_len, nwv_staged** out);
+/* keyed form (see nwv_ed25519_verify_batch_keyed): mode-1 runs carry one MSM point per key */
+int nwv_stage_ed25519_keyed(nwv_ctx* ctx, int device_index, size_t n_keys, const uint8_t* keys, size_t n,
+                            const uint32_t* key_idx, const uint8_t* sig, const uint8_t* msg_base,
+                            const uint64_t* msg_off, const uint32_t* msg_len, nwv_staged** out);
 /* mode 0: per-signature verdicts (K1-K4); mode 1: batch verdict through one Pippenger MSM (K5),
  * coefficients keyed by seed32 (NULL: OS entropy).  Asynchronous on the batch's own stream;
  * nwv_staged_sync waits.  Verdicts stay on the device until nwv_staged_fetch, which after a

@@ -61,6 +61,8 @@ def load():
         "nwv_blake2b256_many": ([_vp, _sz, _vp, _vp, _vp, _vp], _i32),
         "nwv_batch_digest_serialized": ([_vp, _sz, _vp, _vp, _vp, _vp, _vp], _i32),
         "nwv_stage_ed25519": ([_vp, _i32, _sz, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(_vp)], _i32),
+        "nwv_stage_ed25519_keyed": ([_vp, _i32, _sz, _vp, _sz, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(_vp)], _i32),
+        "nwv_ed25519_verify_batch_keyed": ([_vp, _sz, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i32),
         "nwv_staged_run": ([_vp, _i32, _vp], _i32),
         "nwv_staged_sync": ([_vp], _i32),
         "nwv_staged_fetch": ([_vp, _vp, ctypes.POINTER(_i32)], _i32),
@@ -159,6 +161,29 @@ class Engine:
                                                  _ptr(offs), _ptr(lens), seed, ctypes.byref(allv),
                                                  _ptr(bits) if want_bits else None))
         return bool(allv.value), (list(unpack_bits(bits, n)) if want_bits else None)
+
+    def verify_batch_keyed(self, keys, key_idx, sigs, msgs, seed=b"\x00" * 32, want_bits=True):
+        """keys: list of distinct 32-byte keys; key_idx[i]: key of signature i; sigs, msgs: per
+        signature -> (all_valid, per-signature verdicts or None)"""
+        n = len(sigs)
+        kb = np.frombuffer(b"".join(keys) or b"\0", dtype=np.uint8)
+        ki = np.asarray(key_idx, dtype=np.uint32)
+        sg = np.frombuffer(b"".join(sigs) or b"\0", dtype=np.uint8)
+        arena, offs, lens = pack_messages(list(msgs))
+        bits = np.zeros((n + 63) // 64 + 1, dtype=np.uint64)
+        allv = _i32(0)
+        _check(self.lib.nwv_ed25519_verify_batch_keyed(self._h, len(keys), _ptr(kb), n, _ptr(ki), _ptr(sg),
+                                                       _ptr(arena), _ptr(offs), _ptr(lens), seed,
+                                                       ctypes.byref(allv), _ptr(bits) if want_bits else None))
+        return bool(allv.value), (list(unpack_bits(bits, n)) if want_bits else None)
+
+    def stage_keyed(self, keys, key_idx, sig, arena, offs, lens, device_index=0):
+        """keys: uint8 [m*32]; key_idx: uint32 [n]; sig uint8 [n*64]"""
+        st = _vp()
+        m = len(keys) // 32
+        _check(self.lib.nwv_stage_ed25519_keyed(self._h, device_index, m, _ptr(keys), len(offs), _ptr(key_idx),
+                                                _ptr(sig), _ptr(arena), _ptr(offs), _ptr(lens), ctypes.byref(st)))
+        return Staged(self, st, len(offs))
 
     def sign_many(self, seeds, msgs):
         n = len(seeds)

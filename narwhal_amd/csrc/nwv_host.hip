@@ -72,11 +72,15 @@ struct EdBuffers {
     DevBuf pk, sig, msg, off, len, kbuf, flags, tables, verdict;
     DevBuf m_scal, m_partial, m_state, m_pts, m_digits, m_cnt, m_tiles, m_entries, m_kstart, m_hpart,
         m_bsum, m_wsum;
+    // keyed batches: distinct keys (m x 32), CSR of signatures by key, per-signature z_i k_i
+    DevBuf keys, koff, ksig, m_ascal;
+    size_t nkeys_distinct = 0;  // 0: every signature is its own A point
     void release() {
         for (DevBuf* b : {&pk, &sig, &msg, &off, &len, &kbuf, &flags, &tables, &verdict, &m_scal,
                           &m_partial, &m_state, &m_pts, &m_digits, &m_cnt, &m_tiles, &m_entries,
-                          &m_kstart, &m_hpart, &m_bsum, &m_wsum})
+                          &m_kstart, &m_hpart, &m_bsum, &m_wsum, &keys, &koff, &ksig, &m_ascal})
             b->release();
+        nkeys_distinct = 0;
     }
 };
 
@@ -153,25 +157,27 @@ int ed_launch(Device& d, EdBuffers& b, size_t n, hipStream_t stream, hipEvent_t*
 }
 
 // ------------------------------------------------------------------ batch MSM (K5) ------
-// Window layout and work decomposition of one batch MSM over np = 2n + 1 points.
+// Window layout and work decomposition of one batch MSM over np = na + 1 + n points (na A
+// points: n, or the m distinct keys of a keyed batch).
 struct MsmPlan {
     MsmLayout lay{};
     uint32_t chunk_pts = 0, chunks = 0, nkeys = 0, ntiles = 0, wg_window = 0;
     uint32_t seg = 0;  // entries per k_msm_bucket lane
-    uint64_t np = 0, cnt_len = 0, max_entries = 0, nseg = 0;
+    uint64_t np = 0, na = 0, cnt_len = 0, max_entries = 0, nseg = 0;
 };
 
 // Base width c minimises  7 Fmul x entries + 18 Fmul x buckets  (SURVEY.md §8d K5 cost model:
 // one mixed addition per nonzero digit, two full additions per bucket in the running-sum
 // reduction).
-MsmPlan msm_plan(size_t n) {
+MsmPlan msm_plan(size_t n, size_t na) {
     MsmPlan p;
-    p.np = 2 * (uint64_t)n + 1;
+    p.na = na;
+    p.np = (uint64_t)na + 1 + n;
     double best = 1e300;
     for (int c = 6; c <= 15; c++) {
         MsmLayout L;
         if (!msm_make_layout(c, L)) continue;
-        const double entries = (double)(n + 1) * L.nw + (double)n * L.nw_z;
+        const double entries = (double)(na + 1) * L.nw + (double)n * L.nw_z;
         const double cost = 7.0 * entries + 18.0 * L.kbase[L.nw];
         if (cost < best) {
             best = cost;
@@ -184,9 +190,9 @@ MsmPlan msm_plan(size_t n) {
     p.cnt_len = (uint64_t)p.nkeys * p.chunks;
     p.ntiles = (uint32_t)((p.cnt_len + 4095) / 4096);
     p.wg_window = (uint32_t)std::min(256, 1 << (p.lay.cmax - 1));
-    p.max_entries = (uint64_t)(n + 1) * p.lay.nw + (uint64_t)n * p.lay.nw_z;
-    // ~4 waves per SIMD of bucket lanes (256 CUs x 4 SIMDs x 4 x 64), 8..64 entries each
-    p.seg = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(16, p.max_entries / (256 * 4 * 4 * 64)));
+    p.max_entries = (uint64_t)(na + 1) * p.lay.nw + (uint64_t)n * p.lay.nw_z;
+    // ~2 waves per SIMD of bucket lanes (256 CUs x 4 SIMDs x 2 x 64), 8..64 entries each
+    p.seg = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, p.max_entries / (256 * 4 * 2 * 64)));
     if (const char* e = std::getenv("NWV_MSM_SEG")) p.seg = (uint32_t)std::max(1L, std::strtol(e, nullptr, 10));
     p.nseg = (p.max_entries + p.seg - 1) / p.seg;
     return p;
@@ -195,7 +201,7 @@ MsmPlan msm_plan(size_t n) {
 int msm_alloc(EdBuffers& b, const MsmPlan& p, size_t n) {
     const size_t nblk = (n + 255) / 256;
     int rc;
-    if ((rc = b.m_scal.ensure(32 * p.np + 32)) || (rc = b.m_partial.ensure(36 * nblk + 36)) ||
+    if ((rc = b.m_scal.ensure(64)) || (b.nkeys_distinct && (rc = b.m_ascal.ensure(32 * n + 32))) || (rc = b.m_partial.ensure(36 * nblk + 36)) ||
         (rc = b.m_state.ensure(64)) ||
         (rc = b.m_pts.ensure((size_t)4 * MSM_PT_WORDS * p.np + 64)) ||
         (rc = b.m_digits.ensure((size_t)2 * p.lay.nw * p.np + 64)) ||
@@ -222,7 +228,8 @@ constexpr int MSM_NEVENTS = MSM_NKERNELS + 1;  // one event before each kernel, 
 int msm_launch(Device& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStream_t stream,
                hipEvent_t* ev) {
     if (n == 0) return NWV_OK;
-    const MsmPlan p = msm_plan(n);
+    const size_t na = b.nkeys_distinct ? b.nkeys_distinct : n;
+    const MsmPlan p = msm_plan(n, na);
     int rc = msm_alloc(b, p, n);
     if (rc) return rc;
     MsmSeed seed;
@@ -236,23 +243,30 @@ int msm_launch(Device& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipS
     NWV_HIP(hipMemsetAsync(state, 0, 8, stream));
     if ((rc = mark(0))) return rc;
     int16_t* digits = b.m_digits.as<int16_t>();
-    hipLaunchKernelGGL(k_msm_scalars, dim3(nblk), dim3(256), 0, stream, (uint64_t)n, b.pk.as<uint8_t>(),
-                       b.sig.as<uint8_t>(), b.msg.as<uint8_t>(), b.off.as<uint64_t>(), b.len.as<uint32_t>(),
-                       seed, p.lay, b.m_scal.as<uint32_t>(), digits, b.m_partial.as<uint32_t>(), state);
+    const int keyed = b.nkeys_distinct ? 1 : 0;
+    hipLaunchKernelGGL(k_msm_scalars, dim3(nblk), dim3(256), 0, stream, (uint64_t)n, (uint64_t)na, keyed,
+                       b.pk.as<uint8_t>(), b.sig.as<uint8_t>(), b.msg.as<uint8_t>(), b.off.as<uint64_t>(),
+                       b.len.as<uint32_t>(), seed, p.lay, b.m_ascal.as<uint32_t>(), digits,
+                       b.m_partial.as<uint32_t>(), state);
+    if (keyed)
+        hipLaunchKernelGGL(k_msm_keysum, dim3((unsigned)na), dim3(256), 0, stream, (uint64_t)n, (uint64_t)na,
+                           p.lay, b.koff.as<uint32_t>(), b.ksig.as<uint32_t>(), b.m_ascal.as<uint32_t>(), digits);
     if ((rc = mark(1))) return rc;
-    hipLaunchKernelGGL(k_msm_bscalar, dim3(1), dim3(256), 0, stream, (uint64_t)n, (uint32_t)nblk, p.lay,
+    hipLaunchKernelGGL(k_msm_bscalar, dim3(1), dim3(256), 0, stream, (uint64_t)n, (uint64_t)na, (uint32_t)nblk,
+                       p.lay,
                        b.m_partial.as<uint32_t>(), d.btab.as<uint32_t>(), b.m_scal.as<uint32_t>(), digits,
                        b.m_pts.as<uint32_t>());
     if ((rc = mark(2))) return rc;
-    const size_t waves = (n + 63) / 64;
-    hipLaunchKernelGGL(k_msm_points, dim3((unsigned)((2 * 64 * waves + 255) / 256)), dim3(256), 0, stream,
-                       (uint64_t)n, b.pk.as<uint8_t>(), b.sig.as<uint8_t>(), b.m_pts.as<uint32_t>(), state);
+    const size_t waves = (n + 63) / 64 + (na + 63) / 64;
+    hipLaunchKernelGGL(k_msm_points, dim3((unsigned)((64 * waves + 255) / 256)), dim3(256), 0, stream,
+                       (uint64_t)n, (uint64_t)na, keyed ? b.keys.as<uint8_t>() : b.pk.as<uint8_t>(),
+                       b.sig.as<uint8_t>(), b.m_pts.as<uint32_t>(), state);
     if ((rc = mark(3))) return rc;
     const dim3 gsort(p.chunks, (unsigned)p.lay.nw);
     const size_t lds_nb = (size_t)4 << (p.lay.cmax - 1);
     uint32_t* cnt = b.m_cnt.as<uint32_t>();
     uint32_t* tiles = b.m_tiles.as<uint32_t>();
-    hipLaunchKernelGGL(k_msm_hist, gsort, dim3(256), lds_nb, stream, (uint64_t)n, p.lay, p.chunk_pts,
+    hipLaunchKernelGGL(k_msm_hist, gsort, dim3(256), lds_nb, stream, (uint64_t)n, (uint64_t)na, p.lay, p.chunk_pts,
                        digits, cnt);
     if ((rc = mark(4))) return rc;
     hipLaunchKernelGGL(k_scan_tile, dim3(p.ntiles), dim3(256), 0, stream, p.cnt_len, cnt, tiles);
@@ -260,7 +274,7 @@ int msm_launch(Device& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipS
     hipLaunchKernelGGL(k_scan_add, dim3((unsigned)((p.cnt_len + 255) / 256)), dim3(256), 0, stream,
                        p.cnt_len, cnt, tiles, p.chunks, b.m_kstart.as<uint32_t>());
     if ((rc = mark(5))) return rc;
-    hipLaunchKernelGGL(k_msm_scatter, gsort, dim3(256), lds_nb, stream, (uint64_t)n, p.lay,
+    hipLaunchKernelGGL(k_msm_scatter, gsort, dim3(256), lds_nb, stream, (uint64_t)n, (uint64_t)na, p.lay,
                        p.chunk_pts, digits, cnt, b.m_entries.as<uint32_t>());
     if ((rc = mark(6))) return rc;
     hipLaunchKernelGGL(k_msm_bucket, dim3((unsigned)((p.nseg + 255) / 256)), dim3(256), 0, stream, p.seg,
@@ -314,6 +328,48 @@ int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, c
     NWV_HIP(hipMemcpyAsync(b.off.p, off.data(), 8 * n, hipMemcpyHostToDevice, d.stream));
     NWV_HIP(hipMemcpyAsync(b.len.p, msg_len + lo, 4 * n, hipMemcpyHostToDevice, d.stream));
     NWV_HIP(hipStreamSynchronize(d.stream));  // `off` is a host temporary
+    b.nkeys_distinct = 0;
+    return NWV_OK;
+}
+
+// Keyed staging: signature i of [lo, hi) is by keys[key_idx[i]].  The distinct keys that occur
+// in the range are renumbered densely, uploaded with the CSR of signatures per key, and pk is
+// expanded per signature (the per-signature fallback reads it).
+int ed_stage_keyed(Device& d, EdBuffers& b, size_t lo, size_t hi, size_t n_keys, const uint8_t* keys,
+                   const uint32_t* key_idx, const uint8_t* sig, const uint8_t* msg_base,
+                   const uint64_t* msg_off, const uint32_t* msg_len) {
+    const size_t n = hi - lo;
+    std::vector<uint32_t> local(n_keys, UINT32_MAX), cnt;
+    std::vector<uint32_t> kid(n);
+    std::vector<uint8_t> klist, pk(32 * n + 16);
+    for (size_t i = 0; i < n; i++) {
+        const uint32_t g = key_idx[lo + i];
+        if (g >= n_keys) return set_err(NWV_ERR_ARG, "key index out of range");
+        if (local[g] == UINT32_MAX) {
+            local[g] = (uint32_t)cnt.size();
+            cnt.push_back(0);
+            klist.insert(klist.end(), keys + 32 * (size_t)g, keys + 32 * (size_t)g + 32);
+        }
+        kid[i] = local[g];
+        cnt[kid[i]]++;
+        std::memcpy(pk.data() + 32 * i, keys + 32 * (size_t)g, 32);
+    }
+    const size_t m = cnt.size();
+    std::vector<uint32_t> koff(m + 1, 0), ksig(n), cur;
+    for (size_t k = 0; k < m; k++) koff[k + 1] = koff[k] + cnt[k];
+    cur.assign(koff.begin(), koff.end() - 1);
+    for (size_t i = 0; i < n; i++) ksig[cur[kid[i]]++] = (uint32_t)i;
+    int rc = ed_stage(d, b, 0, n, pk.data(), sig + 64 * lo, msg_base, msg_off + lo, msg_len + lo);
+    if (rc) return rc;
+    if ((rc = b.keys.ensure(32 * m + 32)) || (rc = b.koff.ensure(4 * m + 8)) || (rc = b.ksig.ensure(4 * n + 8)))
+        return rc;
+    if (m) {
+        NWV_HIP(hipMemcpyAsync(b.keys.p, klist.data(), 32 * m, hipMemcpyHostToDevice, d.stream));
+        NWV_HIP(hipMemcpyAsync(b.koff.p, koff.data(), 4 * (m + 1), hipMemcpyHostToDevice, d.stream));
+    }
+    if (n) NWV_HIP(hipMemcpyAsync(b.ksig.p, ksig.data(), 4 * n, hipMemcpyHostToDevice, d.stream));
+    NWV_HIP(hipStreamSynchronize(d.stream));
+    b.nkeys_distinct = m;
     return NWV_OK;
 }
 
@@ -560,6 +616,35 @@ int nwv_ed25519_verify_batch(nwv_ctx* ctx, size_t n, const uint8_t* pk, const ui
     return rc;
 }
 
+int nwv_ed25519_verify_batch_keyed(nwv_ctx* ctx, size_t n_keys, const uint8_t* keys, size_t n,
+                                   const uint32_t* key_idx, const uint8_t* sig, const uint8_t* msg_base,
+                                   const uint64_t* msg_off, const uint32_t* msg_len,
+                                   const uint8_t seed32[32], int* all_valid, uint64_t* verdict_bits_or_null) {
+    if (!ctx || !all_valid || (n && (!keys || !key_idx || !sig || !msg_off || !msg_len)))
+        return set_err(NWV_ERR_ARG, "null argument");
+    *all_valid = 1;
+    if (n == 0) return NWV_OK;
+    for (size_t i = 0; i < n; i++)
+        if (msg_len[i] && !msg_base) return set_err(NWV_ERR_ARG, "null msg_base");
+    uint8_t seed[32];
+    fill_seed(seed32, seed);
+    std::mutex omu;
+    return for_shards(ctx, n, [&](Device& d, size_t lo, size_t hi) -> int {
+        int r = ed_stage_keyed(d, d.ed, lo, hi, n_keys, keys, key_idx, sig, msg_base, msg_off, msg_len);
+        if (r) return r;
+        uint8_t s2[32];
+        std::memcpy(s2, seed, 32);
+        for (int k = 0; k < 8; k++) s2[24 + k] ^= (uint8_t)((uint64_t)lo >> (8 * k));
+        int ok = 1;
+        r = batch_on_device(d, d.ed, hi - lo, s2, d.stream, &ok,
+                            verdict_bits_or_null ? verdict_bits_or_null + lo / 64 : nullptr);
+        if (r) return r;
+        std::lock_guard<std::mutex> g(omu);
+        if (!ok) *all_valid = 0;
+        return NWV_OK;
+    });
+}
+
 // ---- fastcrypto trait surface ---------------------------------------------------------
 int nwv_ed25519_pubkey_verify(nwv_ctx* ctx, const uint8_t pk[32], const uint8_t* msg,
                               size_t msg_len, const uint8_t sig[64]) {
@@ -645,9 +730,10 @@ int nwv_ed25519_aggregate_batch_verify(nwv_ctx* ctx, size_t n_aggs, const uint8_
 }
 
 // ---- staged (device-resident) batches ---------------------------------------------------
-int nwv_stage_ed25519(nwv_ctx* ctx, int device_index, size_t n, const uint8_t* pk,
-                      const uint8_t* sig, const uint8_t* msg_base, const uint64_t* msg_off,
-                      const uint32_t* msg_len, nwv_staged** out) {
+}  // extern "C"
+
+template <class StageFn>
+static int staged_create(nwv_ctx* ctx, int device_index, size_t n, nwv_staged** out, StageFn stage) {
     if (!ctx || !out || device_index < 0 || device_index >= (int)ctx->devs.size())
         return set_err(NWV_ERR_ARG, "bad context/device");
     *out = nullptr;
@@ -657,7 +743,7 @@ int nwv_stage_ed25519(nwv_ctx* ctx, int device_index, size_t n, const uint8_t* p
     st->n = n;
     std::lock_guard<std::mutex> g(st->dev->mu);
     int rc = with_device(*st->dev);
-    if (!rc) rc = ed_stage(*st->dev, st->buf, 0, n, pk, sig, msg_base, msg_off, msg_len);
+    if (!rc) rc = stage(*st->dev, st->buf);
     if (!rc && hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking) != hipSuccess)
         rc = set_err(NWV_ERR_HIP, "hipStreamCreate");
     for (auto& e : st->ev)
@@ -669,6 +755,25 @@ int nwv_stage_ed25519(nwv_ctx* ctx, int device_index, size_t n, const uint8_t* p
     }
     *out = st;
     return NWV_OK;
+}
+
+extern "C" {
+
+int nwv_stage_ed25519(nwv_ctx* ctx, int device_index, size_t n, const uint8_t* pk,
+                      const uint8_t* sig, const uint8_t* msg_base, const uint64_t* msg_off,
+                      const uint32_t* msg_len, nwv_staged** out) {
+    return staged_create(ctx, device_index, n, out, [&](Device& d, EdBuffers& b) {
+        return ed_stage(d, b, 0, n, pk, sig, msg_base, msg_off, msg_len);
+    });
+}
+
+int nwv_stage_ed25519_keyed(nwv_ctx* ctx, int device_index, size_t n_keys, const uint8_t* keys, size_t n,
+                            const uint32_t* key_idx, const uint8_t* sig, const uint8_t* msg_base,
+                            const uint64_t* msg_off, const uint32_t* msg_len, nwv_staged** out) {
+    if (n && (!keys || !key_idx || !sig || !msg_off || !msg_len)) return set_err(NWV_ERR_ARG, "null argument");
+    return staged_create(ctx, device_index, n, out, [&](Device& d, EdBuffers& b) {
+        return ed_stage_keyed(d, b, 0, n, n_keys, keys, key_idx, sig, msg_base, msg_off, msg_len);
+    });
 }
 
 static int staged_collect_times(nwv_staged* st) {

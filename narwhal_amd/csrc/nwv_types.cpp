@@ -57,13 +57,28 @@ struct DigestBatch {
     }
 };
 
-// Signatures of one call, verified as one batch (MSM; per-signature fallback when it rejects)
+long committee_index(const nwv_committee& c, const uint8_t* pk);
+
+// Signatures of one call, verified as one batch (MSM; per-signature fallback when it rejects).
+// Signers are committee members, so the batch is keyed by committee index
+// (nwv_ed25519_verify_batch_keyed): each member's key is decompressed once per call and carries
+// one MSM point however many of its signatures the call holds.
 struct SigBatch {
-    std::vector<uint8_t> pk, sig, msgs;
+    const nwv_committee* c;
+    std::vector<uint8_t> keys, sig, msgs;  // keys: the committee's, then any non-member signer
+    std::vector<uint32_t> kidx;
     std::vector<uint64_t> off;
     std::vector<uint32_t> len;
+    explicit SigBatch(const nwv_committee* cm) : c(cm) {
+        if (c && c->n) keys.assign(c->keys, c->keys + 32 * c->n);
+    }
     size_t add(const uint8_t* p, const uint8_t* s, const uint8_t* m, size_t mlen) {
-        put(pk, p, 32);
+        long k = c ? committee_index(*c, p) : -1;
+        if (k < 0) {
+            k = (long)(keys.size() / 32);
+            put(keys, p, 32);
+        }
+        kidx.push_back((uint32_t)k);
         put(sig, s, 64);
         off.push_back(msgs.size());
         len.push_back((uint32_t)mlen);
@@ -78,8 +93,8 @@ struct SigBatch {
         msgs.resize(msgs.size() + 16);
         std::vector<uint64_t> bits((n + 63) / 64 + 1, 0);
         int all = 0;
-        int rc = nwv_ed25519_verify_batch(ctx, n, pk.data(), sig.data(), msgs.data(), off.data(),
-                                          len.data(), nullptr, &all, bits.data());
+        int rc = nwv_ed25519_verify_batch_keyed(ctx, keys.size() / 32, keys.data(), n, kidx.data(), sig.data(),
+                                                msgs.data(), off.data(), len.data(), nullptr, &all, bits.data());
         if (rc) return rc;
         for (size_t i = 0; i < n; i++) ok[i] = (uint8_t)((bits[i >> 6] >> (i & 63)) & 1);
         return NWV_OK;
@@ -240,7 +255,7 @@ int nwv_header_verify_many(nwv_ctx* ctx, const nwv_committee* committee, size_t 
     std::vector<uint8_t> dig;
     int rc = db.run(ctx, dig);
     if (rc) return rc;
-    SigBatch sb;
+    SigBatch sb(&c);
     for (size_t i = 0; i < n; i++) results[i] = header_after_digest(h[i], plan[i], dig, &sb, plan[i]);
     std::vector<uint8_t> ok;
     if ((rc = sb.run(ctx, ok))) return rc;
@@ -262,7 +277,7 @@ int nwv_vote_verify_many(nwv_ctx* ctx, const nwv_committee* committee, size_t n,
     std::vector<uint8_t> dig(32 * n);
     int rc = n ? nwv_vote_digest_many(ctx, n, v, dig.data()) : NWV_OK;
     if (rc) return rc;
-    SigBatch sb;
+    SigBatch sb(&c);
     std::vector<long> sig(n, -1);
     for (size_t i = 0; i < n; i++) {
         if (v[i].epoch != c.epoch) results[i] = NWV_DAG_INVALID_EPOCH;
@@ -316,7 +331,7 @@ int nwv_certificate_verify_many(nwv_ctx* ctx, const nwv_committee* committee, si
     int rc = db.run(ctx, dig);
     if (rc) return rc;
     // phase 2: header verdicts, quorum, and the signature batch (header + aggregated)
-    SigBatch sb;
+    SigBatch sb(&c);
     std::vector<long> agg_first(n, -1), agg_count(n, 0);
     std::vector<int32_t> after_header(n, NWV_DAG_OK);
     for (size_t i = 0; i < n; i++) {

@@ -111,3 +111,72 @@ def test_staged_msm_runs_and_times(eng):
     st.free()
     assert allv and bits.all()
     assert len(t) == 9 and all(v > 0 for v in t.values())
+
+
+def _keyed(items):
+    keys, idx = [], {}
+    kidx = []
+    for pk, _, _ in items:
+        if pk not in idx:
+            idx[pk] = len(keys)
+            keys.append(pk)
+        kidx.append(idx[pk])
+    return keys, kidx
+
+
+@pytest.mark.parametrize("n,m", [(1, 1), (300, 4), (5000, 100), (20000, 7)])
+def test_keyed_batches_committee(eng, n, m):
+    """one MSM point per distinct key (configs[1] m = 100 variant, committee batches): valid
+    batches accept; one forged signature is pinpointed exactly"""
+    rnd = np.random.default_rng(n + m)
+    kseeds = [rnd.bytes(32) for _ in range(m)]
+    msgs = [rnd.bytes(32) for _ in range(n)]
+    pk, sg = eng.sign_many([kseeds[i % m] for i in range(n)], msgs)
+    items = [(pk[32 * i:32 * i + 32].tobytes(), sg[64 * i:64 * i + 64].tobytes(), msgs[i]) for i in range(n)]
+    keys, kidx = _keyed(items)
+    assert len(keys) == m
+    ok, bits = eng.verify_batch_keyed(keys, kidx, [s for _, s, _ in items], msgs, seed=b"\x03" * 32)
+    assert ok and all(bits)
+    bad = n // 2
+    s = bytearray(items[bad][1])
+    s[33] ^= 2
+    sigs = [x[1] for x in items]
+    sigs[bad] = bytes(s)
+    ok, bits = eng.verify_batch_keyed(keys, kidx, sigs, msgs)
+    assert not ok and [i for i in range(n) if not bits[i]] == [bad]
+
+
+def test_keyed_golden_and_bad_keys(eng):
+    """golden / ZIP-215 vectors (small-order, non-canonical and undecodable keys) keyed by their
+    raw key bytes: verdicts equal the oracle's, and an unused undecodable key changes nothing"""
+    g = of.load_golden("ed25519_vectors.json")["vectors"]
+    z = of.load_golden("zip215_small_order.json")["vectors"]
+    items = [_v(v) for v in g + z]
+    keys, kidx = _keyed(items)
+    want = [of.verify(*it) for it in items]
+    ok, bits = eng.verify_batch_keyed(keys, kidx, [s for _, s, _ in items], [m for _, _, m in items])
+    assert bits == want and ok == all(want)
+    good = [it for it, w in zip(items, want) if w]
+    keys, kidx = _keyed(good)
+    undecodable = bytes.fromhex("02" + "00" * 31)  # y = 2 is not on the curve
+    assert not of.lib().or_point_decompress_ok(undecodable)
+    ok, bits = eng.verify_batch_keyed(keys + [undecodable], kidx, [s for _, s, _ in good], [m for _, _, m in good])
+    assert ok and all(bits)
+
+
+def test_staged_keyed_msm(eng):
+    from narwhal_amd import _lib
+    rnd = np.random.default_rng(12)
+    m, n = 100, 8192
+    kseeds = [rnd.bytes(32) for _ in range(m)]
+    msgs = [rnd.bytes(512) for _ in range(n)]
+    pk, sg = eng.sign_many([kseeds[i % m] for i in range(n)], msgs)
+    keys = np.concatenate([pk[32 * i:32 * i + 32] for i in range(m)])
+    kidx = np.arange(n, dtype=np.uint32) % m
+    arena, offs, lens = _lib.pack_messages(msgs)
+    st = eng.stage_keyed(keys, kidx, sg, arena, offs, lens)
+    for r in range(2):
+        st.run(mode=1, seed=bytes([r + 1]) * 32)
+    allv, bits = st.fetch()
+    st.free()
+    assert allv and bits.all()
