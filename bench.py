@@ -182,7 +182,7 @@ def main():
     single = []
     for s in range(args.single_steps):
         ts = time.perf_counter()
-        st.run(mode=args.mode, seed=seed(1000 + s))
+        st.run(mode=args.mode, seed=seed(1000 + s), timed=True)
         st.sync()
         single.append((time.perf_counter() - ts) * 1e3)
     kt = st.kernel_times(args.mode, reset=True)

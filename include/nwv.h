@@ -142,6 +142,10 @@ int nwv_stage_ed25519_keyed(nwv_ctx* ctx, int device_index, size_t n_keys, const
  * nwv_staged_sync waits.  Verdicts stay on the device until nwv_staged_fetch, which after a
  * rejected mode-1 run also runs the per-signature fallback (exact bad indices). */
 int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]);
+/* or-ed into nwv_staged_run's mode: launch kernel by kernel with HIP events around each one
+ * (feeds nwv_staged_kernel_times).  Untimed mode-1 runs replay a HIP graph of the batch MSM
+ * captured on the batch's second run. */
+#define NWV_RUN_TIMED 0x100
 int nwv_staged_sync(nwv_staged* st);
 int nwv_staged_fetch(nwv_staged* st, uint64_t* verdict_bits, int* all_valid);
 /* average device time (ms) per run of each pipeline kernel since the last reset, measured

@@ -23,6 +23,7 @@ NWV_ERR_EMPTY = -5
 NWV_ERR_LENGTH = -6
 NWV_FLAG_MSM_ALWAYS = 1
 NWV_FLAG_MSM_NEVER = 2
+NWV_RUN_TIMED = 0x100
 
 
 class NwvError(RuntimeError):
@@ -243,8 +244,10 @@ class Staged:
     def __init__(self, eng, h, n):
         self.eng, self._h, self.n = eng, h, n
 
-    def run(self, mode=0, seed=b"\x00" * 32):
-        _check(self.eng.lib.nwv_staged_run(self._h, mode, seed))
+    def run(self, mode=0, seed=b"\x00" * 32, timed=False):
+        """mode 0 per-signature pipeline, 1 batch MSM (graph replay); timed: kernel-by-kernel
+        launches bracketed by HIP events (feeds kernel_ms / kernel_times)"""
+        _check(self.eng.lib.nwv_staged_run(self._h, mode | (NWV_RUN_TIMED if timed else 0), seed))
 
     def sync(self):
         _check(self.eng.lib.nwv_staged_sync(self._h))

@@ -25,10 +25,6 @@
 
 using namespace nwv;
 
-struct MsmSeed {
-    uint32_t w[8];
-};
-
 namespace {
 
 __device__ __forceinline__ void msm_load8(const uint8_t* p, uint32_t w[8]) {
@@ -51,7 +47,8 @@ __device__ __forceinline__ void msm_store8(uint32_t* p, const uint32_t w[8]) {
 extern "C" __global__ void __launch_bounds__(256) k_msm_scalars(
     uint64_t n, uint64_t na, int keyed, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
     const uint8_t* __restrict__ msg, const uint64_t* __restrict__ msg_off,
-    const uint32_t* __restrict__ msg_len, MsmSeed seed, MsmLayout lay, uint32_t* __restrict__ ascal,
+    const uint32_t* __restrict__ msg_len, const uint32_t* __restrict__ seedp, MsmLayout lay,
+    uint32_t* __restrict__ ascal,
     int16_t* __restrict__ digits, uint32_t* __restrict__ partial, uint32_t* __restrict__ fail) {
     __shared__ uint32_t zs_lds[256 * 9];
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -63,7 +60,10 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_scalars(
         msm_load8(sig + 64 * i + 32, Sw);
         const uint32_t f = lane_hash(Aw, Rw, Sw, msg + msg_off[i], msg_len[i], k);
         if (f != FLAG_S_OK) atomicOr(fail, 1u);
-        msm_z(seed.w, i, z);
+        uint32_t sd[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) sd[k] = seedp[k];
+        msm_z(sd, i, z);
         sc_mul(z, k, a);
         sc_mul(z, Sw, zs);
         // signed digits straight from registers (window-major rows): R_i always; A_i's scalar

@@ -202,7 +202,7 @@ int msm_alloc(EdBuffers& b, const MsmPlan& p, size_t n) {
     const size_t nblk = (n + 255) / 256;
     int rc;
     if ((rc = b.m_scal.ensure(64)) || (b.nkeys_distinct && (rc = b.m_ascal.ensure(32 * n + 32))) || (rc = b.m_partial.ensure(36 * nblk + 36)) ||
-        (rc = b.m_state.ensure(64)) ||
+        (rc = b.m_state.ensure(128)) ||
         (rc = b.m_pts.ensure((size_t)4 * MSM_PT_WORDS * p.np + 64)) ||
         (rc = b.m_digits.ensure((size_t)2 * p.lay.nw * p.np + 64)) ||
         (rc = b.m_cnt.ensure((size_t)4 * p.cnt_len + 64)) ||
@@ -232,9 +232,8 @@ int msm_launch(Device& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipS
     const MsmPlan p = msm_plan(n, na);
     int rc = msm_alloc(b, p, n);
     if (rc) return rc;
-    MsmSeed seed;
-    std::memcpy(seed.w, seed32, 32);
-    uint32_t* state = b.m_state.as<uint32_t>();
+    uint32_t* state = b.m_state.as<uint32_t>();  // [0] fail flags, [1] verdict, [8..16) seed
+    if (seed32) NWV_HIP(hipMemcpyAsync(state + 8, seed32, 32, hipMemcpyHostToDevice, stream));
     const unsigned nblk = (unsigned)((n + 255) / 256);
     auto mark = [&](int k) -> int {
         if (ev) NWV_HIP(hipEventRecord(ev[k], stream));
@@ -246,7 +245,7 @@ int msm_launch(Device& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipS
     const int keyed = b.nkeys_distinct ? 1 : 0;
     hipLaunchKernelGGL(k_msm_scalars, dim3(nblk), dim3(256), 0, stream, (uint64_t)n, (uint64_t)na, keyed,
                        b.pk.as<uint8_t>(), b.sig.as<uint8_t>(), b.msg.as<uint8_t>(), b.off.as<uint64_t>(),
-                       b.len.as<uint32_t>(), seed, p.lay, b.m_ascal.as<uint32_t>(), digits,
+                       b.len.as<uint32_t>(), state + 8, p.lay, b.m_ascal.as<uint32_t>(), digits,
                        b.m_partial.as<uint32_t>(), state);
     if (keyed)
         hipLaunchKernelGGL(k_msm_keysum, dim3((unsigned)na), dim3(256), 0, stream, (uint64_t)n, (uint64_t)na,
@@ -415,6 +414,8 @@ struct nwv_staged {
     KernelLog log[2];              // [0] per-signature pipeline, [1] batch MSM
     int last_mode = -1;
     bool pending_timing = false;
+    hipGraphExec_t graph = nullptr;  // captured batch MSM (mode 1)
+    bool graph_failed = false;
 };
 
 // Shard [0, n) into contiguous, 64-aligned ranges over the context's devices and run fn(dev,
@@ -792,7 +793,27 @@ static int staged_collect_times(nwv_staged* st) {
     return NWV_OK;
 }
 
+// Capture the batch MSM of a staged batch once into a HIP graph (buffers and plan are fixed for
+// the batch; the per-run seed lives in device memory), so a run is one seed copy + one graph
+// launch instead of ~13 kernel launches.
+static int staged_graph(nwv_staged* st, Device& d) {
+    if (st->graph || st->graph_failed) return NWV_OK;
+    hipGraph_t g = nullptr;
+    NWV_HIP(hipStreamBeginCapture(st->stream, hipStreamCaptureModeThreadLocal));
+    const int rc = msm_launch(d, st->buf, st->n, nullptr, st->stream, nullptr);
+    const hipError_t e = hipStreamEndCapture(st->stream, &g);
+    if (rc || e != hipSuccess || !g || hipGraphInstantiate(&st->graph, g, nullptr, nullptr, 0) != hipSuccess) {
+        st->graph = nullptr;
+        st->graph_failed = true;  // replay through direct launches
+        (void)hipGetLastError();
+    }
+    if (g) (void)hipGraphDestroy(g);
+    return NWV_OK;
+}
+
 int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]) {
+    const bool timed = (mode & NWV_RUN_TIMED) != 0;
+    mode &= ~NWV_RUN_TIMED;
     if (!st || (mode != 0 && mode != 1)) return set_err(NWV_ERR_ARG, "bad staged/mode");
     Device& d = *st->dev;
     std::lock_guard<std::mutex> g(d.mu);
@@ -802,13 +823,21 @@ int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]) {
     if (mode == 1) {
         uint8_t seed[32];
         fill_seed(seed32, seed);
-        rc = msm_launch(d, st->buf, st->n, seed, st->stream, st->ev);
+        if (!timed && st->buf.m_state.p && st->n) {  // buffers exist: replay the captured graph
+            if ((rc = staged_graph(st, d))) return rc;
+        }
+        if (!timed && st->graph) {
+            NWV_HIP(hipMemcpyAsync(st->buf.m_state.as<uint32_t>() + 8, seed, 32, hipMemcpyHostToDevice, st->stream));
+            NWV_HIP(hipGraphLaunch(st->graph, st->stream));
+        } else {
+            rc = msm_launch(d, st->buf, st->n, seed, st->stream, timed ? st->ev : nullptr);
+        }
     } else {
-        rc = ed_launch(d, st->buf, st->n, st->stream, st->ev);
+        rc = ed_launch(d, st->buf, st->n, st->stream, timed ? st->ev : nullptr);
     }
     if (rc) return rc;
     st->last_mode = mode;
-    st->pending_timing = st->n > 0;
+    st->pending_timing = timed && st->n > 0;
     return NWV_OK;
 }
 
@@ -887,6 +916,7 @@ void nwv_staged_free(nwv_staged* st) {
         std::lock_guard<std::mutex> g(st->dev->mu);
         (void)hipSetDevice(st->dev->ordinal);
         if (st->stream) (void)hipStreamSynchronize(st->stream);
+        if (st->graph) (void)hipGraphExecDestroy(st->graph);
         st->buf.release();
         for (auto& e : st->ev)
             if (e) (void)hipEventDestroy(e);

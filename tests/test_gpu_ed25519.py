@@ -159,7 +159,7 @@ def test_staged_resident_batch(eng):
     arena, offs, lens = _lib.pack_messages(msgs)
     st = eng.stage(pk, sg, arena, offs, lens)
     for _ in range(3):
-        st.run(mode=0)
+        st.run(mode=0, timed=True)
     allv, bits = st.fetch()
     ms = st.kernel_ms()
     st.free()

@@ -105,12 +105,34 @@ def test_staged_msm_runs_and_times(eng):
     pk, sg, arena, offs, lens = _lib.soa(items)
     st = eng.stage(pk, sg, arena, offs, lens)
     for r in range(3):
-        st.run(mode=1, seed=bytes([r]) * 32)
+        st.run(mode=1, seed=bytes([r]) * 32, timed=True)
     allv, bits = st.fetch()
     t = st.kernel_times(1)
     st.free()
     assert allv and bits.all()
     assert len(t) == 9 and all(v > 0 for v in t.values())
+
+
+def test_staged_graph_replay_valid_and_invalid(eng):
+    """untimed mode-1 runs replay a captured HIP graph with a fresh seed each time: verdicts stay
+    exact for a valid batch and for one with a forged signature (fallback after fetch)"""
+    from narwhal_amd import _lib
+    items = _synthetic(eng, 3000, 64, seed=21)
+    pk, sg, arena, offs, lens = _lib.soa(items)
+    st = eng.stage(pk, sg, arena, offs, lens)
+    for r in range(5):
+        st.run(mode=1, seed=bytes([r + 9]) * 32)
+        allv, bits = st.fetch()
+        assert allv and bits.all()
+    st.free()
+    sg2 = sg.copy()
+    sg2[64 * 1234 + 50] ^= 8
+    st = eng.stage(pk, sg2, arena, offs, lens)
+    for r in range(4):
+        st.run(mode=1, seed=bytes([r + 1]) * 32)
+        allv, bits = st.fetch()
+        assert not allv and list(np.flatnonzero(~bits)) == [1234]
+    st.free()
 
 
 def _keyed(items):

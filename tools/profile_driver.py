@@ -25,7 +25,7 @@ def main():
     pk, sg, msgs, offs, lens = bench.synth(eng, args.n, args.msg_len, seed=7)
     st = eng.stage(pk, sg, msgs, offs, lens)
     for r in range(args.reps):
-        st.run(mode=args.mode, seed=bytes([r + 1]) * 32)
+        st.run(mode=args.mode, seed=bytes([r + 1]) * 32, timed=True)
     allv, bits = st.fetch()
     ms = st.kernel_times(args.mode)
     st.free()
