@@ -823,14 +823,14 @@ int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]) {
     if (mode == 1) {
         uint8_t seed[32];
         fill_seed(seed32, seed);
-        if (!timed && st->buf.m_state.p && st->n) {  // buffers exist: replay the captured graph
-            if ((rc = staged_graph(st, d))) return rc;
-        }
         if (!timed && st->graph) {
             NWV_HIP(hipMemcpyAsync(st->buf.m_state.as<uint32_t>() + 8, seed, 32, hipMemcpyHostToDevice, st->stream));
             NWV_HIP(hipGraphLaunch(st->graph, st->stream));
         } else {
+            // first run of the batch (allocates its buffers) or a timed run; an untimed first run
+            // also captures the graph the later runs replay
             rc = msm_launch(d, st->buf, st->n, seed, st->stream, timed ? st->ev : nullptr);
+            if (!rc && !timed && st->n) rc = staged_graph(st, d);
         }
     } else {
         rc = ed_launch(d, st->buf, st->n, st->stream, timed ? st->ev : nullptr);

@@ -67,6 +67,9 @@ def main():
         st.run(mode=1, seed=bytes([r + 2]) * 32)
     st.sync()
     dt = time.perf_counter() - t0
+    st.kernel_times(1, reset=True)
+    st.run(mode=1, seed=b"\x09" * 32, timed=True)  # one kernel-by-kernel pass for the breakdown
+    st.sync()
     kt = st.kernel_times(1)
     st.free()
     if dist is not None:
