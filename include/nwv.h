@@ -144,7 +144,7 @@ int nwv_stage_ed25519_keyed(nwv_ctx* ctx, int device_index, size_t n_keys, const
 int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]);
 /* or-ed into nwv_staged_run's mode: launch kernel by kernel with HIP events around each one
  * (feeds nwv_staged_kernel_times).  Untimed mode-1 runs replay a HIP graph of the batch MSM
- * captured on the batch's second run. */
+ * captured on the batch's first untimed run. */
 #define NWV_RUN_TIMED 0x100
 int nwv_staged_sync(nwv_staged* st);
 int nwv_staged_fetch(nwv_staged* st, uint64_t* verdict_bits, int* all_valid);
@@ -155,8 +155,8 @@ int nwv_staged_kernel_ms(nwv_staged* st, double avg_ms[3], int reset);
 /* per-kernel average device time (ms) of mode `mode` runs since the last reset: fills up to
  * cap (name, ms) pairs in launch order (names point to static strings) and returns the number
  * of kernels in that pipeline (< 0 on error).  mode 1 (batch MSM, K5) kernels:
- * k_msm_scalars, k_msm_bscalar, k_msm_points, k_msm_recode, k_msm_hist, k_scan,
- * k_msm_scatter, k_msm_bucket, k_msm_window, k_msm_final */
+ * k_msm_scalars, k_msm_bscalar, k_msm_points, k_msm_hist, k_scan, k_msm_scatter,
+ * k_msm_bucket+fixup, k_msm_window, k_msm_final (k_msm_keysum is timed with k_msm_scalars) */
 int nwv_staged_kernel_times(nwv_staged* st, int mode, int cap, const char** names, double* avg_ms,
                             int reset);
 void nwv_staged_free(nwv_staged* st);
