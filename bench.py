@@ -91,6 +91,47 @@ def cpu_baseline(pk, sg, msgs, offs, lens, seconds):
                       f"oracle/nwv_oracle.c batch verifier: Pippenger/Straus as dalek)"}
 
 
+def roofline_entry(kname, kt, mads_launch, peak_t, algorithmic):
+    kms = float(kt.get(kname, 0.0))
+    achieved = mads_launch / (kms * 1e-3) / 1e12 if kms > 0 else None
+    traffic = pmc_traffic(kname)
+    return {
+        "bound": "valu",
+        "kernel": kname,
+        "achieved": achieved,
+        "peak": peak_t,
+        "unit": "T v_mad_u64_u32/s",
+        "frac": (achieved / peak_t) if (peak_t and achieved) else None,
+        "traffic": traffic["bytes"] if traffic else None,
+        "traffic_source": traffic,
+        "algorithmic": algorithmic,
+    }
+
+
+def split_prep_times(args, pk, sg, msgs, offs, lens, reps=5):
+    """per-kernel times of the same batch with hashing and decompression as separate kernels"""
+    import narwhal_amd
+    from narwhal_amd import _lib
+    e = narwhal_amd.Engine(device=0, flags=_lib.NWV_FLAG_MSM_SPLIT_PREP)
+    try:
+        if args.keys:
+            kidx = (np.arange(args.n) % args.keys).astype(np.uint32)
+            st = e.stage_keyed(pk[:32 * args.keys].copy(), kidx, sg, msgs, offs, lens)
+        else:
+            st = e.stage(pk, sg, msgs, offs, lens)
+        st.run(mode=1, seed=b"\x11" * 32, timed=True)
+        st.sync()
+        st.kernel_times(1, reset=True)
+        for r in range(reps):
+            st.run(mode=1, seed=bytes([r + 1]) * 32, timed=True)
+        kt = st.kernel_times(1, reset=True)
+        assert st.fetch()[0]
+        st.free()
+        return kt
+    finally:
+        e.close()
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc pass (FETCH_SIZE
     doubled for gfx950's half-counted wide reads + WRITE_SIZE, MI355X_MICROARCH.md HBM section),
@@ -221,27 +262,28 @@ def main():
         lat = np.array(lat)
         peak = valu_peak()
         peak_t = (peak["v_mad_u64_u32_per_s"] / 1e12) if peak else None
+        npts = args.n + (args.keys or args.n)  # decompressed points: R_i and the A points
         if args.mode == 1:
-            kname, ops = "k_msm_points", OPS_MSM_POINTS
+            # k_msm_prep = SHA-512 challenge hashing + decompression in one grid; only the
+            # decompression's multiply-adds are counted (the hash is add/rotate work), so this
+            # is a lower bound on the kernel's VALU use
+            roof = roofline_entry("k_msm_prep", kt, mads(OPS_MSM_POINTS) // 2 * npts, peak_t,
+                                  f"{mads(OPS_MSM_POINTS) // 2} multiply-adds/point (decompression: "
+                                  f"{OPS_MSM_POINTS[0] // 2} mul x 100 + {OPS_MSM_POINTS[1] // 2} sq x 55) x "
+                                  f"{npts} points per launch; the SHA-512 hashing in the same grid "
+                                  "is not counted")
+            roof["kernel_ms"] = kt
+            kt_split = split_prep_times(args, pk, sg, msgs, offs, lens)
+            roof["decompression_alone"] = roofline_entry(
+                "k_msm_points", kt_split, mads(OPS_MSM_POINTS) // 2 * npts, peak_t,
+                "same multiply-adds, k_msm_points launched on its own (NWV_FLAG_MSM_SPLIT_PREP, "
+                "single stream, timed pass)")
+            roof["decompression_alone"]["kernel_ms"] = kt_split
         else:
-            kname, ops = "k_ed_straus", OPS_STRAUS
-        kms = float(kt.get(kname, 0.0))
-        mads_launch = mads(ops) * args.n
-        achieved = mads_launch / (kms * 1e-3) / 1e12 if kms > 0 else None
-        traffic = pmc_traffic(kname)
-        roof = {
-            "bound": "valu",
-            "kernel": kname,
-            "achieved": achieved,
-            "peak": peak_t,
-            "unit": "T v_mad_u64_u32/s",
-            "frac": (achieved / peak_t) if (peak_t and achieved) else None,
-            "traffic": traffic["bytes"] if traffic else None,
-            "traffic_source": traffic,
-            "algorithmic": f"{mads(ops)} multiply-adds/signature ({ops[0]} mul x 100 + {ops[1]} sq x 55) "
-                           f"x {args.n} signatures per launch",
-            "kernel_ms": kt,
-        }
+            roof = roofline_entry("k_ed_straus", kt, mads(OPS_STRAUS) * args.n, peak_t,
+                                  f"{mads(OPS_STRAUS)} multiply-adds/signature ({OPS_STRAUS[0]} mul x 100 + "
+                                  f"{OPS_STRAUS[1]} sq x 55) x {args.n} signatures per launch")
+            roof["kernel_ms"] = kt
         cpu = None
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(pk, sg, msgs, offs, lens, args.cpu_seconds)

@@ -41,6 +41,9 @@ typedef struct nwv_ctx nwv_ctx;
  * below which the per-signature pipeline runs); these force one or the other. */
 #define NWV_FLAG_MSM_ALWAYS 1u
 #define NWV_FLAG_MSM_NEVER 2u
+/* diagnostic: launch the MSM's hashing (k_msm_scalars) and decompression (k_msm_points) as two
+ * kernels instead of one k_msm_prep grid (per-kernel timing of the decompression alone) */
+#define NWV_FLAG_MSM_SPLIT_PREP 4u
 
 /* ------------------------------------------------------------------ lifecycle ----- */
 /* Process-wide context creation (created once, in Primary::spawn).
@@ -155,8 +158,9 @@ int nwv_staged_kernel_ms(nwv_staged* st, double avg_ms[3], int reset);
 /* per-kernel average device time (ms) of mode `mode` runs since the last reset: fills up to
  * cap (name, ms) pairs in launch order (names point to static strings) and returns the number
  * of kernels in that pipeline (< 0 on error).  mode 1 (batch MSM, K5) kernels:
- * k_msm_scalars, k_msm_bscalar, k_msm_points, k_msm_hist, k_scan, k_msm_scatter,
- * k_msm_bucket+fixup, k_msm_window, k_msm_final (k_msm_keysum is timed with k_msm_scalars) */
+ * k_msm_prep (hash + decompression), k_msm_bscalar, k_msm_hist, k_scan, k_msm_scatter,
+ * k_msm_bucket+fixup, k_msm_window, k_msm_final; k_msm_keysum is timed with k_msm_prep.
+ * Under NWV_FLAG_MSM_SPLIT_PREP k_msm_prep is split into k_msm_scalars and k_msm_points. */
 int nwv_staged_kernel_times(nwv_staged* st, int mode, int cap, const char** names, double* avg_ms,
                             int reset);
 void nwv_staged_free(nwv_staged* st);

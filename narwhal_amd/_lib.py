@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libnwv.so")
+# NWV_LIB selects an in-tree build variant (e.g. lib/libnwv_exp.so) for A/B measurements
+LIB_PATH = os.path.join(_HERE, "lib", os.environ.get("NWV_LIB", "libnwv.so"))
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "nwv.h")
 
 NWV_OK = 0
@@ -23,6 +24,7 @@ NWV_ERR_EMPTY = -5
 NWV_ERR_LENGTH = -6
 NWV_FLAG_MSM_ALWAYS = 1
 NWV_FLAG_MSM_NEVER = 2
+NWV_FLAG_MSM_SPLIT_PREP = 4
 NWV_RUN_TIMED = 0x100
 
 

@@ -44,21 +44,46 @@ __device__ __forceinline__ void msm_store8(uint32_t* p, const uint32_t w[8]) {
 // digits: [window][na+1+n] signed digits of every point's scalar (A points at [0, na), B's
 // entry na written by k_msm_bscalar, R_i at na+1+i); partial: gridDim.x x 9 words (sum of z_i s_i over the workgroup, as a
 // plain 288-bit integer); fail: bit 0 set when any s_i >= l
-extern "C" __global__ void __launch_bounds__(256) k_msm_scalars(
-    uint64_t n, uint64_t na, int keyed, const uint8_t* __restrict__ pk, const uint8_t* __restrict__ sig,
-    const uint8_t* __restrict__ msg, const uint64_t* __restrict__ msg_off,
-    const uint32_t* __restrict__ msg_len, const uint32_t* __restrict__ seedp, MsmLayout lay,
-    uint32_t* __restrict__ ascal,
-    int16_t* __restrict__ digits, uint32_t* __restrict__ partial, uint32_t* __restrict__ fail) {
+struct MsmScalarArgs {
+    uint64_t n, na;
+    int keyed;
+    const uint8_t* pk;
+    const uint8_t* sig;
+    const uint8_t* msg;
+    const uint64_t* msg_off;
+    const uint32_t* msg_len;
+    const uint32_t* seedp;
+    uint32_t* ascal;
+    int16_t* digits;
+    uint32_t* partial;
+    uint32_t* fail;
+};
+struct MsmPointArgs {
+    uint64_t n, na;
+    const uint8_t* apk;
+    const uint8_t* sig;
+    uint32_t* pts;
+    uint32_t* fail;
+};
+
+__device__ __forceinline__ void msm_scalars_block(uint32_t blk, const MsmScalarArgs& g, const MsmLayout& lay) {
+    const uint64_t n = g.n, na = g.na;
+    const uint8_t* __restrict__ pk = g.pk;
+    const uint8_t* __restrict__ sig = g.sig;
+    const uint8_t* __restrict__ msg = g.msg;
+    const uint32_t* __restrict__ seedp = g.seedp;
+    int16_t* __restrict__ digits = g.digits;
+    uint32_t* __restrict__ fail = g.fail;
+    const int keyed = g.keyed;
     __shared__ uint32_t zs_lds[256 * 9];
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t i = (uint64_t)blk * 256 + threadIdx.x;
     uint32_t zs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (i < n) {
         uint32_t Aw[8], Rw[8], Sw[8], k[8], z[8], a[8];
         msm_load8(pk + 32 * i, Aw);
         msm_load8(sig + 64 * i, Rw);
         msm_load8(sig + 64 * i + 32, Sw);
-        const uint32_t f = lane_hash(Aw, Rw, Sw, msg + msg_off[i], msg_len[i], k);
+        const uint32_t f = lane_hash(Aw, Rw, Sw, msg + g.msg_off[i], g.msg_len[i], k);
         if (f != FLAG_S_OK) atomicOr(fail, 1u);
         uint32_t sd[8];
 #pragma unroll
@@ -70,7 +95,7 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_scalars(
         // z_i k_i here when every signature has its own A point, else summed per key by
         // k_msm_keysum first
         const uint64_t np = na + 1 + n;
-        if (keyed) msm_store8(ascal + 8 * i, a);
+        if (keyed) msm_store8(g.ascal + 8 * i, a);
         else msm_recode(a, lay, lay.nw, [&](int w, int d) { digits[(uint64_t)w * np + i] = (int16_t)d; });
         msm_recode(z, lay, lay.nw_z, [&](int w, int d) { digits[(uint64_t)w * np + na + 1 + i] = (int16_t)d; });
     }
@@ -87,7 +112,7 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_scalars(
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long c = 0;
-        uint32_t* out = partial + 9 * blockIdx.x;
+        uint32_t* out = g.partial + 9 * blk;
         for (int k = 0; k < 8; k++) {
             c += col[k];
             out[k] = (uint32_t)c;
@@ -192,20 +217,34 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_bscalar(
 // Decompression, wave-uniform roles: waves [0, ceil(n/64)) decompress R_i into point na+1+i,
 // the following ceil(na/64) waves decompress the A points (apk: per-signature keys, or the
 // distinct keys of a keyed batch) into points [0, na).
-extern "C" __global__ void __launch_bounds__(256) k_msm_points(
-    uint64_t n, uint64_t na, const uint8_t* __restrict__ apk, const uint8_t* __restrict__ sig,
-    uint32_t* __restrict__ pts, uint32_t* __restrict__ fail) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void msm_points_block(uint32_t blk, const MsmPointArgs& g) {
+    const uint64_t n = g.n, na = g.na;
+    const uint64_t t = (uint64_t)blk * 256 + threadIdx.x;
     const uint64_t rwaves = (n + 63) / 64;
     const bool is_r = (t >> 6) < rwaves;
     const uint64_t i = is_r ? t : t - 64 * rwaves;
     if (i >= (is_r ? n : na)) return;
     uint32_t w[8];
-    msm_load8(is_r ? sig + 64 * i : apk + 32 * i, w);
+    msm_load8(is_r ? g.sig + 64 * i : g.apk + 32 * i, w);
     ge_p3 P;
     const bool ok = ge_decompress(w, P);
-    msm_store_point(pts + (size_t)MSM_PT_WORDS * (is_r ? na + 1 + i : i), P);
-    if (!ok) atomicOr(fail, 2u);
+    msm_store_point(g.pts + (size_t)MSM_PT_WORDS * (is_r ? na + 1 + i : i), P);
+    if (!ok) atomicOr(g.fail, 2u);
+}
+
+extern "C" __global__ void __launch_bounds__(256) k_msm_scalars(MsmScalarArgs g, MsmLayout lay) {
+    msm_scalars_block(blockIdx.x, g, lay);
+}
+extern "C" __global__ void __launch_bounds__(256) k_msm_points(MsmPointArgs g) {
+    msm_points_block(blockIdx.x, g);
+}
+// Both in one grid: blocks [0, sblocks) hash / recode (one wave per SIMD at 65,536 signatures,
+// latency-bound on its own), the rest decompress; sharing the SIMDs lets the decompression
+// waves fill the hash waves' issue gaps.
+extern "C" __global__ void __launch_bounds__(256) k_msm_prep(MsmScalarArgs gs, MsmLayout lay, MsmPointArgs gp,
+                                                             uint32_t sblocks) {
+    if (blockIdx.x < sblocks) msm_scalars_block(blockIdx.x, gs, lay);
+    else msm_points_block(blockIdx.x - sblocks, gp);
 }
 
 // points of window w: all na+1+n below nw_z, else the prefix [0, na] (A points and B)

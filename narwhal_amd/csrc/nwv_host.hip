@@ -217,7 +217,12 @@ int msm_alloc(EdBuffers& b, const MsmPlan& p, size_t n) {
 }
 
 static const char* const ED_KERNEL_NAMES[] = {"k_ed_hash", "k_ed_points", "k_ed_straus"};
+// event slots of one batch MSM; nullptr = no kernel in that slot (k_msm_prep runs the hash and
+// the decompression as one grid unless NWV_FLAG_MSM_SPLIT_PREP)
 static const char* const MSM_KERNEL_NAMES[] = {
+    "k_msm_prep", "k_msm_bscalar", nullptr, "k_msm_hist", "k_scan",
+    "k_msm_scatter", "k_msm_bucket+fixup", "k_msm_window", "k_msm_final"};
+static const char* const MSM_KERNEL_NAMES_SPLIT[] = {
     "k_msm_scalars", "k_msm_bscalar", "k_msm_points", "k_msm_hist", "k_scan",
     "k_msm_scatter", "k_msm_bucket+fixup", "k_msm_window", "k_msm_final"};
 constexpr int MSM_NKERNELS = 9;
@@ -243,10 +248,18 @@ int msm_launch(Device& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipS
     if ((rc = mark(0))) return rc;
     int16_t* digits = b.m_digits.as<int16_t>();
     const int keyed = b.nkeys_distinct ? 1 : 0;
-    hipLaunchKernelGGL(k_msm_scalars, dim3(nblk), dim3(256), 0, stream, (uint64_t)n, (uint64_t)na, keyed,
-                       b.pk.as<uint8_t>(), b.sig.as<uint8_t>(), b.msg.as<uint8_t>(), b.off.as<uint64_t>(),
-                       b.len.as<uint32_t>(), state + 8, p.lay, b.m_ascal.as<uint32_t>(), digits,
-                       b.m_partial.as<uint32_t>(), state);
+    const MsmScalarArgs gs{(uint64_t)n, (uint64_t)na, keyed, b.pk.as<uint8_t>(), b.sig.as<uint8_t>(),
+                           b.msg.as<uint8_t>(), b.off.as<uint64_t>(), b.len.as<uint32_t>(), state + 8,
+                           b.m_ascal.as<uint32_t>(), digits, b.m_partial.as<uint32_t>(), state};
+    const MsmPointArgs gp{(uint64_t)n, (uint64_t)na, keyed ? b.keys.as<uint8_t>() : b.pk.as<uint8_t>(),
+                          b.sig.as<uint8_t>(), b.m_pts.as<uint32_t>(), state};
+    const size_t waves = (n + 63) / 64 + (na + 63) / 64;
+    const unsigned pblk = (unsigned)((64 * waves + 255) / 256);
+    const bool fused = !(d.flags & NWV_FLAG_MSM_SPLIT_PREP);
+    if (fused)
+        hipLaunchKernelGGL(k_msm_prep, dim3(nblk + pblk), dim3(256), 0, stream, gs, p.lay, gp, nblk);
+    else
+        hipLaunchKernelGGL(k_msm_scalars, dim3(nblk), dim3(256), 0, stream, gs, p.lay);
     if (keyed)
         hipLaunchKernelGGL(k_msm_keysum, dim3((unsigned)na), dim3(256), 0, stream, (uint64_t)n, (uint64_t)na,
                            p.lay, b.koff.as<uint32_t>(), b.ksig.as<uint32_t>(), b.m_ascal.as<uint32_t>(), digits);
@@ -256,10 +269,7 @@ int msm_launch(Device& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipS
                        b.m_partial.as<uint32_t>(), d.btab.as<uint32_t>(), b.m_scal.as<uint32_t>(), digits,
                        b.m_pts.as<uint32_t>());
     if ((rc = mark(2))) return rc;
-    const size_t waves = (n + 63) / 64 + (na + 63) / 64;
-    hipLaunchKernelGGL(k_msm_points, dim3((unsigned)((64 * waves + 255) / 256)), dim3(256), 0, stream,
-                       (uint64_t)n, (uint64_t)na, keyed ? b.keys.as<uint8_t>() : b.pk.as<uint8_t>(),
-                       b.sig.as<uint8_t>(), b.m_pts.as<uint32_t>(), state);
+    if (!fused) hipLaunchKernelGGL(k_msm_points, dim3(pblk), dim3(256), 0, stream, gp);
     if ((rc = mark(3))) return rc;
     const dim3 gsort(p.chunks, (unsigned)p.lay.nw);
     const size_t lds_nb = (size_t)4 << (p.lay.cmax - 1);
@@ -390,16 +400,18 @@ struct nwv_ctx {
 
 // Per-kernel device time of the staged pipelines (HIP events on the batch's own stream).
 struct KernelLog {
-    std::vector<std::string> names;
+    std::vector<const char*> names;  // static strings
     std::vector<double> ms;
     long runs = 0;
-    void add(const char* const* nm, const float* t, int k) {
+    void add(const char* const* nm, const float* t, int k) {  // nm[i] == nullptr: empty slot
         if (names.empty())
-            for (int i = 0; i < k; i++) {
-                names.emplace_back(nm[i]);
-                ms.push_back(0.0);
-            }
-        for (int i = 0; i < k; i++) ms[i] += t[i];
+            for (int i = 0; i < k; i++)
+                if (nm[i]) {
+                    names.push_back(nm[i]);
+                    ms.push_back(0.0);
+                }
+        for (int i = 0, j = 0; i < k; i++)
+            if (nm[i]) ms[j++] += t[i];
         runs++;
     }
 };
@@ -783,7 +795,8 @@ static int staged_collect_times(nwv_staged* st) {
     if (st->last_mode == 1) {
         NWV_HIP(hipEventSynchronize(st->ev[MSM_NKERNELS]));
         for (int i = 0; i < MSM_NKERNELS; i++) NWV_HIP(hipEventElapsedTime(&t[i], st->ev[i], st->ev[i + 1]));
-        st->log[1].add(MSM_KERNEL_NAMES, t, MSM_NKERNELS);
+        st->log[1].add((st->dev->flags & NWV_FLAG_MSM_SPLIT_PREP) ? MSM_KERNEL_NAMES_SPLIT : MSM_KERNEL_NAMES, t,
+                       MSM_NKERNELS);
     } else {
         NWV_HIP(hipEventSynchronize(st->ev[3]));
         for (int i = 0; i < 3; i++) NWV_HIP(hipEventElapsedTime(&t[i], st->ev[i], st->ev[i + 1]));
@@ -902,7 +915,7 @@ int nwv_staged_kernel_times(nwv_staged* st, int mode, int cap, const char** name
     KernelLog& l = st->log[mode];
     const int k = std::min<int>(cap, (int)l.names.size());
     for (int i = 0; i < k; i++) {
-        if (names) names[i] = (mode == 1 ? MSM_KERNEL_NAMES : ED_KERNEL_NAMES)[i];
+        if (names) names[i] = l.names[i];
         if (avg_ms) avg_ms[i] = l.runs ? l.ms[i] / l.runs : 0.0;
     }
     const int total = (int)l.names.size();

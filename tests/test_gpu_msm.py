@@ -99,18 +99,33 @@ def test_adversarial_mix_config4(eng):
     assert bits == want
 
 
-def test_staged_msm_runs_and_times(eng):
+@pytest.mark.parametrize("split", [False, True])
+def test_staged_msm_runs_and_times(eng, split):
+    """timed runs report every kernel of the batch MSM: k_msm_prep (hash + decompression in one
+    grid) by default, k_msm_scalars and k_msm_points under NWV_FLAG_MSM_SPLIT_PREP; both launch
+    shapes give the same verdicts, including the exact bad set"""
     from narwhal_amd import _lib
+    e = _lib.Engine(device=0, flags=_lib.NWV_FLAG_MSM_ALWAYS | _lib.NWV_FLAG_MSM_SPLIT_PREP) if split else eng
     items = _synthetic(eng, 8192, 512, seed=9)
     pk, sg, arena, offs, lens = _lib.soa(items)
-    st = eng.stage(pk, sg, arena, offs, lens)
+    st = e.stage(pk, sg, arena, offs, lens)
     for r in range(3):
         st.run(mode=1, seed=bytes([r]) * 32, timed=True)
     allv, bits = st.fetch()
     t = st.kernel_times(1)
     st.free()
     assert allv and bits.all()
-    assert len(t) == 9 and all(v > 0 for v in t.values())
+    want = (["k_msm_scalars", "k_msm_bscalar", "k_msm_points"] if split else ["k_msm_prep", "k_msm_bscalar"]) + [
+        "k_msm_hist", "k_scan", "k_msm_scatter", "k_msm_bucket+fixup", "k_msm_window", "k_msm_final"]
+    assert list(t) == want and all(v > 0 for v in t.values())
+    bad = [5, 4000, 8191]
+    for i in bad:
+        p, s_, m = items[i]
+        items[i] = (p, s_, m + b"x")
+    ok, vb = e.verify_batch(items)
+    if split:
+        e.close()
+    assert not ok and [i for i in range(len(items)) if not vb[i]] == bad
 
 
 def test_staged_graph_replay_valid_and_invalid(eng):
