@@ -26,6 +26,14 @@ import time
 
 import numpy as np
 
+# Hardware queues per process (HIP's default is 4).  Each resident batch runs on its own stream;
+# with 4 queues the streams share queues and a batch's latency-bound MSM tail (window sums,
+# Horner: a few workgroups for ~0.5 ms) serialises the work queued behind it.  16 queues let
+# the tails of up to 16 batches run beside other batches' bulk kernels
+# (profiles/round1_hwq_sweep.jsonl).  Must be set before the HIP runtime initialises; the GPU
+# boxes export 4, so it is overridden here (NWV_BENCH_HW_QUEUES picks another count).
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("NWV_BENCH_HW_QUEUES", "16")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -91,10 +99,10 @@ def cpu_baseline(pk, sg, msgs, offs, lens, seconds):
                       f"oracle/nwv_oracle.c batch verifier: Pippenger/Straus as dalek)"}
 
 
-def roofline_entry(kname, kt, mads_launch, peak_t, algorithmic):
+def roofline_entry(kname, kt, mads_launch, peak_t, algorithmic, n):
     kms = float(kt.get(kname, 0.0))
     achieved = mads_launch / (kms * 1e-3) / 1e12 if kms > 0 else None
-    traffic = pmc_traffic(kname)
+    traffic = pmc_traffic(kname, n)
     return {
         "bound": "valu",
         "kernel": kname,
@@ -132,7 +140,7 @@ def split_prep_times(args, pk, sg, msgs, offs, lens, reps=5):
         e.close()
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, n):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc pass (FETCH_SIZE
     doubled for gfx950's half-counted wide reads + WRITE_SIZE, MI355X_MICROARCH.md HBM section),
     or None when no profile for it is committed."""
@@ -142,6 +150,8 @@ def pmc_traffic(kernel):
             with open(f) as fh:
                 d = json.load(fh)
             k = d.get("kernels", {}).get(kernel)
+            if d.get("n") != n:
+                continue
             if k and "FETCH_SIZE" in k and "WRITE_SIZE" in k:
                 return {"bytes": 2 * k["FETCH_SIZE"] * 1024 + k["WRITE_SIZE"] * 1024,
                         "source": os.path.relpath(f, ROOT), "n": d.get("n")}
@@ -153,15 +163,15 @@ def pmc_traffic(kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=6)
+    ap.add_argument("--steps", type=int, default=96)
+    ap.add_argument("--warmup", type=int, default=24)
     ap.add_argument("--n", type=int, default=65536, help="signatures per batch (per GPU)")
     ap.add_argument("--msg-len", type=int, default=512)
     ap.add_argument("--mode", type=int, default=1, help="1 batch MSM (K5), 0 per-signature pipeline")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-reps", type=int, default=300)
-    ap.add_argument("--inflight", type=int, default=3,
+    ap.add_argument("--inflight", type=int, default=12,
                     help="resident batches in flight on separate streams (step s runs batch s %% K)")
     ap.add_argument("--keys", type=int, default=0,
                     help="distinct verifying keys (0: one per signature, the configs[1] worst case; "
@@ -271,18 +281,18 @@ def main():
                                   f"{mads(OPS_MSM_POINTS) // 2} multiply-adds/point (decompression: "
                                   f"{OPS_MSM_POINTS[0] // 2} mul x 100 + {OPS_MSM_POINTS[1] // 2} sq x 55) x "
                                   f"{npts} points per launch; the SHA-512 hashing in the same grid "
-                                  "is not counted")
+                                  "is not counted", args.n)
             roof["kernel_ms"] = kt
             kt_split = split_prep_times(args, pk, sg, msgs, offs, lens)
             roof["decompression_alone"] = roofline_entry(
                 "k_msm_points", kt_split, mads(OPS_MSM_POINTS) // 2 * npts, peak_t,
                 "same multiply-adds, k_msm_points launched on its own (NWV_FLAG_MSM_SPLIT_PREP, "
-                "single stream, timed pass)")
+                "single stream, timed pass)", args.n)
             roof["decompression_alone"]["kernel_ms"] = kt_split
         else:
             roof = roofline_entry("k_ed_straus", kt, mads(OPS_STRAUS) * args.n, peak_t,
                                   f"{mads(OPS_STRAUS)} multiply-adds/signature ({OPS_STRAUS[0]} mul x 100 + "
-                                  f"{OPS_STRAUS[1]} sq x 55) x {args.n} signatures per launch")
+                                  f"{OPS_STRAUS[1]} sq x 55) x {args.n} signatures per launch", args.n)
             roof["kernel_ms"] = kt
         cpu = None
         if not args.no_cpu_baseline:
