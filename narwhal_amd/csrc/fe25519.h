@@ -119,10 +119,13 @@ NWV_HD fe fe_carry64(uint64_t h[10]) {
     c = h[4] >> 26; h[5] += c; h[4] &= M26;
     c = h[8] >> 26; h[9] += c; h[8] &= M26;
     c = h[9] >> 25; h[0] += c * 19; h[9] &= M25;
-    c = h[0] >> 26; h[1] += c; h[0] &= M26;
     fe r;
 #pragma unroll
-    for (int i = 0; i < 10; i++) r.v[i] = (uint32_t)h[i];
+    for (int i = 2; i < 10; i++) r.v[i] = (uint32_t)h[i];
+    // last carry in 32 bits: limbs 0 and 1 leave as plain 32-bit values (keeps the compiler
+    // from carrying them as 64-bit quantities into the next multiply)
+    r.v[0] = (uint32_t)h[0] & M26;
+    r.v[1] = (uint32_t)h[1] + (uint32_t)(h[0] >> 26);
     return r;
 }
 
@@ -187,9 +190,13 @@ NWV_HD fe fe_sq(const fe& f) {
     return r;
 }
 
+NWV_HD void fe_pin(fe& a);
 NWV_HD fe fe_sqn(fe f, int n) {
 #pragma unroll 1
-    for (int i = 0; i < n; i++) f = fe_sq(f);
+    for (int i = 0; i < n; i++) {
+        fe_pin(f);  // loop-carried limbs stay plain 32-bit values
+        f = fe_sq(f);
+    }
     return f;
 }
 

@@ -368,7 +368,7 @@ extern "C" __global__ void __launch_bounds__(256) k_scan_add(uint64_t len, uint3
 // written out: to bsum[key] if the key starts in this chunk (complete, or the key's first piece),
 // else to hpart[q] (a continuation from earlier chunks, completed by k_msm_fixup).  Every lane
 // does the same number of additions whatever the bucket sizes.
-// one 128-byte record as eight 16-byte loads (affine Niels words 0..29)
+// one 128-byte record as eight 16-byte loads (affine Niels words 0..29, two padding words)
 __device__ __forceinline__ void msm_load_raw(const uint32_t* __restrict__ pts, uint32_t v, uint32_t w[32]) {
     const uint4* e = reinterpret_cast<const uint4*>(pts + (size_t)MSM_PT_WORDS * (v & ~MSM_NEG));
 #pragma unroll
@@ -377,10 +377,16 @@ __device__ __forceinline__ void msm_load_raw(const uint32_t* __restrict__ pts, u
         w[4 * k] = t.x; w[4 * k + 1] = t.y; w[4 * k + 2] = t.z; w[4 * k + 3] = t.w;
     }
 }
-__device__ __forceinline__ ge_precomp msm_point_of(const uint32_t w[32], uint32_t v) {
+// zero: a runtime 0 the compiler cannot see through.  Folding the padding words into the sign
+// test keeps their registers live until the record is used; a dead load destination is reused
+// by the register allocator at once, which forces a wait on the whole prefetch.
+__device__ __forceinline__ ge_precomp msm_point_of(const uint32_t w[32], uint32_t v, uint32_t zero) {
+    v |= (w[30] | w[31]) & zero;
     return msm_point_select(load_fe(w), load_fe(w + 10), load_fe(w + 20), (v & MSM_NEG) != 0);
 }
 
+// Two record buffers alternate (the loop is unrolled by two, so neither is copied) and entry
+// indices are read two entries ahead, so a record's load is in flight for a whole addition.
 extern "C" __global__ void __launch_bounds__(256) k_msm_bucket(
     uint32_t T, uint32_t nkeys, const uint32_t* __restrict__ total, const uint32_t* __restrict__ entries,
     const uint32_t* __restrict__ kstart, const uint32_t* __restrict__ pts, uint32_t* __restrict__ bsum,
@@ -400,16 +406,10 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_bucket(
     uint32_t kend = key + 1 < nkeys ? kstart[key + 1] : E;
     bool head = kstart[key] < k0;
     ge_p3 acc = ge_p3_identity();
-    uint32_t nv = entries[k0], nw[32];
-    msm_load_raw(pts, nv, nw);
-#pragma unroll 1
-    for (uint32_t k = (uint32_t)k0; k < k1; k++) {
-        const ge_precomp cur = msm_point_of(nw, nv);
-        if (k + 1 < k1) {
-            nv = entries[k + 1];
-            msm_load_raw(pts, nv, nw);
-        }
-        acc = ge_p1p1_to_p3(ge_madd(acc, cur));
+    // add entry k (record w, index word v); close the key segment when it ends here
+    const uint32_t zero = 0u - (T >> 31);  // T < 2^31: all-zero, opaque to the compiler
+    auto step = [&](const uint32_t* w, uint32_t v, uint32_t k) {
+        acc = ge_p1p1_to_p3(ge_madd(acc, msm_point_of(w, v, zero)));
         if (k + 1 == k1 || k + 1 == kend) {
             store_p3(head ? hpart + (size_t)P3_WORDS * (k0 / T) : bsum + (size_t)P3_WORDS * key, acc);
             acc = ge_p3_identity();
@@ -421,6 +421,29 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_bucket(
                 } while (kend <= k + 1);
             }
         }
+    };
+    // loads are unconditional (indices clamped into the chunk): branch-free code lets the
+    // compiler count outstanding loads exactly instead of waiting for all of them
+    const uint32_t klast = k1 - 1;
+    auto at = [&](uint32_t k) { return entries[k < klast ? k : klast]; };
+    uint32_t wa[32], wb[32];
+    uint32_t va = entries[k0];
+    uint32_t vb = at((uint32_t)k0 + 1);
+    msm_load_raw(pts, va, wa);
+#pragma unroll 1
+    for (uint32_t k = (uint32_t)k0;; k += 2) {
+        // index loads go out before the record loads: the memory counter is in order, so a
+        // wait for an index never waits for a record still in flight
+        const uint32_t vc = at(k + 2);
+        msm_load_raw(pts, vb, wb);
+        step(wa, va, k);
+        if (k + 1 >= k1) break;
+        const uint32_t vd = at(k + 3);
+        msm_load_raw(pts, vc, wa);
+        step(wb, vb, k + 1);
+        if (k + 2 >= k1) break;
+        va = vc;
+        vb = vd;
     }
 }
 
