@@ -124,7 +124,7 @@ extern "C" __global__ void __launch_bounds__(256) k_sign(
     ge_compress(straus_sB_minus_kA(zero, a, nullptr, btab, ident), Aw);
     const uint8_t* m = msg + msg_off[i];
     const uint32_t mlen = msg_len[i];
-    sha512_prefixed(st, prefix, mlen, [&](uint32_t j) -> uint32_t { return ld_u32_unaligned(m + 4 * j); });
+    sha512_prefixed_msg(st, prefix, m, mlen);
     uint32_t rh[16], r[8];
     sha512_digest_words(st, rh);
     sc_reduce512(rh, r);

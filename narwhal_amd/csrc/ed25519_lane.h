@@ -47,7 +47,7 @@ NWV_HD void challenge_scalar(const uint32_t Rw[8], const uint32_t Aw[8], const u
         pre[8 + i] = Aw[i];
     }
     sha512_state st;
-    sha512_prefixed(st, pre, mlen, [&](uint32_t j) -> uint32_t { return ld_u32_unaligned(msg + 4 * j); });
+    sha512_prefixed_msg(st, pre, msg, mlen);
     uint32_t hw[16];
     sha512_digest_words(st, hw);
     sc_reduce512(hw, k);

@@ -61,23 +61,52 @@ NWV_HD bool p3_mul8_is_identity(const ge_p3& p) {
     return ge_p1p1_is_identity(t);
 }
 
-// Per-signature random coefficient z_i in [0, 2^128): the first 16 bytes of
-// SHA-512(seed32 || le64(i) || "nwv-z128"). The reference draws z_i from OsRng; here the
-// caller's 32-byte CSPRNG seed keys a PRF so the kernels need no device RNG state.
+// ChaCha20 block function (RFC 8439 2.3): 16 output words for key[8], 32-bit block counter and
+// nonce[3].
+NWV_HD uint32_t chacha_rotl(uint32_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbit(x, x, 32 - n);
+#else
+    return (x << n) | (x >> (32 - n));
+#endif
+}
+NWV_HD void chacha_qr(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) {
+    a += b; d = chacha_rotl(d ^ a, 16);
+    c += d; b = chacha_rotl(b ^ c, 12);
+    a += b; d = chacha_rotl(d ^ a, 8);
+    c += d; b = chacha_rotl(b ^ c, 7);
+}
+NWV_HD void chacha20_block(const uint32_t key[8], uint32_t counter, const uint32_t nonce[3], uint32_t out[16]) {
+    uint32_t x[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key[0], key[1], key[2], key[3],
+                      key[4], key[5], key[6], key[7], counter, nonce[0], nonce[1], nonce[2]};
+    uint32_t s[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) s[k] = x[k];
+#pragma unroll 2
+    for (int r = 0; r < 10; r++) {
+        chacha_qr(x[0], x[4], x[8], x[12]);
+        chacha_qr(x[1], x[5], x[9], x[13]);
+        chacha_qr(x[2], x[6], x[10], x[14]);
+        chacha_qr(x[3], x[7], x[11], x[15]);
+        chacha_qr(x[0], x[5], x[10], x[15]);
+        chacha_qr(x[1], x[6], x[11], x[12]);
+        chacha_qr(x[2], x[7], x[8], x[13]);
+        chacha_qr(x[3], x[4], x[9], x[14]);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) out[k] = x[k] + s[k];
+}
+
+// Per-signature random coefficient z_i in [0, 2^128): the first 16 bytes of the ChaCha20 block
+// keyed by the caller's 32-byte seed with counter = low word of i and nonce = (high word of i,
+// "nwv-", "z128").  ed25519-consensus draws z_i from the thread RNG (a ChaCha CSPRNG in rand);
+// here the caller's CSPRNG seed keys the stream so the kernels need no device RNG state.
 NWV_HD void msm_z(const uint32_t seed[8], uint64_t i, uint32_t z[8]) {
-    uint32_t pre[12];
+    const uint32_t nonce[3] = {(uint32_t)(i >> 32), 0x2d76776eu /* "nwv-" */, 0x3832317au /* "z128" */};
+    uint32_t blk[16];
+    chacha20_block(seed, (uint32_t)i, nonce, blk);
 #pragma unroll
-    for (int k = 0; k < 8; k++) pre[k] = seed[k];
-    pre[8] = (uint32_t)i;
-    pre[9] = (uint32_t)(i >> 32);
-    pre[10] = 0x2d76776eu;  // "nwv-"
-    pre[11] = 0x3832317au;  // "z128" (little-endian words)
-    sha512_state st;
-    sha512_prefixed(st, pre, 0, [](uint32_t) -> uint32_t { return 0u; });
-    uint32_t h[16];
-    sha512_digest_words(st, h);
-#pragma unroll
-    for (int k = 0; k < 8; k++) z[k] = k < 4 ? h[k] : 0u;
+    for (int k = 0; k < 8; k++) z[k] = k < 4 ? blk[k] : 0u;
 }
 
 // Window layout.  Windows have near-equal widths <= c chosen so that every window's bucket range

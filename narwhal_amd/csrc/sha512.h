@@ -52,15 +52,39 @@ NWV_HD u64p shr(u64p x, int n) {  // 0 < n < 32
     return u64p{funnel_r(x.hi, x.lo, n), x.hi >> n};
 }
 NWV_HD u64p add(u64p a, u64p b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // exactly v_add_co_u32 + v_addc_co_u32 (the plain C form also materialises the carry as a
+    // value with v_cndmask)
+    unsigned c, c2;
+    const uint32_t lo = __builtin_addc(a.lo, b.lo, 0u, &c);
+    const uint32_t hi = __builtin_addc(a.hi, b.hi, c, &c2);
+    return u64p{lo, hi};
+#else
     const uint64_t t = (uint64_t)a.lo + b.lo;
     return u64p{(uint32_t)t, a.hi + b.hi + (uint32_t)(t >> 32)};
+#endif
 }
-NWV_HD u64p xor3(u64p a, u64p b, u64p c) { return u64p{a.lo ^ b.lo ^ c.lo, a.hi ^ b.hi ^ c.hi}; }
+NWV_HD uint32_t xor3_32(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // one v_bitop3_b32 (a ^ b ^ c)
+#else
+    return a ^ b ^ c;
+#endif
+}
+NWV_HD u64p xor3(u64p a, u64p b, u64p c) { return u64p{xor3_32(a.lo, b.lo, c.lo), xor3_32(a.hi, b.hi, c.hi)}; }
+// Ch and Maj as one v_bitop3_b32 per half (truth tables 0xCA and 0xE8 over (x, y, z))
+NWV_HD uint32_t bitop3_32(uint32_t x, uint32_t y, uint32_t z, int tt) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (uint32_t)(tt == 0xCA ? __builtin_amdgcn_bitop3_b32(x, y, z, 0xCA) : __builtin_amdgcn_bitop3_b32(x, y, z, 0xE8));
+#else
+    return tt == 0xCA ? ((x & y) ^ (~x & z)) : ((x & y) ^ (x & z) ^ (y & z));
+#endif
+}
 NWV_HD u64p ch(u64p e, u64p f, u64p g) {
-    return u64p{(e.lo & f.lo) ^ (~e.lo & g.lo), (e.hi & f.hi) ^ (~e.hi & g.hi)};
+    return u64p{bitop3_32(e.lo, f.lo, g.lo, 0xCA), bitop3_32(e.hi, f.hi, g.hi, 0xCA)};
 }
 NWV_HD u64p maj(u64p a, u64p b, u64p c) {
-    return u64p{(a.lo & b.lo) ^ (a.lo & c.lo) ^ (b.lo & c.lo), (a.hi & b.hi) ^ (a.hi & c.hi) ^ (b.hi & c.hi)};
+    return u64p{bitop3_32(a.lo, b.lo, c.lo, 0xE8), bitop3_32(a.hi, b.hi, c.hi, 0xE8)};
 }
 NWV_HD uint32_t bswap32(uint32_t x) {
     return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
@@ -176,6 +200,77 @@ NWV_HD void sha512_prefixed(sha512_state& s, const uint32_t (&prefix)[NP], uint3
             w[t] = u64p{half[1], half[0]};
         }
         if (blk == nblocks - 1) w[15] = u64p{total * 8, total >> 29};  // 128-bit length
+        sha512_compress(s, w);
+    }
+}
+
+// 32 consecutive little-endian message words from byte address p (any alignment; the arena is
+// padded past its last message): eight 16-byte loads from the dword-aligned address below p,
+// one more dword, and a funnel shift by p's byte offset
+NWV_HD void ld_block_unaligned(const uint8_t* p, uint32_t out[32]) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t* base = (const uint32_t*)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3) * 8;
+    uint32_t raw[33];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        uint4 t;
+        __builtin_memcpy(&t, base + 4 * k, 16);
+        raw[4 * k] = t.x; raw[4 * k + 1] = t.y; raw[4 * k + 2] = t.z; raw[4 * k + 3] = t.w;
+    }
+    raw[32] = base[32];
+#pragma unroll
+    for (int j = 0; j < 32; j++) out[j] = funnel_r(raw[j + 1], raw[j], (int)sh);
+}
+
+// SHA-512 of prefix || msg[0 .. mlen): sha512_prefixed with the message read from memory; every
+// block that lies wholly inside the message is fetched as one 128-byte unaligned block (nine
+// vector loads instead of sixty-four dword loads and a per-word padding test).
+template <int NP>
+NWV_HD void sha512_prefixed_msg(sha512_state& s, const uint32_t (&prefix)[NP], const uint8_t* msg, uint32_t mlen) {
+    static_assert(NP <= 32, "prefix must fit in the first block");
+    sha512_init(s);
+    const uint32_t total = 4 * NP + mlen;
+    const uint32_t nblocks = (total + 17 + 127) / 128;
+    u64p w[16];
+#pragma unroll
+    for (int t = 0; t < 16; t++) {
+        uint32_t half[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int q = 2 * t + u;
+            const uint32_t pos = 4u * q;
+            uint32_t v;
+            if (q < NP) v = prefix[q];
+            else v = (pos < total) ? ld_u32_unaligned(msg + 4 * (q - NP)) : 0u;
+            half[u] = bswap32(sha_pad_word(v, pos, total));
+        }
+        w[t] = u64p{half[1], half[0]};
+    }
+    if (nblocks == 1) w[15] = u64p{total * 8, total >> 29};
+    sha512_compress(s, w);
+#pragma unroll 1
+    for (uint32_t blk = 1; blk < nblocks; blk++) {
+        if (blk * 128 + 128 <= total) {
+            uint32_t m[32];
+            ld_block_unaligned(msg + (blk * 128 - 4 * NP), m);
+#pragma unroll
+            for (int t = 0; t < 16; t++) w[t] = u64p{bswap32(m[2 * t + 1]), bswap32(m[2 * t])};
+        } else {
+#pragma unroll
+            for (int t = 0; t < 16; t++) {
+                uint32_t half[2];
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const uint32_t q = blk * 32 + 2 * t + u;
+                    const uint32_t pos = 4u * q;
+                    const uint32_t v = (pos < total) ? ld_u32_unaligned(msg + 4 * (q - NP)) : 0u;
+                    half[u] = bswap32(sha_pad_word(v, pos, total));
+                }
+                w[t] = u64p{half[1], half[0]};
+            }
+            if (blk == nblocks - 1) w[15] = u64p{total * 8, total >> 29};  // 128-bit length
+        }
         sha512_compress(s, w);
     }
 }

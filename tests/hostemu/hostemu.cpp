@@ -89,17 +89,21 @@ void he_sc_reduce(const uint8_t* in64, uint8_t* out32) {
 }
 
 // SHA-512 of (64-byte register prefix || msg), the challenge layout R || A || M
-void he_sha512_p64(const uint8_t* prefix64, const uint8_t* msg, uint32_t len, uint8_t* out64) {
-    std::vector<uint8_t> m(len + 64, 0);
-    if (len) std::memcpy(m.data(), msg, len);
+// (the message is placed `shift` bytes past an aligned address: the block loader's funnel shift)
+void he_sha512_p64_at(const uint8_t* prefix64, const uint8_t* msg, uint32_t len, uint32_t shift, uint8_t* out64) {
+    std::vector<uint8_t> m(len + 64 + 16, 0xA5);
+    if (len) std::memcpy(m.data() + shift, msg, len);
     uint32_t pre[16];
     std::memcpy(pre, prefix64, 64);
-    const uint8_t* mp = m.data();
+    const uint8_t* mp = m.data() + shift;
     sha512_state st;
-    sha512_prefixed(st, pre, len, [&](uint32_t j) -> uint32_t { return ld_u32_unaligned(mp + 4 * j); });
+    sha512_prefixed_msg(st, pre, mp, len);
     uint32_t out[16];
     sha512_digest_words(st, out);
     std::memcpy(out64, out, 64);
+}
+void he_sha512_p64(const uint8_t* prefix64, const uint8_t* msg, uint32_t len, uint8_t* out64) {
+    he_sha512_p64_at(prefix64, msg, len, 0, out64);
 }
 
 void he_blake2b256(const uint8_t* msg, uint64_t len, uint8_t* out32) {
@@ -144,7 +148,7 @@ void he_sign(const uint8_t* seed, const uint8_t* msg, uint32_t len, uint8_t* pk_
     uint32_t Aw[8], Rw[8];
     ge_compress(straus_sB_minus_kA(zero, a, nullptr, g_btab.data(), ident), Aw);
     const uint8_t* mp = m.data();
-    sha512_prefixed(st, prefix, len, [&](uint32_t j) -> uint32_t { return ld_u32_unaligned(mp + 4 * j); });
+    sha512_prefixed_msg(st, prefix, mp, len);
     uint32_t rh[16], r[8];
     sha512_digest_words(st, rh);
     sc_reduce512(rh, r);
@@ -283,6 +287,14 @@ int he_msm_layout(int c, int* out) {
     out[1] = lay.nw_z;
     for (int w = 0; w < lay.nw; w++) out[2 + w] = lay.width[w];
     return lay.nw;
+}
+
+void he_chacha20_block(const uint8_t* key32, uint32_t counter, const uint8_t* nonce12, uint8_t* out64) {
+    uint32_t key[8], nonce[3], out[16];
+    words(key32, key);
+    std::memcpy(nonce, nonce12, 12);
+    chacha20_block(key, counter, nonce, out);
+    std::memcpy(out64, out, 64);
 }
 
 void he_msm_z(const uint8_t* seed32, uint64_t i, uint8_t* z32) {

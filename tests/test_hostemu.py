@@ -22,6 +22,8 @@ def he():
     lib = ctypes.CDLL(HE_PATH)
     lib.he_verify.argtypes = [ctypes.c_char_p] * 3 + [ctypes.c_uint32]
     lib.he_sha512_p64.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p]
+    lib.he_sha512_p64_at.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32,
+                                     ctypes.c_void_p]
     lib.he_blake2b256.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p]
     lib.he_sc_reduce.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
     lib.he_sign.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
@@ -80,6 +82,9 @@ def test_hashes_and_scalars(he):
         m = bytes(rnd.getrandbits(8) for _ in range(n))
         he.he_sha512_p64(pre, m, n, out)
         assert out.raw == hashlib.sha512(pre + m).digest()
+        for shift in (1, 2, 3, 5, 13):  # unaligned messages through the 128-byte block loader
+            he.he_sha512_p64_at(pre, m, n, shift, out)
+            assert out.raw == hashlib.sha512(pre + m).digest(), (n, shift)
     g = of.load_golden("hash_vectors.json")
     for v in g["blake2b256"]:
         m = bytes.fromhex(v["msg"])

@@ -6,6 +6,7 @@ import ctypes
 import hashlib
 import os
 import random
+import struct
 
 import numpy as np
 import pytest
@@ -89,12 +90,82 @@ def test_recoding_identity(he, c, bits):
                 assert d[2 * w + 1] >= 0
 
 
+def _chacha20_block_py(key, counter, nonce):
+    """RFC 8439 section 2.3, written out from the RFC text (test reference)"""
+    def rotl(v, n):
+        return ((v << n) | (v >> (32 - n))) & 0xFFFFFFFF
+
+    def qr(x, a, b, c, d):
+        x[a] = (x[a] + x[b]) & 0xFFFFFFFF; x[d] = rotl(x[d] ^ x[a], 16)
+        x[c] = (x[c] + x[d]) & 0xFFFFFFFF; x[b] = rotl(x[b] ^ x[c], 12)
+        x[a] = (x[a] + x[b]) & 0xFFFFFFFF; x[d] = rotl(x[d] ^ x[a], 8)
+        x[c] = (x[c] + x[d]) & 0xFFFFFFFF; x[b] = rotl(x[b] ^ x[c], 7)
+
+    s = [0x61707865, 0x3320646e, 0x79622d32, 0x6b206574] + list(struct.unpack("<8I", key)) + [counter] + \
+        list(struct.unpack("<3I", nonce))
+    x = list(s)
+    for _ in range(10):
+        qr(x, 0, 4, 8, 12); qr(x, 1, 5, 9, 13); qr(x, 2, 6, 10, 14); qr(x, 3, 7, 11, 15)
+        qr(x, 0, 5, 10, 15); qr(x, 1, 6, 11, 12); qr(x, 2, 7, 8, 13); qr(x, 3, 4, 9, 14)
+    return struct.pack("<16I", *[(a + b) & 0xFFFFFFFF for a, b in zip(x, s)])
+
+
+# RFC 8439 section 2.3.2 test vector (key 00..1f, counter 1, nonce 00:00:00:09:00:00:00:4a:00:00:00:00)
+RFC8439_BLOCK = bytes.fromhex(
+    "10f1e7e4d13b5915500fdd1fa32071c4c7d1f4c733c068030422aa9ac3d46c4e"
+    "d2826446079faa0914c2d705d98b02a2b5129cd1de164eb9cbd083e8a2503c4e")
+
+
+def _openssl_chacha20(key, counter, nonce):
+    """independent implementation: OpenSSL's EVP_chacha20 keystream (None if unavailable)"""
+    try:
+        lib = ctypes.CDLL("libcrypto.so.3")
+    except OSError:
+        return None
+    lib.EVP_CIPHER_CTX_new.restype = ctypes.c_void_p
+    lib.EVP_chacha20.restype = ctypes.c_void_p
+    lib.EVP_EncryptInit_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_char_p,
+                                       ctypes.c_char_p]
+    lib.EVP_EncryptUpdate.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int),
+                                      ctypes.c_char_p, ctypes.c_int]
+    lib.EVP_CIPHER_CTX_free.argtypes = [ctypes.c_void_p]
+    ctx = lib.EVP_CIPHER_CTX_new()
+    iv = struct.pack("<I", counter) + nonce
+    assert lib.EVP_EncryptInit_ex(ctx, lib.EVP_chacha20(), None, key, iv) == 1
+    out = ctypes.create_string_buffer(64)
+    n = ctypes.c_int(0)
+    assert lib.EVP_EncryptUpdate(ctx, out, ctypes.byref(n), bytes(64), 64) == 1
+    lib.EVP_CIPHER_CTX_free(ctx)
+    return out.raw
+
+
+def test_chacha20_block(he):
+    """the coefficient PRF's block function: RFC 8439 vector, the RFC's algorithm in Python, and
+    OpenSSL's ChaCha20 keystream on random keys / counters / nonces"""
+    he.he_chacha20_block.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_void_p]
+    out = ctypes.create_string_buffer(64)
+    key, nonce = bytes(range(32)), bytes.fromhex("000000090000004a00000000")
+    assert _chacha20_block_py(key, 1, nonce) == RFC8439_BLOCK
+    he.he_chacha20_block(key, 1, nonce, out)
+    assert out.raw == RFC8439_BLOCK
+    rnd = random.Random(8439)
+    for _ in range(20):
+        key, nonce, ctr = rnd.randbytes(32), rnd.randbytes(12), rnd.getrandbits(32)
+        he.he_chacha20_block(key, ctr, nonce, out)
+        assert out.raw == _chacha20_block_py(key, ctr, nonce)
+        ossl = _openssl_chacha20(key, ctr, nonce)
+        if ossl is not None:
+            assert out.raw == ossl
+
+
 def test_z_prf(he):
+    """z_i = first 16 bytes of ChaCha20(key = seed, counter = low word of i, nonce = high word of
+    i || "nwv-" || "z128")"""
     out = ctypes.create_string_buffer(32)
     seed = bytes(range(32))
     for i in (0, 1, 2**32 + 5, 123456789):
         he.he_msm_z(seed, i, out)
-        want = hashlib.sha512(seed + i.to_bytes(8, "little") + b"nwv-z128").digest()[:16]
+        want = _chacha20_block_py(seed, i & 0xFFFFFFFF, struct.pack("<I", i >> 32) + b"nwv-z128")[:16]
         assert out.raw == want + bytes(16)
 
 
