@@ -134,9 +134,11 @@ NWV_HD void msm_split(MsmLayout& L, int first, int count, int total_bits) {
 }
 
 // base width c (6..16) -> layout; false if it does not fit MSM_MAX_WINDOWS
-NWV_HD bool msm_make_layout(int c, MsmLayout& L) {
+// c_lo bounds the widths of the z range (every point has digits there), c_hi those above it
+// (only the A points and B: far fewer entries when a keyed batch has few distinct keys)
+NWV_HD bool msm_make_layout2(int c_lo, int c_hi, MsmLayout& L) {
     const int lo_bits = MSM_BITS_Z + 1, hi_bits = MSM_BITS_FULL + 1 - lo_bits;
-    const int nz = (lo_bits + c - 1) / c, nh = (hi_bits + c - 1) / c;
+    const int nz = (lo_bits + c_lo - 1) / c_lo, nh = (hi_bits + c_hi - 1) / c_hi;
     if (nz + nh > MSM_MAX_WINDOWS) return false;
     L.nw = nz + nh;
     L.nw_z = nz;
@@ -156,6 +158,7 @@ NWV_HD bool msm_make_layout(int c, MsmLayout& L) {
     L.pad = 0;
     return true;
 }
+NWV_HD bool msm_make_layout(int c, MsmLayout& L) { return msm_make_layout2(c, c, L); }
 
 // raw bits [pos, pos + width) of a 256-bit little-endian scalar (width <= 16)
 NWV_HD uint32_t msm_window_bits(const uint32_t s[8], int pos, int width) {

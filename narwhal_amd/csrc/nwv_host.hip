@@ -174,16 +174,19 @@ MsmPlan msm_plan(size_t n, size_t na) {
     p.na = na;
     p.np = (uint64_t)na + 1 + n;
     double best = 1e300;
-    for (int c = 6; c <= 15; c++) {
-        MsmLayout L;
-        if (!msm_make_layout(c, L)) continue;
-        const double entries = (double)(na + 1) * L.nw + (double)n * L.nw_z;
-        const double cost = 7.0 * entries + 18.0 * L.kbase[L.nw];
-        if (cost < best) {
-            best = cost;
-            p.lay = L;
+    // window widths: ~7 field multiplies per bucket entry against ~18 per bucket (running sums),
+    // chosen separately for the z range (all na + 1 + n points) and the range above it (na + 1)
+    for (int c_lo = 6; c_lo <= 15; c_lo++)
+        for (int c_hi = 3; c_hi <= 15; c_hi++) {
+            MsmLayout L;
+            if (!msm_make_layout2(c_lo, c_hi, L)) continue;
+            const double entries = (double)(na + 1) * L.nw + (double)n * L.nw_z;
+            const double cost = 7.0 * entries + 18.0 * L.kbase[L.nw];
+            if (cost < best) {
+                best = cost;
+                p.lay = L;
+            }
         }
-    }
     p.chunk_pts = (uint32_t)std::max<uint64_t>(8192, (p.np + 63) / 64);
     p.chunks = (uint32_t)((p.np + p.chunk_pts - 1) / p.chunk_pts);
     p.nkeys = p.lay.kbase[p.lay.nw];
