@@ -406,6 +406,12 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_bucket(
     uint32_t kend = key + 1 < nkeys ? kstart[key + 1] : E;
     bool head = kstart[key] < k0;
     ge_p3 acc = ge_p3_identity();
+    // kend of the next key (kstart[key + 2]) is read after every step, so closing a segment does
+    // not wait for a load of its own: some lane of a wave closes one almost every step (buckets
+    // average ~24 entries at 65,536 signatures)
+    const uint32_t klim = nkeys - 1;
+    auto next_end = [&]() { return kstart[key + 2 < klim ? key + 2 : klim]; };
+    uint32_t pf_val = next_end();
     // add entry k (record w, index word v); close the key segment when it ends here
     const uint32_t zero = 0u - (T >> 31);  // T < 2^31: all-zero, opaque to the compiler
     auto step = [&](const uint32_t* w, uint32_t v, uint32_t k) {
@@ -415,10 +421,12 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_bucket(
             acc = ge_p3_identity();
             head = false;
             if (k + 1 < k1) {
-                do {  // next non-empty key
+                kend = key + 2 < nkeys ? pf_val : E;
+                key++;
+                while (kend <= k + 1) {  // empty keys (sparse batches)
                     key++;
                     kend = key + 1 < nkeys ? kstart[key + 1] : E;
-                } while (kend <= k + 1);
+                }
             }
         }
     };
@@ -437,10 +445,12 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_bucket(
         const uint32_t vc = at(k + 2);
         msm_load_raw(pts, vb, wb);
         step(wa, va, k);
+        pf_val = next_end();
         if (k + 1 >= k1) break;
         const uint32_t vd = at(k + 3);
         msm_load_raw(pts, vc, wa);
         step(wb, vb, k + 1);
+        pf_val = next_end();
         if (k + 2 >= k1) break;
         va = vc;
         vb = vd;
