@@ -183,11 +183,23 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("NWV_BENCH_ONE_DEVICE") == "1":
+        local = 0  # rehearsal of the multi-rank path on a one-GPU box (ranks share device 0)
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist
-        dist.init_process_group("gloo")  # host-side barrier / max only: no data-path collective
+        # host-side barrier / max only: no data-path collective.  Gloo prints its connection
+        # messages on fd 1; they go to stderr so stdout carries only the result line.
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
 
     import narwhal_amd
     from narwhal_amd import _lib
