@@ -1,0 +1,337 @@
+// fe_row.h -- GF(2^255-19) spread over a 16-lane DPP row, for latency-bound point chains.
+//
+// The batch MSM ends in one dependent chain: the Horner over the window sums (~250 doublings
+// plus one addition per window, SURVEY §8a a9: the reference's batch::Verifier computes the
+// same multiscalar sum on one CPU core).  That chain runs on a single wave, where a lane-local
+// field multiply (100 v_mad_u64_u32 on ten 26/25-bit limbs, fe25519.h) is pure issue latency.
+// Here one field element lives on one row of 16 lanes, lane k holding limb k of radix 2^16, so
+// a multiply is a 16-step cyclic convolution (2^256 = 38 mod p) with one 64-bit multiply-add per
+// lane per step, and the four rows of a wave compute the four independent multiplies of a
+// doubling or an addition at once.  Row data movement is DPP within a row (row_shr / row_shl /
+// row_share / row_ror) and the gfx950 permlane16/32 swaps across rows (gather4).
+//
+// The code is generic over the lane type so the same functions run on the host for tests:
+//   device:  V = uint32_t (this lane), M = bool, DPP / permlane builtins;
+//   host:    V = 64 lanes of one wave, every operation checked for 32/64-bit overflow
+//            (tests/hostemu, NWV_BOUNDS_CHECK), DPP / permlane emulated with the semantics
+//            measured on gfx950 (tools/probe/dpp_probe.hip).
+//
+// Magnitudes: mul() takes operands with limbs a_k, b_k such that the column sums fit (checked
+// on the host): in practice "loose" limbs <= 2^17.7.  Its output has limbs < 2^16 + 2^11 on
+// lanes 1..15 and < 2^17 on lane 0 (three carry passes).  sub uses 8p, whose limbs (>= 2^18)
+// dominate any loose limb.
+#pragma once
+#include "fe25519.h"
+
+namespace nwv {
+namespace rowf {
+
+#if defined(__HIP_DEVICE_COMPILE__)
+
+using V = uint32_t;
+using V64 = uint64_t;
+using M = bool;
+__device__ __forceinline__ V lane_id() { return __lane_id(); }
+__device__ __forceinline__ V bc(uint32_t x) { return x; }
+__device__ __forceinline__ V mul24(V a, V b) { return __umul24(a, b); }
+__device__ __forceinline__ V mul32(V a, V b) { return a * b; }
+__device__ __forceinline__ V64 mad64(V a, V b, V64 c) { return (uint64_t)a * b + c; }
+__device__ __forceinline__ V64 zero64() { return 0; }
+__device__ __forceinline__ V lo16(V64 x) { return (uint32_t)x & 0xFFFFu; }
+__device__ __forceinline__ V shr16(V64 x) { return (uint32_t)(x >> 16); }
+__device__ __forceinline__ V sel(M m, V a, V b) { return m ? b : a; }
+__device__ __forceinline__ M row_is(int q) { return ((__lane_id() >> 4) & 3) == (uint32_t)q; }
+__device__ __forceinline__ M limb_is(int k) { return (__lane_id() & 15) == (uint32_t)k; }
+template <int R>
+__device__ __forceinline__ V shr(V x) { return (V)__builtin_amdgcn_mov_dpp((int)x, 0x110 + R, 0xF, 0xF, true); }
+template <int R>
+__device__ __forceinline__ V shl(V x) { return (V)__builtin_amdgcn_mov_dpp((int)x, 0x100 + R, 0xF, 0xF, true); }
+template <int R>
+__device__ __forceinline__ V share(V x) { return (V)__builtin_amdgcn_mov_dpp((int)x, 0x150 + R, 0xF, 0xF, true); }
+__device__ __forceinline__ V ror1(V x) { return (V)__builtin_amdgcn_mov_dpp((int)x, 0x121, 0xF, 0xF, true); }
+// v_permlane16_swap: old.rows(1,3) <-> src.rows(0,2);  v_permlane32_swap: old.rows(2,3) <-> src.rows(0,1)
+__device__ __forceinline__ void swap16(V& a, V& b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+    a = r[0];
+    b = r[1];
+}
+__device__ __forceinline__ void swap32(V& a, V& b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+    a = r[0];
+    b = r[1];
+}
+// per-lane LDS / memory access
+__device__ __forceinline__ V ld(const uint32_t* base, V idx) { return base[idx]; }
+__device__ __forceinline__ void st(uint32_t* base, V idx, V x, M m) {
+    if (m) base[idx] = x;
+}
+
+#else  // host emulation of one wave
+
+#include <cstdio>
+#include <cstdlib>
+
+struct V {
+    uint32_t l[64];
+};
+struct V64 {
+    uint64_t l[64];
+};
+struct M {
+    bool l[64];
+};
+#define NWV_ROW_FOR for (int i = 0; i < 64; i++)
+inline void row_check(bool ok) {
+    if (!ok) {
+        fprintf(stderr, "fe_row: magnitude overflow\n");
+        abort();
+    }
+}
+inline V bc(uint32_t x) { V r; NWV_ROW_FOR r.l[i] = x; return r; }
+inline V lane_id() { V r; NWV_ROW_FOR r.l[i] = (uint32_t)i; return r; }
+inline V operator+(V a, V b) {
+    V r;
+    NWV_ROW_FOR { const uint64_t s = (uint64_t)a.l[i] + b.l[i]; row_check(s >> 32 == 0); r.l[i] = (uint32_t)s; }
+    return r;
+}
+inline V operator-(V a, V b) {
+    V r;
+    NWV_ROW_FOR { row_check(a.l[i] >= b.l[i]); r.l[i] = a.l[i] - b.l[i]; }
+    return r;
+}
+inline V operator&(V a, uint32_t m) { V r; NWV_ROW_FOR r.l[i] = a.l[i] & m; return r; }
+inline V operator>>(V a, int s) { V r; NWV_ROW_FOR r.l[i] = a.l[i] >> s; return r; }
+inline V mul24(V a, V b) {
+    V r;
+    NWV_ROW_FOR {
+        row_check(a.l[i] < (1u << 24) && b.l[i] < (1u << 24));
+        const uint64_t p = (uint64_t)a.l[i] * b.l[i];
+        row_check(p >> 32 == 0);
+        r.l[i] = (uint32_t)p;
+    }
+    return r;
+}
+inline V mul32(V a, V b) {
+    V r;
+    NWV_ROW_FOR { const uint64_t p = (uint64_t)a.l[i] * b.l[i]; row_check(p >> 32 == 0); r.l[i] = (uint32_t)p; }
+    return r;
+}
+inline V64 zero64() { V64 r; NWV_ROW_FOR r.l[i] = 0; return r; }
+inline V64 mad64(V a, V b, V64 c) {
+    V64 r;
+    NWV_ROW_FOR {
+        const unsigned __int128 s = (unsigned __int128)a.l[i] * b.l[i] + c.l[i];
+        row_check((s >> 64) == 0);
+        r.l[i] = (uint64_t)s;
+    }
+    return r;
+}
+inline V lo16(V64 x) { V r; NWV_ROW_FOR r.l[i] = (uint32_t)x.l[i] & 0xFFFFu; return r; }
+// the device takes bits 16..47 of the column: the column must stay below 2^48
+inline V shr16(V64 x) { V r; NWV_ROW_FOR { row_check(x.l[i] >> 48 == 0); r.l[i] = (uint32_t)(x.l[i] >> 16); } return r; }
+inline V sel(M m, V a, V b) { V r; NWV_ROW_FOR r.l[i] = m.l[i] ? b.l[i] : a.l[i]; return r; }
+inline M row_is(int q) { M m; NWV_ROW_FOR m.l[i] = ((i >> 4) & 3) == q; return m; }
+inline M limb_is(int k) { M m; NWV_ROW_FOR m.l[i] = (i & 15) == k; return m; }
+template <int R>
+inline V shr(V x) { V r; NWV_ROW_FOR r.l[i] = (i & 15) >= R ? x.l[i - R] : 0u; return r; }
+template <int R>
+inline V shl(V x) { V r; NWV_ROW_FOR r.l[i] = (i & 15) + R <= 15 ? x.l[i + R] : 0u; return r; }
+template <int R>
+inline V share(V x) { V r; NWV_ROW_FOR r.l[i] = x.l[(i & ~15) + R]; return r; }
+inline V ror1(V x) { V r; NWV_ROW_FOR r.l[i] = x.l[(i & ~15) + (((i & 15) + 15) & 15)]; return r; }
+inline void swap16(V& a, V& b) {
+    V ra = a, rb = b;
+    NWV_ROW_FOR {
+        const int row = i >> 4, j = i & 15;
+        if (row & 1) ra.l[i] = b.l[(row - 1) * 16 + j];  // old rows 1,3 <- src rows 0,2
+        else rb.l[i] = a.l[(row + 1) * 16 + j];          // src rows 0,2 <- old rows 1,3
+    }
+    a = ra;
+    b = rb;
+}
+inline void swap32(V& a, V& b) {
+    V ra = a, rb = b;
+    NWV_ROW_FOR {
+        if (i >= 32) ra.l[i] = b.l[i - 32];  // old rows 2,3 <- src rows 0,1
+        else rb.l[i] = a.l[i + 32];          // src rows 0,1 <- old rows 2,3
+    }
+    a = ra;
+    b = rb;
+}
+inline V ld(const uint32_t* base, V idx) { V r; NWV_ROW_FOR r.l[i] = base[idx.l[i]]; return r; }
+inline void st(uint32_t* base, V idx, V x, M m) { NWV_ROW_FOR if (m.l[i]) base[idx.l[i]] = x.l[i]; }
+#undef NWV_ROW_FOR
+
+#endif
+
+// ---- field operations on a row -------------------------------------------------------------
+
+struct RowConsts {
+    V w15;  // carry-out weight: 38 on limb 15 (2^256 = 38 mod p), 1 elsewhere
+    V k8p;  // limb k of 8p: 8 * (0xFFED | 0xFFFF | 0x7FFF)
+    M r1, r2, r3;
+};
+NWV_HD RowConsts row_consts() {
+    RowConsts c;
+    c.w15 = sel(limb_is(15), bc(1), bc(38));
+    c.k8p = sel(limb_is(0), sel(limb_is(15), bc(8u * 0xFFFFu), bc(8u * 0x7FFFu)), bc(8u * 0xFFEDu));
+    c.r1 = row_is(1);
+    c.r2 = row_is(2);
+    c.r3 = row_is(3);
+    return c;
+}
+
+// value of row q selected per row: row 0 a, row 1 b, row 2 c, row 3 d
+NWV_HD V rowsel(const RowConsts& k, V a, V b, V c, V d) { return sel(k.r3, sel(k.r2, sel(k.r1, a, b), c), d); }
+
+// x0..x3 <- row q's element of x, broadcast to every row (3 permlane swaps)
+NWV_HD void gather4(V x, V& x0, V& x1, V& x2, V& x3) {
+    V a = x, b = x;
+    swap16(a, b);  // a = [x0 x0 x2 x2], b = [x1 x1 x3 x3]
+    V a2 = a, b2 = b;
+    swap32(a, a2);  // a = [x0 x0 x0 x0], a2 = [x2 x2 x2 x2]
+    swap32(b, b2);
+    x0 = a;
+    x1 = b;
+    x2 = a2;
+    x3 = b2;
+}
+
+// one carry pass over 32-bit limbs: limb k keeps 16 bits and receives limb k-1's carry (limb 0
+// receives 38 x limb 15's); needs limbs < 2^32 and carries < 2^24 / 38
+NWV_HD V carry32(V x, const RowConsts& k) { return (x & 0xFFFFu) + ror1(mul24(x >> 16, k.w15)); }
+
+NWV_HD V sub(V a, V b, const RowConsts& k) { return a + k.k8p - b; }
+
+template <int R>
+NWV_HD void mul_step(V a, V a38, V b, V64& acc) {
+    // lane k: a_{k-R} (k >= R) or 38 a_{k-R+16} (k < R), times b_R
+    acc = mad64(shr<R>(a) + shl<16 - R>(a38), share<R>(b), acc);
+}
+
+// a * b mod p (every row its own product)
+NWV_HD V mul(V a, V b, const RowConsts& k) {
+    const V a38 = mul24(a, bc(38));
+    V64 acc = mad64(a, share<0>(b), zero64());
+    mul_step<1>(a, a38, b, acc);
+    mul_step<2>(a, a38, b, acc);
+    mul_step<3>(a, a38, b, acc);
+    mul_step<4>(a, a38, b, acc);
+    mul_step<5>(a, a38, b, acc);
+    mul_step<6>(a, a38, b, acc);
+    mul_step<7>(a, a38, b, acc);
+    mul_step<8>(a, a38, b, acc);
+    mul_step<9>(a, a38, b, acc);
+    mul_step<10>(a, a38, b, acc);
+    mul_step<11>(a, a38, b, acc);
+    mul_step<12>(a, a38, b, acc);
+    mul_step<13>(a, a38, b, acc);
+    mul_step<14>(a, a38, b, acc);
+    mul_step<15>(a, a38, b, acc);
+    // first pass on the 64-bit columns (< 2^48): limb 15's carry x38 stays < 2^32
+    const V x = lo16(acc) + ror1(mul32(shr16(acc), k.w15));
+    return carry32(carry32(x, k), k);
+}
+
+// ---- points: every row holds the whole point (X, Y, Z, T one V each) ------------------------
+
+struct RowP3 {
+    V X, Y, Z, T;
+};
+
+// completed (X1 : Y1 : Z1 : T1) -> extended: rows compute X1 T1, Y1 Z1, Z1 T1, X1 Y1
+NWV_HD RowP3 row_complete(V X1, V Y1, V Z1, V T1, const RowConsts& k) {
+    const V o1 = carry32(rowsel(k, X1, Y1, Z1, X1), k);
+    const V o2 = carry32(rowsel(k, T1, Z1, T1, Y1), k);
+    RowP3 r;
+    gather4(mul(o1, o2, k), r.X, r.Y, r.Z, r.T);
+    return r;
+}
+
+// [2] p: rows square X, Y, Z, X + Y (T of the input unused)
+NWV_HD RowP3 row_dbl(const RowP3& p, const RowConsts& k) {
+    const V in = rowsel(k, p.X, p.Y, p.Z, p.X + p.Y);
+    V XX, YY, ZZ, S;
+    gather4(mul(in, in, k), XX, YY, ZZ, S);
+    const V Y1 = YY + XX;
+    const V Z1 = carry32(sub(YY, XX, k), k);
+    const V X1 = sub(S, Y1, k);
+    const V T1 = sub(ZZ + ZZ, Z1, k);
+    return row_complete(X1, Y1, Z1, T1, k);
+}
+
+// p + q, q in cached form held row-wise: row 0 Y+X, row 1 Y-X, row 2 2dT, row 3 2Z (limbs < 2^16)
+NWV_HD RowP3 row_add_cached(const RowP3& p, V qc, const RowConsts& k) {
+    const V in = carry32(rowsel(k, p.Y + p.X, sub(p.Y, p.X, k), p.T, p.Z), k);
+    V PP, MM, TT, ZZ;
+    gather4(mul(in, qc, k), PP, MM, TT, ZZ);
+    return row_complete(sub(PP, MM, k), PP + MM, ZZ + TT, sub(ZZ, TT, k), k);
+}
+
+// Horner over the window sums of an MSM layout on one wave, then [8]:
+//   d = W_{nw-1};  d = [2^width[w]] d + W_w  for w = nw-2 .. 0;  d = [8] d.
+// cq: [nw][4][16] row limbs of each window sum in cached form (Y+X | Y-X | 2dT | 2Z);
+// top: [4][16] row limbs of W_{nw-1} (X | Y | Z | T).  Row 0 writes d's X | Y | Z limbs to
+// out[0..48).
+template <class Layout>
+NWV_HD void row_horner(const uint32_t* cq, const uint32_t* top, const Layout& lay, uint32_t* out) {
+    const RowConsts k = row_consts();
+    const V lane = lane_id() & 63u;
+    const V limb = lane & 15u;
+    RowP3 d{ld(top, limb), ld(top, limb + bc(16)), ld(top, limb + bc(32)), ld(top, limb + bc(48))};
+#pragma unroll 1
+    for (int w = lay.nw - 2; w >= 0; w--) {
+#pragma unroll 1
+        for (int i = 0; i < lay.width[w]; i++) d = row_dbl(d, k);
+        d = row_add_cached(d, ld(cq, bc(64u * (uint32_t)w) + lane), k);
+    }
+#pragma unroll 1
+    for (int i = 0; i < 3; i++) d = row_dbl(d, k);
+    const M r0 = row_is(0);
+    st(out, limb, d.X, r0);
+    st(out, limb + bc(16), d.Y, r0);
+    st(out, limb + bc(32), d.Z, r0);
+}
+
+}  // namespace rowf
+
+// ---- conversions between the lane-local ten-limb form and 16-bit row limbs ----------------
+
+// 16 limbs of 16 bits (value < 2^256) of a field element, from its canonical words
+NWV_HD void fe_to_limbs16(const fe& a, uint32_t out[16]) {
+    uint32_t w[8];
+    fe_freeze(a, w);
+#pragma unroll
+    for (int k = 0; k < 16; k++) out[k] = (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+}
+// field element from 16 loose limbs (each < 2^32): sum x_k 2^(16k) reduced below 2^255
+NWV_HD fe fe_from_limbs16(const uint32_t x[16]) {
+    uint32_t y[16];
+    uint64_t t = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        t += x[k];
+        y[k] = (uint32_t)t & 0xFFFFu;
+        t >>= 16;
+    }
+    // fold 2^256 = 38 (t < 2^17), then bit 255 (2^255 = 19), twice each to settle the carries
+#pragma unroll 1
+    for (int it = 0; it < 2; it++) {
+        uint64_t c = t * 38 + (uint64_t)(y[15] >> 15) * 19;
+        y[15] &= 0x7FFFu;
+        t = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            c += y[k];
+            y[k] = (uint32_t)c & 0xFFFFu;
+            c >>= 16;
+        }
+        t = c;
+    }
+    uint32_t w[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) w[j] = y[2 * j] | (y[2 * j + 1] << 16);
+    return fe_from_words(w);
+}
+
+}  // namespace nwv

@@ -16,11 +16,13 @@
 //   k_msm_fixup     lane per bucket: joins the pieces of buckets that span chunks
 //   k_msm_window    workgroup per window: sum_b b S_b (segment running sums + LDS suffix scan
 //                   + LDS tree), 256 lanes
-//   k_msm_final     Horner over windows, [8], identity test -> batch verdict word
+//   k_msm_final     Horner over windows on 16-lane rows (fe_row.h), [8], identity test ->
+//                   batch verdict word
 // The counting sort keeps every histogram / cursor atomic in LDS; the only global atomics are
 // the (rare) failure flags.  Entry order inside a bucket depends on LDS atomic order, which
 // changes the projective representation of a bucket sum but never the group element, so the
 // verdict is deterministic.
+#include "fe_row.h"
 #include "msm.h"
 
 using namespace nwv;
@@ -527,75 +529,37 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_window(MsmLayout lay, co
     if (g == 0) store_p3(wsum + (size_t)P3_WORDS * w, x);
 }
 
-// ---- the window Horner on a lane quad ----------------------------------------------------
-// The Horner over windows is one chain of ~241 doublings.  Each doubling's four squarings
-// (X^2, Y^2, Z^2, (X+Y)^2) and the three multiplies of its completed->projective step are
-// independent, so lane q of a quad computes the q-th one and the results are broadcast back with
-// DPP quad_perm moves: the chain issues 1 squaring + 1 multiply per doubling instead of 4 + 3.
-namespace {
-template <int SRC>
-__device__ __forceinline__ fe quad_bcast(const fe& a) {
-    constexpr int ctrl = SRC | (SRC << 2) | (SRC << 4) | (SRC << 6);
-    fe r;
-#pragma unroll
-    for (int i = 0; i < 10; i++) r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.v[i], ctrl, 0xF, 0xF, false);
-    return r;
-}
-__device__ __forceinline__ fe pick4(int q, const fe& a, const fe& b, const fe& c, const fe& d) {
-    return fe_select(fe_select(a, b, q == 1), fe_select(c, d, q == 3), q >= 2);
-}
-// r <- [2^k] r, every lane of the quad holding the whole point
-__device__ __forceinline__ ge_p2 quad_dbl_n(ge_p2 r, int k, int q) {
-#pragma unroll 1
-    for (int i = 0; i < k; i++) {
-        const fe sq = fe_sq(pick4(q, r.X, r.Y, r.Z, fe_add(r.X, r.Y)));
-        const fe XX = quad_bcast<0>(sq), YY = quad_bcast<1>(sq), ZZ = quad_bcast<2>(sq), S = quad_bcast<3>(sq);
-        const fe Y1 = fe_carry(fe_add(YY, XX));
-        const fe Z1 = fe_carry(fe_sub(YY, XX));
-        const fe X1 = fe_sub(S, Y1);
-        const fe T1 = fe_sub(fe_carry(fe_add(ZZ, ZZ)), Z1);
-        const fe m = fe_mul(pick4(q, X1, Y1, Z1, Z1), pick4(q, T1, Z1, T1, T1));
-        r.X = quad_bcast<0>(m);
-        r.Y = quad_bcast<1>(m);
-        r.Z = quad_bcast<2>(m);
-    }
-    return r;
-}
-// p (projective, Z != 0 representation of an extended point) + q (extended), result extended
-__device__ __forceinline__ ge_p3 quad_add(const ge_p3& p, const ge_p3& o, int q) {
-    const ge_cached c = ge_p3_to_cached(o);
-    // PP = (Y+X)(Y'+X'), MM = (Y-X)(Y'-X'), TT2d = T * 2dT', ZZ2 = Z * 2Z'
-    const fe m1 = fe_mul(pick4(q, fe_add(p.Y, p.X), fe_sub(p.Y, p.X), p.T, p.Z),
-                         pick4(q, c.YpX, c.YmX, c.T2d, c.Z2));
-    const fe PP = quad_bcast<0>(m1), MM = quad_bcast<1>(m1), TT = quad_bcast<2>(m1), ZZ = quad_bcast<3>(m1);
-    const fe X1 = fe_sub(PP, MM), Y1 = fe_add(PP, MM), Z1 = fe_add(ZZ, TT), T1 = fe_sub(ZZ, TT);
-    const fe m2 = fe_mul(pick4(q, X1, Y1, Z1, X1), pick4(q, T1, Z1, T1, Y1));
-    return ge_p3{quad_bcast<0>(m2), quad_bcast<1>(m2), quad_bcast<2>(m2), quad_bcast<3>(m2)};
-}
-}  // namespace
-
-// Horner over windows, [8], identity: *verdict = 1 iff accepted and nothing failed.  One wave;
-// every quad runs the same chain (lane 0 writes the verdict).
+// Horner over windows, [8], identity: *verdict = 1 iff accepted and nothing failed.  One wave:
+// lanes w < nw convert window sum w to cached form and 16-bit row limbs (LDS), then the chain
+// runs row-parallel (fe_row.h): each doubling / addition is two levels of four multiplies, one
+// per row, each spread over the row's 16 lanes.
 extern "C" __global__ void __launch_bounds__(64) k_msm_final(MsmLayout lay, const uint32_t* __restrict__ wsum,
                                                              const uint32_t* __restrict__ fail,
                                                              uint32_t* __restrict__ verdict) {
-    const int q = threadIdx.x & 3;
-    const int nw = lay.nw;
-    ge_p3 d = load_p3(wsum + (size_t)P3_WORDS * (nw - 1));
-#pragma unroll 1
-    for (int w = nw - 2; w >= 0; w--) {
-        ge_p2 r = quad_dbl_n(ge_p3_to_p2(d), lay.width[w] - 1, q);
-        // last doubling left completed, then -> extended (4 multiplies on the quad)
-        const fe sq = fe_sq(pick4(q, r.X, r.Y, r.Z, fe_add(r.X, r.Y)));
-        const fe XX = quad_bcast<0>(sq), YY = quad_bcast<1>(sq), ZZ = quad_bcast<2>(sq), S = quad_bcast<3>(sq);
-        const fe Y1 = fe_carry(fe_add(YY, XX));
-        const fe Z1 = fe_carry(fe_sub(YY, XX));
-        const fe X1 = fe_sub(S, Y1);
-        const fe T1 = fe_sub(fe_carry(fe_add(ZZ, ZZ)), Z1);
-        const fe m = fe_mul(pick4(q, X1, Y1, Z1, X1), pick4(q, T1, Z1, T1, Y1));
-        d = ge_p3{quad_bcast<0>(m), quad_bcast<1>(m), quad_bcast<2>(m), quad_bcast<3>(m)};
-        d = quad_add(d, load_p3(wsum + (size_t)P3_WORDS * w), q);
+    __shared__ uint32_t cq[MSM_MAX_WINDOWS * 64];
+    __shared__ uint32_t top[64];
+    __shared__ uint32_t fin[48];
+    const int t = threadIdx.x, nw = lay.nw;
+    if (t < nw) {
+        const ge_p3 p = load_p3(wsum + (size_t)P3_WORDS * t);
+        const ge_cached c = ge_p3_to_cached(p);
+        fe_to_limbs16(c.YpX, cq + 64 * t);
+        fe_to_limbs16(c.YmX, cq + 64 * t + 16);
+        fe_to_limbs16(c.T2d, cq + 64 * t + 32);
+        fe_to_limbs16(c.Z2, cq + 64 * t + 48);
+        if (t == nw - 1) {
+            fe_to_limbs16(p.X, top);
+            fe_to_limbs16(p.Y, top + 16);
+            fe_to_limbs16(p.Z, top + 32);
+            fe_to_limbs16(p.T, top + 48);
+        }
     }
-    const bool ok = p3_mul8_is_identity(d) && *fail == 0;
-    if (threadIdx.x == 0) *verdict = ok ? 1u : 0u;
+    __syncthreads();
+    rowf::row_horner(cq, top, lay, fin);
+    __syncthreads();
+    if (t == 0) {
+        const fe X = fe_from_limbs16(fin), Y = fe_from_limbs16(fin + 16), Z = fe_from_limbs16(fin + 32);
+        const bool ok = fe_is_zero(X) && fe_eq(Y, Z) && *fail == 0;
+        *verdict = ok ? 1u : 0u;
+    }
 }

@@ -43,9 +43,11 @@ constexpr size_t MSG_PAD = 64;  // over-read slack after every message arena
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
+    bool view = false;  // p points into another buffer (the staging arena): never freed here
     int ensure(size_t bytes) {
         if (bytes <= cap) return NWV_OK;
-        if (p) (void)hipFree(p);
+        if (p && !view) (void)hipFree(p);
+        view = false;
         p = nullptr;
         cap = 0;
         size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
@@ -58,12 +60,43 @@ struct DevBuf {
         return NWV_OK;
     }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p && !view) (void)hipFree(p);
         p = nullptr;
         cap = 0;
+        view = false;
+    }
+    void set_view(void* base, size_t bytes) {
+        release();
+        p = base;
+        cap = bytes;
+        view = true;
     }
     template <class T>
     T* as() const { return static_cast<T*>(p); }
+};
+
+// Pinned host staging buffer: inputs are packed here and cross PCIe in one DMA
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return NWV_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 16);
+        if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) {
+            p = nullptr;
+            return set_err(NWV_ERR_OOM, "hipHostMalloc");
+        }
+        cap = want;
+        return NWV_OK;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
 };
 
 // Device-resident inputs + intermediates of one Ed25519 batch: the per-signature pipeline
@@ -74,11 +107,12 @@ struct EdBuffers {
         m_bsum, m_wsum;
     // keyed batches: distinct keys (m x 32), CSR of signatures by key, per-signature z_i k_i
     DevBuf keys, koff, ksig, m_ascal;
+    DevBuf in;  // staging arena: pk, sig, off, len, m_state and msg are views into it
     size_t nkeys_distinct = 0;  // 0: every signature is its own A point
     void release() {
         for (DevBuf* b : {&pk, &sig, &msg, &off, &len, &kbuf, &flags, &tables, &verdict, &m_scal,
                           &m_partial, &m_state, &m_pts, &m_digits, &m_cnt, &m_tiles, &m_entries,
-                          &m_kstart, &m_hpart, &m_bsum, &m_wsum, &keys, &koff, &ksig, &m_ascal})
+                          &m_kstart, &m_hpart, &m_bsum, &m_wsum, &keys, &koff, &ksig, &m_ascal, &in})
             b->release();
         nkeys_distinct = 0;
     }
@@ -91,6 +125,8 @@ struct Device {
     std::mutex mu;
     DevBuf btab;
     EdBuffers ed;
+    PinnedBuf hstage;              // host side of ed_stage's single H2D copy
+    hipEvent_t hstage_ev = nullptr;  // recorded after that copy; hstage is reusable once it fires
     DevBuf b2_base, b2_off, b2_len, b2_out, b2_packed, b2_plen, b2_err;
 };
 
@@ -107,6 +143,7 @@ int device_open(Device& d, int ordinal) {
         return set_err(NWV_ERR_NODEV, std::string("device is ") + prop.gcnArchName + ", need gfx950");
     NWV_HIP(hipSetDevice(ordinal));
     NWV_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    NWV_HIP(hipEventCreateWithFlags(&d.hstage_ev, hipEventDisableTiming));
     int rc = d.btab.ensure((BASE_TABLE_WORDS + CACHED_ENTRY_WORDS) * sizeof(uint32_t));
     if (rc) return rc;
     hipLaunchKernelGGL(k_base_table, dim3((BASE_TABLE_ENTRIES + 63) / 64), dim3(64), 0, d.stream,
@@ -122,6 +159,9 @@ void device_close(Device& d) {
     if (d.stream) (void)hipStreamSynchronize(d.stream);
     d.btab.release();
     d.ed.release();
+    d.hstage.release();
+    if (d.hstage_ev) (void)hipEventDestroy(d.hstage_ev);
+    d.hstage_ev = nullptr;
     for (DevBuf* b : {&d.b2_base, &d.b2_off, &d.b2_len, &d.b2_out, &d.b2_packed, &d.b2_plen, &d.b2_err})
         b->release();
     if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -234,20 +274,20 @@ constexpr int MSM_NEVENTS = MSM_NKERNELS + 1;  // one event before each kernel, 
 // Launch the batch MSM on resident buffers; the verdict word (1 = batch accepted) is
 // m_state[1] (m_state[0] = failure flags).  ev: MSM_NEVENTS events or null.
 int msm_launch(Device& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStream_t stream,
-               hipEvent_t* ev) {
+               hipEvent_t* ev, bool state_ready) {
     if (n == 0) return NWV_OK;
     const size_t na = b.nkeys_distinct ? b.nkeys_distinct : n;
     const MsmPlan p = msm_plan(n, na);
     int rc = msm_alloc(b, p, n);
     if (rc) return rc;
     uint32_t* state = b.m_state.as<uint32_t>();  // [0] fail flags, [1] verdict, [8..16) seed
-    if (seed32) NWV_HIP(hipMemcpyAsync(state + 8, seed32, 32, hipMemcpyHostToDevice, stream));
+    if (seed32 && !state_ready) NWV_HIP(hipMemcpyAsync(state + 8, seed32, 32, hipMemcpyHostToDevice, stream));
     const unsigned nblk = (unsigned)((n + 255) / 256);
     auto mark = [&](int k) -> int {
         if (ev) NWV_HIP(hipEventRecord(ev[k], stream));
         return NWV_OK;
     };
-    NWV_HIP(hipMemsetAsync(state, 0, 8, stream));
+    if (!state_ready) NWV_HIP(hipMemsetAsync(state, 0, 8, stream));
     if ((rc = mark(0))) return rc;
     int16_t* digits = b.m_digits.as<int16_t>();
     const int keyed = b.nkeys_distinct ? 1 : 0;
@@ -307,39 +347,63 @@ int msm_launch(Device& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipS
 }
 
 // Stage host inputs [lo, hi) onto buffers b of device d (message region rebased).  pk/sig
-// may be null (signing stages seeds separately).
+// may be null (signing stages seeds separately).  Everything is packed into the pinned host
+// buffer and crosses PCIe as ONE async copy into b.in on d.stream (pk, sig, off, len, msg and,
+// with seed32, the MSM state words are views into it); no synchronisation here: work on other
+// streams must wait for d.stream.  seed32 (optional): m_state = {0 flags, 0 verdict, .., seed}
+// so that msm_launch(state_ready) needs neither a memset nor a seed copy.
 int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, const uint8_t* sig,
-             const uint8_t* msg_base, const uint64_t* msg_off, const uint32_t* msg_len) {
+             const uint8_t* msg_base, const uint64_t* msg_off, const uint32_t* msg_len,
+             const uint8_t* seed32) {
     const size_t n = hi - lo;
-    if (!pk || !sig) {
-        int rc;
-        if ((rc = b.pk.ensure(32 * n + 16)) || (rc = b.sig.ensure(64 * n + 16))) return rc;
-    }
     uint64_t mlo = UINT64_MAX, mhi = 0;
     for (size_t i = lo; i < hi; i++) {
         mlo = std::min<uint64_t>(mlo, msg_off[i]);
         mhi = std::max<uint64_t>(mhi, msg_off[i] + msg_len[i]);
     }
     if (n == 0 || mhi < mlo) { mlo = 0; mhi = 0; }
-    std::vector<uint64_t> off(n);
-    for (size_t i = 0; i < n; i++) off[i] = msg_off[lo + i] - mlo;
     const size_t mbytes = (size_t)(mhi - mlo);
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const bool inputs = pk && sig;
+    const size_t o_pk = 0, o_sig = o_pk + (inputs ? up(32 * n + 16) : 0);
+    const size_t o_off = o_sig + (inputs ? up(64 * n + 16) : 0), o_len = o_off + up(8 * n + 8);
+    const size_t o_state = o_len + up(4 * n + 4), o_msg = o_state + 256, total = o_msg + mbytes + MSG_PAD;
     int rc;
-    if ((rc = b.pk.ensure(32 * n + 16)) || (rc = b.sig.ensure(64 * n + 16)) ||
-        (rc = b.msg.ensure(mbytes + MSG_PAD)) || (rc = b.off.ensure(8 * n + 8)) ||
-        (rc = b.len.ensure(4 * n + 4)) || (rc = b.kbuf.ensure(32 * n + 16)) ||
-        (rc = b.flags.ensure(4 * n + 4)) ||
+    if ((rc = b.in.ensure(total)) || (rc = b.kbuf.ensure(32 * n + 16)) || (rc = b.flags.ensure(4 * n + 4)) ||
         (rc = b.tables.ensure((size_t)LANE_SCRATCH_WORDS * 4 * n + 16)) ||
         (rc = b.verdict.ensure(8 * ((n + 63) / 64) + 8)))
         return rc;
-    if (pk) NWV_HIP(hipMemcpyAsync(b.pk.p, pk + 32 * lo, 32 * n, hipMemcpyHostToDevice, d.stream));
-    if (sig) NWV_HIP(hipMemcpyAsync(b.sig.p, sig + 64 * lo, 64 * n, hipMemcpyHostToDevice, d.stream));
-    if (mbytes)
-        NWV_HIP(hipMemcpyAsync(b.msg.p, msg_base + mlo, mbytes, hipMemcpyHostToDevice, d.stream));
-    NWV_HIP(hipMemsetAsync(b.msg.as<uint8_t>() + mbytes, 0, MSG_PAD, d.stream));
-    NWV_HIP(hipMemcpyAsync(b.off.p, off.data(), 8 * n, hipMemcpyHostToDevice, d.stream));
-    NWV_HIP(hipMemcpyAsync(b.len.p, msg_len + lo, 4 * n, hipMemcpyHostToDevice, d.stream));
-    NWV_HIP(hipStreamSynchronize(d.stream));  // `off` is a host temporary
+    // views into the arena are stale once it may have moved: drop the ones not re-pointed below
+    if (!inputs && b.pk.view) b.pk.release();
+    if (!inputs && b.sig.view) b.sig.release();
+    if (!seed32 && b.m_state.view) b.m_state.release();
+    if (!inputs && ((rc = b.pk.ensure(32 * n + 16)) || (rc = b.sig.ensure(64 * n + 16)))) return rc;
+    // the previous call's copy must have left the pinned buffer before it is rewritten
+    NWV_HIP(hipEventSynchronize(d.hstage_ev));
+    if ((rc = d.hstage.ensure(total))) return rc;
+    uint8_t* h = static_cast<uint8_t*>(d.hstage.p);
+    if (inputs) {
+        std::memcpy(h + o_pk, pk + 32 * lo, 32 * n);
+        std::memcpy(h + o_sig, sig + 64 * lo, 64 * n);
+    }
+    uint64_t* hoff = reinterpret_cast<uint64_t*>(h + o_off);
+    for (size_t i = 0; i < n; i++) hoff[i] = msg_off[lo + i] - mlo;
+    std::memcpy(h + o_len, msg_len + lo, 4 * n);
+    std::memset(h + o_state, 0, 256);
+    if (seed32) std::memcpy(h + o_state + 32, seed32, 32);
+    if (mbytes) std::memcpy(h + o_msg, msg_base + mlo, mbytes);
+    std::memset(h + o_msg + mbytes, 0, MSG_PAD);
+    NWV_HIP(hipMemcpyAsync(b.in.p, h, total, hipMemcpyHostToDevice, d.stream));
+    NWV_HIP(hipEventRecord(d.hstage_ev, d.stream));
+    uint8_t* g = b.in.as<uint8_t>();
+    if (inputs) {
+        b.pk.set_view(g + o_pk, 32 * n + 16);
+        b.sig.set_view(g + o_sig, 64 * n + 16);
+    }
+    b.off.set_view(g + o_off, 8 * n + 8);
+    b.len.set_view(g + o_len, 4 * n + 4);
+    b.msg.set_view(g + o_msg, mbytes + MSG_PAD);
+    if (seed32) b.m_state.set_view(g + o_state, 256);
     b.nkeys_distinct = 0;
     return NWV_OK;
 }
@@ -371,7 +435,7 @@ int ed_stage_keyed(Device& d, EdBuffers& b, size_t lo, size_t hi, size_t n_keys,
     for (size_t k = 0; k < m; k++) koff[k + 1] = koff[k] + cnt[k];
     cur.assign(koff.begin(), koff.end() - 1);
     for (size_t i = 0; i < n; i++) ksig[cur[kid[i]]++] = (uint32_t)i;
-    int rc = ed_stage(d, b, 0, n, pk.data(), sig + 64 * lo, msg_base, msg_off + lo, msg_len + lo);
+    int rc = ed_stage(d, b, 0, n, pk.data(), sig + 64 * lo, msg_base, msg_off + lo, msg_len + lo, nullptr);
     if (rc) return rc;
     if ((rc = b.keys.ensure(32 * m + 32)) || (rc = b.koff.ensure(4 * m + 8)) || (rc = b.ksig.ensure(4 * n + 8)))
         return rc;
@@ -525,7 +589,7 @@ int nwv_ed25519_verify_each(nwv_ctx* ctx, size_t n, const uint8_t* pk, const uin
     for (size_t i = 0; i < n; i++)
         if (msg_len[i] && !msg_base) return set_err(NWV_ERR_ARG, "null msg_base");
     return for_shards(ctx, n, [&](Device& d, size_t lo, size_t hi) -> int {
-        int rc = ed_stage(d, d.ed, lo, hi, pk, sig, msg_base, msg_off, msg_len);
+        int rc = ed_stage(d, d.ed, lo, hi, pk, sig, msg_base, msg_off, msg_len, nullptr);
         if (rc) return rc;
         if ((rc = ed_launch(d, d.ed, hi - lo, d.stream, nullptr))) return rc;
         const size_t words = (hi - lo + 63) / 64;
@@ -569,12 +633,12 @@ static void set_ones(uint64_t* bits, size_t lo, size_t hi) {
 // Batch verdict of resident buffers: MSM, then (only if it rejects) the per-signature fallback
 // for the exact bad set.  bits: the shard's verdict words (may be null).
 static int batch_on_device(Device& d, EdBuffers& b, size_t n, const uint8_t seed[32], hipStream_t stream,
-                           int* ok, uint64_t* bits) {
+                           int* ok, uint64_t* bits, bool state_ready = false) {
     int rc;
     const bool use_msm = (d.flags & NWV_FLAG_MSM_ALWAYS) ||
                          (!(d.flags & NWV_FLAG_MSM_NEVER) && n >= msm_min_n());
     if (use_msm) {
-        if ((rc = msm_launch(d, b, n, seed, stream, nullptr))) return rc;
+        if ((rc = msm_launch(d, b, n, seed, stream, nullptr, state_ready))) return rc;
         uint32_t st[2] = {0, 0};
         NWV_HIP(hipMemcpyAsync(st, b.m_state.p, 8, hipMemcpyDeviceToHost, stream));
         NWV_HIP(hipStreamSynchronize(stream));
@@ -615,15 +679,15 @@ int nwv_ed25519_verify_batch(nwv_ctx* ctx, size_t n, const uint8_t* pk, const ui
     std::vector<int> oks(ctx->devs.size(), 1);
     std::mutex omu;
     int rc = for_shards(ctx, n, [&](Device& d, size_t lo, size_t hi) -> int {
-        int r = ed_stage(d, d.ed, lo, hi, pk, sig, msg_base, msg_off, msg_len);
-        if (r) return r;
         // each shard gets its own coefficient stream: seed' = seed with the shard start mixed in
         uint8_t s2[32];
         std::memcpy(s2, seed, 32);
         for (int k = 0; k < 8; k++) s2[24 + k] ^= (uint8_t)((uint64_t)lo >> (8 * k));
+        int r = ed_stage(d, d.ed, lo, hi, pk, sig, msg_base, msg_off, msg_len, s2);
+        if (r) return r;
         int ok = 1;
         r = batch_on_device(d, d.ed, hi - lo, s2, d.stream, &ok,
-                            verdict_bits_or_null ? verdict_bits_or_null + lo / 64 : nullptr);
+                            verdict_bits_or_null ? verdict_bits_or_null + lo / 64 : nullptr, true);
         if (r) return r;
         std::lock_guard<std::mutex> g(omu);
         if (!ok) *all_valid = 0;
@@ -760,6 +824,7 @@ static int staged_create(nwv_ctx* ctx, int device_index, size_t n, nwv_staged** 
     std::lock_guard<std::mutex> g(st->dev->mu);
     int rc = with_device(*st->dev);
     if (!rc) rc = stage(*st->dev, st->buf);
+    if (!rc && hipStreamSynchronize(st->dev->stream) != hipSuccess) rc = set_err(NWV_ERR_HIP, "stage sync");
     if (!rc && hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking) != hipSuccess)
         rc = set_err(NWV_ERR_HIP, "hipStreamCreate");
     for (auto& e : st->ev)
@@ -779,7 +844,7 @@ int nwv_stage_ed25519(nwv_ctx* ctx, int device_index, size_t n, const uint8_t* p
                       const uint8_t* sig, const uint8_t* msg_base, const uint64_t* msg_off,
                       const uint32_t* msg_len, nwv_staged** out) {
     return staged_create(ctx, device_index, n, out, [&](Device& d, EdBuffers& b) {
-        return ed_stage(d, b, 0, n, pk, sig, msg_base, msg_off, msg_len);
+        return ed_stage(d, b, 0, n, pk, sig, msg_base, msg_off, msg_len, nullptr);
     });
 }
 
@@ -816,7 +881,7 @@ static int staged_graph(nwv_staged* st, Device& d) {
     if (st->graph || st->graph_failed) return NWV_OK;
     hipGraph_t g = nullptr;
     NWV_HIP(hipStreamBeginCapture(st->stream, hipStreamCaptureModeThreadLocal));
-    const int rc = msm_launch(d, st->buf, st->n, nullptr, st->stream, nullptr);
+    const int rc = msm_launch(d, st->buf, st->n, nullptr, st->stream, nullptr, false);
     const hipError_t e = hipStreamEndCapture(st->stream, &g);
     if (rc || e != hipSuccess || !g || hipGraphInstantiate(&st->graph, g, nullptr, nullptr, 0) != hipSuccess) {
         st->graph = nullptr;
@@ -845,7 +910,7 @@ int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]) {
         } else {
             // first run of the batch (allocates its buffers) or a timed run; an untimed first run
             // also captures the graph the later runs replay
-            rc = msm_launch(d, st->buf, st->n, seed, st->stream, timed ? st->ev : nullptr);
+            rc = msm_launch(d, st->buf, st->n, seed, st->stream, timed ? st->ev : nullptr, false);
             if (!rc && !timed && st->n) rc = staged_graph(st, d);
         }
     } else {
@@ -1069,7 +1134,7 @@ int nwv_ed25519_sign_many(nwv_ctx* ctx, size_t n, const uint8_t* seeds, const ui
     if (!msg_base) msg_base = empty;
     return for_shards(ctx, n, [&](Device& d, size_t lo, size_t hi) -> int {
         // messages via the Ed25519 staging; seeds go to kbuf, outputs come back in pk / sig
-        int rc = ed_stage(d, d.ed, lo, hi, nullptr, nullptr, msg_base, msg_off, msg_len);
+        int rc = ed_stage(d, d.ed, lo, hi, nullptr, nullptr, msg_base, msg_off, msg_len, nullptr);
         if (rc) return rc;
         const size_t m = hi - lo;
         NWV_HIP(hipMemcpyAsync(d.ed.kbuf.p, seeds + 32 * lo, 32 * m, hipMemcpyHostToDevice, d.stream));

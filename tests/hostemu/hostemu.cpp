@@ -10,6 +10,7 @@ unsigned long long nwv_count_mul = 0, nwv_count_sq = 0;
 
 #include "../../narwhal_amd/csrc/blake2b.h"
 #include "../../narwhal_amd/csrc/ed25519_lane.h"
+#include "../../narwhal_amd/csrc/fe_row.h"
 #include "../../narwhal_amd/csrc/msm.h"
 
 using namespace nwv;
@@ -25,6 +26,35 @@ static void ensure_btab() {
 }
 
 static void words(const uint8_t* p, uint32_t w[8]) { std::memcpy(w, p, 32); }
+
+// k_msm_final on the host: window sums -> cached row limbs (as the kernel's LDS), the row Horner
+// of fe_row.h on the emulated wave, then [8] d == identity.  xyz (optional): canonical words of
+// the X | Y | Z that row 0 hands back.
+static bool row_final_host(const MsmLayout& lay, const uint32_t* ws, uint32_t* xyz) {
+    std::vector<uint32_t> cq((size_t)MSM_MAX_WINDOWS * 64, 0), top(64, 0), fin(48, 0);
+    for (int t = 0; t < lay.nw; t++) {
+        const ge_p3 p = load_p3(ws + (size_t)P3_WORDS * t);
+        const ge_cached c = ge_p3_to_cached(p);
+        fe_to_limbs16(c.YpX, cq.data() + 64 * t);
+        fe_to_limbs16(c.YmX, cq.data() + 64 * t + 16);
+        fe_to_limbs16(c.T2d, cq.data() + 64 * t + 32);
+        fe_to_limbs16(c.Z2, cq.data() + 64 * t + 48);
+        if (t == lay.nw - 1) {
+            fe_to_limbs16(p.X, top.data());
+            fe_to_limbs16(p.Y, top.data() + 16);
+            fe_to_limbs16(p.Z, top.data() + 32);
+            fe_to_limbs16(p.T, top.data() + 48);
+        }
+    }
+    rowf::row_horner(cq.data(), top.data(), lay, fin.data());
+    const fe X = fe_from_limbs16(fin.data()), Y = fe_from_limbs16(fin.data() + 16), Z = fe_from_limbs16(fin.data() + 32);
+    if (xyz) {
+        fe_freeze(X, xyz);
+        fe_freeze(Y, xyz + 8);
+        fe_freeze(Z, xyz + 8 * 2);
+    }
+    return fe_is_zero(X) && fe_eq(Y, Z);
+}
 
 extern "C" {
 
@@ -257,6 +287,8 @@ int he_msm_batch(size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t*
         d = p3_add(d, load_p3(ws.data() + (size_t)P3_WORDS * w));
     }
     const bool eq = p3_mul8_is_identity(d);
+    // the kernel's row-parallel Horner must reach the same verdict
+    if (row_final_host(lay, ws.data(), nullptr) != eq) return -2;
     if (counts) {
         counts[0] = nwv_count_mul;
         counts[1] = nwv_count_sq;
@@ -317,6 +349,49 @@ void he_msm_point_counts(const uint8_t* pk, const uint8_t* sig, unsigned long lo
     msm_store_point(e, P);
     counts[0] = nwv_count_mul;
     counts[1] = nwv_count_sq;
+}
+
+// one field multiply on the emulated wave: a, b given as 16 loose limbs (same in every row);
+// out = row 0's product limbs.  Returns 0 when the four rows disagree.
+int he_row_mul(const uint32_t* a16, const uint32_t* b16, uint32_t* out16) {
+    rowf::V a, b;
+    for (int i = 0; i < 64; i++) {
+        a.l[i] = a16[i & 15];
+        b.l[i] = b16[i & 15];
+    }
+    const rowf::V r = rowf::mul(a, b, rowf::row_consts());
+    for (int i = 0; i < 64; i++)
+        if (r.l[i] != r.l[i & 15]) return 0;
+    for (int k = 0; k < 16; k++) out16[k] = r.l[k];
+    return 1;
+}
+
+// Horner over nw window sums W_w = decompress(pts[w]) (widths[w] bits each): the row path of
+// k_msm_final (xyz_row) against the lane-local chain (xyz_ref), both after [8]; canonical words
+// of X | Y | Z.  Returns -1 if a point does not decode, else the row path's identity verdict.
+int he_row_horner(int nw, const uint8_t* widths, const uint8_t* pts, uint32_t* xyz_row, uint32_t* xyz_ref) {
+    MsmLayout lay{};
+    lay.nw = nw;
+    for (int w = 0; w < nw; w++) lay.width[w] = widths[w];
+    std::vector<uint32_t> ws((size_t)P3_WORDS * nw);
+    for (int w = 0; w < nw; w++) {
+        uint32_t pw[8];
+        words(pts + 32 * w, pw);
+        ge_p3 P;
+        if (!ge_decompress(pw, P)) return -1;
+        store_p3(ws.data() + (size_t)P3_WORDS * w, P);
+    }
+    const bool id = row_final_host(lay, ws.data(), xyz_row);
+    ge_p3 d = load_p3(ws.data() + (size_t)P3_WORDS * (nw - 1));
+    for (int w = nw - 2; w >= 0; w--) {
+        d = p3_dbl_n(d, lay.width[w]);
+        d = p3_add(d, load_p3(ws.data() + (size_t)P3_WORDS * w));
+    }
+    d = p3_dbl_n(d, 3);
+    fe_freeze(d.X, xyz_ref);
+    fe_freeze(d.Y, xyz_ref + 8);
+    fe_freeze(d.Z, xyz_ref + 16);
+    return id ? 1 : 0;
 }
 
 }  // extern "C"
