@@ -140,6 +140,43 @@ def split_prep_times(args, pk, sg, msgs, offs, lens, reps=5):
         e.close()
 
 
+def pmc_kernel(kernel, n):
+    """(counters, source) of `kernel` in the newest committed rocprofv3 --pmc summary at batch
+    size n, or (None, None)"""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        k = d.get("kernels", {}).get(kernel)
+        if d.get("n") == n and k:
+            return k, os.path.relpath(f, ROOT)
+    return None, None
+
+
+def valu_issue_entry(kname, kt, n, peak):
+    """VALU instruction throughput of `kernel`: SQ_INSTS_VALU per launch (wave-level
+    instructions, committed PMC pass) over the live event-timed duration, against the
+    full-rate 32-bit VALU issue peak measured on the box (v_add_u32 lane-ops/s / 64 lanes)."""
+    insts, src = 0.0, None
+    for part in kname.split("+"):  # "k_msm_bucket+fixup" is timed as one span
+        k, src = pmc_kernel(part if part.startswith("k_") else "k_msm_" + part, n)
+        if not k or "SQ_INSTS_VALU" not in k:
+            return None
+        insts += k["SQ_INSTS_VALU"]
+    kms = float(kt.get(kname, 0.0))
+    if not peak or kms <= 0:
+        return None
+    rate = insts / (kms * 1e-3) / 1e9
+    pk = peak["v_add_u32_per_s"] / 64 / 1e9
+    return {"kernel": kname, "insts_per_launch": insts, "achieved": rate,
+            "peak": pk, "unit": "G wave-VALU-instr/s", "frac": rate / pk, "source": src,
+            "note": "every VALU instruction priced at the full 32-bit rate; v_mad_u64_u32 "
+                    "issues at about half that rate, so this understates the busy fraction"}
+
+
 def pmc_traffic(kernel, n):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc pass (FETCH_SIZE
     doubled for gfx950's half-counted wide reads + WRITE_SIZE, MI355X_MICROARCH.md HBM section),
@@ -170,7 +207,7 @@ def main():
     ap.add_argument("--mode", type=int, default=1, help="1 batch MSM (K5), 0 per-signature pipeline")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--latency-reps", type=int, default=300)
+    ap.add_argument("--latency-reps", type=int, default=1000)
     ap.add_argument("--inflight", type=int, default=12,
                     help="resident batches in flight on separate streams (step s runs batch s %% K)")
     ap.add_argument("--keys", type=int, default=0,
@@ -295,6 +332,8 @@ def main():
                                   f"{npts} points per launch; the SHA-512 hashing in the same grid "
                                   "is not counted", args.n)
             roof["kernel_ms"] = kt
+            roof["valu_issue"] = {kn: valu_issue_entry(kn, kt, args.n, peak)
+                                  for kn in ("k_msm_prep", "k_msm_bucket+fixup")}
             kt_split = split_prep_times(args, pk, sg, msgs, offs, lens)
             roof["decompression_alone"] = roofline_entry(
                 "k_msm_points", kt_split, mads(OPS_MSM_POINTS) // 2 * npts, peak_t,
