@@ -111,40 +111,62 @@ NWV_HD void sha512_init(sha512_state& s) {
     for (int i = 0; i < 8; i++) s.h[i] = u64p{IV[2 * i], IV[2 * i + 1]};
 }
 
-// One compression; w[16] are the block's big-endian 64-bit words (consumed in place).
-NWV_HD void sha512_compress(sha512_state& s, u64p w[16]) {
-    u64p a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3];
-    u64p e = s.h[4], f = s.h[5], g = s.h[6], h = s.h[7];
-    // 5 groups of 16 rounds: the group loop stays rolled (its round constants are uniform
-    // scalar loads), the 16 rounds inside are unrolled so the w[] window has constant indices
-    // and lives in registers
+// One compression; w[16] are the block's big-endian 64-bit words (consumed in place).  Inside,
+// words are 64-bit values: additions are single v_lshl_add_u64 (no VCC carry chain), rotates
+// are two v_alignbit_b32 on the halves.
+NWV_HD uint64_t rotr64(uint64_t x, int n) {
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    const u64p r = rotr(u64p{lo, hi}, n);
+    return ((uint64_t)r.hi << 32) | r.lo;
+}
+NWV_HD uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
+    return ((uint64_t)xor3_32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) << 32) |
+           xor3_32((uint32_t)a, (uint32_t)b, (uint32_t)c);
+}
+NWV_HD uint64_t bitop3_64(uint64_t a, uint64_t b, uint64_t c, int tt) {
+    return ((uint64_t)bitop3_32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), tt) << 32) |
+           bitop3_32((uint32_t)a, (uint32_t)b, (uint32_t)c, tt);
+}
+NWV_HD uint64_t j64(u64p x) { return ((uint64_t)x.hi << 32) | x.lo; }
+#define NWV_SHA_ROUND(r, wr)                                                                   \
+    do {                                                                                       \
+        const uint64_t S1 = xor3_64(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41));              \
+        const uint64_t kr = ((uint64_t)SHA512_K32[2 * (r) + 1] << 32) | SHA512_K32[2 * (r)];    \
+        const uint64_t t1 = h + S1 + bitop3_64(e, f, g, 0xCA) + kr + (wr);                     \
+        const uint64_t S0 = xor3_64(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39));              \
+        const uint64_t t2 = S0 + bitop3_64(a, b, c, 0xE8);                                     \
+        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;                     \
+    } while (0)
+
+NWV_HD void sha512_compress(sha512_state& s, u64p win[16]) {
+    uint64_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) w[i] = j64(win[i]);
+    uint64_t a = j64(s.h[0]), b = j64(s.h[1]), c = j64(s.h[2]), d = j64(s.h[3]);
+    uint64_t e = j64(s.h[4]), f = j64(s.h[5]), g = j64(s.h[6]), h = j64(s.h[7]);
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        NWV_SHA_ROUND(j, w[j]);
+        if ((j & 3) == 3) NWV_SEQ();
+    }
 #pragma unroll 1
-    for (int grp = 0; grp < 5; grp++) {
+    for (int grp = 1; grp < 5; grp++) {
 #pragma unroll
         for (int j = 0; j < 16; j++) {
-            u64p wr;
-            if (grp == 0) {
-                wr = w[j];
-            } else {
-                const u64p w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
-                const u64p s0 = xor3(rotr(w15, 1), rotr(w15, 8), shr(w15, 7));
-                const u64p s1 = xor3(rotr(w2, 19), rotr(w2, 61), shr(w2, 6));
-                wr = add(add(w[j], s0), add(w[(j + 9) & 15], s1));
-                w[j] = wr;
-            }
-            const int r = 16 * grp + j;
-            const u64p S1 = xor3(rotr(e, 14), rotr(e, 18), rotr(e, 41));
-            const u64p kr = u64p{SHA512_K32[2 * r], SHA512_K32[2 * r + 1]};
-            const u64p t1 = add(add(add(h, S1), add(ch(e, f, g), kr)), wr);
-            const u64p S0 = xor3(rotr(a, 28), rotr(a, 34), rotr(a, 39));
-            const u64p t2 = add(S0, maj(a, b, c));
-            h = g; g = f; f = e; e = add(d, t1); d = c; c = b; b = a; a = add(t1, t2);
-            if ((j & 3) == 3) NWV_SEQ();  // keep the schedule expansion from running ahead
+            const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+            const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), w15 >> 7);
+            const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), w2 >> 6);
+            const uint64_t wr = w[j] + s0 + w[(j + 9) & 15] + s1;
+            w[j] = wr;
+            NWV_SHA_ROUND(16 * grp + j, wr);
+            if ((j & 3) == 3) NWV_SEQ();
         }
     }
-    s.h[0] = add(s.h[0], a); s.h[1] = add(s.h[1], b); s.h[2] = add(s.h[2], c); s.h[3] = add(s.h[3], d);
-    s.h[4] = add(s.h[4], e); s.h[5] = add(s.h[5], f); s.h[6] = add(s.h[6], g); s.h[7] = add(s.h[7], h);
+    const uint64_t o[8] = {a, b, c, d, e, f, g, h};
+#pragma unroll
+    for (int i = 0; i < 8; i++) s.h[i] = add(s.h[i], u64p{(uint32_t)o[i], (uint32_t)(o[i] >> 32)});
 }
+#undef NWV_SHA_ROUND
 
 // stream word at byte position pos: v = raw little-endian word, trimmed to `total` bytes and
 // carrying the 0x80 terminator when the stream ends inside it
