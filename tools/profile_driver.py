@@ -20,8 +20,11 @@ def main():
     ap.add_argument("--msg-len", type=int, default=512)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--mode", type=int, default=0, help="0 per-signature pipeline, 1 batch MSM")
+    ap.add_argument("--split", action="store_true",
+                    help="hash and decompression as separate kernels (NWV_FLAG_MSM_SPLIT_PREP)")
     args = ap.parse_args()
-    eng = narwhal_amd.Engine(device=0)
+    from narwhal_amd import _lib
+    eng = narwhal_amd.Engine(device=0, flags=_lib.NWV_FLAG_MSM_SPLIT_PREP if args.split else 0)
     pk, sg, msgs, offs, lens = bench.synth(eng, args.n, args.msg_len, seed=7)
     st = eng.stage(pk, sg, msgs, offs, lens)
     for r in range(args.reps):

@@ -46,6 +46,43 @@ __global__ void __launch_bounds__(256) k_mullo(void* outp, uint32_t a0, int iter
     if (s == 0x1234567) ((decltype(s)*)outp)[0] = s;
 }
 
+// gfx950 64-bit integer forms used by the field and SHA-512 code (SQ_INSTS_VALU_INT64 class)
+__global__ void __launch_bounds__(256) k_add64(void* outp, uint32_t a0, int iters) {
+    uint64_t acc[CH];
+    for (int c = 0; c < CH; c++) acc[c] = c + threadIdx.x;
+    const uint64_t b = a0 + blockIdx.x;
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+        for (int c = 0; c < CH; c++) asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(acc[c]) : "v"(b));
+    }
+    uint64_t s = 0;
+    for (int c = 0; c < CH; c++) s ^= acc[c];
+    if (s == 0x1234567) ((decltype(s)*)outp)[0] = s;
+}
+__global__ void __launch_bounds__(256) k_shr64(void* outp, uint32_t a0, int iters) {
+    uint64_t acc[CH];
+    for (int c = 0; c < CH; c++) acc[c] = c + threadIdx.x + ((uint64_t)a0 << 40);
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+        for (int c = 0; c < CH; c++) asm volatile("v_lshrrev_b64 %0, 1, %0" : "+v"(acc[c]));
+    }
+    uint64_t s = 0;
+    for (int c = 0; c < CH; c++) s ^= acc[c];
+    if (s == 0x1234567) ((decltype(s)*)outp)[0] = s;
+}
+__global__ void __launch_bounds__(256) k_alignbit(void* outp, uint32_t a0, int iters) {
+    uint32_t acc[CH];
+    for (int c = 0; c < CH; c++) acc[c] = c + threadIdx.x + 1;
+    uint32_t b = a0 + blockIdx.x;
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+        for (int c = 0; c < CH; c++) asm volatile("v_alignbit_b32 %0, %1, %0, 7" : "+v"(acc[c]) : "v"(b));
+    }
+    uint32_t s = 0;
+    for (int c = 0; c < CH; c++) s ^= acc[c];
+    if (s == 0x1234567) ((decltype(s)*)outp)[0] = s;
+}
+
 template <class K>
 double rate(K kern, void* out, int iters, int blocks) {
     hipEvent_t e0, e1;
@@ -70,14 +107,18 @@ int main() {
     hipGetDeviceProperties(&p, 0);
     const int blocks = p.multiProcessorCount * 8;
     const int iters = 1 << 14;
-    double mad = 0, add = 0, mul = 0;
+    double mad = 0, add = 0, mul = 0, add64 = 0, shr64 = 0, alb = 0;
     for (int r = 0; r < 3; r++) {
         mad = std::max(mad, rate(k_mad, out, iters, blocks));
         add = std::max(add, rate(k_add, out, iters, blocks));
         mul = std::max(mul, rate(k_mullo, out, iters, blocks));
+        add64 = std::max(add64, rate(k_add64, out, iters, blocks));
+        shr64 = std::max(shr64, rate(k_shr64, out, iters, blocks));
+        alb = std::max(alb, rate(k_alignbit, out, iters, blocks));
     }
     printf("{\"device\": \"%s\", \"cus\": %d, \"clock_khz\": %d, \"v_mad_u64_u32_per_s\": %.4e, "
-           "\"v_add_u32_per_s\": %.4e, \"v_mul_lo_u32_per_s\": %.4e}\n",
-           p.gcnArchName, p.multiProcessorCount, p.clockRate, mad, add, mul);
+           "\"v_add_u32_per_s\": %.4e, \"v_mul_lo_u32_per_s\": %.4e, \"v_lshl_add_u64_per_s\": %.4e, "
+           "\"v_lshrrev_b64_per_s\": %.4e, \"v_alignbit_b32_per_s\": %.4e}\n",
+           p.gcnArchName, p.multiProcessorCount, p.clockRate, mad, add, mul, add64, shr64, alb);
     return 0;
 }
