@@ -171,10 +171,18 @@ def valu_issue_entry(kname, kt, n, peak):
         return None
     rate = insts / (kms * 1e-3) / 1e9
     pk = peak["v_add_u32_per_s"] / 64 / 1e9
-    return {"kernel": kname, "insts_per_launch": insts, "achieved": rate,
-            "peak": pk, "unit": "G wave-VALU-instr/s", "frac": rate / pk, "source": src,
-            "note": "every VALU instruction priced at the full 32-bit rate; v_mad_u64_u32 "
-                    "issues at about half that rate, so this understates the busy fraction"}
+    out = {"kernel": kname, "insts_per_launch": insts, "achieved": rate, "peak": pk,
+           "unit": "G wave-VALU-instr/s", "frac": rate / pk, "source": src,
+           "note": "frac prices every VALU instruction at the VOP2 rate (v_add_u32, a lower bound on "
+                   "the busy fraction); frac_vop3 at the measured rate of 64-bit-encoded VOP3 forms "
+                   "(v_mad_u64_u32 is one; so are v_alignbit_b32, v_lshl_add_u64, v_lshrrev_b64, "
+                   "which issue at about half the VOP2 rate): an upper bound"}
+    vop3 = [peak.get(k) for k in ("v_lshl_add_u64_per_s", "v_lshrrev_b64_per_s", "v_alignbit_b32_per_s")]
+    if all(vop3):
+        pk3 = sum(vop3) / len(vop3) / 64 / 1e9
+        out["peak_vop3"] = pk3
+        out["frac_vop3"] = rate / pk3
+    return out
 
 
 def pmc_traffic(kernel, n):
