@@ -99,6 +99,78 @@ def cpu_baseline(pk, sg, msgs, offs, lens, seconds):
                       f"oracle/nwv_oracle.c batch verifier: Pippenger/Straus as dalek)"}
 
 
+def cpu_baseline_configs(legs, data, threads):
+    """CPU legs of C1 / C4 / C5 on the host cores (the oracle: dalek's algorithms in C, the
+    reference's control flow in Python), and the check that the GPU's C4 verdict bits equal the
+    oracle's per-signature verdicts"""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import hashlib
+    from concurrent.futures import ThreadPoolExecutor
+    import oracle_ffi as of  # checker / CPU baseline only
+    import narwhal_types as nt
+
+    def ocom(c):
+        return nt.Committee(list(c.keys), list(c.stakes), c.epoch, [list(w) for w in c.workers])
+
+    def hdict(h):
+        return {"author": h.author, "round": h.round, "epoch": h.epoch, "payload": list(h.payload),
+                "parents": list(h.parents), "id": h.id, "signature": h.signature}
+
+    def cert_verify(c, cert):
+        """Certificate::verify as the reference runs it: header check, quorum, then the
+        aggregate signature as ONE batch verification (ed25519-consensus batch::Verifier)"""
+        h = hdict(cert.header)
+        r = nt.header_verify(c, h, of.verify)
+        if r:
+            return r
+        pks = [c.keys[a] for a in cert.signed_authorities]
+        if sum(c.stakes[a] for a in cert.signed_authorities) < c.quorum_threshold():
+            return nt.REQUIRES_QUORUM
+        d = nt.certificate_digest(h["id"], h["round"], h["epoch"], h["author"])
+        return 0 if of.verify_batch([(pk, s, d) for pk, s in zip(pks, cert.aggregated_signature)]) else 1
+
+    def timed(fn, reps):
+        ts = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t)
+        return float(np.median(ts)) * 1e3
+
+    out = {}
+    c1 = data["C1"]
+    com1 = ocom(c1["committee"])
+    assert cert_verify(com1, c1["cert"]) == 0
+    out["C1"] = {"certificate_verify_n4_ms": timed(lambda: cert_verify(com1, c1["cert"]), 200),
+                 "verify_batch_1024_m32_ms": timed(lambda: of.verify_batch(c1["items"]), 20), "cores": 1}
+    c4 = data["C4"]
+    pk, sig, msg, offs, lens = of.pack(c4["items"])
+    t = time.perf_counter()
+    ok = of.verify_batch_mt(pk, sig, msg, offs, lens, threads)
+    bits = of.verify_each_mt(pk, sig, msg, offs, lens, threads)
+    dt = time.perf_counter() - t
+    ref = [bool((int(bits[i >> 6]) >> (i & 63)) & 1) for i in range(len(offs))]
+    out["C4"] = {"ms_per_batch": dt * 1e3, "sigs_per_s": len(offs) / dt, "cores": threads,
+                 "batch_verdict": ok, "gpu_bits_equal_oracle": ref == list(c4["bits"])}
+    c5 = data["C5"]
+    com5 = ocom(c5["committee"])
+
+    def round_cpu():
+        assert all(cert_verify(com5, c) == 0 for c in c5["certs"])
+        assert all(nt.header_verify(com5, hdict(h), of.verify) == 0 for h in c5["headers"])
+        assert all(nt.vote_verify(com5, {"id": v.id, "round": v.round, "epoch": v.epoch, "origin": v.origin,
+                                         "author": v.author, "signature": v.signature}, of.verify) == 0
+                   for v in c5["votes"])
+    ms5 = timed(round_cpu, 3)
+    with ThreadPoolExecutor(threads) as ex:
+        msd = timed(lambda: list(ex.map(lambda b: hashlib.blake2b(b, digest_size=32).digest(), c5["batches"])), 3)
+    out["C5"] = {"verify_ms_per_round": ms5, "verify_cores": 1,
+                 "verify_sigs_per_s": legs["C5"]["signatures_per_round"] / (ms5 * 1e-3),
+                 "worker_batch_digests_ms_per_round": msd, "digest_threads": threads}
+    return out
+
+
 def roofline_entry(kname, kt, mads_launch, peak_t, algorithmic, n):
     kms = float(kt.get(kname, 0.0))
     achieved = mads_launch / (kms * 1e-3) / 1e12 if kms > 0 else None
@@ -221,6 +293,8 @@ def main():
     ap.add_argument("--keys", type=int, default=0,
                     help="distinct verifying keys (0: one per signature, the configs[1] worst case; "
                          "100: its committee variant, keyed batch MSM)")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the C1 / C4 / C5 legs (other BASELINE.json configs, GPU and CPU)")
     ap.add_argument("--single-steps", type=int, default=8,
                     help="single-stream steps timed after the run (step latency, per-kernel times)")
     args = ap.parse_args()
@@ -356,6 +430,19 @@ def main():
         cpu = None
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(pk, sg, msgs, offs, lens, args.cpu_seconds)
+        configs = None
+        if not args.no_configs:
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            import config_legs as CL
+            configs, cdata = {}, {}
+            configs["C1"], cdata["C1"] = CL.leg_c1(eng)
+            configs["C4"], cdata["C4"] = CL.leg_c4(eng)
+            configs["C5"], cdata["C5"] = CL.leg_c5(eng)
+            if not args.no_cpu_baseline:
+                threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+                for k, v in cpu_baseline_configs(configs, cdata, threads).items():
+                    configs[k]["cpu_baseline"] = v
+            del cdata
         result = {
             "metric": "Ed25519 sigs verified/sec",
             "value": value,
@@ -382,6 +469,7 @@ def main():
                                     "p99": float(np.percentile(lat, 99)), "reps": len(lat)},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "configs": configs,
             "valu_ubench": peak,
         }
         print(json.dumps(result), flush=True)

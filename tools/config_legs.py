@@ -1,0 +1,227 @@
+"""GPU legs of BASELINE.json's other configs, measured beside the headline (bench.py --configs):
+
+  C1  Certificate::verify of a 4-node committee (header signature + 3 votes), host -> host, and
+      verify_batch of 1,024 random signatures over 32-byte messages (p50 / p99);
+  C4  a 65,536-signature batch with 1 % adversarial entries: the batch MSM rejects, the
+      per-signature pipeline returns the exact verdict bits (time per batch, bad set);
+  C5  a 100-node committee DAG round: validate_certificates over 100 certificates (header
+      signature + 67 votes each), Header::verify of the 100 headers, Vote::verify of 99 votes, and
+      BLAKE2b-256 of the 100 worker batches (500,224 B each), streamed over many rounds.
+
+Fixtures are built with the product only (GPU signer, GPU digests, nwv_certificate_new); the CPU
+legs that time the oracle live in bench.py (cpu_baseline_configs)."""
+import ctypes
+import hashlib
+import time
+
+import numpy as np
+
+from narwhal_amd import _lib
+from narwhal_amd import types as T
+
+L_ORDER = 2**252 + 27742317777372353535851937790883648493
+
+
+def _seed(tag, i):
+    return hashlib.sha256(tag + i.to_bytes(4, "little")).digest()
+
+
+def _pcts(xs):
+    a = np.array(xs) * 1e3
+    return {"p50_ms": float(np.percentile(a, 50)), "p99_ms": float(np.percentile(a, 99)), "reps": len(xs)}
+
+
+def committee_fixture(eng, n, tag=b"nwv-bench-committee"):
+    seeds = [_seed(tag, i) for i in range(n)]
+    pk, _ = eng.sign_many(seeds, [b""] * n)
+    keys = [pk[32 * i:32 * i + 32].tobytes() for i in range(n)]
+    return seeds, keys, T.Committee(list(keys), [1] * n, 0, [[0, 1, 2, 3]] * n)
+
+
+def worker_batch(author, n_tx=977, tx_len=512):
+    """node/src/benchmark_client.rs:153-168 transactions: [tag u8][counter u64 BE][zero pad]"""
+    out = bytearray()
+    for c in range(n_tx):
+        tx = bytearray(tx_len)
+        tx[0] = 1 if c == 0 else 0  # sample transaction tag on the first one
+        tx[1:9] = (author * 1_000_000 + c).to_bytes(8, "big")
+        out += tx
+    return bytes(out)
+
+
+def dag_round(eng, seeds, keys, committee, payload_digests=None, parents=None):
+    """one round: every authority's header (signed), the quorum's votes, the certificates"""
+    n = len(keys)
+    q = committee.quorum_threshold()
+    if parents is None:
+        parents = T.certificate_digests(eng, T.Certificate.genesis(committee))
+    headers = []
+    for a in range(n):
+        pay = [(payload_digests[a], a % 4)] if payload_digests else []
+        headers.append(T.Header(author=keys[a], round=1, epoch=0, payload=pay, parents=list(parents)))
+    for h, d in zip(headers, T.header_digests(eng, headers)):
+        h.id = d
+    _, hs = eng.sign_many(seeds, [h.id for h in headers])
+    for a, h in enumerate(headers):
+        h.signature = hs[64 * a:64 * a + 64].tobytes()
+    voters = [[i for i in range(n) if i != a][:q] for a in range(n)]
+    votes = [T.Vote(headers[a].id, 1, 0, keys[a], keys[v]) for a in range(n) for v in voters[a]]
+    vd = T.vote_digests(eng, votes)
+    vseeds = [seeds[v] for a in range(n) for v in voters[a]]
+    _, vs = eng.sign_many(vseeds, vd)
+    for k, v in enumerate(votes):
+        v.signature = vs[64 * k:64 * k + 64].tobytes()
+    certs = []
+    for a in range(n):
+        vv = votes[a * q:(a + 1) * q]
+        certs.append(T.Certificate.new(committee, headers[a], [(v.author, v.signature) for v in vv]))
+    return headers, votes, certs
+
+
+def leg_c1(eng, reps=300):
+    seeds, keys, com = committee_fixture(eng, 4, b"nwv-bench-c1")
+    headers, votes, certs = dag_round(eng, seeds, keys, com)
+    cert = certs[-1]
+    T.verify(eng, com, cert)  # raises on any DagError
+    keep = T._Keep()
+    cc = com._c(keep)
+    carr = (T._Certificate * 1)(cert._c(keep))
+    res = (ctypes.c_int32 * 1)()
+    lib = T.lib()
+    lat = []
+    for r in range(reps + 5):
+        t = time.perf_counter()
+        rc = lib.nwv_certificate_verify_many(eng._h, ctypes.byref(cc), 1, carr, res)
+        if r >= 5:
+            lat.append(time.perf_counter() - t)
+        assert rc == 0 and res[0] == 0
+    # verify_batch of 1,024 random signatures, 32-byte messages, distinct keys
+    rng = np.random.default_rng(11)
+    n = 1024
+    bseeds = [rng.bytes(32) for _ in range(n)]
+    msgs = [rng.bytes(32) for _ in range(n)]
+    pk, sg = eng.sign_many(bseeds, msgs)
+    items = [(pk[32 * i:32 * i + 32].tobytes(), sg[64 * i:64 * i + 64].tobytes(), msgs[i]) for i in range(n)]
+    apk, asg, arena, offs, lens = _lib.soa(items)
+    allv = _lib._i32(0)
+    blat = []
+    for r in range(reps + 5):
+        t = time.perf_counter()
+        _lib._check(eng.lib.nwv_ed25519_verify_batch(eng._h, n, _lib._ptr(apk), _lib._ptr(asg), _lib._ptr(arena),
+                                                     _lib._ptr(offs), _lib._ptr(lens), bytes([r % 256]) * 32,
+                                                     ctypes.byref(allv), None))
+        assert allv.value == 1
+        if r >= 5:
+            blat.append(time.perf_counter() - t)
+    return {"certificate_verify_n4": _pcts(lat), "verify_batch_1024_m32": _pcts(blat)}, \
+        {"committee": com, "cert": cert, "items": items}
+
+
+def adversarial_batch(eng, n=65536, frac=0.01, seed=4, mlen=512):
+    """C4: n signatures, frac of them adversarial at seeded positions, categories in turn:
+    bit-flipped R, bit-flipped s, wrong message, s + l (non-canonical scalar), and the ZIP-215
+    small-order entries A = R = identity with s = 0 (accepted by the cofactored equation)"""
+    rng = np.random.default_rng(seed)
+    seeds = [rng.bytes(32) for _ in range(n)]
+    msgs = [rng.bytes(mlen) for _ in range(n)]
+    pk, sg = eng.sign_many(seeds, msgs)
+    pk, sg = pk.copy(), sg.copy()
+    pos = np.sort(rng.choice(n, size=int(n * frac), replace=False))
+    ident = np.zeros(32, dtype=np.uint8)
+    ident[0] = 1
+    cats = []
+    for j, i in enumerate(pos):
+        c = j % 5
+        cats.append(c)
+        if c == 0:
+            sg[64 * i + 3] ^= 0x10
+        elif c == 1:
+            sg[64 * i + 40] ^= 0x01
+        elif c == 2:
+            msgs[i] = bytes([msgs[i][0] ^ 0x80]) + msgs[i][1:]
+        elif c == 3:
+            s = int.from_bytes(sg[64 * i + 32:64 * i + 64].tobytes(), "little") + L_ORDER
+            sg[64 * i + 32:64 * i + 64] = np.frombuffer(s.to_bytes(32, "little"), dtype=np.uint8)
+        else:
+            pk[32 * i:32 * i + 32] = ident
+            sg[64 * i:64 * i + 32] = ident
+            sg[64 * i + 32:64 * i + 64] = 0
+    items = [(pk[32 * i:32 * i + 32].tobytes(), sg[64 * i:64 * i + 64].tobytes(), msgs[i]) for i in range(n)]
+    expect_bad = sorted(int(i) for i, c in zip(pos, cats) if c != 4)
+    return items, [int(i) for i in pos], expect_bad
+
+
+def leg_c4(eng, reps=5):
+    """host arrays already packed (as a Rust caller holds them): the timed region is the C call,
+    H2D + batch MSM + per-signature fallback + D2H"""
+    items, pos, expect_bad = adversarial_batch(eng)
+    n = len(items)
+    pk, sig, arena, offs, lens = _lib.soa(items)
+    bitsbuf = np.zeros((n + 63) // 64 + 1, dtype=np.uint64)
+    allv = _lib._i32(0)
+    ts = []
+    for r in range(reps + 1):
+        t = time.perf_counter()
+        _lib._check(eng.lib.nwv_ed25519_verify_batch(eng._h, n, _lib._ptr(pk), _lib._ptr(sig), _lib._ptr(arena),
+                                                     _lib._ptr(offs), _lib._ptr(lens), bytes([r + 1]) * 32,
+                                                     ctypes.byref(allv), _lib._ptr(bitsbuf)))
+        if r >= 1:
+            ts.append(time.perf_counter() - t)
+    ok = bool(allv.value)
+    bits = list(_lib.unpack_bits(bitsbuf, n))
+    bad = [i for i, b in enumerate(bits) if not b]
+    med = float(np.median(ts))
+    return {"n": n, "adversarial": len(pos), "batch_verdict": ok, "bad": len(bad),
+            "bad_set_equals_injected": bad == expect_bad, "ms_per_batch_host_to_host": med * 1e3,
+            "sigs_per_s": n / med}, {"items": items, "pos": pos, "bits": bits}
+
+
+def leg_c5(eng, rounds=50):
+    seeds, keys, com = committee_fixture(eng, 100, b"nwv-bench-c5")
+    batches = [worker_batch(a) for a in range(100)]
+    pd = eng.blake2b256_many(batches)
+    headers, votes, certs = dag_round(eng, seeds, keys, com, payload_digests=pd)
+    vsample = votes[:99]
+    # the C structs are built once (a Rust caller passes its own objects by pointer); the timed
+    # region is the three C calls and the digest call, each host -> host
+    ok, bad = T.validate_certificates(eng, com, certs)
+    assert ok and not bad and not any(T.verify_headers(eng, com, headers)) and not any(T.verify_votes(eng, com, vsample))
+    keep = T._Keep()
+    cc = com._c(keep)
+    carr = (T._Certificate * len(certs))(*[c._c(keep) for c in certs])
+    harr = (T._Header * len(headers))(*[h._c(keep) for h in headers])
+    varr = (T._Vote * len(vsample))(*[v._c(keep) for v in vsample])
+    hres = (ctypes.c_int32 * len(headers))()
+    vres = (ctypes.c_int32 * len(vsample))()
+    nbad = ctypes.c_size_t(0)
+    idx = (ctypes.c_size_t * len(certs))()
+    lib = T.lib()
+    blens = np.array([len(b) for b in batches], dtype=np.uint64)
+    boffs = np.zeros(len(batches), dtype=np.uint64)
+    boffs[1:] = np.cumsum(blens[:-1], dtype=np.uint64)
+    barena = np.frombuffer(b"".join(batches) + bytes(16), dtype=np.uint8)
+    bout = np.zeros(32 * len(batches), dtype=np.uint8)
+    t_sig, t_dig = [], []
+    for r in range(rounds + 2):
+        t0 = time.perf_counter()
+        rc = lib.nwv_validate_certificates(eng._h, ctypes.byref(cc), len(certs), carr, ctypes.byref(nbad), idx)
+        rh = lib.nwv_header_verify_many(eng._h, ctypes.byref(cc), len(headers), harr, hres)
+        rv = lib.nwv_vote_verify_many(eng._h, ctypes.byref(cc), len(vsample), varr, vres)
+        t1 = time.perf_counter()
+        rb = eng.lib.nwv_blake2b256_many(eng._h, len(batches), _lib._ptr(barena), _lib._ptr(boffs),
+                                         _lib._ptr(blens), _lib._ptr(bout))
+        t2 = time.perf_counter()
+        d = [bout[32 * i:32 * i + 32].tobytes() for i in range(len(batches))]
+        assert rc == rh == rv == rb == 0 and nbad.value == 0 and not any(hres) and not any(vres) and d == pd
+        if r >= 2:
+            t_sig.append(t1 - t0)
+            t_dig.append(t2 - t1)
+    nsig = sum(1 + len(c.aggregated_signature) for c in certs) + len(headers) + len(vsample)
+    ms = float(np.median(t_sig)) * 1e3
+    return {"rounds": rounds, "signatures_per_round": nsig,
+            "verify_ms_per_round": ms, "verify_sigs_per_s": nsig / (ms * 1e-3),
+            "worker_batch_digests_ms_per_round": float(np.median(t_dig)) * 1e3,
+            "note": "one round = validate_certificates(100 certs x (1 + 67) sigs) + 100 Header::verify + "
+                    "99 Vote::verify (three C calls on prepared structs, host -> host) and BLAKE2b-256 of 100 x 500,224 B "
+                    "worker batches (one GPU call)"}, \
+        {"committee": com, "certs": certs, "headers": headers, "votes": vsample, "batches": batches}
