@@ -37,6 +37,8 @@ __device__ __forceinline__ V mul24(V a, V b) { return __umul24(a, b); }
 __device__ __forceinline__ V mul32(V a, V b) { return a * b; }
 __device__ __forceinline__ V64 mad64(V a, V b, V64 c) { return (uint64_t)a * b + c; }
 __device__ __forceinline__ V64 zero64() { return 0; }
+__device__ __forceinline__ V64 add64(V64 a, V64 b) { return a + b; }
+__device__ __forceinline__ void phase_fence() { __builtin_amdgcn_sched_barrier(0); }
 __device__ __forceinline__ V lo16(V64 x) { return (uint32_t)x & 0xFFFFu; }
 __device__ __forceinline__ V shr16(V64 x) { return (uint32_t)(x >> 16); }
 __device__ __forceinline__ V sel(M m, V a, V b) { return m ? b : a; }
@@ -117,6 +119,12 @@ inline V mul32(V a, V b) {
     return r;
 }
 inline V64 zero64() { V64 r; NWV_ROW_FOR r.l[i] = 0; return r; }
+inline V64 add64(V64 a, V64 b) {
+    V64 r;
+    NWV_ROW_FOR { r.l[i] = a.l[i] + b.l[i]; row_check(r.l[i] >= a.l[i]); }
+    return r;
+}
+inline void phase_fence() {}
 inline V64 mad64(V a, V b, V64 c) {
     V64 r;
     NWV_ROW_FOR {
@@ -203,31 +211,32 @@ NWV_HD V carry32(V x, const RowConsts& k) { return (x & 0xFFFFu) + ror1(mul24(x 
 
 NWV_HD V sub(V a, V b, const RowConsts& k) { return a + k.k8p - b; }
 
-template <int R>
-NWV_HD void mul_step(V a, V a38, V b, V64& acc) {
-    // lane k: a_{k-R} (k >= R) or 38 a_{k-R+16} (k < R), times b_R
-    acc = mad64(shr<R>(a) + shl<16 - R>(a38), share<R>(b), acc);
-}
-
-// a * b mod p (every row its own product)
+// a * b mod p (every row its own product).  Lane k accumulates sum_R op_R * b_R with op_R =
+// a_{k-R} (k >= R) or 38 a_{k-R+16} (k < R).  All sixteen operand pairs are formed first (DPP
+// moves with no dependence on each other, so no DPP read-after-write waits), then two
+// independent multiply-add chains (even / odd R) halve the dependent chain of the convolution.
 NWV_HD V mul(V a, V b, const RowConsts& k) {
     const V a38 = mul24(a, bc(38));
-    V64 acc = mad64(a, share<0>(b), zero64());
-    mul_step<1>(a, a38, b, acc);
-    mul_step<2>(a, a38, b, acc);
-    mul_step<3>(a, a38, b, acc);
-    mul_step<4>(a, a38, b, acc);
-    mul_step<5>(a, a38, b, acc);
-    mul_step<6>(a, a38, b, acc);
-    mul_step<7>(a, a38, b, acc);
-    mul_step<8>(a, a38, b, acc);
-    mul_step<9>(a, a38, b, acc);
-    mul_step<10>(a, a38, b, acc);
-    mul_step<11>(a, a38, b, acc);
-    mul_step<12>(a, a38, b, acc);
-    mul_step<13>(a, a38, b, acc);
-    mul_step<14>(a, a38, b, acc);
-    mul_step<15>(a, a38, b, acc);
+    V op[16], bs[16];
+    op[0] = a;
+    bs[0] = share<0>(b);
+#define NWV_ROW_OPERANDS(R)                    \
+    op[R] = shr<R>(a) + shl<16 - R>(a38);      \
+    bs[R] = share<R>(b);
+    NWV_ROW_OPERANDS(1) NWV_ROW_OPERANDS(2) NWV_ROW_OPERANDS(3) NWV_ROW_OPERANDS(4)
+    NWV_ROW_OPERANDS(5) NWV_ROW_OPERANDS(6) NWV_ROW_OPERANDS(7) NWV_ROW_OPERANDS(8)
+    NWV_ROW_OPERANDS(9) NWV_ROW_OPERANDS(10) NWV_ROW_OPERANDS(11) NWV_ROW_OPERANDS(12)
+    NWV_ROW_OPERANDS(13) NWV_ROW_OPERANDS(14) NWV_ROW_OPERANDS(15)
+#undef NWV_ROW_OPERANDS
+    phase_fence();
+    V64 acc0 = mad64(op[0], bs[0], zero64());
+    V64 acc1 = mad64(op[1], bs[1], zero64());
+#pragma unroll
+    for (int r = 2; r < 16; r += 2) {
+        acc0 = mad64(op[r], bs[r], acc0);
+        acc1 = mad64(op[r + 1], bs[r + 1], acc1);
+    }
+    const V64 acc = add64(acc0, acc1);
     // first pass on the 64-bit columns (< 2^48): limb 15's carry x38 stays < 2^32
     const V x = lo16(acc) + ror1(mul32(shr16(acc), k.w15));
     return carry32(carry32(x, k), k);
