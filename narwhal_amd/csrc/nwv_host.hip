@@ -346,6 +346,27 @@ int msm_launch(Device& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipS
     return NWV_OK;
 }
 
+// Host-side packing copy into the pinned staging buffer: a 65,536 x 512 B batch is ~40 MB, which
+// one thread copies at a few GB/s (longer than the PCIe transfer and the batch MSM together), so
+// copies above 4 MiB are split over up to 8 host threads.
+static void pack_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
+    constexpr size_t kMin = (size_t)4 << 20;
+    const size_t parts = std::min<size_t>(8, bytes / kMin);
+    if (parts < 2) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    const size_t step = ((bytes + parts - 1) / parts + 63) & ~(size_t)63;
+    std::vector<std::thread> th;
+    for (size_t k = 1; k < parts; k++) {
+        const size_t o = k * step;
+        if (o >= bytes) break;
+        th.emplace_back([=] { std::memcpy(dst + o, src + o, std::min(step, bytes - o)); });
+    }
+    std::memcpy(dst, src, std::min(step, bytes));
+    for (auto& t : th) t.join();
+}
+
 // Stage host inputs [lo, hi) onto buffers b of device d (message region rebased).  pk/sig
 // may be null (signing stages seeds separately).  Everything is packed into the pinned host
 // buffer and crosses PCIe as ONE async copy into b.in on d.stream (pk, sig, off, len, msg and,
@@ -383,15 +404,15 @@ int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, c
     if ((rc = d.hstage.ensure(total))) return rc;
     uint8_t* h = static_cast<uint8_t*>(d.hstage.p);
     if (inputs) {
-        std::memcpy(h + o_pk, pk + 32 * lo, 32 * n);
-        std::memcpy(h + o_sig, sig + 64 * lo, 64 * n);
+        pack_copy(h + o_pk, pk + 32 * lo, 32 * n);
+        pack_copy(h + o_sig, sig + 64 * lo, 64 * n);
     }
     uint64_t* hoff = reinterpret_cast<uint64_t*>(h + o_off);
     for (size_t i = 0; i < n; i++) hoff[i] = msg_off[lo + i] - mlo;
     std::memcpy(h + o_len, msg_len + lo, 4 * n);
     std::memset(h + o_state, 0, 256);
     if (seed32) std::memcpy(h + o_state + 32, seed32, 32);
-    if (mbytes) std::memcpy(h + o_msg, msg_base + mlo, mbytes);
+    if (mbytes) pack_copy(h + o_msg, msg_base + mlo, mbytes);
     std::memset(h + o_msg + mbytes, 0, MSG_PAD);
     NWV_HIP(hipMemcpyAsync(b.in.p, h, total, hipMemcpyHostToDevice, d.stream));
     NWV_HIP(hipEventRecord(d.hstage_ev, d.stream));
