@@ -57,15 +57,29 @@ __device__ __forceinline__ uint64_t quad_rot(uint64_t x) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, false);
     return (uint64_t)lo | ((uint64_t)hi << 32);
 }
-__device__ __forceinline__ uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
-// G on native 64-bit words: the adds become single v_lshl_add_u64 (gfx950), which shortens the
-// dependent chain that bounds a long message's latency
+// rotation as two independent v_alignbit_b32 on the halves (one dependent level; the shift/or
+// form the compiler picks for (x >> n) | (x << (64 - n)) is two)
+__device__ __forceinline__ uint64_t rotr64(uint64_t x, int n) {
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    if (n == 32) return ((uint64_t)lo << 32) | hi;
+    const u64p r = rotr(u64p{lo, hi}, n);
+    return ((uint64_t)r.hi << 32) | r.lo;
+}
+// G on native 64-bit words: the adds become single v_lshl_add_u64 (gfx950).  The message word is
+// added to a before b is (a + m does not wait for b, the previous G's last result), so each half
+// of G has one dependent add less on the chain that bounds a long message's latency.
+// opaque to reassociation: LLVM would otherwise rewrite (a + m) + b as (m + b) + a
+__device__ __forceinline__ uint64_t pinned_sum(uint64_t a, uint64_t m) {
+    uint64_t t = a + m;
+    __asm__("" : "+v"(t));
+    return t;
+}
 __device__ __forceinline__ void b2_g(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d, uint64_t x, uint64_t y) {
-    a = a + b + x;
+    a = b + pinned_sum(a, x);
     d = rotr64(d ^ a, 32);
     c = c + d;
     b = rotr64(b ^ c, 24);
-    a = a + b + y;
+    a = b + pinned_sum(a, y);
     d = rotr64(d ^ a, 16);
     c = c + d;
     b = rotr64(b ^ c, 63);
