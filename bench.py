@@ -280,8 +280,8 @@ def pmc_traffic(kernel, n):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=96)
-    ap.add_argument("--warmup", type=int, default=24)
+    ap.add_argument("--steps", type=int, default=192)
+    ap.add_argument("--warmup", type=int, default=48)
     ap.add_argument("--n", type=int, default=65536, help="signatures per batch (per GPU)")
     ap.add_argument("--msg-len", type=int, default=512)
     ap.add_argument("--mode", type=int, default=1, help="1 batch MSM (K5), 0 per-signature pipeline")
