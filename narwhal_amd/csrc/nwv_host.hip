@@ -358,12 +358,19 @@ static void pack_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
     }
     const size_t step = ((bytes + parts - 1) / parts + 63) & ~(size_t)63;
     std::vector<std::thread> th;
+    size_t done = step;  // bytes [0, done) are this thread's, the rest the helpers'
     for (size_t k = 1; k < parts; k++) {
         const size_t o = k * step;
         if (o >= bytes) break;
-        th.emplace_back([=] { std::memcpy(dst + o, src + o, std::min(step, bytes - o)); });
+        try {
+            th.emplace_back([=] { std::memcpy(dst + o, src + o, std::min(step, bytes - o)); });
+        } catch (...) {  // no thread available: this thread copies the remainder (never throw
+            break;       // across the C ABI)
+        }
+        done = o + step;
     }
     std::memcpy(dst, src, std::min(step, bytes));
+    if (done < bytes) std::memcpy(dst + done, src + done, bytes - done);
     for (auto& t : th) t.join();
 }
 
@@ -536,8 +543,15 @@ static int for_shards(nwv_ctx* ctx, size_t n, Fn fn) {
             int rc = with_device(d);
             rcs[k] = rc ? rc : fn(d, lo, hi);
         };
-        if (nd == 1) run();
-        else th.emplace_back(run);
+        if (nd == 1) {
+            run();
+        } else {
+            try {
+                th.emplace_back(run);
+            } catch (...) {  // no host thread: run this shard inline (never throw across the C ABI)
+                run();
+            }
+        }
     }
     for (auto& t : th) t.join();
     for (int rc : rcs)
@@ -1102,8 +1116,15 @@ int nwv_blake2b256_many(nwv_ctx* ctx, size_t n, const uint8_t* base, const uint6
             }
             rcs[k] = rc;
         };
-        if (nd == 1) run();
-        else th.emplace_back(run);
+        if (nd == 1) {
+            run();
+        } else {
+            try {
+                th.emplace_back(run);
+            } catch (...) {  // no host thread: run this shard inline (never throw across the C ABI)
+                run();
+            }
+        }
     }
     for (auto& t : th) t.join();
     for (int rc : rcs)
