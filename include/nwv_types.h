@@ -110,6 +110,16 @@ int nwv_vote_verify_many(nwv_ctx* ctx, const nwv_committee* committee, size_t n,
                          int32_t* results);
 int nwv_certificate_verify_many(nwv_ctx* ctx, const nwv_committee* committee, size_t n,
                                 const nwv_certificate* c, int32_t* results);
+/* Mixed batch: the headers, votes and certificates a primary's Core has queued
+ * (Core::sanitize_header / sanitize_vote / sanitize_certificate, primary/src/core.rs:497-573)
+ * verified by ONE call: every digest of all three kinds in one BLAKE2b launch and every signature
+ * in one batch MSM.  Each results array receives exactly what the matching *_many call would
+ * (and so what Header::verify :150-183, Vote::verify :307-328, Certificate::verify :487-537
+ * return item by item).  Any count may be 0 (its pointers may then be NULL). */
+int nwv_verify_mixed_many(nwv_ctx* ctx, const nwv_committee* committee, size_t n_headers,
+                          const nwv_header* headers, int32_t* header_results, size_t n_votes,
+                          const nwv_vote* votes, int32_t* vote_results, size_t n_certs,
+                          const nwv_certificate* certs, int32_t* cert_results);
 
 /* CertificatesResponse::validate_certificates: the certificates present in a response (absent
  * entries are simply not passed) are all verified; *n_invalid receives the number of invalid

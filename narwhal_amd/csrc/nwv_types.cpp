@@ -244,77 +244,35 @@ int nwv_certificate_digest(nwv_ctx* ctx, const nwv_certificate* c, uint8_t out[3
     return nwv_certificate_digest_many(ctx, 1, c, out);
 }
 
-// ------------------------------------------------------------------ Header::verify -----
-int nwv_header_verify_many(nwv_ctx* ctx, const nwv_committee* committee, size_t n, const nwv_header* h,
-                           int32_t* results) {
-    if (!ctx || !valid_args(committee) || (n && (!h || !results))) return NWV_ERR_ARG;
-    const nwv_committee& c = *committee;
-    DigestBatch db;
-    std::vector<HeaderPlan> plan(n);
-    for (size_t i = 0; i < n; i++) plan_header(c, h[i], db, plan[i]);
-    std::vector<uint8_t> dig;
-    int rc = db.run(ctx, dig);
-    if (rc) return rc;
-    SigBatch sb(&c);
-    for (size_t i = 0; i < n; i++) results[i] = header_after_digest(h[i], plan[i], dig, &sb, plan[i]);
-    std::vector<uint8_t> ok;
-    if ((rc = sb.run(ctx, ok))) return rc;
-    for (size_t i = 0; i < n; i++)
-        if (results[i] == NWV_DAG_OK && plan[i].sig >= 0 && !ok[plan[i].sig]) results[i] = NWV_DAG_INVALID_SIGNATURE;
-    return NWV_OK;
-}
-int nwv_header_verify(nwv_ctx* ctx, const nwv_committee* committee, const nwv_header* h) {
-    int32_t r = 0;
-    int rc = nwv_header_verify_many(ctx, committee, 1, h, &r);
-    return rc ? rc : r;
-}
-
-// ------------------------------------------------------------------ Vote::verify -------
-int nwv_vote_verify_many(nwv_ctx* ctx, const nwv_committee* committee, size_t n, const nwv_vote* v,
-                         int32_t* results) {
-    if (!ctx || !valid_args(committee) || (n && (!v || !results))) return NWV_ERR_ARG;
-    const nwv_committee& c = *committee;
-    std::vector<uint8_t> dig(32 * n);
-    int rc = n ? nwv_vote_digest_many(ctx, n, v, dig.data()) : NWV_OK;
-    if (rc) return rc;
-    SigBatch sb(&c);
-    std::vector<long> sig(n, -1);
-    for (size_t i = 0; i < n; i++) {
-        if (v[i].epoch != c.epoch) results[i] = NWV_DAG_INVALID_EPOCH;
-        else if (committee_stake(c, v[i].author) == 0) results[i] = NWV_DAG_UNKNOWN_AUTHORITY;
-        else {
-            results[i] = NWV_DAG_OK;
-            sig[i] = (long)sb.add(v[i].author, v[i].signature, dig.data() + 32 * i, 32);
-        }
-    }
-    std::vector<uint8_t> ok;
-    if ((rc = sb.run(ctx, ok))) return rc;
-    for (size_t i = 0; i < n; i++)
-        if (sig[i] >= 0 && !ok[sig[i]]) results[i] = NWV_DAG_INVALID_SIGNATURE;
-    return NWV_OK;
-}
-int nwv_vote_verify(nwv_ctx* ctx, const nwv_committee* committee, const nwv_vote* v) {
-    int32_t r = 0;
-    int rc = nwv_vote_verify_many(ctx, committee, 1, v, &r);
-    return rc ? rc : r;
-}
-
-// ------------------------------------------------------------------ Certificate::verify -
-int nwv_certificate_verify_many(nwv_ctx* ctx, const nwv_committee* committee, size_t n,
-                                const nwv_certificate* cs, int32_t* results) {
-    if (!ctx || !valid_args(committee) || (n && (!cs || !results))) return NWV_ERR_ARG;
-    const nwv_committee& c = *committee;
+// ------------------------------------------------------------------ mixed batches ------
+// Headers, votes and certificates of one call (Core::sanitize_header / sanitize_vote /
+// sanitize_certificate, primary/src/core.rs:497-573, and CertificatesResponse::
+// validate_certificates, responses.rs:95-141): every digest of the call in one BLAKE2b launch,
+// every signature in one keyed batch MSM, then each item's verdict in the reference's check
+// order (Header::verify :150-183, Vote::verify :307-328, Certificate::verify :487-537).
+}  // extern "C"
+namespace {
+int verify_mixed(nwv_ctx* ctx, const nwv_committee& c, size_t nh, const nwv_header* h, int32_t* hres,
+                 size_t nv, const nwv_vote* v, int32_t* vres, size_t nc, const nwv_certificate* cs,
+                 int32_t* cres) {
     const uint64_t quorum = quorum_threshold(c);
-    // phase 1: host checks and every digest (header ids to re-derive, certificate digests)
+    // phase 1: host checks and every digest (header ids to re-derive, vote and certificate digests)
     DigestBatch db;
-    std::vector<HeaderPlan> plan(n);
-    std::vector<long> cdig(n, -1);
-    std::vector<uint8_t> done(n, 0);
-    for (size_t i = 0; i < n; i++) {
+    std::vector<HeaderPlan> hplan(nh), cplan(nc);
+    for (size_t i = 0; i < nh; i++) plan_header(c, h[i], db, hplan[i]);
+    std::vector<long> vdig(nv, -1);
+    for (size_t i = 0; i < nv; i++) {
+        vdig[i] = (long)db.add_begin();
+        id_round_epoch_origin(v[i].id, v[i].round, v[i].epoch, v[i].origin, db.arena);
+        db.add_end();
+    }
+    std::vector<long> cdig(nc, -1);
+    std::vector<uint8_t> done(nc, 0);
+    for (size_t i = 0; i < nc; i++) {
         const nwv_certificate& x = cs[i];
-        results[i] = NWV_DAG_OK;
+        cres[i] = NWV_DAG_OK;
         if (x.header.epoch != c.epoch) {  // Certificate::verify's own epoch check
-            results[i] = NWV_DAG_INVALID_EPOCH;
+            cres[i] = NWV_DAG_INVALID_EPOCH;
             done[i] = 1;
             continue;
         }
@@ -322,7 +280,7 @@ int nwv_certificate_verify_many(nwv_ctx* ctx, const nwv_committee* committee, si
             done[i] = 1;
             continue;
         }
-        plan_header(c, x.header, db, plan[i]);
+        plan_header(c, x.header, db, cplan[i]);
         cdig[i] = (long)db.add_begin();
         id_round_epoch_origin(x.header.id, x.header.round, x.header.epoch, x.header.author, db.arena);
         db.add_end();
@@ -330,23 +288,34 @@ int nwv_certificate_verify_many(nwv_ctx* ctx, const nwv_committee* committee, si
     std::vector<uint8_t> dig;
     int rc = db.run(ctx, dig);
     if (rc) return rc;
-    // phase 2: header verdicts, quorum, and the signature batch (header + aggregated)
+    // phase 2: host verdicts up to the signatures, and the one signature batch
     SigBatch sb(&c);
-    std::vector<long> agg_first(n, -1), agg_count(n, 0);
-    std::vector<int32_t> after_header(n, NWV_DAG_OK);
-    for (size_t i = 0; i < n; i++) {
+    for (size_t i = 0; i < nh; i++) hres[i] = header_after_digest(h[i], hplan[i], dig, &sb, hplan[i]);
+    std::vector<long> vsig(nv, -1);
+    for (size_t i = 0; i < nv; i++) {
+        if (v[i].epoch != c.epoch) vres[i] = NWV_DAG_INVALID_EPOCH;
+        else if (committee_stake(c, v[i].author) == 0) vres[i] = NWV_DAG_UNKNOWN_AUTHORITY;
+        else {
+            vres[i] = NWV_DAG_OK;
+            vsig[i] = (long)sb.add(v[i].author, v[i].signature, dig.data() + 32 * vdig[i], 32);
+        }
+    }
+    std::vector<long> agg_first(nc, -1), agg_count(nc, 0);
+    std::vector<int32_t> after_header(nc, NWV_DAG_OK);
+    std::vector<size_t> pks;
+    for (size_t i = 0; i < nc; i++) {
         if (done[i]) continue;
         const nwv_certificate& x = cs[i];
-        const int hr = header_after_digest(x.header, plan[i], dig, &sb, plan[i]);
+        const int hr = header_after_digest(x.header, cplan[i], dig, &sb, cplan[i]);
         if (hr) {
-            results[i] = hr;
+            cres[i] = hr;
             done[i] = 1;
             continue;
         }
         // bitmap -> pks in committee order, as the filter at :505-520
         uint64_t weight = 0;
         size_t it = 0;
-        std::vector<size_t> pks;
+        pks.clear();
         for (size_t a = 0; a < c.n; a++) {
             if (it < x.n_signed && x.signed_authorities[it] == (uint32_t)a) {
                 weight += c.stakes[a];
@@ -372,23 +341,69 @@ int nwv_certificate_verify_many(nwv_ctx* ctx, const nwv_committee* committee, si
     }
     std::vector<uint8_t> ok;
     if ((rc = sb.run(ctx, ok))) return rc;
-    for (size_t i = 0; i < n; i++) {
+    // phase 3: signature verdicts
+    for (size_t i = 0; i < nh; i++)
+        if (hres[i] == NWV_DAG_OK && hplan[i].sig >= 0 && !ok[hplan[i].sig]) hres[i] = NWV_DAG_INVALID_SIGNATURE;
+    for (size_t i = 0; i < nv; i++)
+        if (vsig[i] >= 0 && !ok[vsig[i]]) vres[i] = NWV_DAG_INVALID_SIGNATURE;
+    for (size_t i = 0; i < nc; i++) {
         if (done[i]) continue;
-        if (plan[i].sig >= 0 && !ok[plan[i].sig]) {  // Header::verify's signature comes first
-            results[i] = NWV_DAG_INVALID_SIGNATURE;
+        if (cplan[i].sig >= 0 && !ok[cplan[i].sig]) {  // Header::verify's signature comes first
+            cres[i] = NWV_DAG_INVALID_SIGNATURE;
             continue;
         }
         if (after_header[i]) {
-            results[i] = after_header[i];
+            cres[i] = after_header[i];
             continue;
         }
         for (long k = 0; k < agg_count[i]; k++)
             if (!ok[agg_first[i] + k]) {
-                results[i] = NWV_DAG_INVALID_SIGNATURE;
+                cres[i] = NWV_DAG_INVALID_SIGNATURE;
                 break;
             }
     }
     return NWV_OK;
+}
+}  // namespace
+extern "C" {
+
+int nwv_verify_mixed_many(nwv_ctx* ctx, const nwv_committee* committee, size_t n_headers,
+                          const nwv_header* headers, int32_t* header_results, size_t n_votes,
+                          const nwv_vote* votes, int32_t* vote_results, size_t n_certs,
+                          const nwv_certificate* certs, int32_t* cert_results) {
+    if (!ctx || !valid_args(committee) || (n_headers && (!headers || !header_results)) ||
+        (n_votes && (!votes || !vote_results)) || (n_certs && (!certs || !cert_results)))
+        return NWV_ERR_ARG;
+    return verify_mixed(ctx, *committee, n_headers, headers, header_results, n_votes, votes, vote_results,
+                        n_certs, certs, cert_results);
+}
+
+// ------------------------------------------------------------------ Header::verify -----
+int nwv_header_verify_many(nwv_ctx* ctx, const nwv_committee* committee, size_t n, const nwv_header* h,
+                           int32_t* results) {
+    return nwv_verify_mixed_many(ctx, committee, n, h, results, 0, nullptr, nullptr, 0, nullptr, nullptr);
+}
+int nwv_header_verify(nwv_ctx* ctx, const nwv_committee* committee, const nwv_header* h) {
+    int32_t r = 0;
+    int rc = nwv_header_verify_many(ctx, committee, 1, h, &r);
+    return rc ? rc : r;
+}
+
+// ------------------------------------------------------------------ Vote::verify -------
+int nwv_vote_verify_many(nwv_ctx* ctx, const nwv_committee* committee, size_t n, const nwv_vote* v,
+                         int32_t* results) {
+    return nwv_verify_mixed_many(ctx, committee, 0, nullptr, nullptr, n, v, results, 0, nullptr, nullptr);
+}
+int nwv_vote_verify(nwv_ctx* ctx, const nwv_committee* committee, const nwv_vote* v) {
+    int32_t r = 0;
+    int rc = nwv_vote_verify_many(ctx, committee, 1, v, &r);
+    return rc ? rc : r;
+}
+
+// ------------------------------------------------------------------ Certificate::verify -
+int nwv_certificate_verify_many(nwv_ctx* ctx, const nwv_committee* committee, size_t n,
+                                const nwv_certificate* cs, int32_t* results) {
+    return nwv_verify_mixed_many(ctx, committee, 0, nullptr, nullptr, 0, nullptr, nullptr, n, cs, results);
 }
 int nwv_certificate_verify(nwv_ctx* ctx, const nwv_committee* committee, const nwv_certificate* c) {
     int32_t r = 0;

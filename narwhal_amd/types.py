@@ -94,6 +94,8 @@ _SIGS = {
     "nwv_header_verify_many": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     "nwv_vote_verify_many": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     "nwv_certificate_verify_many": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "nwv_verify_mixed_many": ([ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p] * 3,
+                              ctypes.c_int),
     "nwv_validate_certificates": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                    ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     "nwv_certificate_new": ([ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
@@ -300,6 +302,25 @@ def verify_votes(engine, committee, votes) -> List[int]:
 
 def verify_certificates(engine, committee, certs) -> List[int]:
     return _many(engine, lib().nwv_certificate_verify_many, committee, list(certs))
+
+
+def verify_mixed(engine, committee, headers=(), votes=(), certs=()):
+    """One coalesced call for the headers, votes and certificates a Core has queued
+    (Core::sanitize_*, primary/src/core.rs:497-573): one digest launch, one batch MSM.
+    -> (header codes, vote codes, certificate codes), NWV_DAG_* (0 = Ok)"""
+    keep = _Keep()
+    c = committee._c(keep)
+    args = []
+    outs = []
+    for items, cls in ((list(headers), _Header), (list(votes), _Vote), (list(certs), _Certificate)):
+        n = len(items)
+        arr = (cls * max(n, 1))(*[it._c(keep) for it in items])
+        res = (ctypes.c_int32 * max(n, 1))()
+        keep.objs += [arr, res]
+        args += [n, ctypes.cast(arr, ctypes.c_void_p), ctypes.cast(res, ctypes.c_void_p)]
+        outs.append((res, n))
+    _lib._check(lib().nwv_verify_mixed_many(engine._h, ctypes.byref(c), *args))
+    return tuple(list(r[:n]) for r, n in outs)
 
 
 def verify(engine, committee, item):

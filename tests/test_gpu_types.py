@@ -173,3 +173,38 @@ def test_validate_certificates_dag_round_100(eng):
     ok, idx = T.validate_certificates(eng, c, [tu.certificate(x) for x in good])
     assert ok and idx == []
     assert T.validate_certificates(eng, c, []) == (True, [])
+
+
+def test_verify_mixed_matches_oracle(eng):
+    """nwv_verify_mixed_many: headers, votes and certificates of every DagError kind in ONE call
+    (one digest launch, one batch MSM) give the codes the reference's per-item verify returns,
+    and the same codes as the per-kind *_many calls; empty kinds are allowed."""
+    rnd = random.Random(11)
+    fx = nt.CommitteeFixture(10, of.pubkey, of.sign, seed=5)
+    c = tu.committee(fx.committee)
+    cases = _mutations(fx, rnd)
+    heads = [h for h, _ in cases if h is not None]
+    certs = [cert for _, cert in cases]
+    h = fx.header()
+    vs = fx.votes(h)
+    vs[1] = dict(vs[1], epoch=5)
+    vs[2] = dict(vs[2], author=of.pubkey(b"\x02" * 32))
+    vs[3] = dict(vs[3], signature=bytes(64))
+    H = [tu.header(x) for x in heads]
+    V = [tu.vote(v) for v in vs]
+    C = [tu.certificate(x) for x in certs]
+    gh, gv, gc = T.verify_mixed(eng, c, H, V, C)
+    assert gh == [nt.header_verify(fx.committee, x, _ver) for x in heads]
+    assert gv == [nt.vote_verify(fx.committee, v, _ver) for v in vs]
+    assert gc == [nt.certificate_verify(fx.committee, x, _ver) for x in certs]
+    assert gh == T.verify_headers(eng, c, H) and gv == T.verify_votes(eng, c, V)
+    assert gc == T.verify_certificates(eng, c, C)
+    # all-valid mix (the MSM accepts without fallback), and empty kinds
+    good_h = [x for x, code in zip(H, gh) if code == 0]
+    good_c = [x for x, code in zip(C, gc) if code == 0]
+    good_v = [x for x, code in zip(V, gv) if code == 0]
+    assert good_h and good_c and good_v
+    assert T.verify_mixed(eng, c, good_h, good_v, good_c) == ([0] * len(good_h), [0] * len(good_v),
+                                                               [0] * len(good_c))
+    assert T.verify_mixed(eng, c, votes=good_v) == ([], [0] * len(good_v), [])
+    assert T.verify_mixed(eng, c) == ([], [], [])
