@@ -380,9 +380,18 @@ static void pack_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
 // with seed32, the MSM state words are views into it); no synchronisation here: work on other
 // streams must wait for d.stream.  seed32 (optional): m_state = {0 flags, 0 verdict, .., seed}
 // so that msm_launch(state_ready) needs neither a memset nor a seed copy.
+// Keyed batches' per-call tables (distinct keys, CSR of signatures per key), packed into the
+// same arena so that a keyed batch still crosses PCIe as one copy with no host synchronisation
+struct KeyedTail {
+    const uint8_t* keys;   // m x 32
+    size_t m;
+    const uint32_t* koff;  // m + 1
+    const uint32_t* ksig;  // n
+};
+
 int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, const uint8_t* sig,
              const uint8_t* msg_base, const uint64_t* msg_off, const uint32_t* msg_len,
-             const uint8_t* seed32) {
+             const uint8_t* seed32, const KeyedTail* kt = nullptr) {
     const size_t n = hi - lo;
     uint64_t mlo = UINT64_MAX, mhi = 0;
     for (size_t i = lo; i < hi; i++) {
@@ -395,7 +404,10 @@ int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, c
     const bool inputs = pk && sig;
     const size_t o_pk = 0, o_sig = o_pk + (inputs ? up(32 * n + 16) : 0);
     const size_t o_off = o_sig + (inputs ? up(64 * n + 16) : 0), o_len = o_off + up(8 * n + 8);
-    const size_t o_state = o_len + up(4 * n + 4), o_msg = o_state + 256, total = o_msg + mbytes + MSG_PAD;
+    const size_t o_state = o_len + up(4 * n + 4), o_msg = o_state + 256, o_keys = up(o_msg + mbytes + MSG_PAD);
+    const size_t m = kt ? kt->m : 0;
+    const size_t o_koff = o_keys + (kt ? up(32 * m + 32) : 0), o_ksig = o_koff + (kt ? up(4 * m + 8) : 0);
+    const size_t total = o_ksig + (kt ? up(4 * n + 8) : 0);
     int rc;
     if ((rc = b.in.ensure(total)) || (rc = b.kbuf.ensure(32 * n + 16)) || (rc = b.flags.ensure(4 * n + 4)) ||
         (rc = b.tables.ensure((size_t)LANE_SCRATCH_WORDS * 4 * n + 16)) ||
@@ -405,6 +417,9 @@ int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, c
     if (!inputs && b.pk.view) b.pk.release();
     if (!inputs && b.sig.view) b.sig.release();
     if (!seed32 && b.m_state.view) b.m_state.release();
+    if (!kt)
+        for (DevBuf* v : {&b.keys, &b.koff, &b.ksig})
+            if (v->view) v->release();
     if (!inputs && ((rc = b.pk.ensure(32 * n + 16)) || (rc = b.sig.ensure(64 * n + 16)))) return rc;
     // the previous call's copy must have left the pinned buffer before it is rewritten
     NWV_HIP(hipEventSynchronize(d.hstage_ev));
@@ -421,6 +436,11 @@ int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, c
     if (seed32) std::memcpy(h + o_state + 32, seed32, 32);
     if (mbytes) pack_copy(h + o_msg, msg_base + mlo, mbytes);
     std::memset(h + o_msg + mbytes, 0, MSG_PAD);
+    if (kt) {
+        if (m) std::memcpy(h + o_keys, kt->keys, 32 * m);
+        std::memcpy(h + o_koff, kt->koff, 4 * (m + 1));
+        if (n) std::memcpy(h + o_ksig, kt->ksig, 4 * n);
+    }
     NWV_HIP(hipMemcpyAsync(b.in.p, h, total, hipMemcpyHostToDevice, d.stream));
     NWV_HIP(hipEventRecord(d.hstage_ev, d.stream));
     uint8_t* g = b.in.as<uint8_t>();
@@ -432,7 +452,12 @@ int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, c
     b.len.set_view(g + o_len, 4 * n + 4);
     b.msg.set_view(g + o_msg, mbytes + MSG_PAD);
     if (seed32) b.m_state.set_view(g + o_state, 256);
-    b.nkeys_distinct = 0;
+    if (kt) {
+        b.keys.set_view(g + o_keys, 32 * m + 32);
+        b.koff.set_view(g + o_koff, 4 * m + 8);
+        b.ksig.set_view(g + o_ksig, 4 * n + 8);
+    }
+    b.nkeys_distinct = m;
     return NWV_OK;
 }
 
@@ -441,11 +466,16 @@ int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, c
 // expanded per signature (the per-signature fallback reads it).
 int ed_stage_keyed(Device& d, EdBuffers& b, size_t lo, size_t hi, size_t n_keys, const uint8_t* keys,
                    const uint32_t* key_idx, const uint8_t* sig, const uint8_t* msg_base,
-                   const uint64_t* msg_off, const uint32_t* msg_len) {
+                   const uint64_t* msg_off, const uint32_t* msg_len, const uint8_t* seed32) {
     const size_t n = hi - lo;
-    std::vector<uint32_t> local(n_keys, UINT32_MAX), cnt;
-    std::vector<uint32_t> kid(n);
-    std::vector<uint8_t> klist, pk(32 * n + 16);
+    // per-thread scratch reused across calls (fresh large vectors are page-faulted in every call)
+    thread_local std::vector<uint32_t> local, cnt, kid, koff, ksig, cur;
+    thread_local std::vector<uint8_t> klist, pk;
+    local.assign(n_keys, UINT32_MAX);
+    cnt.clear();
+    kid.resize(n);
+    klist.clear();
+    pk.resize(32 * n + 16);
     for (size_t i = 0; i < n; i++) {
         const uint32_t g = key_idx[lo + i];
         if (g >= n_keys) return set_err(NWV_ERR_ARG, "key index out of range");
@@ -459,22 +489,13 @@ int ed_stage_keyed(Device& d, EdBuffers& b, size_t lo, size_t hi, size_t n_keys,
         std::memcpy(pk.data() + 32 * i, keys + 32 * (size_t)g, 32);
     }
     const size_t m = cnt.size();
-    std::vector<uint32_t> koff(m + 1, 0), ksig(n), cur;
+    koff.assign(m + 1, 0);
+    ksig.resize(n);
     for (size_t k = 0; k < m; k++) koff[k + 1] = koff[k] + cnt[k];
     cur.assign(koff.begin(), koff.end() - 1);
     for (size_t i = 0; i < n; i++) ksig[cur[kid[i]]++] = (uint32_t)i;
-    int rc = ed_stage(d, b, 0, n, pk.data(), sig + 64 * lo, msg_base, msg_off + lo, msg_len + lo, nullptr);
-    if (rc) return rc;
-    if ((rc = b.keys.ensure(32 * m + 32)) || (rc = b.koff.ensure(4 * m + 8)) || (rc = b.ksig.ensure(4 * n + 8)))
-        return rc;
-    if (m) {
-        NWV_HIP(hipMemcpyAsync(b.keys.p, klist.data(), 32 * m, hipMemcpyHostToDevice, d.stream));
-        NWV_HIP(hipMemcpyAsync(b.koff.p, koff.data(), 4 * (m + 1), hipMemcpyHostToDevice, d.stream));
-    }
-    if (n) NWV_HIP(hipMemcpyAsync(b.ksig.p, ksig.data(), 4 * n, hipMemcpyHostToDevice, d.stream));
-    NWV_HIP(hipStreamSynchronize(d.stream));
-    b.nkeys_distinct = m;
-    return NWV_OK;
+    const KeyedTail kt{klist.data(), m, koff.data(), ksig.data()};
+    return ed_stage(d, b, 0, n, pk.data(), sig + 64 * lo, msg_base, msg_off + lo, msg_len + lo, seed32, &kt);
 }
 
 bool verdicts_all_valid(const uint64_t* bits, size_t n) {
@@ -745,14 +766,14 @@ int nwv_ed25519_verify_batch_keyed(nwv_ctx* ctx, size_t n_keys, const uint8_t* k
     fill_seed(seed32, seed);
     std::mutex omu;
     return for_shards(ctx, n, [&](Device& d, size_t lo, size_t hi) -> int {
-        int r = ed_stage_keyed(d, d.ed, lo, hi, n_keys, keys, key_idx, sig, msg_base, msg_off, msg_len);
-        if (r) return r;
         uint8_t s2[32];
         std::memcpy(s2, seed, 32);
         for (int k = 0; k < 8; k++) s2[24 + k] ^= (uint8_t)((uint64_t)lo >> (8 * k));
+        int r = ed_stage_keyed(d, d.ed, lo, hi, n_keys, keys, key_idx, sig, msg_base, msg_off, msg_len, s2);
+        if (r) return r;
         int ok = 1;
         r = batch_on_device(d, d.ed, hi - lo, s2, d.stream, &ok,
-                            verdict_bits_or_null ? verdict_bits_or_null + lo / 64 : nullptr);
+                            verdict_bits_or_null ? verdict_bits_or_null + lo / 64 : nullptr, true);
         if (r) return r;
         std::lock_guard<std::mutex> g(omu);
         if (!ok) *all_valid = 0;
@@ -888,7 +909,7 @@ int nwv_stage_ed25519_keyed(nwv_ctx* ctx, int device_index, size_t n_keys, const
                             const uint64_t* msg_off, const uint32_t* msg_len, nwv_staged** out) {
     if (n && (!keys || !key_idx || !sig || !msg_off || !msg_len)) return set_err(NWV_ERR_ARG, "null argument");
     return staged_create(ctx, device_index, n, out, [&](Device& d, EdBuffers& b) {
-        return ed_stage_keyed(d, b, 0, n, n_keys, keys, key_idx, sig, msg_base, msg_off, msg_len);
+        return ed_stage_keyed(d, b, 0, n, n_keys, keys, key_idx, sig, msg_base, msg_off, msg_len, nullptr);
     });
 }
 

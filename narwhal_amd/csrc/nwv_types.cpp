@@ -3,6 +3,9 @@
 // every digest and every signature goes to the device through the C ABI of include/nwv.h, with
 // the *_many forms batching a whole call into one BLAKE2b launch and one batch MSM.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -10,6 +13,15 @@
 #include "../../include/nwv_types.h"
 
 namespace {
+
+// NWV_HOST_TRACE=1: host-side phase timestamps of the mixed-batch path on stderr (diagnostics)
+void htrace(const char* what) {
+    static const bool on = std::getenv("NWV_HOST_TRACE") != nullptr;
+    if (!on) return;
+    const double us = std::chrono::duration<double, std::micro>(
+                          std::chrono::steady_clock::now().time_since_epoch()).count();
+    std::fprintf(stderr, "nwv-trace %.1f %s\n", us, what);
+}
 
 void put_le64(std::vector<uint8_t>& b, uint64_t v) {
     for (int i = 0; i < 8; i++) b.push_back((uint8_t)(v >> (8 * i)));
@@ -29,7 +41,7 @@ void header_preimage(const nwv_header& h, std::vector<uint8_t>& b) {
         put(b, h.payload_digests + 32 * i, 32);
         put_le32(b, h.payload_workers[i]);
     }
-    for (size_t i = 0; i < h.n_parents; i++) put(b, h.parents + 32 * i, 32);
+    if (h.n_parents) put(b, h.parents, 32 * h.n_parents);  // contiguous, already in BTreeSet order
 }
 // Vote::digest (:351-364) and Certificate::digest (:594-607): id || round_le || epoch_le || origin
 void id_round_epoch_origin(const uint8_t* id, uint64_t round, uint64_t epoch, const uint8_t* origin,
@@ -40,10 +52,17 @@ void id_round_epoch_origin(const uint8_t* id, uint64_t round, uint64_t epoch, co
     put(b, origin, 32);
 }
 
-// Preimages appended to one arena, hashed in one nwv_blake2b256_many launch
+// Preimages appended to one arena, hashed in one nwv_blake2b256_many launch.  The batches of a
+// call live in thread_local storage (reset per call): fresh multi-100 KB vectors per call would be
+// page-faulted in every time, which costs more host time than the GPU work of a committee round.
 struct DigestBatch {
     std::vector<uint8_t> arena;
     std::vector<uint64_t> off, len;
+    void reset() {
+        arena.clear();
+        off.clear();
+        len.clear();
+    }
     size_t add_begin() {
         off.push_back(arena.size());
         return off.size() - 1;
@@ -69,8 +88,40 @@ struct SigBatch {
     std::vector<uint32_t> kidx;
     std::vector<uint64_t> off;
     std::vector<uint32_t> len;
-    explicit SigBatch(const nwv_committee* cm) : c(cm) {
+    std::vector<uint64_t> bits;
+    std::vector<uint8_t> ok;
+    void reset(const nwv_committee* cm) {
+        c = cm;
+        keys.clear();
+        sig.clear();
+        msgs.clear();
+        kidx.clear();
+        off.clear();
+        len.clear();
         if (c && c->n) keys.assign(c->keys, c->keys + 32 * c->n);
+    }
+    // a message several signatures share (a certificate's digest) is stored once
+    uint64_t add_msg(const uint8_t* m, size_t mlen) {
+        const uint64_t o = msgs.size();
+        put(msgs, m, mlen);
+        return o;
+    }
+    // signer k = committee index (known for certificate signers: no key lookup)
+    size_t add_at(long k, const uint8_t* s, uint64_t moff, size_t mlen) {
+        kidx.push_back((uint32_t)k);
+        put(sig, s, 64);
+        off.push_back(moff);
+        len.push_back((uint32_t)mlen);
+        return off.size() - 1;
+    }
+    // q signatures (contiguous 64-byte records) by committee members ks[0..q) over one message
+    size_t add_run(const size_t* ks, size_t q, const uint8_t* s, uint64_t moff, size_t mlen) {
+        const size_t first = off.size();
+        for (size_t k = 0; k < q; k++) kidx.push_back((uint32_t)ks[k]);
+        put(sig, s, 64 * q);
+        off.insert(off.end(), q, moff);
+        len.insert(len.end(), q, (uint32_t)mlen);
+        return first;
     }
     size_t add(const uint8_t* p, const uint8_t* s, const uint8_t* m, size_t mlen) {
         long k = c ? committee_index(*c, p) : -1;
@@ -78,20 +129,15 @@ struct SigBatch {
             k = (long)(keys.size() / 32);
             put(keys, p, 32);
         }
-        kidx.push_back((uint32_t)k);
-        put(sig, s, 64);
-        off.push_back(msgs.size());
-        len.push_back((uint32_t)mlen);
-        put(msgs, m, mlen);
-        return off.size() - 1;
+        return add_at(k, s, add_msg(m, mlen), mlen);
     }
     size_t size() const { return off.size(); }
-    int run(nwv_ctx* ctx, std::vector<uint8_t>& ok) {
+    int run(nwv_ctx* ctx) {
         const size_t n = size();
         ok.assign(n, 1);
         if (n == 0) return NWV_OK;
         msgs.resize(msgs.size() + 16);
-        std::vector<uint64_t> bits((n + 63) / 64 + 1, 0);
+        bits.assign((n + 63) / 64 + 1, 0);
         int all = 0;
         int rc = nwv_ed25519_verify_batch_keyed(ctx, keys.size() / 32, keys.data(), n, kidx.data(), sig.data(),
                                                 msgs.data(), off.data(), len.data(), nullptr, &all, bits.data());
@@ -256,8 +302,10 @@ int verify_mixed(nwv_ctx* ctx, const nwv_committee& c, size_t nh, const nwv_head
                  size_t nv, const nwv_vote* v, int32_t* vres, size_t nc, const nwv_certificate* cs,
                  int32_t* cres) {
     const uint64_t quorum = quorum_threshold(c);
+    htrace("mixed:start");
     // phase 1: host checks and every digest (header ids to re-derive, vote and certificate digests)
-    DigestBatch db;
+    thread_local DigestBatch db;
+    db.reset();
     std::vector<HeaderPlan> hplan(nh), cplan(nc);
     for (size_t i = 0; i < nh; i++) plan_header(c, h[i], db, hplan[i]);
     std::vector<long> vdig(nv, -1);
@@ -285,11 +333,14 @@ int verify_mixed(nwv_ctx* ctx, const nwv_committee& c, size_t nh, const nwv_head
         id_round_epoch_origin(x.header.id, x.header.round, x.header.epoch, x.header.author, db.arena);
         db.add_end();
     }
-    std::vector<uint8_t> dig;
+    thread_local std::vector<uint8_t> dig;
+    htrace("mixed:preimages");
     int rc = db.run(ctx, dig);
     if (rc) return rc;
+    htrace("mixed:digests");
     // phase 2: host verdicts up to the signatures, and the one signature batch
-    SigBatch sb(&c);
+    thread_local SigBatch sb;
+    sb.reset(&c);
     for (size_t i = 0; i < nh; i++) hres[i] = header_after_digest(h[i], hplan[i], dig, &sb, hplan[i]);
     std::vector<long> vsig(nv, -1);
     for (size_t i = 0; i < nv; i++) {
@@ -332,15 +383,14 @@ int verify_mixed(nwv_ctx* ctx, const nwv_committee& c, size_t nh, const nwv_head
             after_header[i] = NWV_DAG_INVALID_SIGNATURE;
             continue;
         }
-        const uint8_t* d = dig.data() + 32 * cdig[i];
-        for (size_t k = 0; k < pks.size(); k++) {
-            const long idx = (long)sb.add(c.keys + 32 * pks[k], x.aggregated_signature + 64 * k, d, 32);
-            if (k == 0) agg_first[i] = idx;
-        }
+        const uint64_t moff = sb.add_msg(dig.data() + 32 * cdig[i], 32);
+        agg_first[i] = (long)sb.add_run(pks.data(), pks.size(), x.aggregated_signature, moff, 32);
         agg_count[i] = (long)pks.size();
     }
-    std::vector<uint8_t> ok;
-    if ((rc = sb.run(ctx, ok))) return rc;
+    htrace("mixed:sigbatch");
+    if ((rc = sb.run(ctx))) return rc;
+    const std::vector<uint8_t>& ok = sb.ok;
+    htrace("mixed:verified");
     // phase 3: signature verdicts
     for (size_t i = 0; i < nh; i++)
         if (hres[i] == NWV_DAG_OK && hplan[i].sig >= 0 && !ok[hplan[i].sig]) hres[i] = NWV_DAG_INVALID_SIGNATURE;
