@@ -91,6 +91,18 @@ int nwv_ed25519_verify_batch_keyed(nwv_ctx* ctx, size_t n_keys, const uint8_t* k
                                    const uint32_t* key_idx, const uint8_t* sig, const uint8_t* msg_base,
                                    const uint64_t* msg_off, const uint32_t* msg_len,
                                    const uint8_t seed32[32], int* all_valid, uint64_t* verdict_bits_or_null);
+/* Digest-then-verify: the n_pre preimages are hashed with BLAKE2b-256 on the
+ * device (digests_out receives them, n_pre x 32) and signature i is checked over the 32-byte
+ * digest digest_idx[i] straight from device memory, with no host round trip between the hash and
+ * the batch verification.  This is how Narwhal signs: a vote's / certificate's signatures are over
+ * Vote::digest / Certificate::digest (types/src/primary.rs:351-364, :594-607) and a header's over
+ * its id = Header::digest (:209-227).  Otherwise as nwv_ed25519_verify_batch_keyed. */
+int nwv_ed25519_verify_batch_keyed_digests(nwv_ctx* ctx, size_t n_pre, const uint8_t* pre_base,
+                                           const uint64_t* pre_off, const uint64_t* pre_len,
+                                           uint8_t* digests_out, size_t n_keys, const uint8_t* keys,
+                                           size_t n, const uint32_t* key_idx, const uint8_t* sig,
+                                           const uint32_t* digest_idx, const uint8_t seed32[32],
+                                           int* all_valid, uint64_t* verdict_bits_or_null);
 
 /* ---- fastcrypto 0.1.2 trait surface (Ed25519 scheme module; contract of
  *      crypto/src/bls12377/mod.rs:264-291 and :485-577) ---- */

@@ -66,6 +66,8 @@ def load():
         "nwv_stage_ed25519": ([_vp, _i32, _sz, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(_vp)], _i32),
         "nwv_stage_ed25519_keyed": ([_vp, _i32, _sz, _vp, _sz, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(_vp)], _i32),
         "nwv_ed25519_verify_batch_keyed": ([_vp, _sz, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i32),
+        "nwv_ed25519_verify_batch_keyed_digests": ([_vp, _sz, _vp, _vp, _vp, _vp, _sz, _vp, _sz, _vp, _vp, _vp, _vp,
+                                                    _vp, _vp], _i32),
         "nwv_staged_run": ([_vp, _i32, _vp], _i32),
         "nwv_staged_sync": ([_vp], _i32),
         "nwv_staged_fetch": ([_vp, _vp, ctypes.POINTER(_i32)], _i32),
@@ -179,6 +181,27 @@ class Engine:
                                                        _ptr(arena), _ptr(offs), _ptr(lens), seed,
                                                        ctypes.byref(allv), _ptr(bits) if want_bits else None))
         return bool(allv.value), (list(unpack_bits(bits, n)) if want_bits else None)
+
+    def verify_batch_keyed_digests(self, preimages, keys, key_idx, sigs, digest_idx, seed=b"\x00" * 32):
+        """BLAKE2b-256 of every preimage on the device, then signature i over digest digest_idx[i]
+        -> (digests, all_valid, per-signature verdicts)"""
+        n, m = len(sigs), len(preimages)
+        lens = np.fromiter((len(x) for x in preimages), dtype=np.uint64, count=m)
+        offs = np.zeros(m, dtype=np.uint64)
+        if m:
+            offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        arena = np.frombuffer(b"".join(preimages) + b"\0" * 16, dtype=np.uint8)
+        dig = np.zeros(32 * max(m, 1), dtype=np.uint8)
+        kb = np.frombuffer(b"".join(keys) or b"\0", dtype=np.uint8)
+        ki = np.asarray(key_idx, dtype=np.uint32)
+        di = np.asarray(digest_idx, dtype=np.uint32)
+        sg = np.frombuffer(b"".join(sigs) or b"\0", dtype=np.uint8)
+        bits = np.zeros((n + 63) // 64 + 1, dtype=np.uint64)
+        allv = _i32(0)
+        _check(self.lib.nwv_ed25519_verify_batch_keyed_digests(
+            self._h, m, _ptr(arena), _ptr(offs), _ptr(lens), _ptr(dig), len(keys), _ptr(kb), n, _ptr(ki),
+            _ptr(sg), _ptr(di), seed, ctypes.byref(allv), _ptr(bits)))
+        return [dig[32 * i:32 * i + 32].tobytes() for i in range(m)], bool(allv.value), list(unpack_bits(bits, n))
 
     def stage_keyed(self, keys, key_idx, sig, arena, offs, lens, device_index=0):
         """keys: uint8 [m*32]; key_idx: uint32 [n]; sig uint8 [n*64]"""

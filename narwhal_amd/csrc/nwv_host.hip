@@ -391,7 +391,7 @@ struct KeyedTail {
 
 int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, const uint8_t* sig,
              const uint8_t* msg_base, const uint64_t* msg_off, const uint32_t* msg_len,
-             const uint8_t* seed32, const KeyedTail* kt = nullptr) {
+             const uint8_t* seed32, const KeyedTail* kt = nullptr, const DevBuf* dev_msg = nullptr) {
     const size_t n = hi - lo;
     uint64_t mlo = UINT64_MAX, mhi = 0;
     for (size_t i = lo; i < hi; i++) {
@@ -399,6 +399,12 @@ int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, c
         mhi = std::max<uint64_t>(mhi, msg_off[i] + msg_len[i]);
     }
     if (n == 0 || mhi < mlo) { mlo = 0; mhi = 0; }
+    // dev_msg: the messages are already on the device (offsets index it as they are)
+    if (dev_msg) {
+        if (mhi + MSG_PAD > dev_msg->cap) return set_err(NWV_ERR_ARG, "device message offset out of range");
+        mlo = 0;
+        mhi = 0;
+    }
     const size_t mbytes = (size_t)(mhi - mlo);
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const bool inputs = pk && sig;
@@ -450,7 +456,8 @@ int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, c
     }
     b.off.set_view(g + o_off, 8 * n + 8);
     b.len.set_view(g + o_len, 4 * n + 4);
-    b.msg.set_view(g + o_msg, mbytes + MSG_PAD);
+    if (dev_msg) b.msg.set_view(dev_msg->p, dev_msg->cap);
+    else b.msg.set_view(g + o_msg, mbytes + MSG_PAD);
     if (seed32) b.m_state.set_view(g + o_state, 256);
     if (kt) {
         b.keys.set_view(g + o_keys, 32 * m + 32);
@@ -466,7 +473,8 @@ int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, c
 // expanded per signature (the per-signature fallback reads it).
 int ed_stage_keyed(Device& d, EdBuffers& b, size_t lo, size_t hi, size_t n_keys, const uint8_t* keys,
                    const uint32_t* key_idx, const uint8_t* sig, const uint8_t* msg_base,
-                   const uint64_t* msg_off, const uint32_t* msg_len, const uint8_t* seed32) {
+                   const uint64_t* msg_off, const uint32_t* msg_len, const uint8_t* seed32,
+                   const DevBuf* dev_msg = nullptr) {
     const size_t n = hi - lo;
     // per-thread scratch reused across calls (fresh large vectors are page-faulted in every call)
     thread_local std::vector<uint32_t> local, cnt, kid, koff, ksig, cur;
@@ -495,7 +503,8 @@ int ed_stage_keyed(Device& d, EdBuffers& b, size_t lo, size_t hi, size_t n_keys,
     cur.assign(koff.begin(), koff.end() - 1);
     for (size_t i = 0; i < n; i++) ksig[cur[kid[i]]++] = (uint32_t)i;
     const KeyedTail kt{klist.data(), m, koff.data(), ksig.data()};
-    return ed_stage(d, b, 0, n, pk.data(), sig + 64 * lo, msg_base, msg_off + lo, msg_len + lo, seed32, &kt);
+    return ed_stage(d, b, 0, n, pk.data(), sig + 64 * lo, msg_base, msg_off + lo, msg_len + lo, seed32, &kt,
+                    dev_msg);
 }
 
 bool verdicts_all_valid(const uint64_t* bits, size_t n) {
@@ -1150,6 +1159,62 @@ int nwv_blake2b256_many(nwv_ctx* ctx, size_t n, const uint8_t* base, const uint6
     for (auto& t : th) t.join();
     for (int rc : rcs)
         if (rc) return rc;
+    return NWV_OK;
+}
+
+int nwv_ed25519_verify_batch_keyed_digests(nwv_ctx* ctx, size_t n_pre, const uint8_t* pre_base,
+                                           const uint64_t* pre_off, const uint64_t* pre_len,
+                                           uint8_t* digests_out, size_t n_keys, const uint8_t* keys,
+                                           size_t n, const uint32_t* key_idx, const uint8_t* sig,
+                                           const uint32_t* digest_idx, const uint8_t seed32[32],
+                                           int* all_valid, uint64_t* verdict_bits_or_null) {
+    if (!ctx || !all_valid || (n_pre && (!pre_off || !pre_len || !digests_out)) ||
+        (n && (!keys || !key_idx || !sig || !digest_idx)))
+        return set_err(NWV_ERR_ARG, "null argument");
+    for (size_t i = 0; i < n; i++)
+        if (digest_idx[i] >= n_pre) return set_err(NWV_ERR_ARG, "digest index out of range");
+    *all_valid = 1;
+    // message i = digest digest_idx[i]: 32 bytes at 32 * digest_idx[i] of the digest array
+    thread_local std::vector<uint64_t> moff;
+    thread_local std::vector<uint32_t> mlen;
+    moff.resize(n);
+    mlen.assign(n, 32u);
+    for (size_t i = 0; i < n; i++) moff[i] = 32ull * digest_idx[i];
+    if (ctx->devs.size() != 1 || n_pre == 0 || n == 0) {
+        // several devices: the digests come back to the host and the signatures are sharded
+        int rc = nwv_blake2b256_many(ctx, n_pre, pre_base, pre_off, pre_len, digests_out);
+        if (rc || n == 0) return rc;
+        return nwv_ed25519_verify_batch_keyed(ctx, n_keys, keys, n, key_idx, sig, digests_out, moff.data(),
+                                              mlen.data(), seed32, all_valid, verdict_bits_or_null);
+    }
+    static const uint8_t empty[1] = {0};
+    if (!pre_base) pre_base = empty;
+    uint8_t seed[32];
+    fill_seed(seed32, seed);
+    Device& d = *ctx->devs[0];
+    std::lock_guard<std::mutex> g(d.mu);
+    int rc = with_device(d);
+    std::vector<uint64_t> roff;
+    if (!rc) rc = b2_stage(d, n_pre, pre_base, pre_off, pre_len, 0, n_pre, roff);
+    if (rc) return rc;
+    // the digests stay on the device as the message arena of the batch (over-read slack included)
+    if ((rc = d.b2_out.ensure(32 * n_pre + 4 * MSG_PAD))) return rc;
+    uint64_t maxlen = 0;
+    for (size_t k = 0; k < n_pre; k++) maxlen = std::max<uint64_t>(maxlen, pre_len[k]);
+    NWV_HIP(hipMemsetAsync(d.b2_out.as<uint8_t>() + 32 * n_pre, 0, 4 * MSG_PAD, d.stream));
+    b2_launch(d, n_pre, maxlen, d.b2_base.as<uint8_t>(), d.b2_off.as<uint64_t>(), d.b2_len.as<uint64_t>(),
+              d.b2_out.as<uint32_t>());
+    NWV_HIP(hipGetLastError());
+    // no host round trip: the batch is staged behind the hash on the same stream
+    rc = ed_stage_keyed(d, d.ed, 0, n, n_keys, keys, key_idx, sig, nullptr, moff.data(), mlen.data(), seed,
+                        &d.b2_out);
+    if (rc) return rc;
+    int ok = 1;
+    rc = batch_on_device(d, d.ed, n, seed, d.stream, &ok, verdict_bits_or_null, true);
+    if (rc) return rc;
+    if (!ok) *all_valid = 0;
+    NWV_HIP(hipMemcpyAsync(digests_out, d.b2_out.p, 32 * n_pre, hipMemcpyDeviceToHost, d.stream));
+    NWV_HIP(hipStreamSynchronize(d.stream));
     return NWV_OK;
 }
 

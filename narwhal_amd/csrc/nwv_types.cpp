@@ -78,75 +78,6 @@ struct DigestBatch {
 
 long committee_index(const nwv_committee& c, const uint8_t* pk);
 
-// Signatures of one call, verified as one batch (MSM; per-signature fallback when it rejects).
-// Signers are committee members, so the batch is keyed by committee index
-// (nwv_ed25519_verify_batch_keyed): each member's key is decompressed once per call and carries
-// one MSM point however many of its signatures the call holds.
-struct SigBatch {
-    const nwv_committee* c;
-    std::vector<uint8_t> keys, sig, msgs;  // keys: the committee's, then any non-member signer
-    std::vector<uint32_t> kidx;
-    std::vector<uint64_t> off;
-    std::vector<uint32_t> len;
-    std::vector<uint64_t> bits;
-    std::vector<uint8_t> ok;
-    void reset(const nwv_committee* cm) {
-        c = cm;
-        keys.clear();
-        sig.clear();
-        msgs.clear();
-        kidx.clear();
-        off.clear();
-        len.clear();
-        if (c && c->n) keys.assign(c->keys, c->keys + 32 * c->n);
-    }
-    // a message several signatures share (a certificate's digest) is stored once
-    uint64_t add_msg(const uint8_t* m, size_t mlen) {
-        const uint64_t o = msgs.size();
-        put(msgs, m, mlen);
-        return o;
-    }
-    // signer k = committee index (known for certificate signers: no key lookup)
-    size_t add_at(long k, const uint8_t* s, uint64_t moff, size_t mlen) {
-        kidx.push_back((uint32_t)k);
-        put(sig, s, 64);
-        off.push_back(moff);
-        len.push_back((uint32_t)mlen);
-        return off.size() - 1;
-    }
-    // q signatures (contiguous 64-byte records) by committee members ks[0..q) over one message
-    size_t add_run(const size_t* ks, size_t q, const uint8_t* s, uint64_t moff, size_t mlen) {
-        const size_t first = off.size();
-        for (size_t k = 0; k < q; k++) kidx.push_back((uint32_t)ks[k]);
-        put(sig, s, 64 * q);
-        off.insert(off.end(), q, moff);
-        len.insert(len.end(), q, (uint32_t)mlen);
-        return first;
-    }
-    size_t add(const uint8_t* p, const uint8_t* s, const uint8_t* m, size_t mlen) {
-        long k = c ? committee_index(*c, p) : -1;
-        if (k < 0) {
-            k = (long)(keys.size() / 32);
-            put(keys, p, 32);
-        }
-        return add_at(k, s, add_msg(m, mlen), mlen);
-    }
-    size_t size() const { return off.size(); }
-    int run(nwv_ctx* ctx) {
-        const size_t n = size();
-        ok.assign(n, 1);
-        if (n == 0) return NWV_OK;
-        msgs.resize(msgs.size() + 16);
-        bits.assign((n + 63) / 64 + 1, 0);
-        int all = 0;
-        int rc = nwv_ed25519_verify_batch_keyed(ctx, keys.size() / 32, keys.data(), n, kidx.data(), sig.data(),
-                                                msgs.data(), off.data(), len.data(), nullptr, &all, bits.data());
-        if (rc) return rc;
-        for (size_t i = 0; i < n; i++) ok[i] = (uint8_t)((bits[i >> 6] >> (i & 63)) & 1);
-        return NWV_OK;
-    }
-};
-
 // Committee lookups (keys sorted by bytes, as the BTreeMap)
 long committee_index(const nwv_committee& c, const uint8_t* pk) {
     size_t lo = 0, hi = c.n;
@@ -214,16 +145,6 @@ void plan_header(const nwv_committee& c, const nwv_header& h, DigestBatch& db, H
             p.post = NWV_DAG_MALFORMED_HEADER;
             return;
         }
-}
-
-// verdict of Header::verify once digests are known; queues the signature when reached
-int header_after_digest(const nwv_header& h, const HeaderPlan& p, const std::vector<uint8_t>& dig,
-                        SigBatch* sb, HeaderPlan& pw) {
-    if (p.pre) return p.pre;
-    if (std::memcmp(dig.data() + 32 * p.digest, h.id, 32) != 0) return NWV_DAG_INVALID_HEADER_ID;
-    if (p.post) return p.post;
-    if (sb) pw.sig = (long)sb->add(h.author, h.signature, h.id, 32);
-    return NWV_DAG_OK;
 }
 
 bool valid_args(const nwv_committee* c) {
@@ -298,24 +219,96 @@ int nwv_certificate_digest(nwv_ctx* ctx, const nwv_certificate* c, uint8_t out[3
 // order (Header::verify :150-183, Vote::verify :307-328, Certificate::verify :487-537).
 }  // extern "C"
 namespace {
+// Signatures of a mixed call, each over one of the call's digests (by index): the digests are
+// hashed and the signatures verified by ONE engine call with no host round trip in between
+// (nwv_ed25519_verify_batch_keyed_digests).  A header's signature is checked over its computed
+// digest: whenever that verdict is used the id equals the digest (else InvalidHeaderId comes
+// first), so the bytes are the ones the reference verifies.
+struct DigestSigBatch {
+    const nwv_committee* c = nullptr;
+    std::vector<uint8_t> keys, sig, ok;
+    std::vector<uint32_t> kidx, didx;
+    std::vector<uint64_t> bits;
+    void reset(const nwv_committee* cm) {
+        c = cm;
+        keys.clear();
+        sig.clear();
+        kidx.clear();
+        didx.clear();
+        if (c && c->n) keys.assign(c->keys, c->keys + 32 * c->n);
+    }
+    size_t add_run(const size_t* ks, size_t q, const uint8_t* s, size_t digest) {
+        const size_t first = kidx.size();
+        for (size_t k = 0; k < q; k++) kidx.push_back((uint32_t)ks[k]);
+        put(sig, s, 64 * q);
+        didx.insert(didx.end(), q, (uint32_t)digest);
+        return first;
+    }
+    size_t add(const uint8_t* p, const uint8_t* s, size_t digest) {
+        long k = committee_index(*c, p);
+        if (k < 0) {  // not reached by the verify paths (unknown authors fail first); kept total
+            k = (long)(keys.size() / 32);
+            put(keys, p, 32);
+        }
+        const size_t kk = (size_t)k;
+        return add_run(&kk, 1, s, digest);
+    }
+    int run(nwv_ctx* ctx, DigestBatch& db, std::vector<uint8_t>& dig) {
+        const size_t n = kidx.size(), m = db.off.size();
+        ok.assign(n, 1);
+        dig.assign(32 * m, 0);
+        if (m == 0) return NWV_OK;
+        db.arena.resize(db.arena.size() + 16);
+        bits.assign((n + 63) / 64 + 1, 0);
+        int all = 0;
+        int rc = nwv_ed25519_verify_batch_keyed_digests(ctx, m, db.arena.data(), db.off.data(), db.len.data(),
+                                                        dig.data(), keys.size() / 32, keys.data(), n, kidx.data(),
+                                                        sig.data(), didx.data(), nullptr, &all, bits.data());
+        if (rc) return rc;
+        for (size_t i = 0; i < n; i++) ok[i] = (uint8_t)((bits[i >> 6] >> (i & 63)) & 1);
+        return NWV_OK;
+    }
+};
+
+// Header::verify up to its signature, once the digest is known (epoch, id, authority / workers)
+int header_checks(const nwv_header& h, const HeaderPlan& p, const std::vector<uint8_t>& dig) {
+    if (p.pre) return p.pre;
+    if (std::memcmp(dig.data() + 32 * p.digest, h.id, 32) != 0) return NWV_DAG_INVALID_HEADER_ID;
+    return p.post;
+}
+
 int verify_mixed(nwv_ctx* ctx, const nwv_committee& c, size_t nh, const nwv_header* h, int32_t* hres,
                  size_t nv, const nwv_vote* v, int32_t* vres, size_t nc, const nwv_certificate* cs,
                  int32_t* cres) {
     const uint64_t quorum = quorum_threshold(c);
     htrace("mixed:start");
-    // phase 1: host checks and every digest (header ids to re-derive, vote and certificate digests)
+    // phase 1 (host only): every preimage, and every signature a verdict may depend on, over
+    // the index of the digest it signs
     thread_local DigestBatch db;
+    thread_local DigestSigBatch sb;
     db.reset();
+    sb.reset(&c);
     std::vector<HeaderPlan> hplan(nh), cplan(nc);
-    for (size_t i = 0; i < nh; i++) plan_header(c, h[i], db, hplan[i]);
-    std::vector<long> vdig(nv, -1);
+    for (size_t i = 0; i < nh; i++) {
+        plan_header(c, h[i], db, hplan[i]);
+        if (!hplan[i].pre && !hplan[i].post) hplan[i].sig = (long)sb.add(h[i].author, h[i].signature, hplan[i].digest);
+    }
+    std::vector<long> vsig(nv, -1);
     for (size_t i = 0; i < nv; i++) {
-        vdig[i] = (long)db.add_begin();
+        const size_t dg = db.add_begin();
         id_round_epoch_origin(v[i].id, v[i].round, v[i].epoch, v[i].origin, db.arena);
         db.add_end();
+        if (v[i].epoch != c.epoch) vres[i] = NWV_DAG_INVALID_EPOCH;
+        else if (committee_stake(c, v[i].author) == 0) vres[i] = NWV_DAG_UNKNOWN_AUTHORITY;
+        else {
+            vres[i] = NWV_DAG_OK;
+            vsig[i] = (long)sb.add(v[i].author, v[i].signature, dg);
+        }
     }
-    std::vector<long> cdig(nc, -1);
     std::vector<uint8_t> done(nc, 0);
+    std::vector<long> agg_first(nc, -1), agg_count(nc, 0);
+    std::vector<int32_t> after_header(nc, NWV_DAG_OK);
+    std::vector<size_t> pks;
     for (size_t i = 0; i < nc; i++) {
         const nwv_certificate& x = cs[i];
         cres[i] = NWV_DAG_OK;
@@ -328,41 +321,13 @@ int verify_mixed(nwv_ctx* ctx, const nwv_committee& c, size_t nh, const nwv_head
             done[i] = 1;
             continue;
         }
-        plan_header(c, x.header, db, cplan[i]);
-        cdig[i] = (long)db.add_begin();
+        HeaderPlan& hp = cplan[i];
+        plan_header(c, x.header, db, hp);
+        const size_t cdig = db.add_begin();
         id_round_epoch_origin(x.header.id, x.header.round, x.header.epoch, x.header.author, db.arena);
         db.add_end();
-    }
-    thread_local std::vector<uint8_t> dig;
-    htrace("mixed:preimages");
-    int rc = db.run(ctx, dig);
-    if (rc) return rc;
-    htrace("mixed:digests");
-    // phase 2: host verdicts up to the signatures, and the one signature batch
-    thread_local SigBatch sb;
-    sb.reset(&c);
-    for (size_t i = 0; i < nh; i++) hres[i] = header_after_digest(h[i], hplan[i], dig, &sb, hplan[i]);
-    std::vector<long> vsig(nv, -1);
-    for (size_t i = 0; i < nv; i++) {
-        if (v[i].epoch != c.epoch) vres[i] = NWV_DAG_INVALID_EPOCH;
-        else if (committee_stake(c, v[i].author) == 0) vres[i] = NWV_DAG_UNKNOWN_AUTHORITY;
-        else {
-            vres[i] = NWV_DAG_OK;
-            vsig[i] = (long)sb.add(v[i].author, v[i].signature, dig.data() + 32 * vdig[i], 32);
-        }
-    }
-    std::vector<long> agg_first(nc, -1), agg_count(nc, 0);
-    std::vector<int32_t> after_header(nc, NWV_DAG_OK);
-    std::vector<size_t> pks;
-    for (size_t i = 0; i < nc; i++) {
-        if (done[i]) continue;
-        const nwv_certificate& x = cs[i];
-        const int hr = header_after_digest(x.header, cplan[i], dig, &sb, cplan[i]);
-        if (hr) {
-            cres[i] = hr;
-            done[i] = 1;
-            continue;
-        }
+        if (hp.pre || hp.post) continue;  // the header's own error decides
+        hp.sig = (long)sb.add(x.header.author, x.header.signature, hp.digest);
         // bitmap -> pks in committee order, as the filter at :505-520
         uint64_t weight = 0;
         size_t it = 0;
@@ -383,21 +348,30 @@ int verify_mixed(nwv_ctx* ctx, const nwv_committee& c, size_t nh, const nwv_head
             after_header[i] = NWV_DAG_INVALID_SIGNATURE;
             continue;
         }
-        const uint64_t moff = sb.add_msg(dig.data() + 32 * cdig[i], 32);
-        agg_first[i] = (long)sb.add_run(pks.data(), pks.size(), x.aggregated_signature, moff, 32);
+        agg_first[i] = (long)sb.add_run(pks.data(), pks.size(), x.aggregated_signature, cdig);
         agg_count[i] = (long)pks.size();
     }
-    htrace("mixed:sigbatch");
-    if ((rc = sb.run(ctx))) return rc;
-    const std::vector<uint8_t>& ok = sb.ok;
+    htrace("mixed:batch");
+    // phase 2: one engine call (digests, then the signatures over them, on the device)
+    thread_local std::vector<uint8_t> dig;
+    int rc = sb.run(ctx, db, dig);
+    if (rc) return rc;
     htrace("mixed:verified");
-    // phase 3: signature verdicts
-    for (size_t i = 0; i < nh; i++)
+    const std::vector<uint8_t>& ok = sb.ok;
+    // phase 3: verdicts in the reference's check order
+    for (size_t i = 0; i < nh; i++) {
+        hres[i] = header_checks(h[i], hplan[i], dig);
         if (hres[i] == NWV_DAG_OK && hplan[i].sig >= 0 && !ok[hplan[i].sig]) hres[i] = NWV_DAG_INVALID_SIGNATURE;
+    }
     for (size_t i = 0; i < nv; i++)
         if (vsig[i] >= 0 && !ok[vsig[i]]) vres[i] = NWV_DAG_INVALID_SIGNATURE;
     for (size_t i = 0; i < nc; i++) {
         if (done[i]) continue;
+        const int hr = header_checks(cs[i].header, cplan[i], dig);
+        if (hr) {
+            cres[i] = hr;
+            continue;
+        }
         if (cplan[i].sig >= 0 && !ok[cplan[i].sig]) {  // Header::verify's signature comes first
             cres[i] = NWV_DAG_INVALID_SIGNATURE;
             continue;

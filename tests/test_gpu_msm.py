@@ -217,3 +217,41 @@ def test_staged_keyed_msm(eng):
     allv, bits = st.fetch()
     st.free()
     assert allv and bits.all()
+
+
+@pytest.mark.parametrize("n_pre,n_sig", [(1, 1), (40, 700), (300, 7000)])
+def test_keyed_digests_hash_then_verify(eng, n_pre, n_sig):
+    """nwv_ed25519_verify_batch_keyed_digests: the preimages' BLAKE2b-256 digests
+    come back equal to the oracle's, and signature i is checked over digest digest_idx[i] from
+    device memory: verdicts equal the oracle's over the same bytes, a forged signature and a
+    signature over another digest are pinpointed, an out-of-range digest index is an argument
+    error"""
+    rnd = random.Random(n_pre * 7 + n_sig)
+    pre = [rnd.randbytes(rnd.choice([80, 127, 128, 129, 2200])) for _ in range(n_pre)]
+    want_dig = [of.blake2b256(x) for x in pre]
+    m = min(100, n_sig)
+    kseeds = [rnd.randbytes(32) for _ in range(m)]
+    didx = [rnd.randrange(n_pre) for _ in range(n_sig)]
+    msgs = [want_dig[j] for j in didx]
+    pk, sg = eng.sign_many([kseeds[i % m] for i in range(n_sig)], msgs)
+    items = [(pk[32 * i:32 * i + 32].tobytes(), sg[64 * i:64 * i + 64].tobytes(), msgs[i]) for i in range(n_sig)]
+    keys, kidx = _keyed(items)
+    sigs = [s for _, s, _ in items]
+    dig, ok, bits = eng.verify_batch_keyed_digests(pre, keys, kidx, sigs, didx, seed=b"\x05" * 32)
+    assert dig == want_dig and ok and all(bits)
+    bad = {n_sig // 2}
+    s = bytearray(sigs[n_sig // 2])
+    s[40] ^= 1
+    sigs[n_sig // 2] = bytes(s)
+    didx2 = list(didx)
+    if n_pre > 1:  # signature 0 now points at a digest it did not sign
+        didx2[0] = (didx[0] + 1) % n_pre
+        bad.add(0)
+    dig, ok, bits = eng.verify_batch_keyed_digests(pre, keys, kidx, sigs, didx2)
+    assert dig == want_dig and not ok
+    assert {i for i in range(n_sig) if not bits[i]} == bad
+    if n_sig <= 700:
+        want = [of.verify(items[i][0], sigs[i], want_dig[didx2[i]]) for i in range(n_sig)]
+        assert bits == want
+    with pytest.raises(Exception):
+        eng.verify_batch_keyed_digests(pre, keys, kidx, sigs, [n_pre] * n_sig)

@@ -13,15 +13,23 @@
 extern "C" int nwv_blake2b256_many(nwv_ctx*, size_t n, const uint8_t* base, const uint64_t* off,
                                    const uint64_t* len, uint8_t* out) {
     for (size_t i = 0; i < n; i++) {
-        uint64_t h = 1469598103934665603ull;
-        for (uint64_t k = 0; k < len[i]; k++) h = (h ^ base[off[i] + k]) * 1099511628211ull;
+        uint64_t h = 1469598103934665603ull;  // cheap stand-in: 8 bytes per step
+        for (uint64_t k = 0; k + 8 <= len[i]; k += 8) {
+            uint64_t w;
+            std::memcpy(&w, base + off[i] + k, 8);
+            h = (h ^ w) * 1099511628211ull;
+        }
+        for (uint64_t k = len[i] & ~7ull; k < len[i]; k++) h = (h ^ base[off[i] + k]) * 1099511628211ull;
         for (int w = 0; w < 4; w++) std::memcpy(out + 32 * i + 8 * w, &(h += w), 8);
     }
     return NWV_OK;
 }
-extern "C" int nwv_ed25519_verify_batch_keyed(nwv_ctx*, size_t, const uint8_t*, size_t n, const uint32_t*,
-                                              const uint8_t*, const uint8_t*, const uint64_t*, const uint32_t*,
-                                              const uint8_t*, int* all_valid, uint64_t* bits) {
+extern "C" int nwv_ed25519_verify_batch_keyed_digests(nwv_ctx* ctx, size_t n_pre, const uint8_t* base,
+                                                      const uint64_t* off, const uint64_t* len, uint8_t* dig,
+                                                      size_t, const uint8_t*, size_t n, const uint32_t*,
+                                                      const uint8_t*, const uint32_t*, const uint8_t*,
+                                                      int* all_valid, uint64_t* bits) {
+    nwv_blake2b256_many(ctx, n_pre, base, off, len, dig);
     *all_valid = 1;
     if (bits) std::memset(bits, 0xff, 8 * ((n + 63) / 64));
     return NWV_OK;
