@@ -128,6 +128,10 @@ struct Device {
     PinnedBuf hstage;              // host side of ed_stage's single H2D copy
     hipEvent_t hstage_ev = nullptr;  // recorded after that copy; hstage is reusable once it fires
     DevBuf b2_base, b2_off, b2_len, b2_out, b2_packed, b2_plen, b2_err;
+    DevBuf b2_in;                  // small digest batches: off, len and bytes in one arena
+    PinnedBuf b2stage;             // host side of that arena's single H2D copy
+    PinnedBuf b2dig;               // digests of a digest-then-verify call, copied back early
+    hipEvent_t b2stage_ev = nullptr;
 };
 
 int with_device(Device& d) {
@@ -144,6 +148,7 @@ int device_open(Device& d, int ordinal) {
     NWV_HIP(hipSetDevice(ordinal));
     NWV_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     NWV_HIP(hipEventCreateWithFlags(&d.hstage_ev, hipEventDisableTiming));
+    NWV_HIP(hipEventCreateWithFlags(&d.b2stage_ev, hipEventDisableTiming));
     int rc = d.btab.ensure((BASE_TABLE_WORDS + CACHED_ENTRY_WORDS) * sizeof(uint32_t));
     if (rc) return rc;
     hipLaunchKernelGGL(k_base_table, dim3((BASE_TABLE_ENTRIES + 63) / 64), dim3(64), 0, d.stream,
@@ -162,7 +167,11 @@ void device_close(Device& d) {
     d.hstage.release();
     if (d.hstage_ev) (void)hipEventDestroy(d.hstage_ev);
     d.hstage_ev = nullptr;
-    for (DevBuf* b : {&d.b2_base, &d.b2_off, &d.b2_len, &d.b2_out, &d.b2_packed, &d.b2_plen, &d.b2_err})
+    if (d.b2stage_ev) (void)hipEventDestroy(d.b2stage_ev);
+    d.b2stage_ev = nullptr;
+    d.b2stage.release();
+    d.b2dig.release();
+    for (DevBuf* b : {&d.b2_base, &d.b2_off, &d.b2_len, &d.b2_out, &d.b2_packed, &d.b2_plen, &d.b2_err, &d.b2_in})
         b->release();
     if (d.stream) (void)hipStreamDestroy(d.stream);
     d.stream = nullptr;
@@ -1090,8 +1099,15 @@ static void b2_launch(Device& d, size_t m, uint64_t maxlen, const uint8_t* base,
                            (uint64_t)m, base, off, len, out);
 }
 
+// device pointers of a staged digest batch (views into b2_in, or the b2_base/off/len buffers)
+struct B2Staged {
+    const uint8_t* base;
+    const uint64_t* off;
+    const uint64_t* len;
+};
+
 static int b2_stage(Device& d, size_t n, const uint8_t* base, const uint64_t* off,
-                    const uint64_t* len, size_t lo, size_t hi, std::vector<uint64_t>& roff) {
+                    const uint64_t* len, size_t lo, size_t hi, std::vector<uint64_t>& roff, B2Staged& st) {
     uint64_t mlo = UINT64_MAX, mhi = 0;
     for (size_t i = lo; i < hi; i++) {
         mlo = std::min<uint64_t>(mlo, off[i]);
@@ -1102,14 +1118,35 @@ static int b2_stage(Device& d, size_t n, const uint8_t* base, const uint64_t* of
     roff.resize(m);
     for (size_t i = 0; i < m; i++) roff[i] = off[lo + i] - mlo;
     int rc;
+    (void)n;
+    // small batches (header / vote / certificate preimages): offsets, lengths and bytes packed into
+    // pinned memory and sent as ONE copy; large ones (worker batches) keep the driver's pipelined
+    // pageable path, which overlaps its own staging with the DMA
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_len = up(8 * m + 8), o_bytes = o_len + up(8 * m + 8), total = o_bytes + bytes + MSG_PAD;
+    if (total <= ((size_t)4 << 20)) {
+        if ((rc = d.b2_in.ensure(total)) || (rc = d.b2_out.ensure(32 * m + 32))) return rc;
+        NWV_HIP(hipEventSynchronize(d.b2stage_ev));
+        if ((rc = d.b2stage.ensure(total))) return rc;
+        uint8_t* h = static_cast<uint8_t*>(d.b2stage.p);
+        std::memcpy(h, roff.data(), 8 * m);
+        std::memcpy(h + o_len, len + lo, 8 * m);
+        if (bytes) std::memcpy(h + o_bytes, base + mlo, bytes);
+        std::memset(h + o_bytes + bytes, 0, MSG_PAD);
+        NWV_HIP(hipMemcpyAsync(d.b2_in.p, h, total, hipMemcpyHostToDevice, d.stream));
+        NWV_HIP(hipEventRecord(d.b2stage_ev, d.stream));
+        const uint8_t* g = d.b2_in.as<uint8_t>();
+        st = B2Staged{g + o_bytes, reinterpret_cast<const uint64_t*>(g), reinterpret_cast<const uint64_t*>(g + o_len)};
+        return NWV_OK;
+    }
     if ((rc = d.b2_base.ensure(bytes + MSG_PAD)) || (rc = d.b2_off.ensure(8 * m + 8)) ||
         (rc = d.b2_len.ensure(8 * m + 8)) || (rc = d.b2_out.ensure(32 * m + 32)))
         return rc;
-    (void)n;
     if (bytes) NWV_HIP(hipMemcpyAsync(d.b2_base.p, base + mlo, bytes, hipMemcpyHostToDevice, d.stream));
     NWV_HIP(hipMemsetAsync(d.b2_base.as<uint8_t>() + bytes, 0, MSG_PAD, d.stream));
     NWV_HIP(hipMemcpyAsync(d.b2_off.p, roff.data(), 8 * m, hipMemcpyHostToDevice, d.stream));
     NWV_HIP(hipMemcpyAsync(d.b2_len.p, len + lo, 8 * m, hipMemcpyHostToDevice, d.stream));
+    st = B2Staged{d.b2_base.as<uint8_t>(), d.b2_off.as<uint64_t>(), d.b2_len.as<uint64_t>()};
     return NWV_OK;
 }
 
@@ -1131,13 +1168,13 @@ int nwv_blake2b256_many(nwv_ctx* ctx, size_t n, const uint8_t* base, const uint6
             std::lock_guard<std::mutex> g(d.mu);
             std::vector<uint64_t> roff;
             int rc = with_device(d);
-            if (!rc) rc = b2_stage(d, n, base, off, len, lo, hi, roff);
+            B2Staged st{};
+            if (!rc) rc = b2_stage(d, n, base, off, len, lo, hi, roff, st);
             if (!rc) {
                 const size_t m = hi - lo;
                 uint64_t maxlen = 0;
                 for (size_t k2 = lo; k2 < hi; k2++) maxlen = std::max<uint64_t>(maxlen, len[k2]);
-                b2_launch(d, m, maxlen, d.b2_base.as<uint8_t>(), d.b2_off.as<uint64_t>(),
-                          d.b2_len.as<uint64_t>(), d.b2_out.as<uint32_t>());
+                b2_launch(d, m, maxlen, st.base, st.off, st.len, d.b2_out.as<uint32_t>());
                 hipError_t e = hipGetLastError();
                 if (e == hipSuccess) e = hipMemcpyAsync(out + 32 * lo, d.b2_out.p, 32 * m,
                                                         hipMemcpyDeviceToHost, d.stream);
@@ -1195,16 +1232,20 @@ int nwv_ed25519_verify_batch_keyed_digests(nwv_ctx* ctx, size_t n_pre, const uin
     std::lock_guard<std::mutex> g(d.mu);
     int rc = with_device(d);
     std::vector<uint64_t> roff;
-    if (!rc) rc = b2_stage(d, n_pre, pre_base, pre_off, pre_len, 0, n_pre, roff);
+    B2Staged st{};
+    if (!rc) rc = b2_stage(d, n_pre, pre_base, pre_off, pre_len, 0, n_pre, roff, st);
     if (rc) return rc;
     // the digests stay on the device as the message arena of the batch (over-read slack included)
     if ((rc = d.b2_out.ensure(32 * n_pre + 4 * MSG_PAD))) return rc;
     uint64_t maxlen = 0;
     for (size_t k = 0; k < n_pre; k++) maxlen = std::max<uint64_t>(maxlen, pre_len[k]);
     NWV_HIP(hipMemsetAsync(d.b2_out.as<uint8_t>() + 32 * n_pre, 0, 4 * MSG_PAD, d.stream));
-    b2_launch(d, n_pre, maxlen, d.b2_base.as<uint8_t>(), d.b2_off.as<uint64_t>(), d.b2_len.as<uint64_t>(),
-              d.b2_out.as<uint32_t>());
+    b2_launch(d, n_pre, maxlen, st.base, st.off, st.len, d.b2_out.as<uint32_t>());
     NWV_HIP(hipGetLastError());
+    // the digests head back to pinned memory right behind the hash (stream order), so the only
+    // wait left is the verdict's
+    if ((rc = d.b2dig.ensure(32 * n_pre))) return rc;
+    NWV_HIP(hipMemcpyAsync(d.b2dig.p, d.b2_out.p, 32 * n_pre, hipMemcpyDeviceToHost, d.stream));
     // no host round trip: the batch is staged behind the hash on the same stream
     rc = ed_stage_keyed(d, d.ed, 0, n, n_keys, keys, key_idx, sig, nullptr, moff.data(), mlen.data(), seed,
                         &d.b2_out);
@@ -1213,8 +1254,8 @@ int nwv_ed25519_verify_batch_keyed_digests(nwv_ctx* ctx, size_t n_pre, const uin
     rc = batch_on_device(d, d.ed, n, seed, d.stream, &ok, verdict_bits_or_null, true);
     if (rc) return rc;
     if (!ok) *all_valid = 0;
-    NWV_HIP(hipMemcpyAsync(digests_out, d.b2_out.p, 32 * n_pre, hipMemcpyDeviceToHost, d.stream));
-    NWV_HIP(hipStreamSynchronize(d.stream));
+    NWV_HIP(hipStreamSynchronize(d.stream));  // already synchronised by the verdict read
+    std::memcpy(digests_out, d.b2dig.p, 32 * n_pre);
     return NWV_OK;
 }
 
@@ -1227,7 +1268,8 @@ int nwv_batch_digest_serialized(nwv_ctx* ctx, size_t n, const uint8_t* base, con
     std::lock_guard<std::mutex> g(d.mu);
     int rc = with_device(d);
     std::vector<uint64_t> roff;
-    if (!rc) rc = b2_stage(d, n, base, off, len, 0, n, roff);
+    B2Staged st{};
+    if (!rc) rc = b2_stage(d, n, base, off, len, 0, n, roff, st);
     if (rc) return rc;
     size_t bytes = 0;
     for (size_t i = 0; i < n; i++) bytes = std::max<size_t>(bytes, roff[i] + len[i]);
@@ -1236,11 +1278,10 @@ int nwv_batch_digest_serialized(nwv_ctx* ctx, size_t n, const uint8_t* base, con
         return rc;
     NWV_HIP(hipMemsetAsync(d.b2_packed.p, 0, bytes + MSG_PAD, d.stream));
     hipLaunchKernelGGL(k_batch_compact, dim3((unsigned)n), dim3(256), 0, d.stream, (uint64_t)n,
-                       d.b2_base.as<uint8_t>(), d.b2_off.as<uint64_t>(), d.b2_len.as<uint64_t>(),
-                       d.b2_packed.as<uint8_t>(), d.b2_plen.as<uint64_t>(), d.b2_err.as<int64_t>());
+                       st.base, st.off, st.len, d.b2_packed.as<uint8_t>(), d.b2_plen.as<uint64_t>(), d.b2_err.as<int64_t>());
     uint64_t maxlen = 0;
     for (size_t k2 = 0; k2 < n; k2++) maxlen = std::max<uint64_t>(maxlen, len[k2]);
-    b2_launch(d, n, maxlen, d.b2_packed.as<uint8_t>(), d.b2_off.as<uint64_t>(), d.b2_plen.as<uint64_t>(),
+    b2_launch(d, n, maxlen, d.b2_packed.as<uint8_t>(), st.off, d.b2_plen.as<uint64_t>(),
               d.b2_out.as<uint32_t>());
     NWV_HIP(hipGetLastError());
     NWV_HIP(hipMemcpyAsync(out, d.b2_out.p, 32 * n, hipMemcpyDeviceToHost, d.stream));
