@@ -14,4 +14,5 @@ timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d $O/mr2 -o p --output-format csv
 timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE -d $O/mr3 -o p --output-format csv -- $D > $O/mr3.log 2>&1
 python tools/pmc_summary.py --n 65536 --note "rocprofv3 --pmc, separate passes, tools/profile_driver.py --mode 1 (batch MSM, timed kernel-by-kernel runs), per-dispatch averages; FETCH_SIZE/WRITE_SIZE in KiB as reported (gfx950 FETCH_SIZE counts wide streaming reads at 1/2); SQ_INSTS_VALU_INT64 = v_mad_u64_u32 and the other 64-bit integer forms" --out $O/msm_pmc_n65536.json $O/mr1 $O/mr2 $O/mr3
 timeout -k 10 300 python -u tools/firehose_bench.py --n 2097152 --reps 3 > $O/fh_2m.json 2> $O/fh_2m.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_bench -o bench --output-format csv -- python bench.py --no-cpu-baseline --no-configs --latency-reps 10 > $O/prof_bench.log 2>&1
 echo ALLDONE
