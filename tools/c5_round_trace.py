@@ -14,9 +14,9 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 
-def timeline(d):
+def timeline(d, prefix="c5"):
     ev = []
-    for name in ("c5_kernel_trace.csv", "c5_memory_copy_trace.csv"):
+    for name in (f"{prefix}_kernel_trace.csv", f"{prefix}_memory_copy_trace.csv"):
         p = os.path.join(d, name)
         if not os.path.exists(p):
             continue
