@@ -398,10 +398,18 @@ static void pack_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
 // threads take 2 MiB pieces in order, copy each into the pinned buffer and queue its DMA on
 // `stream` at once, so the copy engine starts on the first pieces while the rest are packed
 // (C4, 33.5 MB of messages: pack ~0.74 ms then DMA ~0.72 ms back to back before).
-static int pack_copy_h2d(int ordinal, uint8_t* dev_dst, uint8_t* host_dst, const uint8_t* src, size_t bytes,
+struct PackSeg {
+    size_t off;          // offset in the arena (host and device alike)
+    const uint8_t* src;  // caller's bytes
+    size_t len;
+};
+static int pack_copy_h2d(int ordinal, uint8_t* dev_base, uint8_t* host_base, const std::vector<PackSeg>& segs,
                          hipStream_t stream) {
     constexpr size_t kPiece = (size_t)2 << 20;
-    const size_t pieces = (bytes + kPiece - 1) / kPiece;
+    std::vector<PackSeg> pieces;
+    for (const PackSeg& g : segs)
+        for (size_t o = 0; o < g.len; o += kPiece)
+            pieces.push_back(PackSeg{g.off + o, g.src + o, std::min(kPiece, g.len - o)});
     std::atomic<size_t> next{0};
     std::atomic<int> err{0};
     auto work = [&](bool helper) {
@@ -409,15 +417,16 @@ static int pack_copy_h2d(int ordinal, uint8_t* dev_dst, uint8_t* host_dst, const
             err.store(1);
             return;
         }
-        for (size_t k; (k = next.fetch_add(1)) < pieces;) {
-            const size_t o = k * kPiece, len = std::min(kPiece, bytes - o);
-            std::memcpy(host_dst + o, src + o, len);
-            if (hipMemcpyAsync(dev_dst + o, host_dst + o, len, hipMemcpyHostToDevice, stream) != hipSuccess)
+        for (size_t k; (k = next.fetch_add(1)) < pieces.size();) {
+            const PackSeg& q = pieces[k];
+            std::memcpy(host_base + q.off, q.src, q.len);
+            if (hipMemcpyAsync(dev_base + q.off, host_base + q.off, q.len, hipMemcpyHostToDevice, stream) !=
+                hipSuccess)
                 err.store(1);
         }
     };
     std::vector<std::thread> th;
-    const size_t helpers = std::min<size_t>(7, pieces > 1 ? pieces - 1 : 0);
+    const size_t helpers = std::min<size_t>(7, pieces.size() > 1 ? pieces.size() - 1 : 0);
     for (size_t t = 0; t < helpers; t++) {
         try {
             th.emplace_back(work, true);
@@ -488,7 +497,10 @@ int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, c
     NWV_HIP(hipEventSynchronize(d.hstage_ev));
     if ((rc = d.hstage.ensure(total))) return rc;
     uint8_t* h = static_cast<uint8_t*>(d.hstage.p);
-    if (inputs) {
+    // large stagings: the caller's pk / sig / message bytes are packed piece by piece with each
+    // piece's DMA queued at once (pack_copy_h2d); the small computed regions go first
+    const bool piped = 96 * (inputs ? n : 0) + mbytes >= ((size_t)16 << 20);
+    if (inputs && !piped) {
         pack_copy(h + o_pk, pk + 32 * lo, 32 * n);
         pack_copy(h + o_sig, sig + 64 * lo, 64 * n);
     }
@@ -497,7 +509,6 @@ int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, c
     std::memcpy(h + o_len, msg_len + lo, 4 * n);
     std::memset(h + o_state, 0, 256);
     if (seed32) std::memcpy(h + o_state + 32, seed32, 32);
-    const bool piped = mbytes >= ((size_t)16 << 20);
     if (mbytes && !piped) pack_copy(h + o_msg, msg_base + mlo, mbytes);
     std::memset(h + o_msg + mbytes, 0, MSG_PAD);
     if (kt) {
@@ -507,11 +518,17 @@ int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, c
     }
     htrace("stage:packed");
     if (piped) {
-        // everything before the messages, the messages piece by piece as they are packed, then
-        // the padding and keyed tables behind them
+        // offsets, lengths and MSM state, then pk / sig / messages piece by piece as they are
+        // packed, then the padding and keyed tables behind them
         uint8_t* gdev = b.in.as<uint8_t>();
-        NWV_HIP(hipMemcpyAsync(gdev, h, o_msg, hipMemcpyHostToDevice, d.stream));
-        int prc = pack_copy_h2d(d.ordinal, gdev + o_msg, h + o_msg, msg_base + mlo, mbytes, d.stream);
+        NWV_HIP(hipMemcpyAsync(gdev + o_off, h + o_off, o_msg - o_off, hipMemcpyHostToDevice, d.stream));
+        std::vector<PackSeg> segs;
+        if (inputs) {
+            segs.push_back(PackSeg{o_pk, pk + 32 * lo, 32 * n});
+            segs.push_back(PackSeg{o_sig, sig + 64 * lo, 64 * n});
+        }
+        if (mbytes) segs.push_back(PackSeg{o_msg, msg_base + mlo, mbytes});
+        int prc = pack_copy_h2d(d.ordinal, gdev, h, segs, d.stream);
         if (prc) return prc;
         NWV_HIP(hipMemcpyAsync(gdev + o_msg + mbytes, h + o_msg + mbytes, total - o_msg - mbytes,
                                hipMemcpyHostToDevice, d.stream));
