@@ -208,3 +208,29 @@ def test_verify_mixed_matches_oracle(eng):
                                                                [0] * len(good_c))
     assert T.verify_mixed(eng, c, votes=good_v) == ([], [0] * len(good_v), [])
     assert T.verify_mixed(eng, c) == ([], [], [])
+
+
+def test_verify_mixed_concurrent_threads(eng):
+    """nwv_verify_mixed_many from 6 host threads on one context (per-thread batch buffers, the
+    device lock around each engine call): every thread gets the codes of the serial call"""
+    from concurrent.futures import ThreadPoolExecutor
+    rnd = random.Random(21)
+    fx = nt.CommitteeFixture(10, of.pubkey, of.sign, seed=9)
+    c = tu.committee(fx.committee)
+    cases = _mutations(fx, rnd)
+    H = [tu.header(h) for h, _ in cases if h is not None]
+    C = [tu.certificate(x) for _, x in cases]
+    h = fx.header()
+    vs = fx.votes(h)
+    vs[2] = dict(vs[2], signature=bytes(64))
+    V = [tu.vote(v) for v in vs]
+    want = T.verify_mixed(eng, c, H, V, C)
+
+    def run(k):
+        # thread k verifies a rotation of the item lists, so the batches differ between threads
+        r = k % max(1, len(C))
+        got = T.verify_mixed(eng, c, H, V, C[r:] + C[:r])
+        return got == (want[0], want[1], want[2][r:] + want[2][:r])
+
+    with ThreadPoolExecutor(6) as ex:
+        assert all(ex.map(run, range(24)))
