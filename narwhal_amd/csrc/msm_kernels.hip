@@ -300,8 +300,12 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_scatter(
 }
 
 // ---- exclusive scan of u32 counts (tiles of 4096: 256 threads x 16) ----------------------
+// kstart != null: the whole array is one tile (small batches), so this launch also finishes the
+// scan: kstart[key] = a[key * chunks], tile_sum[0] = 0 and tile_sum[1] = total, i.e. what
+// k_scan_tiles and k_scan_add produce for several tiles
 extern "C" __global__ void __launch_bounds__(256) k_scan_tile(uint64_t len, uint32_t* __restrict__ a,
-                                                              uint32_t* __restrict__ tile_sum) {
+                                                              uint32_t* __restrict__ tile_sum, uint32_t chunks,
+                                                              uint32_t* __restrict__ kstart) {
     __shared__ uint32_t sh[256];
     const uint64_t base = (uint64_t)blockIdx.x * 4096 + threadIdx.x * 16;
     uint32_t v[16], s = 0;
@@ -321,10 +325,20 @@ extern "C" __global__ void __launch_bounds__(256) k_scan_tile(uint64_t len, uint
     uint32_t run = sh[threadIdx.x] - s;  // exclusive prefix of this thread
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        if (base + k < len) a[base + k] = run;
+        if (base + k < len) {
+            a[base + k] = run;
+            if (kstart && (base + k) % chunks == 0) kstart[(base + k) / chunks] = run;
+        }
         run += v[k];
     }
-    if (threadIdx.x == 255) tile_sum[blockIdx.x] = sh[255];
+    if (threadIdx.x == 255) {
+        if (kstart) {
+            tile_sum[0] = 0;
+            tile_sum[1] = sh[255];
+        } else {
+            tile_sum[blockIdx.x] = sh[255];
+        }
+    }
 }
 
 // one workgroup: exclusive scan of the tile sums in place; tile_sum[ntiles] = total

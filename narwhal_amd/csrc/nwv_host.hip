@@ -341,10 +341,16 @@ int msm_launch(Device& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipS
     hipLaunchKernelGGL(k_msm_hist, gsort, dim3(256), lds_nb, stream, (uint64_t)n, (uint64_t)na, p.lay, p.chunk_pts,
                        digits, cnt);
     if ((rc = mark(4))) return rc;
-    hipLaunchKernelGGL(k_scan_tile, dim3(p.ntiles), dim3(256), 0, stream, p.cnt_len, cnt, tiles);
-    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, stream, p.ntiles, tiles);
-    hipLaunchKernelGGL(k_scan_add, dim3((unsigned)((p.cnt_len + 255) / 256)), dim3(256), 0, stream,
-                       p.cnt_len, cnt, tiles, p.chunks, b.m_kstart.as<uint32_t>());
+    if (p.ntiles == 1) {  // one tile: the tile scan finishes the whole scan (two launches fewer)
+        hipLaunchKernelGGL(k_scan_tile, dim3(1), dim3(256), 0, stream, p.cnt_len, cnt, tiles, p.chunks,
+                           b.m_kstart.as<uint32_t>());
+    } else {
+        hipLaunchKernelGGL(k_scan_tile, dim3(p.ntiles), dim3(256), 0, stream, p.cnt_len, cnt, tiles, p.chunks,
+                           (uint32_t*)nullptr);
+        hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, stream, p.ntiles, tiles);
+        hipLaunchKernelGGL(k_scan_add, dim3((unsigned)((p.cnt_len + 255) / 256)), dim3(256), 0, stream,
+                           p.cnt_len, cnt, tiles, p.chunks, b.m_kstart.as<uint32_t>());
+    }
     if ((rc = mark(5))) return rc;
     hipLaunchKernelGGL(k_msm_scatter, gsort, dim3(256), lds_nb, stream, (uint64_t)n, (uint64_t)na, p.lay,
                        p.chunk_pts, digits, cnt, b.m_entries.as<uint32_t>());
