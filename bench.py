@@ -1,57 +1,92 @@
 #!/usr/bin/env python3
 """bench.py -- Ed25519 signatures verified per second on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): verify_batch of 65,536 valid signatures over 512-byte
-messages, distinct keys, synthetic (seeded keys and messages, signed on the GPU).  A "step" is
-one batch verdict over one whole resident batch (inputs already in HBM): by default the batch
-MSM (K5: k_msm_scalars -> k_msm_points -> counting sort -> buckets -> window sums -> Horner,
-ed25519_consensus batch::Verifier semantics); --mode 0 runs the per-signature pipeline instead
-(K1-K4, per-signature verdict bits whose AND is the batch verdict).  --inflight K keeps K
-resident batches on K streams and issues the steps round-robin (a verification firehose: each
-step still verifies one full 65,536-signature batch); the single-stream step time is reported
-beside it.  With --gpus N the driver launches one rank per GPU (torch.distributed.run); each rank
-verifies its own batches (weak scaling, signature-index sharding, no data-path collective: the
-only exchange is the host-side max of the step times and the AND of verdicts over gloo).
+N = 1 (default): BASELINE.json configs[1].  A step is one batch verdict over one resident batch of
+65,536 valid signatures with 512-byte messages and distinct keys (synthetic: seeded keys and
+messages, RFC 8032 signatures made on the GPU), through the batch MSM (K5, ed25519_consensus
+batch::Verifier semantics).  --inflight K keeps K resident batches on K streams and issues the
+steps round-robin; the single-stream step time is reported beside it.
 
-Extra fields: roofline (VALU: 32x32->64 multiply-adds of the dominant bulk kernel vs the measured
-v_mad_u64_u32 peak), cpu_baseline (the oracle's multi-threaded batch verifier on the host
-cores, rank 0 only), p50/p99 latency of a 1,024-signature batch host->host, per-kernel times.
+N > 1 (--gpus N): BASELINE.json configs[2], the firehose.  16,777,216 signatures (32-byte messages)
+are sharded by contiguous 64-aligned index ranges over the N ranks, one process per GPU; a step is
+one pass over all 16M (every rank verifies its resident shard, as sub-shards of <= 2,097,152 on
+their own streams).  Strong scaling: the total is fixed.  There is no data-path collective: after
+the timed region the ranks exchange only the max of their times and, once, their verdict bitmaps
+(one all_gather over gloo) for the exact-bad-set check.  Without WORLD_SIZE in the environment,
+--gpus N spawns the N rank processes itself (before anything touches the GPU);
+torch.distributed.run launches them the same way.
+
+Extra fields: roofline (dominant kernel) and roofline_per_kernel, cpu_baseline (the oracle's
+batch verifier on the host's usable cores, rank 0, N = 1), host_to_host (pipelined verification of
+host-resident batches, PCIe included), latency of a 1,024-signature batch host -> host, the C3
+firehose on one GPU, and the C1 / C4 / C5 legs with their CPU counterparts.
 """
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
 
 # Hardware queues per process (HIP's default is 4).  Each resident batch runs on its own stream;
-# with 4 queues the streams share queues and a batch's latency-bound MSM tail (window sums,
-# Horner: a few workgroups for ~0.5 ms) serialises the work queued behind it.  16 queues let
-# the tails of up to 16 batches run beside other batches' bulk kernels
-# (profiles/round1_hwq_sweep.jsonl).  Must be set before the HIP runtime initialises; the GPU
-# boxes export 4, so it is overridden here (NWV_BENCH_HW_QUEUES picks another count).
+# with 4 queues the streams share queues and a batch's latency-bound MSM tail serialises the work
+# queued behind it (profiles/round1_hwq_sweep.jsonl).  Must be set before the HIP runtime
+# initialises (NWV_BENCH_HW_QUEUES picks another count).
 os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("NWV_BENCH_HW_QUEUES", "16")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# Algorithmic field operations per signature, counted on the host-emulation build
-# (tests/test_hostemu.py::test_phase_op_counts and tests/test_msm_hostemu.py pin these
-# numbers): (mul, sq) per phase.
-OPS_POINTS = (111, 514)
+FIREHOSE_N = 16777216
+SUBSHARD = 2097152
+
+# Algorithmic field multiplications (one 255-bit product: a 10 x 10 limb schoolbook = 100
+# v_mad_u64_u32; a squaring 55), counted on the host-emulation build
+# (tests/test_hostemu.py::test_phase_op_counts, tests/test_msm_hostemu.py)
+MADS_PER_MUL, MADS_PER_SQ = 100, 55
+OPS_POINTS = (111, 514)      # k_ed_points, per signature: decompress R and A + 0..8 A table
+OPS_MSM_POINTS = (48, 514)   # MSM decompression, per signature: R_i and A_i
+MADS_DECOMPRESS = (OPS_MSM_POINTS[0] * MADS_PER_MUL + OPS_MSM_POINTS[1] * MADS_PER_SQ) // 2  # per point
+MADS_MIXED_ADD = 7 * MADS_PER_MUL                          # per bucket entry (affine Niels)
+MADS_ADD = 9 * MADS_PER_MUL                                # extended + extended
+MADS_DBL = 4 * MADS_PER_MUL + 4 * MADS_PER_SQ              # projective doubling
 OPS_STRAUS = (1505, 1020)
-OPS_MSM_POINTS = (48, 514)  # k_msm_points: decompress R and A + affine Niels entries
-MADS_PER_MUL, MADS_PER_SQ = 100, 55  # 10x10 and 55-term schoolbook, one v_mad_u64_u32 each
-
-
-def mads(ops):
-    return ops[0] * MADS_PER_MUL + ops[1] * MADS_PER_SQ
+# guide-derived VALU peaks (MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32 x 2.4 GHz, a wave64 VALU
+# instruction issues over 2 cycles): 78.6 T lane-ops/s for full-rate 32-bit forms; the 64-bit
+# result VOP3 forms (v_mad_u64_u32) issue at half that
+GUIDE_VALU32 = 256 * 4 * 32 * 2.4e9
+GUIDE_MAD64 = GUIDE_VALU32 / 2
+HBM_PEAK_GBS = 8000.0
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def usable_cpus():
+    """CPUs this process may use: its affinity set, capped by the cgroup CPU quota and by the
+    job's thread budget (OMP_NUM_THREADS; the GPU box exposes the whole machine to nproc but
+    grants each job a share of 16).  NWV_CPU_THREADS overrides."""
+    if os.environ.get("NWV_CPU_THREADS"):
+        return max(1, int(os.environ["NWV_CPU_THREADS"]))
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        n = min(n, max(1, int(os.environ["OMP_NUM_THREADS"])))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(p))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
 
 
 def valu_peak():
@@ -73,36 +108,59 @@ def synth(eng, n, mlen, seed, keys=0):
     seeds = rng.integers(0, 256, size=32 * n, dtype=np.uint8)
     if keys:
         seeds = np.tile(seeds[:32 * keys], (n + keys - 1) // keys)[:32 * n].copy()
-    msgs = rng.integers(0, 256, size=n * mlen + 16, dtype=np.uint8)
-    offs = np.arange(n, dtype=np.uint64) * mlen
+    msgs = rng.integers(0, 256, size=n * mlen + 64, dtype=np.uint8)
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(mlen)
     lens = np.full(n, mlen, dtype=np.uint32)
     pk, sg = eng.sign_many_arrays(seeds, msgs, offs, lens)
     return pk, sg, msgs, offs, lens
 
 
-def cpu_baseline(pk, sg, msgs, offs, lens, seconds):
+def firehose_shard_data(eng, lo, hi, mlen=32):
+    """signatures [lo, hi) of the configs[2] firehose: key seed and message derived from the global
+    index, so every rank signs only its own shard and no signature data crosses ranks"""
+    m = hi - lo
+    idx = np.arange(lo, hi, dtype=np.uint64)
+    seeds = np.zeros((m, 32), dtype=np.uint8)
+    seeds[:, :8] = idx.view(np.uint8).reshape(m, 8)
+    seeds[:, 8] = 0xA5
+    msgs = np.zeros((m, mlen), dtype=np.uint8)
+    msgs[:, :8] = (idx * np.uint64(0x9E3779B97F4A7C15)).view(np.uint8).reshape(m, 8)
+    msgs = np.concatenate([msgs.reshape(-1), np.zeros(64, np.uint8)])
+    offs = np.arange(m, dtype=np.uint64) * np.uint64(mlen)
+    lens = np.full(m, mlen, dtype=np.uint32)
+    pk, sg = eng.sign_many_arrays(seeds.reshape(-1), msgs, offs, lens)
+    return pk, sg, msgs, offs, lens
+
+
+# ------------------------------------------------------------------------------- CPU legs --
+def cpu_baseline(pk, sg, msgs, offs, lens, seconds, threads):
+    """the oracle's batch verifier (dalek's algorithms in C: radix-2^51, Pippenger) over the SAME
+    65,536 x 512 B batch, split by index over `threads` host threads"""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi as of  # the checker; timed here as the CPU baseline only
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
-    n = min(len(offs), 8192)
-    done, t0 = 0, time.perf_counter()
+    n = len(offs)
+    P, S, M = pk[:32 * n].tobytes(), sg[:64 * n].tobytes(), msgs.tobytes()
+    done, reps, t0 = 0, 0, time.perf_counter()
     while True:
-        ok = of.verify_batch_mt(pk[:32 * n].tobytes(), sg[:64 * n].tobytes(), msgs.tobytes(),
-                                offs[:n].copy(), lens[:n].copy(), threads)
+        ok = of.verify_batch_mt(P, S, M, offs.copy(), lens.copy(), threads, seed=os.urandom(32))
         assert ok, "CPU baseline rejected a valid batch"
         done += n
+        reps += 1
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
     return {"value": done / dt, "unit": "sigs/s", "cores": threads, "kind": "port",
-            "sample": f"{done} sigs ({n}-sig batches of 512 B messages, {threads} threads, "
-                      f"oracle/nwv_oracle.c batch verifier: Pippenger/Straus as dalek)"}
+            "sample": f"{reps} x the same {n}-signature batch of 512 B messages (configs[1]), "
+                      f"split by index over {threads} threads (all CPUs granted to this job), "
+                      "oracle/nwv_oracle.c batch verifier: radix-2^51 field and Pippenger as "
+                      "curve25519-dalek-ng u64_backend / ed25519-consensus",
+            "ms_per_batch": dt / reps * 1e3}
 
 
 def cpu_baseline_configs(legs, data, threads):
-    """CPU legs of C1 / C4 / C5 on the host cores (the oracle: dalek's algorithms in C, the
-    reference's control flow in Python), and the check that the GPU's C4 verdict bits equal the
-    oracle's per-signature verdicts"""
+    """CPU legs of C1 / C4 / C5 (the oracle: dalek's algorithms in C, the reference's control flow
+    in Python).  C1 and C5's signature checks run on ONE core: the reference verifies inside its
+    single Core task (primary/src/core.rs:614-714); C4 and the C5 digests use `threads` threads."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import hashlib
@@ -143,16 +201,17 @@ def cpu_baseline_configs(legs, data, threads):
     com1 = ocom(c1["committee"])
     assert cert_verify(com1, c1["cert"]) == 0
     out["C1"] = {"certificate_verify_n4_ms": timed(lambda: cert_verify(com1, c1["cert"]), 200),
-                 "verify_batch_1024_m32_ms": timed(lambda: of.verify_batch(c1["items"]), 20), "cores": 1}
+                 "verify_batch_1024_m32_ms": timed(lambda: of.verify_batch(c1["items"]), 20), "cores": 1,
+                 "note": "one core, as the reference's single Core task verifies"}
     c4 = data["C4"]
     pk, sig, msg, offs, lens = of.pack(c4["items"])
     t = time.perf_counter()
     ok = of.verify_batch_mt(pk, sig, msg, offs, lens, threads)
     bits = of.verify_each_mt(pk, sig, msg, offs, lens, threads)
     dt = time.perf_counter() - t
-    ref = [bool((int(bits[i >> 6]) >> (i & 63)) & 1) for i in range(len(offs))]
+    ref = np.unpackbits(bits.view(np.uint8), bitorder="little")[:len(offs)].astype(bool)
     out["C4"] = {"ms_per_batch": dt * 1e3, "sigs_per_s": len(offs) / dt, "cores": threads,
-                 "batch_verdict": ok, "gpu_bits_equal_oracle": ref == list(c4["bits"])}
+                 "batch_verdict": ok, "gpu_bits_equal_oracle": bool((ref == np.asarray(c4["bits"])).all())}
     c5 = data["C5"]
     com5 = ocom(c5["committee"])
 
@@ -165,53 +224,16 @@ def cpu_baseline_configs(legs, data, threads):
     ms5 = timed(round_cpu, 3)
     with ThreadPoolExecutor(threads) as ex:
         msd = timed(lambda: list(ex.map(lambda b: hashlib.blake2b(b, digest_size=32).digest(), c5["batches"])), 3)
+    one = c5["batches"][0]
+    ms1 = timed(lambda: hashlib.blake2b(one, digest_size=32).digest(), 20)
     out["C5"] = {"verify_ms_per_round": ms5, "verify_cores": 1,
                  "verify_sigs_per_s": legs["C5"]["signatures_per_round"] / (ms5 * 1e-3),
-                 "worker_batch_digests_ms_per_round": msd, "digest_threads": threads}
+                 "worker_batch_digests_ms_per_round": msd, "digest_threads": threads,
+                 "one_worker_batch_digest_ms_1core": ms1}
     return out
 
 
-def roofline_entry(kname, kt, mads_launch, peak_t, algorithmic, n):
-    kms = float(kt.get(kname, 0.0))
-    achieved = mads_launch / (kms * 1e-3) / 1e12 if kms > 0 else None
-    traffic = pmc_traffic(kname, n)
-    return {
-        "bound": "valu",
-        "kernel": kname,
-        "achieved": achieved,
-        "peak": peak_t,
-        "unit": "T v_mad_u64_u32/s",
-        "frac": (achieved / peak_t) if (peak_t and achieved) else None,
-        "traffic": traffic["bytes"] if traffic else None,
-        "traffic_source": traffic,
-        "algorithmic": algorithmic,
-    }
-
-
-def split_prep_times(args, pk, sg, msgs, offs, lens, reps=5):
-    """per-kernel times of the same batch with hashing and decompression as separate kernels"""
-    import narwhal_amd
-    from narwhal_amd import _lib
-    e = narwhal_amd.Engine(device=0, flags=_lib.NWV_FLAG_MSM_SPLIT_PREP)
-    try:
-        if args.keys:
-            kidx = (np.arange(args.n) % args.keys).astype(np.uint32)
-            st = e.stage_keyed(pk[:32 * args.keys].copy(), kidx, sg, msgs, offs, lens)
-        else:
-            st = e.stage(pk, sg, msgs, offs, lens)
-        st.run(mode=1, seed=b"\x11" * 32, timed=True)
-        st.sync()
-        st.kernel_times(1, reset=True)
-        for r in range(reps):
-            st.run(mode=1, seed=bytes([r + 1]) * 32, timed=True)
-        kt = st.kernel_times(1, reset=True)
-        assert st.fetch()[0]
-        st.free()
-        return kt
-    finally:
-        e.close()
-
-
+# ------------------------------------------------------------------------------ roofline --
 def pmc_kernel(kernel, n):
     """(counters, source) of `kernel` in the newest committed rocprofv3 --pmc summary at batch
     size n, or (None, None)"""
@@ -228,52 +250,331 @@ def pmc_kernel(kernel, n):
     return None, None
 
 
-def valu_issue_entry(kname, kt, n, peak):
-    """VALU instruction throughput of `kernel`: SQ_INSTS_VALU per launch (wave-level
-    instructions, committed PMC pass) over the live event-timed duration, against the
-    full-rate 32-bit VALU issue peak measured on the box (v_add_u32 lane-ops/s / 64 lanes)."""
-    insts, src = 0.0, None
-    for part in kname.split("+"):  # "k_msm_bucket+fixup" is timed as one span
-        k, src = pmc_kernel(part if part.startswith("k_") else "k_msm_" + part, n)
-        if not k or "SQ_INSTS_VALU" not in k:
+def pmc_traffic(kernels, n):
+    """HBM bytes per launch from the committed rocprofv3 --pmc passes (FETCH_SIZE doubled for
+    gfx950's half-counted wide reads + WRITE_SIZE, MI355X_MICROARCH.md HBM section)"""
+    total, srcs = 0.0, set()
+    for k in kernels:
+        c, src = pmc_kernel(k, n)
+        if not c or "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
             return None
-        insts += k["SQ_INSTS_VALU"]
-    kms = float(kt.get(kname, 0.0))
+        total += 2 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024
+        srcs.add(src)
+    return {"bytes": total, "source": sorted(srcs)}
+
+
+def issue_floor(kernels, n, kms, peak):
+    """mix-weighted VALU issue floor: the committed PMC pass's wave-level VALU instructions of the
+    kernel, the 64-bit integer forms (SQ_INSTS_VALU_INT64) priced at the measured v_mad_u64_u32
+    rate and the rest at the measured v_add_u32 rate, against the live kernel time"""
     if not peak or kms <= 0:
         return None
-    rate = insts / (kms * 1e-3) / 1e9
-    pk = peak["v_add_u32_per_s"] / 64 / 1e9
-    out = {"kernel": kname, "insts_per_launch": insts, "achieved": rate, "peak": pk,
-           "unit": "G wave-VALU-instr/s", "frac": rate / pk, "source": src,
-           "note": "frac prices every VALU instruction at the VOP2 rate (v_add_u32, a lower bound on "
-                   "the busy fraction); frac_vop3 at the measured rate of 64-bit-encoded VOP3 forms "
-                   "(v_mad_u64_u32 is one; so are v_alignbit_b32, v_lshl_add_u64, v_lshrrev_b64, "
-                   "which issue at about half the VOP2 rate): an upper bound"}
-    vop3 = [peak.get(k) for k in ("v_lshl_add_u64_per_s", "v_lshrrev_b64_per_s", "v_alignbit_b32_per_s")]
-    if all(vop3):
-        pk3 = sum(vop3) / len(vop3) / 64 / 1e9
-        out["peak_vop3"] = pk3
-        out["frac_vop3"] = rate / pk3
+    v = i64 = 0.0
+    srcs = set()
+    for k in kernels:
+        c, src = pmc_kernel(k, n)
+        if not c or "SQ_INSTS_VALU" not in c or "SQ_INSTS_VALU_INT64" not in c:
+            return None
+        v += c["SQ_INSTS_VALU"]
+        i64 += c["SQ_INSTS_VALU_INT64"]
+        srcs.add(src)
+    floor_s = i64 * 64 / peak["v_mad_u64_u32_per_s"] + (v - i64) * 64 / peak["v_add_u32_per_s"]
+    return {"valu_insts_per_launch": v, "int64_insts": i64, "floor_ms": floor_s * 1e3,
+            "frac": floor_s / (kms * 1e-3), "source": sorted(srcs)}
+
+
+def kernel_rooflines(kt, stats, n, na, peak):
+    """roofline of every kernel of the batch MSM from its single-stream, event-timed duration"""
+    mad_peak = peak["v_mad_u64_u32_per_s"] / 1e12 if peak else None
+    nw, nwz, buckets, E = stats["windows"], stats["windows_z"], stats["buckets"], stats["entries"]
+    digit_slots = (na + 1) * nw + n * nwz
+    cnt_len = buckets * stats["chunks"]
+    out = {}
+
+    def valu(name, pmc, mads, what):
+        kms = kt.get(name, 0.0)
+        a = mads / (kms * 1e-3) / 1e12 if kms > 0 else None
+        out[name] = {"bound": "valu", "achieved": a, "unit": "T v_mad_u64_u32/s", "peak": mad_peak,
+                     "frac": (a / mad_peak) if (a and mad_peak) else None,
+                     "peak_guide": GUIDE_MAD64 / 1e12, "frac_guide": (a / (GUIDE_MAD64 / 1e12)) if a else None,
+                     "algorithmic": what, "mads_per_launch": mads, "kernel_ms": kms,
+                     "traffic": (pmc_traffic(pmc, n) or {}).get("bytes"),
+                     "issue_floor": issue_floor(pmc, n, kms, peak)}
+
+    def mem(name, pmc, nbytes, what):
+        kms = kt.get(name, 0.0)
+        a = nbytes / (kms * 1e-3) / 1e9 if kms > 0 else None
+        tr = pmc_traffic(pmc, n)
+        out[name] = {"bound": "hbm", "achieved": a, "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                     "frac": (a / HBM_PEAK_GBS) if a else None, "algorithmic": what,
+                     "bytes_per_launch": nbytes, "kernel_ms": kms,
+                     "traffic": tr["bytes"] if tr else None,
+                     "traffic_over_algorithmic": (tr["bytes"] / nbytes) if tr and nbytes else None}
+
+    valu("k_msm_prep", ["k_msm_prep"], MADS_DECOMPRESS * (na + n),
+         f"{MADS_DECOMPRESS} multiply-adds per decompressed point (24 mul + 257 sq) x {na + n} points "
+         "(R_i and the A points); the SHA-512 hashing in the same grid is not counted (a lower bound)")
+    mem("k_msm_hist", ["k_msm_hist"], 2 * digit_slots + 4 * cnt_len,
+        f"read the i16 digit rows ({digit_slots} slots), write {cnt_len} u32 counts")
+    mem("k_scan", ["k_scan_tile", "k_scan_tiles", "k_scan_add"], 8 * cnt_len, f"read + write {cnt_len} u32 counts")
+    mem("k_msm_scatter", ["k_msm_scatter"], 2 * digit_slots + 4 * cnt_len + 4 * E,
+        f"read the digit rows and the {cnt_len} bucket offsets, write {E} u32 entries")
+    valu("k_msm_bucket+fixup", ["k_msm_bucket", "k_msm_fixup"], MADS_MIXED_ADD * E,
+         f"{MADS_MIXED_ADD} multiply-adds per bucket entry (one mixed addition, 7 mul) x {E} entries")
+    valu("k_msm_window", ["k_msm_window"], 2 * MADS_ADD * buckets,
+         f"two extended additions ({MADS_ADD} multiply-adds each) per bucket x {buckets} buckets "
+         "(running-sum reduction)")
+    doublings = 253
+    valu("k_msm_final", ["k_msm_final"], doublings * MADS_DBL + nw * MADS_ADD,
+         f"Horner over {nw} windows: ~{doublings} doublings + {nw} additions, one dependent chain "
+         "(latency-bound by construction)")
     return out
 
 
-def pmc_traffic(kernel, n):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc pass (FETCH_SIZE
-    doubled for gfx950's half-counted wide reads + WRITE_SIZE, MI355X_MICROARCH.md HBM section),
-    or None when no profile for it is committed."""
-    import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
-        try:
-            with open(f) as fh:
-                d = json.load(fh)
-            k = d.get("kernels", {}).get(kernel)
-            if d.get("n") != n:
-                continue
-            if k and "FETCH_SIZE" in k and "WRITE_SIZE" in k:
-                return {"bytes": 2 * k["FETCH_SIZE"] * 1024 + k["WRITE_SIZE"] * 1024,
-                        "source": os.path.relpath(f, ROOT), "n": d.get("n")}
-        except (OSError, ValueError):
-            continue
+# ------------------------------------------------------------------------------- N = 1 ----
+def run_headline(args, eng, rank, world, dist):
+    from narwhal_amd import _lib
+    pk, sg, msgs, offs, lens = synth(eng, args.n, args.msg_len, seed=1000 + rank, keys=args.keys)
+    if args.keys:
+        kidx = np.arange(args.n, dtype=np.uint32) % np.uint32(args.keys)
+        stages = [eng.stage_keyed(pk[:32 * args.keys].copy(), kidx, sg, msgs, offs, lens)
+                  for _ in range(max(1, args.inflight))]
+    else:
+        stages = [eng.stage(pk, sg, msgs, offs, lens) for _ in range(max(1, args.inflight))]
+
+    def check_all(what):
+        for s_ in stages:
+            allv, bits = s_.fetch()
+            if not (allv and bits.all()):
+                raise SystemExit(f"verification of a valid synthetic batch failed ({what})")
+
+    # setup (untimed, not counted as warmup): every stage's first run allocates its MSM scratch
+    # and captures its HIP graph; every verdict is checked
+    for s_ in stages:
+        s_.run(mode=args.mode)
+    check_all("setup")
+    for w in range(args.warmup):
+        stages[w % len(stages)].run(mode=args.mode)  # seed None: OS entropy, as OsRng
+    check_all("warmup")
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        stages[s % len(stages)].run(mode=args.mode)
+    for s_ in stages:
+        s_.sync()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
+    check_all("timed region: last run of every stage")
+    # single-stream pass: step latency and per-kernel device times without overlap
+    st = stages[0]
+    st.kernel_times(args.mode, reset=True)
+    single = []
+    for s in range(args.single_steps):
+        ts = time.perf_counter()
+        st.run(mode=args.mode, timed=True)
+        st.sync()
+        single.append((time.perf_counter() - ts) * 1e3)
+    kt = st.kernel_times(args.mode, reset=True)
+    stats = st.msm_stats() if args.mode == 1 else None
+    assert st.fetch()[0]
+    for s_ in stages:
+        s_.free()
+    return {"dt": dt, "single": single, "kt": kt, "stats": stats, "data": (pk, sg, msgs, offs, lens)}
+
+
+def latency_1k(eng, data, reps):
+    """1,024-signature batch, host buffers in -> verdict out (H2D + D2H included)"""
+    from narwhal_amd import _lib
+    pk, sg, msgs, offs, lens = data
+    n1 = 1024
+    lat = []
+    bitsbuf = np.zeros(n1 // 64 + 1, dtype=np.uint64)
+    allv = _lib._i32(0)
+    for r in range(reps + 5):
+        t = time.perf_counter()
+        rc = eng.lib.nwv_ed25519_verify_batch(eng._h, n1, pk.ctypes.data, sg.ctypes.data, msgs.ctypes.data,
+                                              offs.ctypes.data, lens.ctypes.data, None, _lib.ctypes.byref(allv),
+                                              bitsbuf.ctypes.data)
+        if r >= 5:
+            lat.append((time.perf_counter() - t) * 1e3)
+        assert rc == 0 and allv.value == 1
+    lat = np.array(lat)
+    return {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)), "reps": len(lat)}
+
+
+def host_to_host(eng, data, threads, seconds):
+    """host-resident batches verified end to end (pack + H2D + MSM + verdict D2H per call) by
+    `threads` host threads on one context: the library's lanes overlap one call's copy with
+    another's kernels.  This is the rate a verify_batch caller holding host buffers sees."""
+    from narwhal_amd import _lib
+    pk, sg, msgs, offs, lens = data
+    n = len(offs)
+    counts = [0] * threads
+    stop = time.perf_counter() + seconds
+    err = []
+
+    def worker(k):
+        allv = _lib._i32(0)
+        while time.perf_counter() < stop:
+            rc = eng.lib.nwv_ed25519_verify_batch(eng._h, n, pk.ctypes.data, sg.ctypes.data, msgs.ctypes.data,
+                                                  offs.ctypes.data, lens.ctypes.data, None,
+                                                  _lib.ctypes.byref(allv), None)
+            if rc != 0 or allv.value != 1:
+                err.append(rc)
+                return
+            counts[k] += 1
+
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(threads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    dt = time.perf_counter() - t0
+    if err:
+        raise SystemExit(f"host-to-host verification failed: {err}")
+    calls = sum(counts)
+    return {"sigs_per_s": calls * n / dt, "calls": calls, "threads": threads, "seconds": dt,
+            "bytes_per_call_h2d": int(96 * n + int(lens.sum()) + 12 * n),
+            "note": "nwv_ed25519_verify_batch on host buffers (65,536 x 512 B): pinned packing, H2D, "
+                    "batch MSM, verdict D2H; PCIe Gen5 x16 (63 GB/s spec) bounds it"}
+
+
+def firehose_pass(eng, lo, hi, reps, warm=1, dist=None):
+    """verify [lo, hi) of the firehose as resident sub-shards of <= SUBSHARD on their own streams:
+    returns (seconds for `reps` passes, data, stages' kernel times)"""
+    pk, sg, msgs, offs, lens = firehose_shard_data(eng, lo, hi)
+    m = hi - lo
+    subs = []
+    for a in range(0, m, SUBSHARD):
+        b = min(m, a + SUBSHARD)
+        subs.append(eng.stage(pk[32 * a:32 * b], sg[64 * a:64 * b], msgs, offs[a:b], lens[a:b]))
+    for st in subs:
+        for _ in range(warm):
+            st.run(mode=1)
+        allv, bits = st.fetch()
+        if not (allv and bits.all()):
+            raise SystemExit("firehose sub-shard of valid signatures rejected")
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        for st in subs:
+            st.run(mode=1)
+    for st in subs:
+        st.sync()
+    dt = time.perf_counter() - t0
+    ok = True
+    for st in subs:
+        allv, bits = st.fetch()
+        ok &= bool(allv and bits.all())
+    if not ok:
+        raise SystemExit("firehose pass of valid signatures rejected")
+    subs[0].kernel_times(1, reset=True)
+    subs[0].run(mode=1, timed=True)
+    kt = subs[0].kernel_times(1, reset=True)
+    for st in subs:
+        st.free()
+    return dt, (pk, sg, msgs, offs, lens), kt, len(subs)
+
+
+def firehose_bad_set(eng, data, lo, hi, n_total, dist):
+    """the exact-bad-set path of the firehose: seeded global indices corrupted, each rank verifies
+    its shard as one batch (fallback only because it rejects), verdict bitmaps merged on the host
+    (one all_gather over gloo); the merged bad set must equal the injected one"""
+    from narwhal_amd import firehose as fh
+    pk, sg, msgs, offs, lens = data
+    rng = np.random.default_rng(4)
+    bad = sorted(int(x) for x in rng.choice(n_total, size=64, replace=False))
+    sg2 = sg.copy()
+    for g in bad:
+        if lo <= g < hi:
+            sg2[64 * (g - lo) + 40] ^= 1
+    verify = fh.gpu_shard_verifier(eng, pk, sg2, msgs, offs, lens)
+    t0 = time.perf_counter()
+    ok, words = fh.firehose(lambda a, b: verify(a - lo, b - lo), n_total, dist)
+    dt = time.perf_counter() - t0
+    bits = np.unpackbits(words.view(np.uint8), bitorder="little")[:n_total]
+    got = np.flatnonzero(bits == 0).tolist()
+    return {"injected": len(bad), "found": len(got), "exact": got == bad and not ok, "seconds": dt}
+
+
+def run_firehose(args, eng, rank, world, dist):
+    """configs[2]: 16,777,216 signatures over `world` ranks, one pass per step"""
+    from narwhal_amd import firehose as fh
+    import torch
+    lo, hi = fh.shard_range(FIREHOSE_N, world, rank)
+    dt, data, kt, nsub = firehose_pass(eng, lo, hi, args.steps, warm=1 + args.warmup, dist=dist)
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    badset = firehose_bad_set(eng, data, lo, hi, FIREHOSE_N, dist)
+    o = torch.tensor([int(badset["exact"])], dtype=torch.int32)
+    dist.all_reduce(o, op=dist.ReduceOp.MIN)
+    if not o.item():
+        raise SystemExit("firehose exact-bad-set check failed")
+    if rank != 0:
+        return None
+    return {
+        "metric": "Ed25519 sigs verified/sec",
+        "value": FIREHOSE_N * args.steps / dt,
+        "unit": "sigs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (key seeds and 32 B messages derived from the global index, RFC 8032 "
+                "signatures made on each rank's GPU)",
+        "config": {"workload": "firehose of 16,777,216 sigs sharded by index over the GPUs, host "
+                               "verdict-bitmap merge (BASELINE.json configs[2])",
+                   "sigs_total": FIREHOSE_N, "sigs_per_gpu": hi - lo, "subshards_per_gpu": nsub,
+                   "msg_len": 32, "parallelism": f"signature-index shards x{world}, no collective"},
+        "kernel_ms_rank0_subshard": kt,
+        "exact_bad_set": badset,
+    }
+
+
+def run_firehose_dry(args, rank, world, dist):
+    """NWV_BENCH_DRYRUN=1 (CPU tests of the rank spawn and the verdict merge, no GPU): the same
+    sharding, timing and gloo bitmap merge as run_firehose, with a shard verifier that rejects
+    exactly the injected indices instead of the engine"""
+    from narwhal_amd import firehose as fh
+    import torch
+    n_total = int(os.environ.get("NWV_BENCH_DRYRUN_N", "1048576"))
+    lo, hi = fh.shard_range(n_total, world, rank)
+    rng = np.random.default_rng(4)
+    bad = sorted(int(x) for x in rng.choice(n_total, size=64, replace=False))
+
+    def verify(a, b):
+        v = np.ones(b - a, dtype=bool)
+        for g in bad:
+            if a <= g < b:
+                v[g - a] = False
+        w = np.zeros(((b - a + 63) // 64) * 8, dtype=np.uint8)
+        pb = np.packbits(v, bitorder="little")
+        w[:pb.size] = pb
+        return bool(v.all()), w.view(np.uint64)
+
+    dist.barrier()
+    t0 = time.perf_counter()
+    ok, words = fh.firehose(verify, n_total, dist)
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    bits = np.unpackbits(words.view(np.uint8), bitorder="little")[:n_total]
+    exact = np.flatnonzero(bits == 0).tolist() == bad and not ok
+    if rank == 0:
+        return {"metric": "Ed25519 sigs verified/sec", "value": n_total / float(t.item()), "unit": "sigs/s",
+                "n_gpus": world, "steps": 1, "warmup": 0, "dry_run": True, "scaling": "strong",
+                "config": {"workload": "firehose plumbing dry run (no GPU)", "sigs_total": n_total,
+                           "sigs_per_rank": hi - lo},
+                "exact_bad_set": {"injected": len(bad), "exact": exact}}
     return None
 
 
@@ -282,10 +583,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=192)
     ap.add_argument("--warmup", type=int, default=48)
-    ap.add_argument("--n", type=int, default=65536, help="signatures per batch (per GPU)")
+    ap.add_argument("--n", type=int, default=65536, help="signatures per batch (N = 1 headline)")
     ap.add_argument("--msg-len", type=int, default=512)
     ap.add_argument("--mode", type=int, default=1, help="1 batch MSM (K5), 0 per-signature pipeline")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-reps", type=int, default=1000)
     ap.add_argument("--inflight", type=int, default=12,
@@ -294,22 +595,39 @@ def main():
                     help="distinct verifying keys (0: one per signature, the configs[1] worst case; "
                          "100: its committee variant, keyed batch MSM)")
     ap.add_argument("--no-configs", action="store_true",
-                    help="skip the C1 / C4 / C5 legs (other BASELINE.json configs, GPU and CPU)")
+                    help="skip the C1 / C3 / C4 / C5 legs (other BASELINE.json configs, GPU and CPU)")
     ap.add_argument("--single-steps", type=int, default=8,
                     help="single-stream steps timed after the run (step latency, per-kernel times)")
+    ap.add_argument("--h2h-seconds", type=float, default=2.0)
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU, started before anything touches the GPU (never an exec)
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        procs = []
+        for r in range(args.gpus):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                       LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                          stdout=None if r == 0 else sys.stderr))
+        rcs = [p.wait() for p in procs]
+        sys.exit(next((rc if rc > 0 else 1 for rc in rcs if rc != 0), 0))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}")
     if os.environ.get("NWV_BENCH_ONE_DEVICE") == "1":
         local = 0  # rehearsal of the multi-rank path on a one-GPU box (ranks share device 0)
     dist = None
     if world > 1:
-        import torch
         import torch.distributed as dist
-        # host-side barrier / max only: no data-path collective.  Gloo prints its connection
-        # messages on fd 1; they go to stderr so stdout carries only the result line.
+        # host-side barrier / max / bitmap merge only: no data-path collective.  Gloo prints its
+        # connection messages on fd 1; they go to stderr so stdout carries only the result line.
         sys.stdout.flush()
         saved = os.dup(1)
         os.dup2(2, 1)
@@ -320,162 +638,103 @@ def main():
             os.dup2(saved, 1)
             os.close(saved)
 
+    if os.environ.get("NWV_BENCH_DRYRUN") == "1":
+        if dist is None:
+            raise SystemExit("NWV_BENCH_DRYRUN needs --gpus N > 1")
+        result = run_firehose_dry(args, rank, world, dist)
+        if result is not None:
+            print(json.dumps(result), flush=True)
+        dist.destroy_process_group()
+        return
+
     import narwhal_amd
-    from narwhal_amd import _lib
 
     eng = narwhal_amd.Engine(device=local)
-    pk, sg, msgs, offs, lens = synth(eng, args.n, args.msg_len, seed=1000 + rank, keys=args.keys)
-    if args.keys:
-        kidx = np.arange(args.n, dtype=np.uint32) % np.uint32(args.keys)
-        stages = [eng.stage_keyed(pk[:32 * args.keys].copy(), kidx, sg, msgs, offs, lens)
-                  for _ in range(max(1, args.inflight))]
-    else:
-        stages = [eng.stage(pk, sg, msgs, offs, lens) for _ in range(max(1, args.inflight))]
-    seed = lambda s_: (bytes([(s_ * 7 + rank) % 256]) * 32)
-
-    def sync_all():
-        for s_ in stages:
-            s_.sync()
-
-    for w in range(args.warmup):
-        stages[w % len(stages)].run(mode=args.mode, seed=seed(w))
-    sync_all()
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    barrier()
-    sync_all()
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        stages[s % len(stages)].run(mode=args.mode, seed=seed(s))
-    sync_all()
-    t1 = time.perf_counter()
-    barrier()
-    dt = t1 - t0
-    ok = 1
-    for s_ in stages:
-        all_valid, bits = s_.fetch()
-        ok &= int(bool(all_valid) and bool(bits.all()))
-    # single-stream pass: step latency and per-kernel device times without overlap
-    st = stages[0]
-    st.kernel_times(args.mode, reset=True)
-    single = []
-    for s in range(args.single_steps):
-        ts = time.perf_counter()
-        st.run(mode=args.mode, seed=seed(1000 + s), timed=True)
-        st.sync()
-        single.append((time.perf_counter() - ts) * 1e3)
-    kt = st.kernel_times(args.mode, reset=True)
-    ok &= int(st.fetch()[0])
-    if dist is not None:
-        import torch
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        o = torch.tensor([ok], dtype=torch.int32)
-        dist.all_reduce(o, op=dist.ReduceOp.MIN)
-        ok = int(o.item())
-    for s_ in stages:
-        s_.free()
-    if not ok:
-        raise SystemExit("verification of a valid synthetic batch failed")
-
-    total = world * args.n * args.steps
-    value = total / dt
-    result = None
-    if rank == 0:
-        # latency: 1,024-signature batch, host buffers in -> verdict out (H2D + D2H included)
-        n1 = 1024
-        lat = []
-        pk1, sg1 = pk[:32 * n1], sg[:64 * n1]
-        bitsbuf = np.zeros(n1 // 64 + 1, dtype=np.uint64)
-        allv = _lib._i32(0)
-        for r in range(args.latency_reps + 5):
-            t = time.perf_counter()
-            rc = eng.lib.nwv_ed25519_verify_batch(eng._h, n1, pk1.ctypes.data, sg1.ctypes.data,
-                                                  msgs.ctypes.data, offs.ctypes.data, lens.ctypes.data,
-                                                  b"\x05" * 32, _lib.ctypes.byref(allv), bitsbuf.ctypes.data)
-            if r >= 5:
-                lat.append((time.perf_counter() - t) * 1e3)
-            assert rc == 0 and allv.value == 1
-        lat = np.array(lat)
-        peak = valu_peak()
-        peak_t = (peak["v_mad_u64_u32_per_s"] / 1e12) if peak else None
-        npts = args.n + (args.keys or args.n)  # decompressed points: R_i and the A points
-        if args.mode == 1:
-            # k_msm_prep = SHA-512 challenge hashing + decompression in one grid; only the
-            # decompression's multiply-adds are counted (the hash is add/rotate work), so this
-            # is a lower bound on the kernel's VALU use
-            roof = roofline_entry("k_msm_prep", kt, mads(OPS_MSM_POINTS) // 2 * npts, peak_t,
-                                  f"{mads(OPS_MSM_POINTS) // 2} multiply-adds/point (decompression: "
-                                  f"{OPS_MSM_POINTS[0] // 2} mul x 100 + {OPS_MSM_POINTS[1] // 2} sq x 55) x "
-                                  f"{npts} points per launch; the SHA-512 hashing in the same grid "
-                                  "is not counted", args.n)
-            roof["kernel_ms"] = kt
-            roof["valu_issue"] = {kn: valu_issue_entry(kn, kt, args.n, peak)
-                                  for kn in ("k_msm_prep", "k_msm_bucket+fixup")}
-            kt_split = split_prep_times(args, pk, sg, msgs, offs, lens)
-            roof["decompression_alone"] = roofline_entry(
-                "k_msm_points", kt_split, mads(OPS_MSM_POINTS) // 2 * npts, peak_t,
-                "same multiply-adds, k_msm_points launched on its own (NWV_FLAG_MSM_SPLIT_PREP, "
-                "single stream, timed pass)", args.n)
-            roof["decompression_alone"]["kernel_ms"] = kt_split
-        else:
-            roof = roofline_entry("k_ed_straus", kt, mads(OPS_STRAUS) * args.n, peak_t,
-                                  f"{mads(OPS_STRAUS)} multiply-adds/signature ({OPS_STRAUS[0]} mul x 100 + "
-                                  f"{OPS_STRAUS[1]} sq x 55) x {args.n} signatures per launch", args.n)
-            roof["kernel_ms"] = kt
-        cpu = None
-        if not args.no_cpu_baseline:
-            cpu = cpu_baseline(pk, sg, msgs, offs, lens, args.cpu_seconds)
-        configs = None
-        if not args.no_configs:
-            sys.path.insert(0, os.path.join(ROOT, "tools"))
-            import config_legs as CL
-            configs, cdata = {}, {}
-            configs["C1"], cdata["C1"] = CL.leg_c1(eng)
-            configs["C4"], cdata["C4"] = CL.leg_c4(eng)
-            configs["C5"], cdata["C5"] = CL.leg_c5(eng)
-            if not args.no_cpu_baseline:
-                threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
-                for k, v in cpu_baseline_configs(configs, cdata, threads).items():
-                    configs[k]["cpu_baseline"] = v
-            del cdata
-        result = {
-            "metric": "Ed25519 sigs verified/sec",
-            "value": value,
-            "unit": "sigs/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": dt / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": "synthetic (seeded keys/messages, RFC 8032 signatures made on the GPU)",
-            "config": {"workload": "verify_batch of 65,536 valid sigs, 512 B messages, distinct keys "
-                                   "(BASELINE.json configs[1]) per GPU",
-                       "sigs_per_batch": args.n, "msg_len": args.msg_len,
-                       "path": "batch MSM (K5)" if args.mode == 1 else "per-signature (K1-K4)",
-                       "distinct_keys": args.keys or args.n,
-                       "parallelism": f"signature-index shards x{world}",
-                       "inflight_batches": len(stages)},
-            "single_stream": {"ms_per_step": float(np.median(single)),
-                              "sigs_per_s": args.n / (float(np.median(single)) * 1e-3) * world},
-            "latency_1k_batch_ms": {"p50": float(np.percentile(lat, 50)),
-                                    "p99": float(np.percentile(lat, 99)), "reps": len(lat)},
-            "roofline": roof,
-            "cpu_baseline": cpu,
-            "configs": configs,
-            "valu_ubench": peak,
-        }
-        print(json.dumps(result), flush=True)
-    eng.close()
-    if dist is not None:
+    if world > 1:
+        result = run_firehose(args, eng, rank, world, dist)
+        if result is not None:
+            print(json.dumps(result), flush=True)
+        eng.close()
         dist.destroy_process_group()
+        return
+
+    h = run_headline(args, eng, rank, world, dist)
+    dt, kt, stats = h["dt"], h["kt"], h["stats"]
+    value = args.n * args.steps / dt
+    threads = usable_cpus()
+    lat = latency_1k(eng, h["data"], args.latency_reps)
+    h2h = host_to_host(eng, h["data"], 4, args.h2h_seconds) if args.h2h_seconds > 0 else None
+    peak = valu_peak()
+    if args.mode == 1:
+        na = args.keys or args.n
+        per = kernel_rooflines(kt, stats, args.n, na, peak)
+        dom = max(per, key=lambda k: per[k]["kernel_ms"])
+        roof = dict(per[dom], kernel=dom,
+                    kernel_share=per[dom]["kernel_ms"] / sum(kt.values()))
+    else:
+        kms = kt.get("k_ed_straus", 0.0)
+        m = (OPS_STRAUS[0] * MADS_PER_MUL + OPS_STRAUS[1] * MADS_PER_SQ) * args.n
+        a = m / (kms * 1e-3) / 1e12 if kms else None
+        pk_ = peak["v_mad_u64_u32_per_s"] / 1e12 if peak else None
+        per = None
+        roof = {"bound": "valu", "kernel": "k_ed_straus", "achieved": a, "peak": pk_, "unit": "T v_mad_u64_u32/s",
+                "frac": a / pk_ if (a and pk_) else None, "traffic": None}
+    cpu = None
+    if not args.no_cpu_baseline:
+        pk, sg, msgs, offs, lens = h["data"]
+        cpu = cpu_baseline(pk, sg, msgs, offs, lens, args.cpu_seconds, threads)
+    configs = None
+    if not args.no_configs:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import config_legs as CL
+        configs, cdata = {}, {}
+        configs["C1"], cdata["C1"] = CL.leg_c1(eng)
+        fdt, _, fkt, nsub = firehose_pass(eng, 0, FIREHOSE_N, 3)
+        configs["C3"] = {"sigs": FIREHOSE_N, "gpus": 1, "subshards": nsub, "sigs_per_s": FIREHOSE_N * 3 / fdt,
+                         "ms_per_pass": fdt / 3 * 1e3, "kernel_ms_subshard": fkt,
+                         "note": "all of configs[2] on ONE GPU as 8 resident 2,097,152-signature sub-shards "
+                                 "(the per-GPU share at 8 GPUs), 32 B messages; --gpus N shards it over N GPUs"}
+        configs["C4"], cdata["C4"] = CL.leg_c4(eng)
+        configs["C5"], cdata["C5"] = CL.leg_c5(eng)
+        if not args.no_cpu_baseline:
+            for k, v in cpu_baseline_configs(configs, cdata, threads).items():
+                configs[k]["cpu_baseline"] = v
+            c5 = configs["C5"]
+            c5["worker_batch_digests_gpu_over_cpu"] = (c5["worker_batch_digests_ms_per_round"] /
+                                                       c5["cpu_baseline"]["worker_batch_digests_ms_per_round"])
+        del cdata
+    result = {
+        "metric": "Ed25519 sigs verified/sec",
+        "value": value,
+        "unit": "sigs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded keys/messages, RFC 8032 signatures made on the GPU)",
+        "config": {"workload": "verify_batch of 65,536 valid sigs, 512 B messages, distinct keys "
+                               "(BASELINE.json configs[1])",
+                   "sigs_per_batch": args.n, "msg_len": args.msg_len,
+                   "path": "batch MSM (K5)" if args.mode == 1 else "per-signature (K1-K4)",
+                   "distinct_keys": args.keys or args.n,
+                   "parallelism": "one GPU", "inflight_batches": args.inflight},
+        "single_stream": {"ms_per_step": float(np.median(h["single"])),
+                          "sigs_per_s": args.n / (float(np.median(h["single"])) * 1e-3)},
+        "latency_1k_batch_ms": lat,
+        "host_to_host": h2h,
+        "roofline": roof,
+        "roofline_per_kernel": per,
+        "msm_shape": stats,
+        "cpu_baseline": cpu,
+        "configs": configs,
+        "valu_ubench": peak,
+    }
+    print(json.dumps(result), flush=True)
+    eng.close()
 
 
 if __name__ == "__main__":

@@ -175,6 +175,11 @@ int nwv_staged_kernel_ms(nwv_staged* st, double avg_ms[3], int reset);
  * Under NWV_FLAG_MSM_SPLIT_PREP k_msm_prep is split into k_msm_scalars and k_msm_points. */
 int nwv_staged_kernel_times(nwv_staged* st, int mode, int cap, const char** names, double* avg_ms,
                             int reset);
+/* shape of the staged batch's MSM (diagnostics for roofline accounting): out[0] points
+ * (na + 1 + n), [1] windows, [2] windows that carry the R_i points (the 128-bit z range),
+ * [3] buckets over all windows, [4] bucket entries of the last mode-1 run (0 before one),
+ * [5] sort chunks, [6] entries per k_msm_bucket lane, [7] A points (n, or the distinct keys) */
+int nwv_staged_msm_stats(nwv_staged* st, uint64_t out[8]);
 void nwv_staged_free(nwv_staged* st);
 
 /* ------------------------------------------------------------------ synthetic data ----- */

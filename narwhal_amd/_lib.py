@@ -74,6 +74,7 @@ def load():
         "nwv_staged_kernel_ms": ([_vp, _vp, _i32], _i32),
         "nwv_staged_kernel_times": ([_vp, _i32, _i32, _vp, _vp, _i32], _i32),
         "nwv_staged_free": ([_vp], None),
+        "nwv_staged_msm_stats": ([_vp, _vp], _i32),
         "nwv_ed25519_sign_many": ([_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp], _i32),
     }
     for name, (args, res) in sig.items():
@@ -99,6 +100,17 @@ def _check(rc, allow=(NWV_OK,)):
     if rc not in allow:
         raise NwvError(rc, load().nwv_last_error().decode(errors="replace"))
     return rc
+
+
+def _seed(seed):
+    """None -> NULL, so the library draws the batch coefficients' key from OS entropy (the
+    reference's OsRng).  A given seed must be exactly 32 bytes: the C side reads 32."""
+    if seed is None:
+        return None
+    seed = bytes(seed)
+    if len(seed) != 32:
+        raise ValueError(f"seed must be 32 bytes, got {len(seed)}")
+    return seed
 
 
 def _ptr(a):
@@ -157,17 +169,17 @@ class Engine:
         pk, sig, arena, offs, lens = soa(items)
         return list(self.verify_each_arrays(pk, sig, arena, offs, lens))
 
-    def verify_batch(self, items, seed=b"\x00" * 32, want_bits=True):
+    def verify_batch(self, items, seed=None, want_bits=True):
         pk, sig, arena, offs, lens = soa(items)
         n = len(items)
         bits = np.zeros((n + 63) // 64 + 1, dtype=np.uint64)
         allv = _i32(0)
         _check(self.lib.nwv_ed25519_verify_batch(self._h, n, _ptr(pk), _ptr(sig), _ptr(arena),
-                                                 _ptr(offs), _ptr(lens), seed, ctypes.byref(allv),
+                                                 _ptr(offs), _ptr(lens), _seed(seed), ctypes.byref(allv),
                                                  _ptr(bits) if want_bits else None))
         return bool(allv.value), (list(unpack_bits(bits, n)) if want_bits else None)
 
-    def verify_batch_keyed(self, keys, key_idx, sigs, msgs, seed=b"\x00" * 32, want_bits=True):
+    def verify_batch_keyed(self, keys, key_idx, sigs, msgs, seed=None, want_bits=True):
         """keys: list of distinct 32-byte keys; key_idx[i]: key of signature i; sigs, msgs: per
         signature -> (all_valid, per-signature verdicts or None)"""
         n = len(sigs)
@@ -178,11 +190,11 @@ class Engine:
         bits = np.zeros((n + 63) // 64 + 1, dtype=np.uint64)
         allv = _i32(0)
         _check(self.lib.nwv_ed25519_verify_batch_keyed(self._h, len(keys), _ptr(kb), n, _ptr(ki), _ptr(sg),
-                                                       _ptr(arena), _ptr(offs), _ptr(lens), seed,
+                                                       _ptr(arena), _ptr(offs), _ptr(lens), _seed(seed),
                                                        ctypes.byref(allv), _ptr(bits) if want_bits else None))
         return bool(allv.value), (list(unpack_bits(bits, n)) if want_bits else None)
 
-    def verify_batch_keyed_digests(self, preimages, keys, key_idx, sigs, digest_idx, seed=b"\x00" * 32):
+    def verify_batch_keyed_digests(self, preimages, keys, key_idx, sigs, digest_idx, seed=None):
         """BLAKE2b-256 of every preimage on the device, then signature i over digest digest_idx[i]
         -> (digests, all_valid, per-signature verdicts)"""
         n, m = len(sigs), len(preimages)
@@ -200,7 +212,7 @@ class Engine:
         allv = _i32(0)
         _check(self.lib.nwv_ed25519_verify_batch_keyed_digests(
             self._h, m, _ptr(arena), _ptr(offs), _ptr(lens), _ptr(dig), len(keys), _ptr(kb), n, _ptr(ki),
-            _ptr(sg), _ptr(di), seed, ctypes.byref(allv), _ptr(bits)))
+            _ptr(sg), _ptr(di), _seed(seed), ctypes.byref(allv), _ptr(bits)))
         return [dig[32 * i:32 * i + 32].tobytes() for i in range(m)], bool(allv.value), list(unpack_bits(bits, n))
 
     def stage_keyed(self, keys, key_idx, sig, arena, offs, lens, device_index=0):
@@ -269,10 +281,10 @@ class Staged:
     def __init__(self, eng, h, n):
         self.eng, self._h, self.n = eng, h, n
 
-    def run(self, mode=0, seed=b"\x00" * 32, timed=False):
+    def run(self, mode=0, seed=None, timed=False):
         """mode 0 per-signature pipeline, 1 batch MSM (graph replay); timed: kernel-by-kernel
         launches bracketed by HIP events (feeds kernel_ms / kernel_times)"""
-        _check(self.eng.lib.nwv_staged_run(self._h, mode | (NWV_RUN_TIMED if timed else 0), seed))
+        _check(self.eng.lib.nwv_staged_run(self._h, mode | (NWV_RUN_TIMED if timed else 0), _seed(seed)))
 
     def sync(self):
         _check(self.eng.lib.nwv_staged_sync(self._h))
@@ -297,6 +309,13 @@ class Staged:
         if k < 0:
             _check(k)
         return {names[i].decode(): float(ms[i]) for i in range(min(k, cap))}
+
+    def msm_stats(self):
+        """{points, windows, windows_z, buckets, entries, chunks, seg, a_points} of the batch MSM"""
+        out = np.zeros(8, dtype=np.uint64)
+        _check(self.eng.lib.nwv_staged_msm_stats(self._h, _ptr(out)))
+        keys = ("points", "windows", "windows_z", "buckets", "entries", "chunks", "seg", "a_points")
+        return {k: int(v) for k, v in zip(keys, out)}
 
     def free(self):
         if self._h:

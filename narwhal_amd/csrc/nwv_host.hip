@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -129,12 +130,18 @@ struct EdBuffers {
     }
 };
 
-struct Device {
+struct Gpu;
+
+// One in-flight call on a device: its own stream, pinned staging buffers and device buffers.  A
+// device keeps a small pool of lanes, so calls from several host threads overlap (one call's H2D
+// copy with another's kernels) instead of queueing behind one device lock.
+struct Lane {
+    Gpu* gpu = nullptr;
     int ordinal = -1;
     uint32_t flags = 0;  // nwv_init flags (NWV_FLAG_*)
+    const DevBuf* btabp = nullptr;  // the device's basepoint table (read-only)
     hipStream_t stream = nullptr;
-    std::mutex mu;
-    DevBuf btab;
+    const DevBuf& btab() const { return *btabp; }
     EdBuffers ed;
     PinnedBuf hstage;              // host side of ed_stage's single H2D copy
     hipEvent_t hstage_ev = nullptr;  // recorded after that copy; hstage is reusable once it fires
@@ -145,35 +152,27 @@ struct Device {
     hipEvent_t b2stage_ev = nullptr;
 };
 
-int with_device(Device& d) {
+// One device of a context: the basepoint table and the pool of lanes (created on demand, up to
+// max_lanes; env NWV_LANES, default 4).
+struct Gpu {
+    int ordinal = -1;
+    uint32_t flags = 0;
+    DevBuf btab;
+    std::mutex mu;  // guards the pool
+    std::condition_variable cv;
+    std::vector<Lane*> lanes, idle;
+    size_t max_lanes = 4;
+};
+
+int with_device(Lane& d) {
     NWV_HIP(hipSetDevice(d.ordinal));
     return NWV_OK;
 }
 
-int device_open(Device& d, int ordinal) {
-    d.ordinal = ordinal;
-    hipDeviceProp_t prop;
-    NWV_HIP(hipGetDeviceProperties(&prop, ordinal));
-    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-        return set_err(NWV_ERR_NODEV, std::string("device is ") + prop.gcnArchName + ", need gfx950");
-    NWV_HIP(hipSetDevice(ordinal));
-    NWV_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-    NWV_HIP(hipEventCreateWithFlags(&d.hstage_ev, hipEventDisableTiming));
-    NWV_HIP(hipEventCreateWithFlags(&d.b2stage_ev, hipEventDisableTiming));
-    int rc = d.btab.ensure((BASE_TABLE_WORDS + CACHED_ENTRY_WORDS) * sizeof(uint32_t));
-    if (rc) return rc;
-    hipLaunchKernelGGL(k_base_table, dim3((BASE_TABLE_ENTRIES + 63) / 64), dim3(64), 0, d.stream,
-                       d.btab.as<uint32_t>());
-    NWV_HIP(hipGetLastError());
-    NWV_HIP(hipStreamSynchronize(d.stream));
-    return NWV_OK;
-}
-
-void device_close(Device& d) {
+void lane_close(Lane& d) {
     if (d.ordinal < 0) return;
     (void)hipSetDevice(d.ordinal);
     if (d.stream) (void)hipStreamSynchronize(d.stream);
-    d.btab.release();
     d.ed.release();
     d.hstage.release();
     if (d.hstage_ev) (void)hipEventDestroy(d.hstage_ev);
@@ -188,6 +187,111 @@ void device_close(Device& d) {
     d.stream = nullptr;
 }
 
+// new lane of g (the calling thread has selected g's device)
+int lane_open(Gpu& g, Lane** out) {
+    *out = nullptr;
+    auto* d = new (std::nothrow) Lane;
+    if (!d) return set_err(NWV_ERR_OOM, "lane allocation");
+    d->gpu = &g;
+    d->ordinal = g.ordinal;
+    d->flags = g.flags;
+    d->btabp = &g.btab;
+    hipError_t e = hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&d->hstage_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&d->b2stage_ev, hipEventDisableTiming);
+    // both events start out complete, so the first wait on them returns at once
+    if (e == hipSuccess) e = hipEventRecord(d->hstage_ev, d->stream);
+    if (e == hipSuccess) e = hipEventRecord(d->b2stage_ev, d->stream);
+    if (e != hipSuccess) {
+        lane_close(*d);
+        delete d;
+        return set_err(NWV_ERR_HIP, std::string("lane: ") + hipGetErrorString(e));
+    }
+    *out = d;
+    return NWV_OK;
+}
+
+// Exclusive use of one lane of g for the scope of a call: an idle lane, a new one while the pool
+// is below max_lanes, else wait for a lane to be returned.
+class LaneRef {
+  public:
+    explicit LaneRef(Gpu& g) : g_(g) {
+        std::unique_lock<std::mutex> lk(g.mu);
+        for (;;) {
+            if (!g.idle.empty()) {
+                lane_ = g.idle.back();
+                g.idle.pop_back();
+                break;
+            }
+            if (g.lanes.size() < g.max_lanes) {
+                Lane* l = nullptr;
+                if (hipSetDevice(g.ordinal) != hipSuccess) {
+                    rc_ = set_err(NWV_ERR_HIP, "hipSetDevice");
+                    return;
+                }
+                if ((rc_ = lane_open(g, &l))) return;
+                g.lanes.push_back(l);
+                lane_ = l;
+                break;
+            }
+            g.cv.wait(lk);
+        }
+        lk.unlock();
+        rc_ = with_device(*lane_);
+    }
+    ~LaneRef() {
+        if (!lane_) return;
+        {
+            std::lock_guard<std::mutex> lk(g_.mu);
+            g_.idle.push_back(lane_);
+        }
+        g_.cv.notify_one();
+    }
+    LaneRef(const LaneRef&) = delete;
+    LaneRef& operator=(const LaneRef&) = delete;
+    int rc() const { return rc_; }
+    Lane& operator*() const { return *lane_; }
+
+  private:
+    Gpu& g_;
+    Lane* lane_ = nullptr;
+    int rc_ = NWV_OK;
+};
+
+int gpu_open(Gpu& g, int ordinal, uint32_t flags) {
+    g.ordinal = ordinal;
+    g.flags = flags;
+    if (const char* e = std::getenv("NWV_LANES")) g.max_lanes = (size_t)std::max(1L, std::strtol(e, nullptr, 10));
+    hipDeviceProp_t prop;
+    NWV_HIP(hipGetDeviceProperties(&prop, ordinal));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return set_err(NWV_ERR_NODEV, std::string("device is ") + prop.gcnArchName + ", need gfx950");
+    NWV_HIP(hipSetDevice(ordinal));
+    int rc = g.btab.ensure((BASE_TABLE_WORDS + CACHED_ENTRY_WORDS) * sizeof(uint32_t));
+    if (rc) return rc;
+    Lane* l = nullptr;
+    if ((rc = lane_open(g, &l))) return rc;
+    g.lanes.push_back(l);
+    g.idle.push_back(l);
+    hipLaunchKernelGGL(k_base_table, dim3((BASE_TABLE_ENTRIES + 63) / 64), dim3(64), 0, l->stream,
+                       g.btab.as<uint32_t>());
+    NWV_HIP(hipGetLastError());
+    NWV_HIP(hipStreamSynchronize(l->stream));
+    return NWV_OK;
+}
+
+void gpu_close(Gpu& g) {
+    if (g.ordinal < 0) return;
+    (void)hipSetDevice(g.ordinal);
+    for (Lane* l : g.lanes) {
+        lane_close(*l);
+        delete l;
+    }
+    g.lanes.clear();
+    g.idle.clear();
+    g.btab.release();
+}
+
 // --------------------------------------------------------------- Ed25519 pipeline ------
 struct KernelTimes {
     double ms[3] = {0, 0, 0};  // hash, points, straus
@@ -196,8 +300,21 @@ struct KernelTimes {
 
 // Launch the three-phase per-signature pipeline on buffers already resident on `d`.
 // Events bracket each kernel on d.stream when `ev` is non-null (ev[0..5]).
-int ed_launch(Device& d, EdBuffers& b, size_t n, hipStream_t stream, hipEvent_t* ev) {
+// Per-signature scratch (k, flags, 2 KiB tables, verdict words): allocated on the first
+// per-signature run of a buffer set, so batches that the MSM accepts never hold it.
+int ed_scratch(EdBuffers& b, size_t n) {
+    int rc;
+    if ((rc = b.kbuf.ensure(32 * n + 16)) || (rc = b.flags.ensure(4 * n + 4)) ||
+        (rc = b.tables.ensure((size_t)LANE_SCRATCH_WORDS * 4 * n + 16)) ||
+        (rc = b.verdict.ensure(8 * ((n + 63) / 64) + 8)))
+        return rc;
+    return NWV_OK;
+}
+
+int ed_launch(Lane& d, EdBuffers& b, size_t n, hipStream_t stream, hipEvent_t* ev) {
     if (n == 0) return NWV_OK;
+    int rc = ed_scratch(b, n);
+    if (rc) return rc;
     const size_t waves = (n + 63) / 64;
     const dim3 blk(256), grid((unsigned)((n + 255) / 256)), grid2((unsigned)((2 * 64 * waves + 255) / 256));
     if (ev) NWV_HIP(hipEventRecord(ev[0], stream));
@@ -210,7 +327,7 @@ int ed_launch(Device& d, EdBuffers& b, size_t n, hipStream_t stream, hipEvent_t*
     if (ev) NWV_HIP(hipEventRecord(ev[2], stream));
     hipLaunchKernelGGL(k_ed_straus, grid, blk, 0, stream, (uint64_t)n, b.sig.as<uint8_t>(),
                        b.kbuf.as<uint8_t>(), b.tables.as<uint32_t>(), b.flags.as<uint32_t>(),
-                       d.btab.as<uint32_t>(), b.verdict.as<uint64_t>());
+                       d.btab().as<uint32_t>(), b.verdict.as<uint64_t>());
     if (ev) NWV_HIP(hipEventRecord(ev[3], stream));
     NWV_HIP(hipGetLastError());
     return NWV_OK;
@@ -293,7 +410,7 @@ constexpr int MSM_NEVENTS = MSM_NKERNELS + 1;  // one event before each kernel, 
 
 // Launch the batch MSM on resident buffers; the verdict word (1 = batch accepted) is
 // m_state[1] (m_state[0] = failure flags).  ev: MSM_NEVENTS events or null.
-int msm_launch(Device& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStream_t stream,
+int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStream_t stream,
                hipEvent_t* ev, bool state_ready) {
     if (n == 0) return NWV_OK;
     const size_t na = b.nkeys_distinct ? b.nkeys_distinct : n;
@@ -329,7 +446,7 @@ int msm_launch(Device& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipS
     if ((rc = mark(1))) return rc;
     hipLaunchKernelGGL(k_msm_bscalar, dim3(1), dim3(256), 0, stream, (uint64_t)n, (uint64_t)na, (uint32_t)nblk,
                        p.lay,
-                       b.m_partial.as<uint32_t>(), d.btab.as<uint32_t>(), b.m_scal.as<uint32_t>(), digits,
+                       b.m_partial.as<uint32_t>(), d.btab().as<uint32_t>(), b.m_scal.as<uint32_t>(), digits,
                        b.m_pts.as<uint32_t>());
     if ((rc = mark(2))) return rc;
     if (!fused) hipLaunchKernelGGL(k_msm_points, dim3(pblk), dim3(256), 0, stream, gp);
@@ -416,14 +533,12 @@ static int pack_copy_h2d(int ordinal, uint8_t* dev_base, uint8_t* host_base, con
     for (const PackSeg& g : segs)
         for (size_t o = 0; o < g.len; o += kPiece)
             pieces.push_back(PackSeg{g.off + o, g.src + o, std::min(kPiece, g.len - o)});
-    std::atomic<size_t> next{0};
+    std::atomic<size_t> next{0}, done{0};
     std::atomic<int> err{0};
     auto work = [&](bool helper) {
-        if (helper && hipSetDevice(ordinal) != hipSuccess) {
-            err.store(1);
-            return;
-        }
-        for (size_t k; (k = next.fetch_add(1)) < pieces.size();) {
+        // a helper that cannot select the device takes no piece (the others copy them all)
+        if (helper && hipSetDevice(ordinal) != hipSuccess) return;
+        for (size_t k; (k = next.fetch_add(1)) < pieces.size(); done.fetch_add(1)) {
             const PackSeg& q = pieces[k];
             std::memcpy(host_base + q.off, q.src, q.len);
             if (hipMemcpyAsync(dev_base + q.off, host_base + q.off, q.len, hipMemcpyHostToDevice, stream) !=
@@ -442,7 +557,7 @@ static int pack_copy_h2d(int ordinal, uint8_t* dev_base, uint8_t* host_base, con
     }
     work(false);
     for (auto& t : th) t.join();
-    return err.load() ? set_err(NWV_ERR_HIP, "pipelined staging copy") : NWV_OK;
+    return (err.load() || done.load() != pieces.size()) ? set_err(NWV_ERR_HIP, "pipelined staging copy") : NWV_OK;
 }
 
 // Stage host inputs [lo, hi) onto buffers b of device d (message region rebased).  pk/sig
@@ -460,7 +575,7 @@ struct KeyedTail {
     const uint32_t* ksig;  // n
 };
 
-int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, const uint8_t* sig,
+int ed_stage(Lane& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, const uint8_t* sig,
              const uint8_t* msg_base, const uint64_t* msg_off, const uint32_t* msg_len,
              const uint8_t* seed32, const KeyedTail* kt = nullptr, const DevBuf* dev_msg = nullptr) {
     const size_t n = hi - lo;
@@ -486,10 +601,7 @@ int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, c
     const size_t o_koff = o_keys + (kt ? up(32 * m + 32) : 0), o_ksig = o_koff + (kt ? up(4 * m + 8) : 0);
     const size_t total = o_ksig + (kt ? up(4 * n + 8) : 0);
     int rc;
-    if ((rc = b.in.ensure(total)) || (rc = b.kbuf.ensure(32 * n + 16)) || (rc = b.flags.ensure(4 * n + 4)) ||
-        (rc = b.tables.ensure((size_t)LANE_SCRATCH_WORDS * 4 * n + 16)) ||
-        (rc = b.verdict.ensure(8 * ((n + 63) / 64) + 8)))
-        return rc;
+    if ((rc = b.in.ensure(total))) return rc;
     // views into the arena are stale once it may have moved: drop the ones not re-pointed below
     if (!inputs && b.pk.view) b.pk.release();
     if (!inputs && b.sig.view) b.sig.release();
@@ -535,7 +647,11 @@ int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, c
         }
         if (mbytes) segs.push_back(PackSeg{o_msg, msg_base + mlo, mbytes});
         int prc = pack_copy_h2d(d.ordinal, gdev, h, segs, d.stream);
-        if (prc) return prc;
+        if (prc) {
+            // copies already queued may still read the pinned buffer: the next staging waits
+            (void)hipEventRecord(d.hstage_ev, d.stream);
+            return prc;
+        }
         NWV_HIP(hipMemcpyAsync(gdev + o_msg + mbytes, h + o_msg + mbytes, total - o_msg - mbytes,
                                hipMemcpyHostToDevice, d.stream));
     } else {
@@ -565,7 +681,7 @@ int ed_stage(Device& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, c
 // Keyed staging: signature i of [lo, hi) is by keys[key_idx[i]].  The distinct keys that occur
 // in the range are renumbered densely, uploaded with the CSR of signatures per key, and pk is
 // expanded per signature (the per-signature fallback reads it).
-int ed_stage_keyed(Device& d, EdBuffers& b, size_t lo, size_t hi, size_t n_keys, const uint8_t* keys,
+int ed_stage_keyed(Lane& d, EdBuffers& b, size_t lo, size_t hi, size_t n_keys, const uint8_t* keys,
                    const uint32_t* key_idx, const uint8_t* sig, const uint8_t* msg_base,
                    const uint64_t* msg_off, const uint32_t* msg_len, const uint8_t* seed32,
                    const DevBuf* dev_msg = nullptr) {
@@ -614,7 +730,7 @@ bool verdicts_all_valid(const uint64_t* bits, size_t n) {
 }  // namespace
 
 struct nwv_ctx {
-    std::vector<Device*> devs;
+    std::vector<Gpu*> devs;
 };
 
 // Per-kernel device time of the staged pipelines (HIP events on the batch's own stream).
@@ -637,7 +753,9 @@ struct KernelLog {
 
 struct nwv_staged {
     nwv_ctx* ctx = nullptr;
-    Device* dev = nullptr;
+    Gpu* gpu = nullptr;
+    Lane own;                      // the batch's launch context: its own stream, the device's table
+    std::mutex mu;                 // one call at a time on a staged batch
     EdBuffers buf;
     size_t n = 0;
     hipStream_t stream = nullptr;  // each resident batch runs on its own stream, so several
@@ -662,10 +780,9 @@ static int for_shards(nwv_ctx* ctx, size_t n, Fn fn) {
         const size_t lo = std::min(n, k * per * 64), hi = std::min(n, (k + 1) * per * 64);
         if (lo >= hi) continue;
         auto run = [&, k, lo, hi]() {
-            Device& d = *ctx->devs[k];
-            std::lock_guard<std::mutex> g(d.mu);
-            int rc = with_device(d);
-            rcs[k] = rc ? rc : fn(d, lo, hi);
+            LaneRef lane(*ctx->devs[k]);
+            const int rc = lane.rc();
+            rcs[k] = rc ? rc : fn(*lane, lo, hi);
         };
         if (nd == 1) {
             run();
@@ -694,11 +811,10 @@ static int init_devices(nwv_ctx** out, std::vector<int> ordinals, uint32_t flags
     auto* ctx = new (std::nothrow) nwv_ctx;
     if (!ctx) return set_err(NWV_ERR_OOM, "context allocation");
     for (int o : ordinals) {
-        auto* d = new Device;
-        d->flags = flags;
-        int rc = device_open(*d, o);
+        auto* d = new Gpu;
+        int rc = gpu_open(*d, o, flags);
         if (rc) {
-            device_close(*d);
+            gpu_close(*d);
             delete d;
             nwv_free(ctx);
             return rc;
@@ -730,8 +846,8 @@ int nwv_init_device(nwv_ctx** out, int device_ordinal, uint32_t flags) {
 
 void nwv_free(nwv_ctx* ctx) {
     if (!ctx) return;
-    for (Device* d : ctx->devs) {
-        device_close(*d);
+    for (Gpu* d : ctx->devs) {
+        gpu_close(*d);
         delete d;
     }
     delete ctx;
@@ -747,7 +863,7 @@ int nwv_ed25519_verify_each(nwv_ctx* ctx, size_t n, const uint8_t* pk, const uin
     if (n == 0) return NWV_OK;
     for (size_t i = 0; i < n; i++)
         if (msg_len[i] && !msg_base) return set_err(NWV_ERR_ARG, "null msg_base");
-    return for_shards(ctx, n, [&](Device& d, size_t lo, size_t hi) -> int {
+    return for_shards(ctx, n, [&](Lane& d, size_t lo, size_t hi) -> int {
         int rc = ed_stage(d, d.ed, lo, hi, pk, sig, msg_base, msg_off, msg_len, nullptr);
         if (rc) return rc;
         if ((rc = ed_launch(d, d.ed, hi - lo, d.stream, nullptr))) return rc;
@@ -791,7 +907,7 @@ static void set_ones(uint64_t* bits, size_t lo, size_t hi) {
 
 // Batch verdict of resident buffers: MSM, then (only if it rejects) the per-signature fallback
 // for the exact bad set.  bits: the shard's verdict words (may be null).
-static int batch_on_device(Device& d, EdBuffers& b, size_t n, const uint8_t seed[32], hipStream_t stream,
+static int batch_on_device(Lane& d, EdBuffers& b, size_t n, const uint8_t seed[32], hipStream_t stream,
                            int* ok, uint64_t* bits, bool state_ready = false) {
     int rc;
     const bool use_msm = (d.flags & NWV_FLAG_MSM_ALWAYS) ||
@@ -840,7 +956,7 @@ int nwv_ed25519_verify_batch(nwv_ctx* ctx, size_t n, const uint8_t* pk, const ui
     fill_seed(seed32, seed);
     std::vector<int> oks(ctx->devs.size(), 1);
     std::mutex omu;
-    int rc = for_shards(ctx, n, [&](Device& d, size_t lo, size_t hi) -> int {
+    int rc = for_shards(ctx, n, [&](Lane& d, size_t lo, size_t hi) -> int {
         // each shard gets its own coefficient stream: seed' = seed with the shard start mixed in
         uint8_t s2[32];
         std::memcpy(s2, seed, 32);
@@ -871,7 +987,7 @@ int nwv_ed25519_verify_batch_keyed(nwv_ctx* ctx, size_t n_keys, const uint8_t* k
     uint8_t seed[32];
     fill_seed(seed32, seed);
     std::mutex omu;
-    return for_shards(ctx, n, [&](Device& d, size_t lo, size_t hi) -> int {
+    return for_shards(ctx, n, [&](Lane& d, size_t lo, size_t hi) -> int {
         uint8_t s2[32];
         std::memcpy(s2, seed, 32);
         for (int k = 0; k < 8; k++) s2[24 + k] ^= (uint8_t)((uint64_t)lo >> (8 * k));
@@ -919,7 +1035,7 @@ int nwv_ed25519_verify_batch_empty_fail(nwv_ctx* ctx, const uint8_t* msg, size_t
                                         size_t n_sigs, const uint8_t seed32[32]) {
     if (n_sigs == 0)
         return set_err(NWV_ERR_EMPTY,
-                       "Critical Error! This behaviour can signal something dangerous, and that "
+                       "Critical Error! This behavious can signal something dangerous, and that "
                        "someone may be trying to bypass signature verification through providing "
                        "empty batches.");
     if (n_sigs != n_pks)
@@ -979,19 +1095,34 @@ static int staged_create(nwv_ctx* ctx, int device_index, size_t n, nwv_staged** 
     if (!ctx || !out || device_index < 0 || device_index >= (int)ctx->devs.size())
         return set_err(NWV_ERR_ARG, "bad context/device");
     *out = nullptr;
-    auto* st = new nwv_staged;
+    auto* st = new (std::nothrow) nwv_staged;
+    if (!st) return set_err(NWV_ERR_OOM, "staged allocation");
     st->ctx = ctx;
-    st->dev = ctx->devs[device_index];
+    st->gpu = ctx->devs[device_index];
     st->n = n;
-    std::lock_guard<std::mutex> g(st->dev->mu);
-    int rc = with_device(*st->dev);
-    if (!rc) rc = stage(*st->dev, st->buf);
-    if (!rc && hipStreamSynchronize(st->dev->stream) != hipSuccess) rc = set_err(NWV_ERR_HIP, "stage sync");
+    int rc;
+    {
+        // the inputs cross PCIe through a lane's pinned staging buffer, then stay resident
+        LaneRef lane(*st->gpu);
+        rc = lane.rc();
+        if (!rc) rc = stage(*lane, st->buf);
+        if (!rc && hipStreamSynchronize((*lane).stream) != hipSuccess) rc = set_err(NWV_ERR_HIP, "stage sync");
+    }
+    Lane& o = st->own;
+    o.gpu = st->gpu;
+    o.ordinal = st->gpu->ordinal;
+    o.flags = st->gpu->flags;
+    o.btabp = &st->gpu->btab;
     if (!rc && hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking) != hipSuccess)
         rc = set_err(NWV_ERR_HIP, "hipStreamCreate");
+    o.stream = st->stream;
     for (auto& e : st->ev)
         if (!rc && hipEventCreate(&e) != hipSuccess) rc = set_err(NWV_ERR_HIP, "hipEventCreate");
     if (rc) {
+        o.stream = nullptr;  // owned by st (destroyed below), not by the lane view
+        for (auto& e : st->ev)
+            if (e) (void)hipEventDestroy(e);
+        if (st->stream) (void)hipStreamDestroy(st->stream);
         st->buf.release();
         delete st;
         return rc;
@@ -1005,7 +1136,7 @@ extern "C" {
 int nwv_stage_ed25519(nwv_ctx* ctx, int device_index, size_t n, const uint8_t* pk,
                       const uint8_t* sig, const uint8_t* msg_base, const uint64_t* msg_off,
                       const uint32_t* msg_len, nwv_staged** out) {
-    return staged_create(ctx, device_index, n, out, [&](Device& d, EdBuffers& b) {
+    return staged_create(ctx, device_index, n, out, [&](Lane& d, EdBuffers& b) {
         return ed_stage(d, b, 0, n, pk, sig, msg_base, msg_off, msg_len, nullptr);
     });
 }
@@ -1014,7 +1145,7 @@ int nwv_stage_ed25519_keyed(nwv_ctx* ctx, int device_index, size_t n_keys, const
                             const uint32_t* key_idx, const uint8_t* sig, const uint8_t* msg_base,
                             const uint64_t* msg_off, const uint32_t* msg_len, nwv_staged** out) {
     if (n && (!keys || !key_idx || !sig || !msg_off || !msg_len)) return set_err(NWV_ERR_ARG, "null argument");
-    return staged_create(ctx, device_index, n, out, [&](Device& d, EdBuffers& b) {
+    return staged_create(ctx, device_index, n, out, [&](Lane& d, EdBuffers& b) {
         return ed_stage_keyed(d, b, 0, n, n_keys, keys, key_idx, sig, msg_base, msg_off, msg_len, nullptr);
     });
 }
@@ -1025,7 +1156,7 @@ static int staged_collect_times(nwv_staged* st) {
     if (st->last_mode == 1) {
         NWV_HIP(hipEventSynchronize(st->ev[MSM_NKERNELS]));
         for (int i = 0; i < MSM_NKERNELS; i++) NWV_HIP(hipEventElapsedTime(&t[i], st->ev[i], st->ev[i + 1]));
-        st->log[1].add((st->dev->flags & NWV_FLAG_MSM_SPLIT_PREP) ? MSM_KERNEL_NAMES_SPLIT : MSM_KERNEL_NAMES, t,
+        st->log[1].add((st->own.flags & NWV_FLAG_MSM_SPLIT_PREP) ? MSM_KERNEL_NAMES_SPLIT : MSM_KERNEL_NAMES, t,
                        MSM_NKERNELS);
     } else {
         NWV_HIP(hipEventSynchronize(st->ev[3]));
@@ -1039,11 +1170,11 @@ static int staged_collect_times(nwv_staged* st) {
 // Capture the batch MSM of a staged batch once into a HIP graph (buffers and plan are fixed for
 // the batch; the per-run seed lives in device memory), so a run is one seed copy + one graph
 // launch instead of ~13 kernel launches.
-static int staged_graph(nwv_staged* st, Device& d) {
+static int staged_graph(nwv_staged* st) {
     if (st->graph || st->graph_failed) return NWV_OK;
     hipGraph_t g = nullptr;
     NWV_HIP(hipStreamBeginCapture(st->stream, hipStreamCaptureModeThreadLocal));
-    const int rc = msm_launch(d, st->buf, st->n, nullptr, st->stream, nullptr, false);
+    const int rc = msm_launch(st->own, st->buf, st->n, nullptr, st->stream, nullptr, false);
     const hipError_t e = hipStreamEndCapture(st->stream, &g);
     if (rc || e != hipSuccess || !g || hipGraphInstantiate(&st->graph, g, nullptr, nullptr, 0) != hipSuccess) {
         st->graph = nullptr;
@@ -1058,9 +1189,8 @@ int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]) {
     const bool timed = (mode & NWV_RUN_TIMED) != 0;
     mode &= ~NWV_RUN_TIMED;
     if (!st || (mode != 0 && mode != 1)) return set_err(NWV_ERR_ARG, "bad staged/mode");
-    Device& d = *st->dev;
-    std::lock_guard<std::mutex> g(d.mu);
-    int rc = with_device(d);
+    std::lock_guard<std::mutex> g(st->mu);
+    int rc = with_device(st->own);
     if (rc) return rc;
     if ((rc = staged_collect_times(st))) return rc;
     if (mode == 1) {
@@ -1072,11 +1202,11 @@ int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]) {
         } else {
             // first run of the batch (allocates its buffers) or a timed run; an untimed first run
             // also captures the graph the later runs replay
-            rc = msm_launch(d, st->buf, st->n, seed, st->stream, timed ? st->ev : nullptr, false);
-            if (!rc && !timed && st->n) rc = staged_graph(st, d);
+            rc = msm_launch(st->own, st->buf, st->n, seed, st->stream, timed ? st->ev : nullptr, false);
+            if (!rc && !timed && st->n) rc = staged_graph(st);
         }
     } else {
-        rc = ed_launch(d, st->buf, st->n, st->stream, timed ? st->ev : nullptr);
+        rc = ed_launch(st->own, st->buf, st->n, st->stream, timed ? st->ev : nullptr);
     }
     if (rc) return rc;
     st->last_mode = mode;
@@ -1084,21 +1214,25 @@ int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]) {
     return NWV_OK;
 }
 
-int nwv_staged_sync(nwv_staged* st) {
-    if (!st) return set_err(NWV_ERR_ARG, "null staged");
-    Device& d = *st->dev;
-    std::lock_guard<std::mutex> g(d.mu);
-    int rc = with_device(d);
+static int staged_sync_locked(nwv_staged* st) {
+    int rc = with_device(st->own);
     if (rc) return rc;
     NWV_HIP(hipStreamSynchronize(st->stream));
     return staged_collect_times(st);
+}
+
+int nwv_staged_sync(nwv_staged* st) {
+    if (!st) return set_err(NWV_ERR_ARG, "null staged");
+    std::lock_guard<std::mutex> g(st->mu);
+    return staged_sync_locked(st);
 }
 
 // Verdicts of the last run.  After a batch run (mode 1) that rejected, the per-signature
 // pipeline runs here to pinpoint the bad indices.
 int nwv_staged_fetch(nwv_staged* st, uint64_t* verdict_bits, int* all_valid) {
     if (!st) return set_err(NWV_ERR_ARG, "null staged");
-    int rc = nwv_staged_sync(st);
+    std::lock_guard<std::mutex> g(st->mu);
+    int rc = staged_sync_locked(st);
     if (rc) return rc;
     const size_t words = (st->n + 63) / 64;
     std::vector<uint64_t> tmp;
@@ -1107,29 +1241,29 @@ int nwv_staged_fetch(nwv_staged* st, uint64_t* verdict_bits, int* all_valid) {
         tmp.assign(words + 1, 0);
         bits = tmp.data();
     }
-    Device& d = *st->dev;
-    std::lock_guard<std::mutex> g(d.mu);
-    if ((rc = with_device(d))) return rc;
     if (st->last_mode == 1 && st->n) {
         uint32_t state[2] = {0, 0};
-        NWV_HIP(hipMemcpy(state, st->buf.m_state.p, 8, hipMemcpyDeviceToHost));
+        NWV_HIP(hipMemcpyAsync(state, st->buf.m_state.p, 8, hipMemcpyDeviceToHost, st->stream));
+        NWV_HIP(hipStreamSynchronize(st->stream));
         if (state[1] == 1) {
             std::memset(bits, 0, 8 * words);
             set_ones(bits, 0, st->n);
             if (all_valid) *all_valid = 1;
             return NWV_OK;
         }
-        if ((rc = ed_launch(d, st->buf, st->n, st->stream, nullptr))) return rc;
-        NWV_HIP(hipStreamSynchronize(st->stream));
+        if ((rc = ed_launch(st->own, st->buf, st->n, st->stream, nullptr))) return rc;
     }
-    if (words) NWV_HIP(hipMemcpy(bits, st->buf.verdict.p, 8 * words, hipMemcpyDeviceToHost));
+    if (words && !st->buf.verdict.p) return set_err(NWV_ERR_ARG, "staged batch has not run");
+    if (words) NWV_HIP(hipMemcpyAsync(bits, st->buf.verdict.p, 8 * words, hipMemcpyDeviceToHost, st->stream));
+    NWV_HIP(hipStreamSynchronize(st->stream));
     if (all_valid) *all_valid = verdicts_all_valid(bits, st->n) ? 1 : 0;
     return NWV_OK;
 }
 
 int nwv_staged_kernel_ms(nwv_staged* st, double* avg_ms, int reset) {
     if (!st || !avg_ms) return set_err(NWV_ERR_ARG, "null argument");
-    int rc = nwv_staged_sync(st);
+    std::lock_guard<std::mutex> g(st->mu);
+    int rc = staged_sync_locked(st);
     if (rc) return rc;
     const KernelLog& l = st->log[0];
     for (int k = 0; k < 3; k++) avg_ms[k] = l.runs ? l.ms[k] / l.runs : 0.0;
@@ -1140,7 +1274,8 @@ int nwv_staged_kernel_ms(nwv_staged* st, double* avg_ms, int reset) {
 int nwv_staged_kernel_times(nwv_staged* st, int mode, int cap, const char** names, double* avg_ms,
                             int reset) {
     if (!st || (mode != 0 && mode != 1) || cap < 0) return set_err(NWV_ERR_ARG, "bad argument");
-    int rc = nwv_staged_sync(st);
+    std::lock_guard<std::mutex> g(st->mu);
+    int rc = staged_sync_locked(st);
     if (rc) return rc;
     KernelLog& l = st->log[mode];
     const int k = std::min<int>(cap, (int)l.names.size());
@@ -1153,17 +1288,44 @@ int nwv_staged_kernel_times(nwv_staged* st, int mode, int cap, const char** name
     return total;
 }
 
+int nwv_staged_msm_stats(nwv_staged* st, uint64_t out[8]) {
+    if (!st || !out) return set_err(NWV_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> g(st->mu);
+    int rc = staged_sync_locked(st);
+    if (rc) return rc;
+    std::memset(out, 0, 8 * sizeof(uint64_t));
+    if (!st->n) return NWV_OK;
+    const size_t na = st->buf.nkeys_distinct ? st->buf.nkeys_distinct : st->n;
+    const MsmPlan p = msm_plan(st->n, na);
+    out[0] = p.np;
+    out[1] = (uint64_t)p.lay.nw;
+    out[2] = (uint64_t)p.lay.nw_z;
+    out[3] = p.nkeys;
+    out[5] = p.chunks;
+    out[6] = p.seg;
+    out[7] = na;
+    if (st->buf.m_tiles.p && st->buf.m_tiles.cap >= 4 * ((size_t)p.ntiles + 1)) {
+        uint32_t total = 0;
+        NWV_HIP(hipMemcpyAsync(&total, st->buf.m_tiles.as<uint32_t>() + p.ntiles, 4, hipMemcpyDeviceToHost,
+                               st->stream));
+        NWV_HIP(hipStreamSynchronize(st->stream));
+        out[4] = total;
+    }
+    return NWV_OK;
+}
+
 void nwv_staged_free(nwv_staged* st) {
     if (!st) return;
     {
-        std::lock_guard<std::mutex> g(st->dev->mu);
-        (void)hipSetDevice(st->dev->ordinal);
+        std::lock_guard<std::mutex> g(st->mu);
+        (void)hipSetDevice(st->own.ordinal);
         if (st->stream) (void)hipStreamSynchronize(st->stream);
         if (st->graph) (void)hipGraphExecDestroy(st->graph);
         st->buf.release();
         for (auto& e : st->ev)
             if (e) (void)hipEventDestroy(e);
         if (st->stream) (void)hipStreamDestroy(st->stream);
+        st->own.stream = nullptr;
     }
     delete st;
 }
@@ -1177,7 +1339,7 @@ static uint64_t b2_quad_min() {
     }();
     return v;
 }
-static void b2_launch(Device& d, size_t m, uint64_t maxlen, const uint8_t* base, const uint64_t* off,
+static void b2_launch(Lane& d, size_t m, uint64_t maxlen, const uint8_t* base, const uint64_t* off,
                       const uint64_t* len, uint32_t* out) {
     if (maxlen >= b2_quad_min())
         hipLaunchKernelGGL(k_blake2b_quad, dim3((unsigned)((m + 15) / 16)), dim3(64), 0, d.stream,
@@ -1194,7 +1356,7 @@ struct B2Staged {
     const uint64_t* len;
 };
 
-static int b2_stage(Device& d, size_t n, const uint8_t* base, const uint64_t* off,
+static int b2_stage(Lane& d, size_t n, const uint8_t* base, const uint64_t* off,
                     const uint64_t* len, size_t lo, size_t hi, std::vector<uint64_t>& roff, B2Staged& st) {
     uint64_t mlo = UINT64_MAX, mhi = 0;
     for (size_t i = lo; i < hi; i++) {
@@ -1252,10 +1414,10 @@ int nwv_blake2b256_many(nwv_ctx* ctx, size_t n, const uint8_t* base, const uint6
         const size_t lo = std::min(n, k * per), hi = std::min(n, (k + 1) * per);
         if (lo >= hi) continue;
         auto run = [&, k, lo, hi]() {
-            Device& d = *ctx->devs[k];
-            std::lock_guard<std::mutex> g(d.mu);
+            LaneRef lane(*ctx->devs[k]);
+            Lane& d = *lane;
             std::vector<uint64_t> roff;
-            int rc = with_device(d);
+            int rc = lane.rc();
             B2Staged st{};
             if (!rc) rc = b2_stage(d, n, base, off, len, lo, hi, roff, st);
             if (!rc) {
@@ -1316,9 +1478,9 @@ int nwv_ed25519_verify_batch_keyed_digests(nwv_ctx* ctx, size_t n_pre, const uin
     if (!pre_base) pre_base = empty;
     uint8_t seed[32];
     fill_seed(seed32, seed);
-    Device& d = *ctx->devs[0];
-    std::lock_guard<std::mutex> g(d.mu);
-    int rc = with_device(d);
+    LaneRef lane(*ctx->devs[0]);
+    Lane& d = *lane;
+    int rc = lane.rc();
     std::vector<uint64_t> roff;
     B2Staged st{};
     if (!rc) rc = b2_stage(d, n_pre, pre_base, pre_off, pre_len, 0, n_pre, roff, st);
@@ -1352,9 +1514,9 @@ int nwv_batch_digest_serialized(nwv_ctx* ctx, size_t n, const uint8_t* base, con
     if (!ctx || (n && (!base || !off || !len || !out || !err_offset)))
         return set_err(NWV_ERR_ARG, "null argument");
     if (n == 0) return NWV_OK;
-    Device& d = *ctx->devs[0];
-    std::lock_guard<std::mutex> g(d.mu);
-    int rc = with_device(d);
+    LaneRef lane(*ctx->devs[0]);
+    Lane& d = *lane;
+    int rc = lane.rc();
     std::vector<uint64_t> roff;
     B2Staged st{};
     if (!rc) rc = b2_stage(d, n, base, off, len, 0, n, roff, st);
@@ -1389,15 +1551,16 @@ int nwv_ed25519_sign_many(nwv_ctx* ctx, size_t n, const uint8_t* seeds, const ui
     if (n == 0) return NWV_OK;
     static const uint8_t empty[1] = {0};
     if (!msg_base) msg_base = empty;
-    return for_shards(ctx, n, [&](Device& d, size_t lo, size_t hi) -> int {
+    return for_shards(ctx, n, [&](Lane& d, size_t lo, size_t hi) -> int {
         // messages via the Ed25519 staging; seeds go to kbuf, outputs come back in pk / sig
         int rc = ed_stage(d, d.ed, lo, hi, nullptr, nullptr, msg_base, msg_off, msg_len, nullptr);
         if (rc) return rc;
         const size_t m = hi - lo;
+        if ((rc = d.ed.kbuf.ensure(32 * m + 16))) return rc;
         NWV_HIP(hipMemcpyAsync(d.ed.kbuf.p, seeds + 32 * lo, 32 * m, hipMemcpyHostToDevice, d.stream));
         hipLaunchKernelGGL(k_sign, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, d.stream,
                            (uint64_t)m, d.ed.kbuf.as<uint8_t>(), d.ed.msg.as<uint8_t>(),
-                           d.ed.off.as<uint64_t>(), d.ed.len.as<uint32_t>(), d.btab.as<uint32_t>(),
+                           d.ed.off.as<uint64_t>(), d.ed.len.as<uint32_t>(), d.btab().as<uint32_t>(),
                            d.ed.pk.as<uint8_t>(), d.ed.sig.as<uint8_t>());
         NWV_HIP(hipGetLastError());
         NWV_HIP(hipMemcpyAsync(pk_out + 32 * lo, d.ed.pk.p, 32 * m, hipMemcpyDeviceToHost, d.stream));

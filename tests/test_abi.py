@@ -46,3 +46,18 @@ def test_no_cpu_fallback_without_gpu():
     assert rc == _lib.NWV_ERR_NODEV
     with pytest.raises(narwhal_amd.NwvError):
         narwhal_amd.Engine(device=0)
+
+
+def test_batch_seed_defaults_to_os_entropy():
+    """the batch coefficients z_i must be unpredictable (OsRng in the reference): every Python
+    entry point defaults to seed=None, which passes NULL so the library keys them from OS entropy
+    on each call; a caller-given seed must be exactly 32 bytes (the C side reads 32)"""
+    import inspect
+    assert _lib._seed(None) is None
+    assert _lib._seed(b"\x01" * 32) == b"\x01" * 32
+    for bad in (b"", b"\x01" * 31, b"\x01" * 33):
+        with pytest.raises(ValueError):
+            _lib._seed(bad)
+    for fn in (_lib.Engine.verify_batch, _lib.Engine.verify_batch_keyed, _lib.Engine.verify_batch_keyed_digests,
+               _lib.Staged.run):
+        assert inspect.signature(fn).parameters["seed"].default is None, fn

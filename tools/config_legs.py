@@ -117,44 +117,86 @@ def leg_c1(eng, reps=300):
         {"committee": com, "cert": cert, "items": items}
 
 
+def _golden_adversarial():
+    """every non-honest category of the committed fixtures (B1-B8, built and
+    pinned by oracle/gen_golden.py) and the 196-case ZIP-215 small-order table, as
+    {category: [(pk, sig, msg, expected verdict)]}"""
+    import json
+    import os
+    gdir = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
+    out = {}
+    with open(os.path.join(gdir, "ed25519_vectors.json")) as f:
+        for v in json.load(f)["vectors"]:
+            if v["category"] != "honest":
+                out.setdefault(v["category"], []).append(
+                    (bytes.fromhex(v["pk"]), bytes.fromhex(v["sig"]), bytes.fromhex(v["msg"]), bool(v["expect"])))
+    with open(os.path.join(gdir, "zip215_small_order.json")) as f:
+        for v in json.load(f)["vectors"]:
+            out.setdefault("B5_zip215_table", []).append(
+                (bytes.fromhex(v["pk"]), bytes.fromhex(v["sig"]), bytes.fromhex(v["msg"]), bool(v["expect"])))
+    return out
+
+
+# categories applied to the batch's own honest entries (512-byte messages)
+INPLACE = ("B1_flip_R_inplace", "B1_flip_s_inplace", "B1_flip_msg_inplace", "B2_s_plus_l_inplace",
+           "B5_identity_A_R_s0_inplace")
+
+
 def adversarial_batch(eng, n=65536, frac=0.01, seed=4, mlen=512):
-    """C4: n signatures, frac of them adversarial at seeded positions, categories in turn:
-    bit-flipped R, bit-flipped s, wrong message, s + l (non-canonical scalar), and the ZIP-215
-    small-order entries A = R = identity with s = 0 (accepted by the cofactored equation)"""
+    """C4: n honest signatures over mlen-byte messages, frac of them replaced at seeded positions
+    by adversarial entries, the categories taken in turn: bit-flipped R / s / message, s + l, the
+    identity A = R with s = 0 (accepted by the cofactored equation), and every Appendix-B category
+    of the golden fixtures (non-canonical R / A, small-order and mixed-order A / R, undecodable R /
+    A, negative zero, with the entries that the cofactored equation accepts and rejects).
+    Returns (items, positions, categories, expected bad indices by construction)."""
     rng = np.random.default_rng(seed)
     seeds = [rng.bytes(32) for _ in range(n)]
     msgs = [rng.bytes(mlen) for _ in range(n)]
     pk, sg = eng.sign_many(seeds, msgs)
     pk, sg = pk.copy(), sg.copy()
     pos = np.sort(rng.choice(n, size=int(n * frac), replace=False))
+    gold = _golden_adversarial()
+    cats = list(INPLACE) + sorted(gold)
     ident = np.zeros(32, dtype=np.uint8)
     ident[0] = 1
-    cats = []
-    for j, i in enumerate(pos):
-        c = j % 5
-        cats.append(c)
-        if c == 0:
-            sg[64 * i + 3] ^= 0x10
-        elif c == 1:
-            sg[64 * i + 40] ^= 0x01
-        elif c == 2:
-            msgs[i] = bytes([msgs[i][0] ^ 0x80]) + msgs[i][1:]
-        elif c == 3:
-            s = int.from_bytes(sg[64 * i + 32:64 * i + 64].tobytes(), "little") + L_ORDER
-            sg[64 * i + 32:64 * i + 64] = np.frombuffer(s.to_bytes(32, "little"), dtype=np.uint8)
-        else:
-            pk[32 * i:32 * i + 32] = ident
-            sg[64 * i:64 * i + 32] = ident
-            sg[64 * i + 32:64 * i + 64] = 0
     items = [(pk[32 * i:32 * i + 32].tobytes(), sg[64 * i:64 * i + 64].tobytes(), msgs[i]) for i in range(n)]
-    expect_bad = sorted(int(i) for i, c in zip(pos, cats) if c != 4)
-    return items, [int(i) for i in pos], expect_bad
+    used, expect_bad, turn = [], [], {}
+    for j, i in enumerate(pos):
+        i = int(i)
+        c = cats[j % len(cats)]
+        used.append(c)
+        p, s, m = items[i]
+        if c in gold:
+            k = turn.get(c, 0)
+            turn[c] = k + 1
+            p, s, m, ok = gold[c][k % len(gold[c])]
+        else:
+            s = bytearray(s)
+            ok = False
+            if c == "B1_flip_R_inplace":
+                s[3] ^= 0x10
+            elif c == "B1_flip_s_inplace":
+                s[40] ^= 0x01
+            elif c == "B1_flip_msg_inplace":
+                m = bytes([m[0] ^ 0x80]) + m[1:]
+            elif c == "B2_s_plus_l_inplace":
+                v = int.from_bytes(bytes(s[32:]), "little") + L_ORDER
+                s[32:] = v.to_bytes(32, "little")
+            else:
+                p = ident.tobytes()
+                s = bytearray(ident.tobytes() + bytes(32))
+                ok = True
+            s = bytes(s)
+        items[i] = (p, s, m)
+        if not ok:
+            expect_bad.append(i)
+    return items, [int(i) for i in pos], used, expect_bad
 
 
 def leg_c4(eng, reps=5):
     """host arrays already packed (as a Rust caller holds them): the timed region is the C call,
     H2D + batch MSM + per-signature fallback + D2H"""
-    items, pos, expect_bad = adversarial_batch(eng)
+    items, pos, cats, expect_bad = adversarial_batch(eng)
     n = len(items)
     pk, sig, arena, offs, lens = _lib.soa(items)
     bitsbuf = np.zeros((n + 63) // 64 + 1, dtype=np.uint64)
@@ -171,7 +213,7 @@ def leg_c4(eng, reps=5):
     bits = list(_lib.unpack_bits(bitsbuf, n))
     bad = [i for i, b in enumerate(bits) if not b]
     med = float(np.median(ts))
-    return {"n": n, "adversarial": len(pos), "batch_verdict": ok, "bad": len(bad),
+    return {"n": n, "adversarial": len(pos), "categories": len(set(cats)), "batch_verdict": ok, "bad": len(bad),
             "bad_set_equals_injected": bad == expect_bad, "ms_per_batch_host_to_host": med * 1e3,
             "sigs_per_s": n / med}, {"items": items, "pos": pos, "bits": bits}
 
