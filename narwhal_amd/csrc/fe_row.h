@@ -302,6 +302,32 @@ NWV_HD void row_horner(const uint32_t* cq, const uint32_t* top, const Layout& la
     st(out, limb + bc(32), d.Z, r0);
 }
 
+// Scaled window sum of the fused MSM tail (k_msm_tail) on one wave, from the window's bit planes:
+//   W = sum_{k < m} 2^k T_k + U  ->  d = T_{m-1};  d = [2] d + T_k (k = m-2 .. 0);  d = d + U;
+//   d = [2^post] d.
+// planes: [m + 1][4][16] row limbs of cached points (Y+X | Y-X | 2dT | 2Z): T_0 .. T_{m-1}, then
+// U.  Row 0 writes d's X | Y | Z | T limbs to out[0..64).
+NWV_HD void row_planes_chain(const uint32_t* planes, int m, int post, uint32_t* out) {
+    const RowConsts k = row_consts();
+    const V lane = lane_id() & 63u;
+    const V limb = lane & 15u;
+    // d = identity (X = 0, Y = Z = 1, T = 0), then the planes from the top
+    RowP3 d{bc(0), sel(limb_is(0), bc(0), bc(1)), sel(limb_is(0), bc(0), bc(1)), bc(0)};
+#pragma unroll 1
+    for (int j = m - 1; j >= 0; j--) {
+        if (j < m - 1) d = row_dbl(d, k);
+        d = row_add_cached(d, ld(planes, bc(64u * (uint32_t)j) + lane), k);
+    }
+    d = row_add_cached(d, ld(planes, bc(64u * (uint32_t)m) + lane), k);
+#pragma unroll 1
+    for (int i = 0; i < post; i++) d = row_dbl(d, k);
+    const M r0 = row_is(0);
+    st(out, limb, d.X, r0);
+    st(out, limb + bc(16), d.Y, r0);
+    st(out, limb + bc(32), d.Z, r0);
+    st(out, limb + bc(48), d.T, r0);
+}
+
 }  // namespace rowf
 
 // ---- conversions between the lane-local ten-limb form and 16-bit row limbs ----------------

@@ -543,6 +543,166 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_window(MsmLayout lay, co
     if (g == 0) store_p3(wsum + (size_t)P3_WORDS * w, x);
 }
 
+// ---- fused tail: window sums, their scaling and the batch verdict in ONE launch ------------
+// The MSM total is  sum_w [2^pos_w] W_w  with  W_w = sum_{b'=0}^{nb-1} (b'+1) S_{w,b'}.  Instead
+// of a window kernel followed by a one-wave Horner (every window sum on the critical path, then
+// ~250 dependent doublings), each window is scaled on its own as soon as its sum is known: only
+// the TOP window's sum precedes the doubling chain, and the other windows overlap it.
+//
+// Window sums by bit planes:  W = sum_k 2^k T_k + U,  T_k = sum over buckets b' with bit k set,
+// U = sum of all buckets.  All planes of 2^m buckets come out of ONE butterfly of depth m: at step
+// o = 1, 2, 4, ..., every lane whose index has bit o clear adds its partner lane + o.  After the
+// last step lane 0 holds U and lane 2^k holds T_k (a lane with lowest set bit k only ever meets
+// lanes of the same lowest set bit, i.e. the T_k tree, and the pair sums move up to lanes with
+// more trailing zeros).  Depth m additions instead of 2m + suffix scan + tree for running sums.
+//
+// grid (S, nw), 256 threads.  Workgroup (s, w) owns chunk s of window w (C = nb / S_w <= 256
+// consecutive buckets, one per lane): its butterfly gives R_s (= the chunk's U) and T_{s,k},
+// k < lg C.  The last-arriving workgroup of window w (agent-scope release / counter / acquire,
+// cdna_hip_programming.md Guideline 16, counter form) combines them with one more butterfly over
+// s, per plane: T_k = sum_s T_{s,k} (k < lg C), and the butterfly of the R_s gives the planes
+// k >= lg C and U.  Its wave 0 then runs, on 16-lane rows (fe_row.h), the m-step plane chain and
+// pos_w + 3 doublings ([8] folded in).  The last window to finish sums the nw scaled windows and
+// tests the identity: *verdict = 1 iff accepted and no failure flag is set.  ctr[0..nw] must be
+// zero at launch (a memset node precedes it).
+struct MsmTailArgs {
+    const uint32_t* bsum;  // [nkeys] bucket sums (P3)
+    uint32_t* part;        // [nw][S][TAIL_PART_SLOTS] chunk planes (P3): R_s, T_{s,0}, T_{s,1}, ...
+    uint32_t* wsc;         // [nw] scaled window sums (P3)
+    uint32_t* ctr;         // [nw + 1] arrival counters
+    const uint32_t* fail;
+    uint32_t* verdict;
+    uint32_t S;
+};
+static constexpr int TAIL_PART_SLOTS = 9;  // R_s + up to 8 planes (C <= 256)
+
+namespace {
+
+__device__ __forceinline__ int tail_lg(int x) {
+    int lg = 0;
+    while ((1 << lg) < x) lg++;
+    return lg;
+}
+
+// counter hand-off of everything this workgroup stored: returns true (uniformly) in the
+// workgroup that arrives last of `expect`, after an agent-scope acquire
+__device__ __forceinline__ bool tail_arrive(uint32_t* ctr, uint32_t expect, uint32_t* flag) {
+    const int t = threadIdx.x;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+    __syncthreads();
+    if (t == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t last = old + 1 == expect ? 1u : 0u;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *flag = last;
+    }
+    __syncthreads();
+    return *flag != 0;
+}
+
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(256) k_msm_tail(MsmLayout lay, MsmTailArgs a) {
+    // 256 point slots of P3_WORDS; row-limb planes reuse the front once the slots are done;
+    // the flag word sits behind the slots
+    extern __shared__ uint32_t lds[];
+    uint32_t* flag = lds + 256 * P3_WORDS;
+    const int t = threadIdx.x, w = blockIdx.y, s = blockIdx.x;
+    const int nb = 1 << (lay.width[w] - 1);
+    const int Sw = (int)a.S < nb ? (int)a.S : nb;
+    if (s >= Sw) return;  // whole workgroup
+    const int C = nb / Sw, lgC = tail_lg(C), lgS = tail_lg(Sw);
+    // ---- chunk butterfly: lane 0 -> R_s, lane 2^k -> T_{s,k}
+    uint32_t* mine = lds + P3_WORDS * t;
+    ge_p3 p = ge_p3_identity();
+    if (t < C) p = load_p3(a.bsum + (size_t)P3_WORDS * ((size_t)lay.kbase[w] + (size_t)s * C + t));
+    for (int o = 1; o < C; o <<= 1) {
+        if (t < C) store_p3(mine, p);
+        __syncthreads();
+        if (t < C && !(t & o)) p = p3_add(p, load_p3(lds + P3_WORDS * (t + o)));
+        __syncthreads();
+    }
+    uint32_t* mypart = a.part + (size_t)P3_WORDS * TAIL_PART_SLOTS * ((size_t)w * a.S + s);
+    if (t == 0) store_p3(mypart, p);
+    if (t < C && t && !(t & (t - 1))) store_p3(mypart + P3_WORDS * (1 + tail_lg(t)), p);
+    if (!tail_arrive(a.ctr + w, (uint32_t)Sw, flag)) return;
+    // ---- last chunk of window w: per plane, a butterfly over the Sw chunks.  Item j = q * Sw + s:
+    // plane group q < lgC sums T_{s,q}; group lgC is the butterfly of the R_s.
+    const int items = (lgC + 1) * Sw, per = (items + 255) / 256;  // items per thread (<= 3)
+    ge_p3 v[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        const int j = t + 256 * r;
+        v[r] = ge_p3_identity();
+        if (r < per && j < items) {
+            const int q = j / Sw, sj = j % Sw;
+            const uint32_t* pp = a.part + (size_t)P3_WORDS * TAIL_PART_SLOTS * ((size_t)w * a.S + sj);
+            v[r] = load_p3(pp + P3_WORDS * (q < lgC ? 1 + q : 0));
+        }
+    }
+    for (int o = 1; o < Sw; o <<= 1) {
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            if (r >= per) break;
+            const int j = t + 256 * r;
+            __syncthreads();
+            if (j < items) store_p3(mine, v[r]);
+            __syncthreads();
+            if (j < items && !((j % Sw) & o)) v[r] = p3_add(v[r], load_p3(lds + P3_WORDS * (t + o)));
+        }
+    }
+    // planes in cached row form: plane k < lgC at item k * Sw; plane lgC + i at item
+    // lgC * Sw + 2^i; U at item lgC * Sw.  Slot order: T_0 .. T_{m-1}, U  (m = lgC + lgS).
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        const int j = t + 256 * r;
+        if (r >= per || j >= items) continue;
+        const int q = j / Sw, sj = j % Sw;
+        int slot = -1;
+        if (q < lgC && sj == 0) slot = q;
+        else if (q == lgC && sj == 0) slot = lgC + lgS;
+        else if (q == lgC && !(sj & (sj - 1))) slot = lgC + tail_lg(sj);
+        if (slot >= 0) store_p3(lds + P3_WORDS * slot, v[r]);  // planes fit slots 0..16
+    }
+    __syncthreads();
+    const int m = lgC + lgS;
+    uint32_t* rows = lds + 32 * P3_WORDS;  // (m + 1) x 64 row limbs, behind the plane slots
+    if (t < 4 * (m + 1)) {
+        const ge_p3 pl = load_p3(lds + P3_WORDS * (t >> 2));
+        const int c = t & 3;
+        fe v2 = c == 0 ? fe_add(pl.Y, pl.X) : c == 1 ? fe_sub(pl.Y, pl.X) : c == 2 ? fe_mul(pl.T, fe_d2())
+                                                                                   : fe_add(pl.Z, pl.Z);
+        fe_to_limbs16(fe_carry(v2), rows + 64 * (t >> 2) + 16 * c);
+    }
+    __syncthreads();
+    uint32_t* out = lds + 16 * P3_WORDS;  // 64 words
+    if (t < 64) rowf::row_planes_chain(rows, m, lay.pos[w] + 3, out);
+    __syncthreads();
+    if (t < 4) store_fe(a.wsc + (size_t)P3_WORDS * w + 10 * t, fe_from_limbs16(out + 16 * t));
+    if (!tail_arrive(a.ctr + lay.nw, (uint32_t)lay.nw, flag)) return;
+    // ---- last window: sum of the nw scaled windows (LDS tree), identity test
+    ge_p3 x = ge_p3_identity();
+    if (t < lay.nw) x = load_p3(a.wsc + (size_t)P3_WORDS * t);
+    int mm = 1;
+    while (mm < lay.nw) mm <<= 1;
+    for (int o = mm / 2; o >= 1; o >>= 1) {
+        if (t < 2 * o) store_p3(mine, x);
+        __syncthreads();
+        if (t < o) x = p3_add(x, load_p3(lds + P3_WORDS * (t + o)));
+        __syncthreads();
+    }
+    if (t == 0) {
+        const bool ok = fe_is_zero(x.X) && fe_eq(x.Y, x.Z) && *a.fail == 0;
+        *a.verdict = ok ? 1u : 0u;
+    }
+}
+
 // Horner over windows, [8], identity: *verdict = 1 iff accepted and nothing failed.  One wave:
 // lanes w < nw convert window sum w to cached form and 16-bit row limbs (LDS), then the chain
 // runs row-parallel (fe_row.h): each doubling / addition is two levels of four multiplies, one

@@ -24,6 +24,9 @@
 
 #include <random>
 
+#include <sys/random.h>
+#include <cerrno>
+
 namespace {
 
 thread_local std::string g_last_error = "";
@@ -116,7 +119,7 @@ struct PinnedBuf {
 struct EdBuffers {
     DevBuf pk, sig, msg, off, len, kbuf, flags, tables, verdict;
     DevBuf m_scal, m_partial, m_state, m_pts, m_digits, m_cnt, m_tiles, m_entries, m_kstart, m_hpart,
-        m_bsum, m_wsum;
+        m_bsum, m_wsum, m_tpart, m_ctr;
     // keyed batches: distinct keys (m x 32), CSR of signatures by key, per-signature z_i k_i
     DevBuf keys, koff, ksig, m_ascal;
     DevBuf in;  // staging arena: pk, sig, off, len, m_state and msg are views into it
@@ -124,7 +127,8 @@ struct EdBuffers {
     void release() {
         for (DevBuf* b : {&pk, &sig, &msg, &off, &len, &kbuf, &flags, &tables, &verdict, &m_scal,
                           &m_partial, &m_state, &m_pts, &m_digits, &m_cnt, &m_tiles, &m_entries,
-                          &m_kstart, &m_hpart, &m_bsum, &m_wsum, &keys, &koff, &ksig, &m_ascal, &in})
+                          &m_kstart, &m_hpart, &m_bsum, &m_wsum, &m_tpart, &m_ctr, &keys, &koff, &ksig, &m_ascal,
+                          &in})
             b->release();
         nkeys_distinct = 0;
     }
@@ -340,6 +344,7 @@ struct MsmPlan {
     MsmLayout lay{};
     uint32_t chunk_pts = 0, chunks = 0, nkeys = 0, ntiles = 0, wg_window = 0;
     uint32_t seg = 0;  // entries per k_msm_bucket lane
+    uint32_t tail_S = 1;  // k_msm_tail: bucket chunks per window
     uint64_t np = 0, na = 0, cnt_len = 0, max_entries = 0, nseg = 0;
 };
 
@@ -375,8 +380,17 @@ MsmPlan msm_plan(size_t n, size_t na) {
     p.seg = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, p.max_entries / (256 * 4 * 2 * 64)));
     if (const char* e = std::getenv("NWV_MSM_SEG")) p.seg = (uint32_t)std::max(1L, std::strtol(e, nullptr, 10));
     p.nseg = (p.max_entries + p.seg - 1) / p.seg;
+    // tail: chunks of at most 256 buckets (one per lane of a k_msm_tail workgroup)
+    p.tail_S = 1;
+    while (((1u << (p.lay.cmax - 1)) / p.tail_S) > 256) p.tail_S <<= 1;
+    if (const char* e = std::getenv("NWV_MSM_TAIL_S")) {
+        const long v = std::strtol(e, nullptr, 10);  // only larger (smaller chunks) than the minimum
+        while (p.tail_S < 64 && (long)(p.tail_S << 1) <= v) p.tail_S <<= 1;
+    }
     return p;
 }
+
+constexpr size_t MSM_CTR_BYTES = 256;  // k_msm_tail arrival counters (nw + 1 <= 49 words)
 
 int msm_alloc(EdBuffers& b, const MsmPlan& p, size_t n) {
     const size_t nblk = (n + 255) / 256;
@@ -391,7 +405,9 @@ int msm_alloc(EdBuffers& b, const MsmPlan& p, size_t n) {
         (rc = b.m_kstart.ensure((size_t)4 * p.nkeys + 64)) ||
         (rc = b.m_hpart.ensure((size_t)4 * P3_WORDS * p.nseg + 64)) ||
         (rc = b.m_bsum.ensure((size_t)4 * P3_WORDS * p.nkeys + 64)) ||
-        (rc = b.m_wsum.ensure((size_t)4 * P3_WORDS * p.lay.nw + 64)))
+        (rc = b.m_wsum.ensure((size_t)4 * P3_WORDS * p.lay.nw + 64)) ||
+        (rc = b.m_tpart.ensure((size_t)4 * P3_WORDS * TAIL_PART_SLOTS * p.lay.nw * p.tail_S + 64)) ||
+        (rc = b.m_ctr.ensure(MSM_CTR_BYTES)))
         return rc;
     return NWV_OK;
 }
@@ -401,10 +417,10 @@ static const char* const ED_KERNEL_NAMES[] = {"k_ed_hash", "k_ed_points", "k_ed_
 // the decompression as one grid unless NWV_FLAG_MSM_SPLIT_PREP)
 static const char* const MSM_KERNEL_NAMES[] = {
     "k_msm_prep", "k_msm_bscalar", nullptr, "k_msm_hist", "k_scan",
-    "k_msm_scatter", "k_msm_bucket+fixup", "k_msm_window", "k_msm_final"};
+    "k_msm_scatter", "k_msm_bucket+fixup", "k_msm_tail", nullptr};
 static const char* const MSM_KERNEL_NAMES_SPLIT[] = {
     "k_msm_scalars", "k_msm_bscalar", "k_msm_points", "k_msm_hist", "k_scan",
-    "k_msm_scatter", "k_msm_bucket+fixup", "k_msm_window", "k_msm_final"};
+    "k_msm_scatter", "k_msm_bucket+fixup", "k_msm_tail", nullptr};
 constexpr int MSM_NKERNELS = 9;
 constexpr int MSM_NEVENTS = MSM_NKERNELS + 1;  // one event before each kernel, one after the last
 
@@ -478,12 +494,14 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     hipLaunchKernelGGL(k_msm_fixup, dim3((p.nkeys + 255) / 256), dim3(256), 0, stream, p.nkeys, p.chunks,
                        p.seg, cnt, tiles + p.ntiles, b.m_hpart.as<uint32_t>(), b.m_bsum.as<uint32_t>());
     if ((rc = mark(7))) return rc;
-    hipLaunchKernelGGL(k_msm_window, dim3((unsigned)p.lay.nw), dim3(p.wg_window),
-                       (size_t)4 * P3_WORDS * p.wg_window, stream, p.lay, b.m_bsum.as<uint32_t>(),
-                       b.m_wsum.as<uint32_t>());
+    // window sums, their scaling and the verdict: one launch (its arrival counters are zeroed by
+    // a memset node first, graph replays included)
+    NWV_HIP(hipMemsetAsync(b.m_ctr.p, 0, MSM_CTR_BYTES, stream));
+    const MsmTailArgs ta{b.m_bsum.as<uint32_t>(), b.m_tpart.as<uint32_t>(), b.m_wsum.as<uint32_t>(),
+                         b.m_ctr.as<uint32_t>(), state, state + 1, p.tail_S};
+    hipLaunchKernelGGL(k_msm_tail, dim3(p.tail_S, (unsigned)p.lay.nw), dim3(256), (size_t)4 * (256 * P3_WORDS + 4),
+                       stream, p.lay, ta);
     if ((rc = mark(8))) return rc;
-    hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, stream, p.lay, b.m_wsum.as<uint32_t>(),
-                       state, state + 1);
     if ((rc = mark(9))) return rc;
     NWV_HIP(hipGetLastError());
     return NWV_OK;
@@ -894,10 +912,18 @@ static void fill_seed(const uint8_t* seed32, uint8_t out[32]) {
         std::memcpy(out, seed32, 32);
         return;
     }
-    std::random_device rd;  // OS entropy, as the reference's OsRng
-    for (int i = 0; i < 32; i += 4) {
-        const uint32_t v = rd();
-        std::memcpy(out + i, &v, 4);
+    // OS entropy, as the reference's OsRng: one getrandom(2) call (std::random_device costs
+    // ~20 us per 4 bytes here, which showed up as host-side launch latency of every batch)
+    size_t got = 0;
+    while (got < 32) {
+        const ssize_t r = getrandom(out + got, 32 - got, 0);
+        if (r > 0) {
+            got += (size_t)r;
+        } else if (r < 0 && errno != EINTR) {
+            std::random_device rd;  // fallback only if the syscall is unavailable
+            for (size_t i = got; i < 32; i++) out[i] = (uint8_t)rd();
+            got = 32;
+        }
     }
 }
 
