@@ -39,6 +39,7 @@ __device__ __forceinline__ V64 mad64(V a, V b, V64 c) { return (uint64_t)a * b +
 __device__ __forceinline__ V64 zero64() { return 0; }
 __device__ __forceinline__ V64 add64(V64 a, V64 b) { return a + b; }
 __device__ __forceinline__ void phase_fence() { __builtin_amdgcn_sched_barrier(0); }
+
 __device__ __forceinline__ V lo16(V64 x) { return (uint32_t)x & 0xFFFFu; }
 __device__ __forceinline__ V shr16(V64 x) { return (uint32_t)(x >> 16); }
 __device__ __forceinline__ V sel(M m, V a, V b) { return m ? b : a; }
@@ -67,6 +68,18 @@ __device__ __forceinline__ V ld(const uint32_t* base, V idx) { return base[idx];
 __device__ __forceinline__ void st(uint32_t* base, V idx, V x, M m) {
     if (m) base[idx] = x;
 }
+__device__ __forceinline__ void st_all(uint32_t* base, V idx, V x) { base[idx] = x; }
+// four consecutive words at a 16-byte aligned index (one ds_read_b128)
+__device__ __forceinline__ void ld4(const uint32_t* base, V idx, V& x0, V& x1, V& x2, V& x3) {
+    const uint4 q = *reinterpret_cast<const uint4*>(base + idx);
+    x0 = q.x;
+    x1 = q.y;
+    x2 = q.z;
+    x3 = q.w;
+}
+// LDS accesses of one wave execute in issue order; this keeps the compiler from moving them
+// across each other when one lane reads what another lane of the wave wrote
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 
 #else  // host emulation of one wave
 
@@ -168,6 +181,17 @@ inline void swap32(V& a, V& b) {
 }
 inline V ld(const uint32_t* base, V idx) { V r; NWV_ROW_FOR r.l[i] = base[idx.l[i]]; return r; }
 inline void st(uint32_t* base, V idx, V x, M m) { NWV_ROW_FOR if (m.l[i]) base[idx.l[i]] = x.l[i]; }
+inline void st_all(uint32_t* base, V idx, V x) { NWV_ROW_FOR base[idx.l[i]] = x.l[i]; }
+inline void ld4(const uint32_t* base, V idx, V& x0, V& x1, V& x2, V& x3) {
+    NWV_ROW_FOR {
+        row_check(idx.l[i] % 4 == 0);
+        x0.l[i] = base[idx.l[i]];
+        x1.l[i] = base[idx.l[i] + 1];
+        x2.l[i] = base[idx.l[i] + 2];
+        x3.l[i] = base[idx.l[i] + 3];
+    }
+}
+inline void lds_order() {}
 #undef NWV_ROW_FOR
 
 #endif
@@ -178,6 +202,7 @@ struct RowConsts {
     V w15;  // carry-out weight: 38 on limb 15 (2^256 = 38 mod p), 1 elsewhere
     V k8p;  // limb k of 8p: 8 * (0xFFED | 0xFFFF | 0x7FFF)
     M r1, r2, r3;
+    uint32_t* sc = nullptr;  // 192 words of LDS for this wave: operands of mul() go through LDS
 };
 NWV_HD RowConsts row_consts() {
     RowConsts c;
@@ -213,9 +238,9 @@ NWV_HD V sub(V a, V b, const RowConsts& k) { return a + k.k8p - b; }
 
 // a * b mod p (every row its own product).  Lane k accumulates sum_R op_R * b_R with op_R =
 // a_{k-R} (k >= R) or 38 a_{k-R+16} (k < R).  All sixteen operand pairs are formed first (DPP
-// moves with no dependence on each other, so no DPP read-after-write waits), then two
-// independent multiply-add chains (even / odd R) halve the dependent chain of the convolution.
-NWV_HD V mul(V a, V b, const RowConsts& k) {
+// moves with no dependence on each other, so no DPP read-after-write waits), then one chain of
+// sixteen multiply-adds.
+NWV_HD V mul_dpp(V a, V b, const RowConsts& k) {
     const V a38 = mul24(a, bc(38));
     V op[16], bs[16];
     op[0] = a;
@@ -229,18 +254,42 @@ NWV_HD V mul(V a, V b, const RowConsts& k) {
     NWV_ROW_OPERANDS(13) NWV_ROW_OPERANDS(14) NWV_ROW_OPERANDS(15)
 #undef NWV_ROW_OPERANDS
     phase_fence();
-    V64 acc0 = mad64(op[0], bs[0], zero64());
-    V64 acc1 = mad64(op[1], bs[1], zero64());
+    V64 acc = mad64(op[0], bs[0], zero64());
 #pragma unroll
-    for (int r = 2; r < 16; r += 2) {
-        acc0 = mad64(op[r], bs[r], acc0);
-        acc1 = mad64(op[r + 1], bs[r + 1], acc1);
-    }
-    const V64 acc = add64(acc0, acc1);
+    for (int r = 1; r < 16; r++) acc = mad64(op[r], bs[r], acc);
     // first pass on the 64-bit columns (< 2^48): limb 15's carry x38 stays < 2^32
     const V x = lo16(acc) + ror1(mul32(shr16(acc), k.w15));
     return carry32(carry32(x, k), k);
 }
+
+// The same product with the operands exchanged through LDS instead of 45 DPP moves: each row
+// writes ext = [38 a | a | b] (48 words), then lane k reads op_R = ext[16 + k - R] (the wrapped,
+// x38 limbs sit below a) and b_R = ext[32 + R] (four 16-byte broadcast reads per row).
+NWV_HD V mul_lds(V a, V b, const RowConsts& k) {
+    const V lane = lane_id() & 63u;
+    const V limb = lane & 15u;
+    const V base = mul32(lane >> 4, bc(48));
+    st_all(k.sc, base + limb, mul24(a, bc(38)));
+    st_all(k.sc, base + bc(16) + limb, a);
+    st_all(k.sc, base + bc(32) + limb, b);
+    lds_order();
+    V op[16], bs[16];
+#pragma unroll
+    for (int r = 0; r < 16; r++) op[r] = ld(k.sc, base + bc(16 - r) + limb);
+#pragma unroll
+    for (int r = 0; r < 16; r += 4) ld4(k.sc, base + bc(32 + r), bs[r], bs[r + 1], bs[r + 2], bs[r + 3]);
+    lds_order();
+    // one multiply-add chain: a wave64 v_mad_u64_u32 is issue-bound, so splitting the chain
+    // (measured: 4 chains, 904 vs 808 cycles per doubling) only adds the final additions
+    V64 acc = mad64(op[0], bs[0], zero64());
+#pragma unroll
+    for (int r = 1; r < 16; r++) acc = mad64(op[r], bs[r], acc);
+    const V x = lo16(acc) + ror1(mul32(shr16(acc), k.w15));
+    return carry32(carry32(x, k), k);
+}
+
+// a * b mod p on every row: the LDS form when the wave has scratch (k.sc), else the DPP form
+NWV_HD V mul(V a, V b, const RowConsts& k) { return k.sc ? mul_lds(a, b, k) : mul_dpp(a, b, k); }
 
 // ---- points: every row holds the whole point (X, Y, Z, T one V each) ------------------------
 
@@ -306,9 +355,10 @@ NWV_HD void row_horner(const uint32_t* cq, const uint32_t* top, const Layout& la
 //   W = sum_{k < m} 2^k T_k + U  ->  d = T_{m-1};  d = [2] d + T_k (k = m-2 .. 0);  d = d + U;
 //   d = [2^post] d.
 // planes: [m + 1][4][16] row limbs of cached points (Y+X | Y-X | 2dT | 2Z): T_0 .. T_{m-1}, then
-// U.  Row 0 writes d's X | Y | Z | T limbs to out[0..64).
-NWV_HD void row_planes_chain(const uint32_t* planes, int m, int post, uint32_t* out) {
-    const RowConsts k = row_consts();
+// U.  Row 0 writes d's X | Y | Z | T limbs to out[0..64).  sc: optional LDS scratch (mul_lds).
+NWV_HD void row_planes_chain(const uint32_t* planes, int m, int post, uint32_t* out, uint32_t* sc = nullptr) {
+    RowConsts k = row_consts();
+    k.sc = sc;  // 192 words of LDS: the multiplies exchange operands through it (mul_lds)
     const V lane = lane_id() & 63u;
     const V limb = lane & 15u;
     // d = identity (X = 0, Y = Z = 1, T = 0), then the planes from the top

@@ -14,10 +14,9 @@
 //   k_msm_bucket    lane per fixed-size chunk of the sorted entries: key-segment sums (mixed
 //                   additions, affine Niels), balanced whatever the bucket sizes
 //   k_msm_fixup     lane per bucket: joins the pieces of buckets that span chunks
-//   k_msm_window    workgroup per window: sum_b b S_b (segment running sums + LDS suffix scan
-//                   + LDS tree), 256 lanes
-//   k_msm_final     Horner over windows on 16-lane rows (fe_row.h), [8], identity test ->
-//                   batch verdict word
+//   k_msm_tail      window sums by bit-plane butterflies, each window scaled on 16-lane rows
+//                   (fe_row.h) as soon as its sum is known, the sum over windows, [8], identity
+//                   test -> batch verdict word (one launch)
 // The counting sort keeps every histogram / cursor atomic in LDS; the only global atomics are
 // the (rare) failure flags.  Entry order inside a bucket depends on LDS atomic order, which
 // changes the projective representation of a bucket sum but never the group element, so the
@@ -495,54 +494,6 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_fixup(
     store_p3(out, acc);
 }
 
-// ---- per-window weighted sum W_w = sum_b b S_{w,b}: one workgroup per window -------------
-// The window's nb buckets are split over Gw = min(blockDim, nb) lanes (L = nb / Gw each); lanes
-// beyond Gw hold empty groups.  lds: blockDim points (40 KiB at 256), reused by scan and tree.
-extern "C" __global__ void __launch_bounds__(256) k_msm_window(MsmLayout lay, const uint32_t* __restrict__ bsum,
-                                                               uint32_t* __restrict__ wsum) {
-    extern __shared__ uint32_t lds[];
-    const int G = blockDim.x, g = threadIdx.x, w = blockIdx.x;
-    const int nb = 1 << (lay.width[w] - 1);
-    const int Gw = nb < G ? nb : G;
-    const int L = nb / Gw;
-    const uint32_t* bw = bsum + (size_t)P3_WORDS * ((size_t)lay.kbase[w] + (size_t)g * L);
-    ge_p3 run, acc;
-    msm_segment_sums(g < Gw ? L : 0, [&](int k) { return load_p3(bw + (size_t)P3_WORDS * k); }, run, acc);
-    // suffix_g = sum_{g' >= g} run_g' (Hillis-Steele: read, barrier, write, barrier)
-    uint32_t* mine = lds + P3_WORDS * g;
-    store_p3(mine, run);
-    __syncthreads();
-    ge_p3 suf = run;
-    for (int o = 1; o < G; o <<= 1) {
-        const bool take = g + o < G;
-        ge_p3 other = ge_p3_identity();
-        if (take) other = load_p3(lds + P3_WORDS * (g + o));
-        __syncthreads();
-        if (take) {
-            suf = p3_add(suf, other);
-            store_p3(mine, suf);
-        }
-        __syncthreads();
-    }
-    // x_g = acc_g + L * suffix_g (g >= 1), then a tree sum of x_g over the workgroup
-    ge_p3 x = acc;
-    if (g >= 1) {
-        int lg = 0;
-        while ((1 << lg) < L) lg++;
-        x = p3_add(x, lg ? p3_dbl_n(suf, lg) : suf);
-    }
-    store_p3(mine, x);
-    __syncthreads();
-    for (int o = G / 2; o >= 1; o >>= 1) {
-        if (g < o) {
-            x = p3_add(x, load_p3(lds + P3_WORDS * (g + o)));
-            store_p3(mine, x);
-        }
-        __syncthreads();
-    }
-    if (g == 0) store_p3(wsum + (size_t)P3_WORDS * w, x);
-}
-
 // ---- fused tail: window sums, their scaling and the batch verdict in ONE launch ------------
 // The MSM total is  sum_w [2^pos_w] W_w  with  W_w = sum_{b'=0}^{nb-1} (b'+1) S_{w,b'}.  Instead
 // of a window kernel followed by a one-wave Horner (every window sum on the critical path, then
@@ -573,6 +524,7 @@ struct MsmTailArgs {
     const uint32_t* fail;
     uint32_t* verdict;
     uint32_t S;
+    unsigned long long* stamps;  // diagnostics (NWV_TAIL_STAMPS): [nw][8] s_memrealtime, or null
 };
 static constexpr int TAIL_PART_SLOTS = 9;  // R_s + up to 8 planes (C <= 256)
 
@@ -607,16 +559,24 @@ __device__ __forceinline__ bool tail_arrive(uint32_t* ctr, uint32_t expect, uint
 
 }  // namespace
 
+#define NWV_TAIL_STAMP(slot)                                                                       \
+    do {                                                                                           \
+        if (a.stamps && t == 0) a.stamps[8 * w + (slot)] = __builtin_amdgcn_s_memrealtime();       \
+    } while (0)
+
 extern "C" __global__ void __launch_bounds__(256) k_msm_tail(MsmLayout lay, MsmTailArgs a) {
     // 256 point slots of P3_WORDS; row-limb planes reuse the front once the slots are done;
     // the flag word sits behind the slots
     extern __shared__ uint32_t lds[];
     uint32_t* flag = lds + 256 * P3_WORDS;
-    const int t = threadIdx.x, w = blockIdx.y, s = blockIdx.x;
+    // top window first: its sum precedes the longest doubling chain, and workgroups are
+    // dispatched in blockIdx order (a grid larger than the chip runs in waves)
+    const int t = threadIdx.x, w = lay.nw - 1 - (int)blockIdx.y, s = blockIdx.x;
     const int nb = 1 << (lay.width[w] - 1);
     const int Sw = (int)a.S < nb ? (int)a.S : nb;
     if (s >= Sw) return;  // whole workgroup
     const int C = nb / Sw, lgC = tail_lg(C), lgS = tail_lg(Sw);
+    if (s == 0) NWV_TAIL_STAMP(0);
     // ---- chunk butterfly: lane 0 -> R_s, lane 2^k -> T_{s,k}
     uint32_t* mine = lds + P3_WORDS * t;
     ge_p3 p = ge_p3_identity();
@@ -631,6 +591,7 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_tail(MsmLayout lay, MsmT
     if (t == 0) store_p3(mypart, p);
     if (t < C && t && !(t & (t - 1))) store_p3(mypart + P3_WORDS * (1 + tail_lg(t)), p);
     if (!tail_arrive(a.ctr + w, (uint32_t)Sw, flag)) return;
+    NWV_TAIL_STAMP(1);
     // ---- last chunk of window w: per plane, a butterfly over the Sw chunks.  Item j = q * Sw + s:
     // plane group q < lgC sums T_{s,q}; group lgC is the butterfly of the R_s.
     const int items = (lgC + 1) * Sw, per = (items + 255) / 256;  // items per thread (<= 3)
@@ -671,6 +632,7 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_tail(MsmLayout lay, MsmT
         if (slot >= 0) store_p3(lds + P3_WORDS * slot, v[r]);  // planes fit slots 0..16
     }
     __syncthreads();
+    NWV_TAIL_STAMP(2);
     const int m = lgC + lgS;
     uint32_t* rows = lds + 32 * P3_WORDS;  // (m + 1) x 64 row limbs, behind the plane slots
     if (t < 4 * (m + 1)) {
@@ -681,11 +643,14 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_tail(MsmLayout lay, MsmT
         fe_to_limbs16(fe_carry(v2), rows + 64 * (t >> 2) + 16 * c);
     }
     __syncthreads();
+    NWV_TAIL_STAMP(3);
     uint32_t* out = lds + 16 * P3_WORDS;  // 64 words
-    if (t < 64) rowf::row_planes_chain(rows, m, lay.pos[w] + 3, out);
+    if (t < 64) rowf::row_planes_chain(rows, m, lay.pos[w] + 3, out, lds + 60 * P3_WORDS);
     __syncthreads();
+    NWV_TAIL_STAMP(4);
     if (t < 4) store_fe(a.wsc + (size_t)P3_WORDS * w + 10 * t, fe_from_limbs16(out + 16 * t));
     if (!tail_arrive(a.ctr + lay.nw, (uint32_t)lay.nw, flag)) return;
+    NWV_TAIL_STAMP(5);
     // ---- last window: sum of the nw scaled windows (LDS tree), identity test
     ge_p3 x = ge_p3_identity();
     if (t < lay.nw) x = load_p3(a.wsc + (size_t)P3_WORDS * t);
@@ -701,39 +666,5 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_tail(MsmLayout lay, MsmT
         const bool ok = fe_is_zero(x.X) && fe_eq(x.Y, x.Z) && *a.fail == 0;
         *a.verdict = ok ? 1u : 0u;
     }
-}
-
-// Horner over windows, [8], identity: *verdict = 1 iff accepted and nothing failed.  One wave:
-// lanes w < nw convert window sum w to cached form and 16-bit row limbs (LDS), then the chain
-// runs row-parallel (fe_row.h): each doubling / addition is two levels of four multiplies, one
-// per row, each spread over the row's 16 lanes.
-extern "C" __global__ void __launch_bounds__(64) k_msm_final(MsmLayout lay, const uint32_t* __restrict__ wsum,
-                                                             const uint32_t* __restrict__ fail,
-                                                             uint32_t* __restrict__ verdict) {
-    __shared__ uint32_t cq[MSM_MAX_WINDOWS * 64];
-    __shared__ uint32_t top[64];
-    __shared__ uint32_t fin[48];
-    const int t = threadIdx.x, nw = lay.nw;
-    if (t < nw) {
-        const ge_p3 p = load_p3(wsum + (size_t)P3_WORDS * t);
-        const ge_cached c = ge_p3_to_cached(p);
-        fe_to_limbs16(c.YpX, cq + 64 * t);
-        fe_to_limbs16(c.YmX, cq + 64 * t + 16);
-        fe_to_limbs16(c.T2d, cq + 64 * t + 32);
-        fe_to_limbs16(c.Z2, cq + 64 * t + 48);
-        if (t == nw - 1) {
-            fe_to_limbs16(p.X, top);
-            fe_to_limbs16(p.Y, top + 16);
-            fe_to_limbs16(p.Z, top + 32);
-            fe_to_limbs16(p.T, top + 48);
-        }
-    }
-    __syncthreads();
-    rowf::row_horner(cq, top, lay, fin);
-    __syncthreads();
-    if (t == 0) {
-        const fe X = fe_from_limbs16(fin), Y = fe_from_limbs16(fin + 16), Z = fe_from_limbs16(fin + 32);
-        const bool ok = fe_is_zero(X) && fe_eq(Y, Z) && *fail == 0;
-        *verdict = ok ? 1u : 0u;
-    }
+    NWV_TAIL_STAMP(6);
 }

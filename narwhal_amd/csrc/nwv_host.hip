@@ -119,7 +119,7 @@ struct PinnedBuf {
 struct EdBuffers {
     DevBuf pk, sig, msg, off, len, kbuf, flags, tables, verdict;
     DevBuf m_scal, m_partial, m_state, m_pts, m_digits, m_cnt, m_tiles, m_entries, m_kstart, m_hpart,
-        m_bsum, m_wsum, m_tpart, m_ctr;
+        m_bsum, m_wsum, m_tpart, m_ctr, m_stamps;
     // keyed batches: distinct keys (m x 32), CSR of signatures by key, per-signature z_i k_i
     DevBuf keys, koff, ksig, m_ascal;
     DevBuf in;  // staging arena: pk, sig, off, len, m_state and msg are views into it
@@ -127,7 +127,7 @@ struct EdBuffers {
     void release() {
         for (DevBuf* b : {&pk, &sig, &msg, &off, &len, &kbuf, &flags, &tables, &verdict, &m_scal,
                           &m_partial, &m_state, &m_pts, &m_digits, &m_cnt, &m_tiles, &m_entries,
-                          &m_kstart, &m_hpart, &m_bsum, &m_wsum, &m_tpart, &m_ctr, &keys, &koff, &ksig, &m_ascal,
+                          &m_kstart, &m_hpart, &m_bsum, &m_wsum, &m_tpart, &m_ctr, &m_stamps, &keys, &koff, &ksig, &m_ascal,
                           &in})
             b->release();
         nkeys_distinct = 0;
@@ -342,7 +342,7 @@ int ed_launch(Lane& d, EdBuffers& b, size_t n, hipStream_t stream, hipEvent_t* e
 // points: n, or the m distinct keys of a keyed batch).
 struct MsmPlan {
     MsmLayout lay{};
-    uint32_t chunk_pts = 0, chunks = 0, nkeys = 0, ntiles = 0, wg_window = 0;
+    uint32_t chunk_pts = 0, chunks = 0, nkeys = 0, ntiles = 0;
     uint32_t seg = 0;  // entries per k_msm_bucket lane
     uint32_t tail_S = 1;  // k_msm_tail: bucket chunks per window
     uint64_t np = 0, na = 0, cnt_len = 0, max_entries = 0, nseg = 0;
@@ -374,7 +374,6 @@ MsmPlan msm_plan(size_t n, size_t na) {
     p.nkeys = p.lay.kbase[p.lay.nw];
     p.cnt_len = (uint64_t)p.nkeys * p.chunks;
     p.ntiles = (uint32_t)((p.cnt_len + 4095) / 4096);
-    p.wg_window = (uint32_t)std::min(256, 1 << (p.lay.cmax - 1));
     p.max_entries = (uint64_t)(na + 1) * p.lay.nw + (uint64_t)n * p.lay.nw_z;
     // ~2 waves per SIMD of bucket lanes (256 CUs x 4 SIMDs x 2 x 64), 8..64 entries each
     p.seg = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, p.max_entries / (256 * 4 * 2 * 64)));
@@ -497,8 +496,15 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     // window sums, their scaling and the verdict: one launch (its arrival counters are zeroed by
     // a memset node first, graph replays included)
     NWV_HIP(hipMemsetAsync(b.m_ctr.p, 0, MSM_CTR_BYTES, stream));
+    static const bool stamps = std::getenv("NWV_TAIL_STAMPS") != nullptr;  // diagnostics only
+    unsigned long long* st_buf = nullptr;
+    if (stamps && (rc = b.m_stamps.ensure(8 * 8 * (size_t)MSM_MAX_WINDOWS))) return rc;
+    if (stamps) {
+        st_buf = b.m_stamps.as<unsigned long long>();
+        NWV_HIP(hipMemsetAsync(st_buf, 0, 8 * 8 * (size_t)MSM_MAX_WINDOWS, stream));
+    }
     const MsmTailArgs ta{b.m_bsum.as<uint32_t>(), b.m_tpart.as<uint32_t>(), b.m_wsum.as<uint32_t>(),
-                         b.m_ctr.as<uint32_t>(), state, state + 1, p.tail_S};
+                         b.m_ctr.as<uint32_t>(), state, state + 1, p.tail_S, st_buf};
     hipLaunchKernelGGL(k_msm_tail, dim3(p.tail_S, (unsigned)p.lay.nw), dim3(256), (size_t)4 * (256 * P3_WORDS + 4),
                        stream, p.lay, ta);
     if ((rc = mark(8))) return rc;
@@ -1184,6 +1190,21 @@ static int staged_collect_times(nwv_staged* st) {
         for (int i = 0; i < MSM_NKERNELS; i++) NWV_HIP(hipEventElapsedTime(&t[i], st->ev[i], st->ev[i + 1]));
         st->log[1].add((st->own.flags & NWV_FLAG_MSM_SPLIT_PREP) ? MSM_KERNEL_NAMES_SPLIT : MSM_KERNEL_NAMES, t,
                        MSM_NKERNELS);
+        if (std::getenv("NWV_TAIL_STAMPS") && st->buf.m_stamps.p) {  // diagnostics: phase times, us
+            std::vector<unsigned long long> h(8 * MSM_MAX_WINDOWS);
+            NWV_HIP(hipMemcpy(h.data(), st->buf.m_stamps.p, 8 * h.size(), hipMemcpyDeviceToHost));
+            unsigned long long t0 = ~0ull;
+            for (int w = 0; w < MSM_MAX_WINDOWS; w++)
+                if (h[8 * w]) t0 = std::min(t0, h[8 * w]);
+            std::fprintf(stderr, "nwv-tail-stamps n=%zu", st->n);
+            for (int w = 0; w < MSM_MAX_WINDOWS; w++) {
+                if (!h[8 * w]) continue;
+                std::fprintf(stderr, " | w%d", w);
+                for (int k = 0; k < 7; k++)
+                    std::fprintf(stderr, " %.1f", h[8 * w + k] ? (double)(h[8 * w + k] - t0) / 100.0 : -1.0);
+            }
+            std::fprintf(stderr, "\n");
+        }
     } else {
         NWV_HIP(hipEventSynchronize(st->ev[3]));
         for (int i = 0; i < 3; i++) NWV_HIP(hipEventElapsedTime(&t[i], st->ev[i], st->ev[i + 1]));

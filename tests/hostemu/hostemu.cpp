@@ -98,7 +98,8 @@ static bool tail_host(const MsmLayout& lay, const uint32_t* bs, uint32_t S) {
             fe_to_limbs16(fe_carry(fe_mul(pl.T, fe_d2())), rows.data() + 64 * k + 32);
             fe_to_limbs16(fe_carry(fe_add(pl.Z, pl.Z)), rows.data() + 64 * k + 48);
         }
-        rowf::row_planes_chain(rows.data(), m, lay.pos[w] + 3, out.data());
+        std::vector<uint32_t> sc(192);
+        rowf::row_planes_chain(rows.data(), m, lay.pos[w] + 3, out.data(), (w & 1) ? sc.data() : nullptr);
         const ge_p3 ws{fe_from_limbs16(out.data()), fe_from_limbs16(out.data() + 16), fe_from_limbs16(out.data() + 32),
                        fe_from_limbs16(out.data() + 48)};
         tot = p3_add(tot, ws);
@@ -405,15 +406,19 @@ void he_msm_point_counts(const uint8_t* pk, const uint8_t* sig, unsigned long lo
     counts[1] = nwv_count_sq;
 }
 
-// one field multiply on the emulated wave: a, b given as 16 loose limbs (same in every row);
-// out = row 0's product limbs.  Returns 0 when the four rows disagree.
-int he_row_mul(const uint32_t* a16, const uint32_t* b16, uint32_t* out16) {
+// one field multiply on the emulated wave (the DPP form, or with use_lds the LDS-operand form): a, b
+// given as 16 loose limbs (same in every row); out = row 0's product limbs.  Returns 0 when the four
+// rows disagree.
+int he_row_mul(const uint32_t* a16, const uint32_t* b16, uint32_t* out16, int use_lds) {
     rowf::V a, b;
     for (int i = 0; i < 64; i++) {
         a.l[i] = a16[i & 15];
         b.l[i] = b16[i & 15];
     }
-    const rowf::V r = rowf::mul(a, b, rowf::row_consts());
+    std::vector<uint32_t> sc(192, 0xDEADBEEFu);
+    rowf::RowConsts k = rowf::row_consts();
+    if (use_lds) k.sc = sc.data();
+    const rowf::V r = rowf::mul(a, b, k);
     for (int i = 0; i < 64; i++)
         if (r.l[i] != r.l[i & 15]) return 0;
     for (int k = 0; k < 16; k++) out16[k] = r.l[k];

@@ -18,31 +18,34 @@ def _val(limbs):
     return sum(int(x) << (16 * k) for k, x in enumerate(limbs))
 
 
-def _row_mul(lib, a, b):
+def _row_mul(lib, a, b, use_lds=0):
     A = np.array(a, dtype=np.uint32)
     B = np.array(b, dtype=np.uint32)
     out = np.zeros(16, dtype=np.uint32)
-    assert lib.he_row_mul(A.ctypes.data, B.ctypes.data, out.ctypes.data) == 1
+    assert lib.he_row_mul(A.ctypes.data, B.ctypes.data, out.ctypes.data, use_lds) == 1
     return [int(x) for x in out]
 
 
 @pytest.fixture(scope="module")
 def lib(he):  # noqa: F811
     vp = ctypes.c_void_p
-    he.he_row_mul.argtypes = [vp, vp, vp]
+    he.he_row_mul.argtypes = [vp, vp, vp, ctypes.c_int]
     he.he_row_horner.argtypes = [ctypes.c_int, vp, vp, vp, vp]
     he.he_decompress.argtypes = [ctypes.c_char_p, vp]
     return he
 
 
+@pytest.mark.parametrize("use_lds", [0, 1])
 @pytest.mark.parametrize("bound", [2**16, 2**16 + 2**11, 2**17, int(2**17.7)])
-def test_row_mul_values_and_output_bounds(lib, bound):
+def test_row_mul_values_and_output_bounds(lib, bound, use_lds):
+    """both operand paths of the row multiply (DPP moves, or the LDS exchange the MSM tail uses)
+    give the product mod p with the documented output bounds"""
     rnd = random.Random(bound)
     cases = [[bound - 1] * 16, [0] * 16, [1] + [0] * 15]
     cases += [[rnd.randrange(bound) for _ in range(16)] for _ in range(60)]
     for a in cases:
         for b in (cases[0], cases[3], [rnd.randrange(bound) for _ in range(16)]):
-            out = _row_mul(lib, a, b)
+            out = _row_mul(lib, a, b, use_lds)
             assert _val(out) % P == (_val(a) * _val(b)) % P
             assert out[0] < 2**17 and max(out[1:]) < 2**16 + 2**11
 
