@@ -4,7 +4,8 @@
 #   make hostemu  tests/_build/libhostemu.so    (test infrastructure: device math on the host)
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
-CSRC := $(wildcard narwhal_amd/csrc/*.h narwhal_amd/csrc/*.hip narwhal_amd/csrc/*.cpp) include/nwv.h include/nwv_types.h
+CSRC := $(wildcard narwhal_amd/csrc/*.h narwhal_amd/csrc/*.hip narwhal_amd/csrc/*.cpp) include/nwv.h include/nwv_types.h \
+	include/nwv_service.h
 
 all: lib oracle hostemu tools
 
@@ -14,14 +15,22 @@ lib: narwhal_amd/lib/libnwv.so
 narwhal_amd/lib/nwv_types.o: narwhal_amd/csrc/nwv_types.cpp include/nwv.h include/nwv_types.h
 	@mkdir -p narwhal_amd/lib
 	g++ -O2 -std=c++17 -fPIC -Wall -c -o $@ $<
-narwhal_amd/lib/libnwv.so: $(CSRC) narwhal_amd/lib/nwv_types.o
+narwhal_amd/lib/nwv_service.o: narwhal_amd/csrc/nwv_service.cpp include/nwv.h include/nwv_types.h include/nwv_service.h
 	@mkdir -p narwhal_amd/lib
-	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -shared -Wall -o $@ narwhal_amd/lib/nwv_types.o narwhal_amd/csrc/nwv_host.hip
+	g++ -O2 -std=c++17 -fPIC -Wall -c -o $@ $<
+narwhal_amd/lib/libnwv.so: $(CSRC) narwhal_amd/lib/nwv_types.o narwhal_amd/lib/nwv_service.o
+	@mkdir -p narwhal_amd/lib
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -shared -Wall -o $@ narwhal_amd/lib/nwv_types.o \
+		narwhal_amd/lib/nwv_service.o narwhal_amd/csrc/nwv_host.hip -lpthread
 
 oracle:
 	$(MAKE) -C oracle
 
-hostemu: tests/_build/libhostemu.so
+hostemu: tests/_build/libhostemu.so tests/_build/libsvcstub.so
+# the batching service's host logic over a stubbed engine (tests/test_service_host.py)
+tests/_build/libsvcstub.so: tests/hostemu/service_stub.cpp narwhal_amd/csrc/nwv_service.cpp include/nwv_service.h
+	@mkdir -p tests/_build
+	g++ -O1 -g -std=c++17 -fPIC -shared -pthread -o $@ tests/hostemu/service_stub.cpp narwhal_amd/csrc/nwv_service.cpp
 tests/_build/libhostemu.so: tests/hostemu/hostemu.cpp $(CSRC)
 	@mkdir -p tests/_build
 	$(HIPCC) -std=c++17 -O1 --offload-host-only -x hip -DNWV_BOUNDS_CHECK -fPIC -shared -o $@ tests/hostemu/hostemu.cpp

@@ -9,7 +9,8 @@
 //   k_msm_points    2 lanes per signature (wave-uniform R / A roles): decompress, store the
 //                   128-byte affine Niels record of each point
 //   k_msm_hist      workgroup (chunk, window): LDS histogram of the window's bucket ids
-//   k_scan_*        exclusive scan of the (window, bucket, chunk)-ordered counts
+//   k_cnt_colsum    bucket totals over the chunks; k_scan_* their exclusive scan (bucket starts);
+//   k_cnt_offsets   the (bucket, chunk) slice offsets
 //   k_msm_scatter   workgroup (chunk, window): LDS cursors place j|sign into bucket order
 //   k_msm_bucket    lane per fixed-size chunk of the sorted entries: key-segment sums (mixed
 //                   additions, affine Niels), balanced whatever the bucket sizes
@@ -253,7 +254,8 @@ __device__ __forceinline__ uint64_t msm_window_points(uint64_t n, uint64_t na, i
     return w < nw_z ? na + 1 + n : na + 1;
 }
 
-// grid (chunks, windows); counts laid out [(kbase[w] + b) * chunks + chunk]
+// grid (chunks, windows); counts laid out window by window, chunk-major inside a window:
+// cnt[kbase[w] * chunks + chunk * nb_w + b], so every workgroup stores one contiguous run
 extern "C" __global__ void __launch_bounds__(256) k_msm_hist(
     uint64_t n, uint64_t na, MsmLayout lay, uint32_t chunk_pts, const int16_t* __restrict__ digits,
     uint32_t* __restrict__ cnt) {
@@ -271,8 +273,52 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_hist(
         if (d) atomicAdd(&hist[(d < 0 ? -d : d) - 1], 1u);
     }
     __syncthreads();
-    for (int b = threadIdx.x; b < nb; b += blockDim.x)
-        cnt[((uint64_t)lay.kbase[w] + b) * chunks + chunk] = hist[b];
+    uint32_t* out = cnt + (uint64_t)lay.kbase[w] * chunks + (uint64_t)chunk * nb;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) out[b] = hist[b];
+}
+
+// window of bucket key k (kbase ascending, at most MSM_MAX_WINDOWS windows)
+__device__ __forceinline__ int msm_key_window(const MsmLayout& lay, uint32_t k) {
+    int lo = 0, hi = lay.nw;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (lay.kbase[mid] <= k) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// lane per bucket key: tot[k] = entries of bucket k over all chunks (coalesced: consecutive
+// keys of a window are consecutive words of every chunk's run)
+extern "C" __global__ void __launch_bounds__(256) k_cnt_colsum(MsmLayout lay, uint32_t chunks,
+                                                                const uint32_t* __restrict__ cnt,
+                                                                uint32_t* __restrict__ tot) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= lay.kbase[lay.nw]) return;
+    const int w = msm_key_window(lay, k);
+    const uint32_t nb = 1u << (lay.width[w] - 1), b = k - lay.kbase[w];
+    const uint32_t* c = cnt + (uint64_t)lay.kbase[w] * chunks + b;
+    uint32_t s = 0;
+    for (uint32_t ch = 0; ch < chunks; ch++) s += c[(uint64_t)ch * nb];
+    tot[k] = s;
+}
+
+// lane per bucket key: the counts become the start offsets of every (bucket, chunk) slice:
+// kstart[k] (the scanned totals) plus the counts of the earlier chunks
+extern "C" __global__ void __launch_bounds__(256) k_cnt_offsets(MsmLayout lay, uint32_t chunks,
+                                                                 uint32_t* __restrict__ cnt,
+                                                                 const uint32_t* __restrict__ kstart) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= lay.kbase[lay.nw]) return;
+    const int w = msm_key_window(lay, k);
+    const uint32_t nb = 1u << (lay.width[w] - 1), b = k - lay.kbase[w];
+    uint32_t* c = cnt + (uint64_t)lay.kbase[w] * chunks + b;
+    uint32_t o = kstart[k];
+    for (uint32_t ch = 0; ch < chunks; ch++) {
+        const uint32_t v = c[(uint64_t)ch * nb];
+        c[(uint64_t)ch * nb] = o;
+        o += v;
+    }
 }
 
 extern "C" __global__ void __launch_bounds__(256) k_msm_scatter(
@@ -281,8 +327,8 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_scatter(
     extern __shared__ uint32_t cur[];
     const int w = blockIdx.y, nw_z = lay.nw_z, nb = 1 << (lay.width[w] - 1);
     const uint32_t chunks = gridDim.x, chunk = blockIdx.x;
-    for (int b = threadIdx.x; b < nb; b += blockDim.x)
-        cur[b] = off[((uint64_t)lay.kbase[w] + b) * chunks + chunk];
+    const uint32_t* mine = off + (uint64_t)lay.kbase[w] * chunks + (uint64_t)chunk * nb;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) cur[b] = mine[b];
     __syncthreads();
     const uint64_t np = na + 1 + n, cnt_w = msm_window_points(n, na, w, nw_z);
     const uint64_t lo = (uint64_t)chunk * chunk_pts;
@@ -302,9 +348,10 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_scatter(
 // kstart != null: the whole array is one tile (small batches), so this launch also finishes the
 // scan: kstart[key] = a[key * chunks], tile_sum[0] = 0 and tile_sum[1] = total, i.e. what
 // k_scan_tiles and k_scan_add produce for several tiles
-extern "C" __global__ void __launch_bounds__(256) k_scan_tile(uint64_t len, uint32_t* __restrict__ a,
+// (a and kstart may be the same array: the scan of the bucket totals runs in place)
+extern "C" __global__ void __launch_bounds__(256) k_scan_tile(uint64_t len, uint32_t* a,
                                                               uint32_t* __restrict__ tile_sum, uint32_t chunks,
-                                                              uint32_t* __restrict__ kstart) {
+                                                              uint32_t* kstart) {
     __shared__ uint32_t sh[256];
     const uint64_t base = (uint64_t)blockIdx.x * 4096 + threadIdx.x * 16;
     uint32_t v[16], s = 0;
@@ -366,9 +413,9 @@ extern "C" __global__ void __launch_bounds__(1024) k_scan_tiles(uint32_t ntiles,
 }
 
 // adds the tile offsets; also gathers kstart[key] = a[key * chunks] (first entry of each key)
-extern "C" __global__ void __launch_bounds__(256) k_scan_add(uint64_t len, uint32_t* __restrict__ a,
+extern "C" __global__ void __launch_bounds__(256) k_scan_add(uint64_t len, uint32_t* a,
                                                              const uint32_t* __restrict__ tile_sum,
-                                                             uint32_t chunks, uint32_t* __restrict__ kstart) {
+                                                             uint32_t chunks, uint32_t* kstart) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < len) {
         const uint32_t v = a[i] + tile_sum[i >> 12];
@@ -475,12 +522,12 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_bucket(
 // One lane per key: empty buckets become the identity; a key spanning chunks i0..i1 adds the
 // continuation pieces hpart[i0+1 .. i1] to its first piece.
 extern "C" __global__ void __launch_bounds__(256) k_msm_fixup(
-    uint32_t nkeys, uint32_t chunks, uint32_t T, const uint32_t* __restrict__ off,
+    uint32_t nkeys, uint32_t T, const uint32_t* __restrict__ kstart,
     const uint32_t* __restrict__ total, const uint32_t* __restrict__ hpart, uint32_t* __restrict__ bsum) {
     const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
     if (key >= nkeys) return;
-    const uint32_t s = off[(uint64_t)key * chunks];
-    const uint32_t e = key + 1 < nkeys ? off[(uint64_t)(key + 1) * chunks] : *total;
+    const uint32_t s = kstart[key];
+    const uint32_t e = key + 1 < nkeys ? kstart[key + 1] : *total;
     uint32_t* out = bsum + (size_t)P3_WORDS * key;
     if (s == e) {
         store_p3(out, ge_p3_identity());
@@ -651,19 +698,39 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_tail(MsmLayout lay, MsmT
     if (t < 4) store_fe(a.wsc + (size_t)P3_WORDS * w + 10 * t, fe_from_limbs16(out + 16 * t));
     if (!tail_arrive(a.ctr + lay.nw, (uint32_t)lay.nw, flag)) return;
     NWV_TAIL_STAMP(5);
-    // ---- last window: sum of the nw scaled windows (LDS tree), identity test
-    ge_p3 x = ge_p3_identity();
-    if (t < lay.nw) x = load_p3(a.wsc + (size_t)P3_WORDS * t);
-    int mm = 1;
-    while (mm < lay.nw) mm <<= 1;
-    for (int o = mm / 2; o >= 1; o >>= 1) {
-        if (t < 2 * o) store_p3(mine, x);
-        __syncthreads();
-        if (t < o) x = p3_add(x, load_p3(lds + P3_WORDS * (t + o)));
-        __syncthreads();
+    // ---- last window: sum of the nw scaled windows on 16-lane rows (wave q adds the windows
+    // w = q mod 4, then wave 0 adds the other three partial sums), identity test
+    uint32_t* cq = lds;                          // [nw][64] cached row limbs
+    uint32_t* part4 = lds + 64 * MSM_MAX_WINDOWS;  // [4][64] partial sums X | Y | Z | T
+    uint32_t* cq4 = part4 + 256;                 // [3][64] cached row limbs of partials 1..3
+    uint32_t* sc = cq4 + 192;                    // [4][192] multiply scratch, one per wave
+    const int nw = lay.nw;
+    if (t < 4 * nw) {
+        const ge_p3 x = load_p3(a.wsc + (size_t)P3_WORDS * (t >> 2));
+        const int c = t & 3;
+        fe v = c == 0 ? fe_add(x.Y, x.X) : c == 1 ? fe_sub(x.Y, x.X) : c == 2 ? fe_mul(x.T, fe_d2()) : fe_add(x.Z, x.Z);
+        fe_to_limbs16(fe_carry(v), cq + 64 * (t >> 2) + 16 * c);
     }
+    __syncthreads();
+    {
+        const int q = t >> 6;  // wave
+        const int cnt = q < nw ? (nw - 1 - q) / 4 + 1 : 0;
+        rowf::row_sum_cached(cq, q, 4, cnt, part4 + 64 * q, sc + 192 * q);
+    }
+    __syncthreads();
+    if (t >= 4 && t < 16) {  // partials 1..3 -> cached row limbs (lane-local conversion)
+        const int q = t >> 2, c = t & 3;
+        const fe X = fe_from_limbs16(part4 + 64 * q), Y = fe_from_limbs16(part4 + 64 * q + 16),
+                 Z = fe_from_limbs16(part4 + 64 * q + 32), T = fe_from_limbs16(part4 + 64 * q + 48);
+        fe v = c == 0 ? fe_add(Y, X) : c == 1 ? fe_sub(Y, X) : c == 2 ? fe_mul(T, fe_d2()) : fe_add(Z, Z);
+        fe_to_limbs16(fe_carry(v), cq4 + 64 * (q - 1) + 16 * c);
+    }
+    __syncthreads();
+    if (t < 64) rowf::row_add_cached_n(part4, cq4, 3, part4, sc);  // partial 0 + partials 1..3
+    __syncthreads();
     if (t == 0) {
-        const bool ok = fe_is_zero(x.X) && fe_eq(x.Y, x.Z) && *a.fail == 0;
+        const fe X = fe_from_limbs16(part4), Y = fe_from_limbs16(part4 + 16), Z = fe_from_limbs16(part4 + 32);
+        const bool ok = fe_is_zero(X) && fe_eq(Y, Z) && *a.fail == 0;
         *a.verdict = ok ? 1u : 0u;
     }
     NWV_TAIL_STAMP(6);

@@ -373,7 +373,7 @@ MsmPlan msm_plan(size_t n, size_t na) {
     p.chunks = (uint32_t)((p.np + p.chunk_pts - 1) / p.chunk_pts);
     p.nkeys = p.lay.kbase[p.lay.nw];
     p.cnt_len = (uint64_t)p.nkeys * p.chunks;
-    p.ntiles = (uint32_t)((p.cnt_len + 4095) / 4096);
+    p.ntiles = (uint32_t)((p.nkeys + 4095) / 4096);  // the scan runs over the bucket totals
     p.max_entries = (uint64_t)(na + 1) * p.lay.nw + (uint64_t)n * p.lay.nw_z;
     // ~2 waves per SIMD of bucket lanes (256 CUs x 4 SIMDs x 2 x 64), 8..64 entries each
     p.seg = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, p.max_entries / (256 * 4 * 2 * 64)));
@@ -473,16 +473,20 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     hipLaunchKernelGGL(k_msm_hist, gsort, dim3(256), lds_nb, stream, (uint64_t)n, (uint64_t)na, p.lay, p.chunk_pts,
                        digits, cnt);
     if ((rc = mark(4))) return rc;
+    // bucket totals -> their exclusive scan in place (kstart: bucket starts, tiles[ntiles] = total
+    // entries) -> slice offsets of every (bucket, chunk) in place of the counts
+    uint32_t* kst = b.m_kstart.as<uint32_t>();
+    const unsigned kgrid = (unsigned)((p.nkeys + 255) / 256);
+    hipLaunchKernelGGL(k_cnt_colsum, dim3(kgrid), dim3(256), 0, stream, p.lay, p.chunks, cnt, kst);
     if (p.ntiles == 1) {  // one tile: the tile scan finishes the whole scan (two launches fewer)
-        hipLaunchKernelGGL(k_scan_tile, dim3(1), dim3(256), 0, stream, p.cnt_len, cnt, tiles, p.chunks,
-                           b.m_kstart.as<uint32_t>());
+        hipLaunchKernelGGL(k_scan_tile, dim3(1), dim3(256), 0, stream, (uint64_t)p.nkeys, kst, tiles, 1u, kst);
     } else {
-        hipLaunchKernelGGL(k_scan_tile, dim3(p.ntiles), dim3(256), 0, stream, p.cnt_len, cnt, tiles, p.chunks,
+        hipLaunchKernelGGL(k_scan_tile, dim3(p.ntiles), dim3(256), 0, stream, (uint64_t)p.nkeys, kst, tiles, 1u,
                            (uint32_t*)nullptr);
         hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, stream, p.ntiles, tiles);
-        hipLaunchKernelGGL(k_scan_add, dim3((unsigned)((p.cnt_len + 255) / 256)), dim3(256), 0, stream,
-                           p.cnt_len, cnt, tiles, p.chunks, b.m_kstart.as<uint32_t>());
+        hipLaunchKernelGGL(k_scan_add, dim3(kgrid), dim3(256), 0, stream, (uint64_t)p.nkeys, kst, tiles, 1u, kst);
     }
+    hipLaunchKernelGGL(k_cnt_offsets, dim3(kgrid), dim3(256), 0, stream, p.lay, p.chunks, cnt, kst);
     if ((rc = mark(5))) return rc;
     hipLaunchKernelGGL(k_msm_scatter, gsort, dim3(256), lds_nb, stream, (uint64_t)n, (uint64_t)na, p.lay,
                        p.chunk_pts, digits, cnt, b.m_entries.as<uint32_t>());
@@ -490,8 +494,8 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     hipLaunchKernelGGL(k_msm_bucket, dim3((unsigned)((p.nseg + 255) / 256)), dim3(256), 0, stream, p.seg,
                        p.nkeys, tiles + p.ntiles, b.m_entries.as<uint32_t>(), b.m_kstart.as<uint32_t>(),
                        b.m_pts.as<uint32_t>(), b.m_bsum.as<uint32_t>(), b.m_hpart.as<uint32_t>());
-    hipLaunchKernelGGL(k_msm_fixup, dim3((p.nkeys + 255) / 256), dim3(256), 0, stream, p.nkeys, p.chunks,
-                       p.seg, cnt, tiles + p.ntiles, b.m_hpart.as<uint32_t>(), b.m_bsum.as<uint32_t>());
+    hipLaunchKernelGGL(k_msm_fixup, dim3((p.nkeys + 255) / 256), dim3(256), 0, stream, p.nkeys,
+                       p.seg, kst, tiles + p.ntiles, b.m_hpart.as<uint32_t>(), b.m_bsum.as<uint32_t>());
     if ((rc = mark(7))) return rc;
     // window sums, their scaling and the verdict: one launch (its arrival counters are zeroed by
     // a memset node first, graph replays included)
@@ -789,6 +793,12 @@ struct nwv_staged {
     bool pending_timing = false;
     hipGraphExec_t graph = nullptr;  // captured batch MSM (mode 1)
     bool graph_failed = false;
+    // per-run coefficient seeds go to the device from a ring of pinned slots, so a graph replay is
+    // two truly asynchronous calls (a pageable copy may wait for the stream)
+    static constexpr int SEED_SLOTS = 64;
+    PinnedBuf seeds;
+    hipEvent_t seed_ev[SEED_SLOTS] = {};
+    uint64_t seed_runs = 0;
 };
 
 // Shard [0, n) into contiguous, 64-aligned ranges over the context's devices and run fn(dev,
@@ -913,24 +923,36 @@ static size_t msm_min_n() {
     return v;
 }
 
+// OS entropy for the batch coefficients, as the reference's OsRng / thread_rng: a per-thread
+// ChaCha20 generator keyed by getrandom(2) (rekeyed every 2^20 seeds) -- a getrandom call per
+// batch cost ~20 us of host time per launch here, std::random_device more
+static void os_entropy(uint8_t* out, size_t len) {
+    size_t got = 0;
+    while (got < len) {
+        const ssize_t r = getrandom(out + got, len - got, 0);
+        if (r > 0) {
+            got += (size_t)r;
+        } else if (r < 0 && errno != EINTR) {
+            std::random_device rd;  // fallback only if the syscall is unavailable
+            for (size_t i = got; i < len; i++) out[i] = (uint8_t)rd();
+            got = len;
+        }
+    }
+}
+
 static void fill_seed(const uint8_t* seed32, uint8_t out[32]) {
     if (seed32) {
         std::memcpy(out, seed32, 32);
         return;
     }
-    // OS entropy, as the reference's OsRng: one getrandom(2) call (std::random_device costs
-    // ~20 us per 4 bytes here, which showed up as host-side launch latency of every batch)
-    size_t got = 0;
-    while (got < 32) {
-        const ssize_t r = getrandom(out + got, 32 - got, 0);
-        if (r > 0) {
-            got += (size_t)r;
-        } else if (r < 0 && errno != EINTR) {
-            std::random_device rd;  // fallback only if the syscall is unavailable
-            for (size_t i = got; i < 32; i++) out[i] = (uint8_t)rd();
-            got = 32;
-        }
-    }
+    thread_local uint32_t key[8];
+    thread_local uint64_t ctr = 0;
+    if ((ctr & ((1u << 20) - 1)) == 0) os_entropy(reinterpret_cast<uint8_t*>(key), sizeof(key));
+    const uint32_t nonce[3] = {(uint32_t)(ctr >> 32), 0x2d76776eu /* "nwv-" */, 0x64656573u /* "seed" */};
+    uint32_t blk[16];
+    nwv::chacha20_block(key, (uint32_t)ctr, nonce, blk);
+    ctr++;
+    std::memcpy(out, blk, 32);
 }
 
 static void set_ones(uint64_t* bits, size_t lo, size_t hi) {
@@ -1244,7 +1266,14 @@ int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]) {
         uint8_t seed[32];
         fill_seed(seed32, seed);
         if (!timed && st->graph) {
-            NWV_HIP(hipMemcpyAsync(st->buf.m_state.as<uint32_t>() + 8, seed, 32, hipMemcpyHostToDevice, st->stream));
+            const int slot = (int)(st->seed_runs++ % nwv_staged::SEED_SLOTS);
+            if ((rc = st->seeds.ensure(32 * nwv_staged::SEED_SLOTS))) return rc;
+            if (!st->seed_ev[slot]) NWV_HIP(hipEventCreateWithFlags(&st->seed_ev[slot], hipEventDisableTiming));
+            else NWV_HIP(hipEventSynchronize(st->seed_ev[slot]));  // the slot's copy of 64 runs ago
+            uint8_t* hs = static_cast<uint8_t*>(st->seeds.p) + 32 * slot;
+            std::memcpy(hs, seed, 32);
+            NWV_HIP(hipMemcpyAsync(st->buf.m_state.as<uint32_t>() + 8, hs, 32, hipMemcpyHostToDevice, st->stream));
+            NWV_HIP(hipEventRecord(st->seed_ev[slot], st->stream));
             NWV_HIP(hipGraphLaunch(st->graph, st->stream));
         } else {
             // first run of the batch (allocates its buffers) or a timed run; an untimed first run
@@ -1368,6 +1397,9 @@ void nwv_staged_free(nwv_staged* st) {
         (void)hipSetDevice(st->own.ordinal);
         if (st->stream) (void)hipStreamSynchronize(st->stream);
         if (st->graph) (void)hipGraphExecDestroy(st->graph);
+        for (auto& e : st->seed_ev)
+            if (e) (void)hipEventDestroy(e);
+        st->seeds.release();
         st->buf.release();
         for (auto& e : st->ev)
             if (e) (void)hipEventDestroy(e);

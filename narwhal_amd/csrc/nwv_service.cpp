@@ -1,0 +1,352 @@
+// nwv_service.cpp -- batching verification service (include/nwv_service.h).
+//
+// Submitters (any threads) enqueue deep copies of headers / votes / certificates; flusher threads
+// coalesce what is pending into one nwv_verify_mixed_many call (include/nwv_types.h: one BLAKE2b
+// launch, one batch MSM on the GPU) and complete every item with its own DagError code, in the
+// role of the Core loop's per-message sanitize_* calls (primary/src/core.rs:497-573, loop
+// :614-714).  Plain host C++ over the C ABI; no GPU code here.
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <set>
+#include <thread>
+#include <vector>
+
+#include "../../include/nwv_service.h"
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+// committee (config/src/lib.rs:488-551) owned by the service; items keep the one current at
+// their submission
+struct OwnedCommittee {
+    std::vector<uint8_t> keys;
+    std::vector<uint64_t> stakes;
+    std::vector<uint32_t> n_workers;
+    std::vector<std::vector<uint32_t>> ids;
+    std::vector<const uint32_t*> id_ptr;
+    nwv_committee view{};
+
+    explicit OwnedCommittee(const nwv_committee& c)
+        : keys(c.keys, c.keys + 32 * c.n), stakes(c.stakes, c.stakes + c.n), ids(c.n), id_ptr(c.n, nullptr) {
+        n_workers.assign(c.n, 0);
+        for (size_t i = 0; i < c.n; i++) {
+            const uint32_t k = c.n_workers ? c.n_workers[i] : 0;
+            n_workers[i] = k;
+            if (k && c.worker_ids && c.worker_ids[i]) ids[i].assign(c.worker_ids[i], c.worker_ids[i] + k);
+            id_ptr[i] = ids[i].empty() ? nullptr : ids[i].data();
+        }
+        view = nwv_committee{c.n, keys.data(), stakes.data(), c.epoch, n_workers.data(), id_ptr.data()};
+    }
+};
+
+enum Kind { HEADER = 0, VOTE = 1, CERT = 2 };
+
+// one submitted message, deep-copied: the views point into bytes / words
+struct Item {
+    Kind kind;
+    std::vector<uint8_t> bytes;
+    std::vector<uint32_t> words;
+    nwv_header h{};
+    nwv_vote v{};
+    nwv_certificate c{};
+    nwv_done_fn done = nullptr;
+    void* user = nullptr;
+    Clock::time_point t;
+    uint64_t seq = 0;
+    std::shared_ptr<const OwnedCommittee> com;
+};
+
+size_t header_bytes(const nwv_header& h) { return 32 + 32 * h.n_payload + 32 * h.n_parents + 32 + 64; }
+
+// copies h into it->bytes / words starting at byte `at` / word `wat`; it->h views the copy
+void copy_header(Item* it, const nwv_header& h, size_t at, size_t wat, nwv_header& out) {
+    uint8_t* b = it->bytes.data() + at;
+    auto put = [&](const uint8_t* src, size_t n) {
+        if (n && src) std::memcpy(b, src, n);
+        else if (n) std::memset(b, 0, n);
+        const uint8_t* r = b;
+        b += n;
+        return r;
+    };
+    out = h;
+    out.author = put(h.author, 32);
+    out.payload_digests = put(h.payload_digests, 32 * h.n_payload);
+    out.parents = put(h.parents, 32 * h.n_parents);
+    out.id = put(h.id, 32);
+    out.signature = put(h.signature, 64);
+    uint32_t* w = it->words.data() + wat;
+    if (h.n_payload && h.payload_workers) std::memcpy(w, h.payload_workers, 4 * h.n_payload);
+    out.payload_workers = h.n_payload ? w : nullptr;
+    if (!h.n_payload) out.payload_digests = nullptr;
+    if (!h.n_parents) out.parents = nullptr;
+}
+
+bool header_ok(const nwv_header* h) {
+    return h && h->author && h->id && h->signature && (!h->n_payload || (h->payload_digests && h->payload_workers)) &&
+           (!h->n_parents || h->parents);
+}
+
+struct Waiter {
+    std::mutex m;
+    std::condition_variable cv;
+    bool done = false;
+    int32_t r = 0;
+};
+void waiter_done(void* user, int32_t r) {
+    auto* w = static_cast<Waiter*>(user);
+    {
+        std::lock_guard<std::mutex> g(w->m);
+        w->r = r;
+        w->done = true;
+    }
+    w->cv.notify_one();
+}
+
+template <class Submit>
+int verify_blocking(Submit submit, int32_t* result) {
+    if (!result) return NWV_ERR_ARG;
+    Waiter w;
+    const int rc = submit(&w);
+    if (rc) return rc;
+    std::unique_lock<std::mutex> lk(w.m);
+    w.cv.wait(lk, [&] { return w.done; });
+    *result = w.r;
+    return w.r < 0 ? w.r : NWV_OK;
+}
+
+}  // namespace
+
+struct nwv_service {
+    nwv_ctx* ctx = nullptr;
+    size_t max_batch = 1;
+    std::chrono::microseconds max_wait{0};
+    std::mutex mu;
+    std::condition_variable cv_work, cv_done;
+    std::deque<std::unique_ptr<Item>> pending;
+    std::set<uint64_t> open;  // sequence numbers submitted and not yet completed
+    std::shared_ptr<const OwnedCommittee> com;
+    uint64_t next_seq = 0, flush_upto = 0;
+    bool stop = false;
+    uint64_t stats[6] = {0, 0, 0, 0, 0, 0};
+    std::vector<std::thread> workers;
+
+    void run();
+    int submit(std::unique_ptr<Item> it, nwv_done_fn done, void* user);
+};
+
+// flusher: waits for a full batch, the oldest item's deadline, a flush request or stop; takes the
+// pending items that share the front item's committee; verifies them in one engine call
+void nwv_service::run() {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+        if (pending.empty()) {
+            if (stop) return;
+            cv_work.wait(lk);
+            continue;
+        }
+        const Item& front = *pending.front();
+        int reason = -1;
+        if (pending.size() >= max_batch) reason = 3;
+        else if (stop || flush_upto > front.seq) reason = 5;
+        else if (Clock::now() >= front.t + max_wait) reason = 4;
+        if (reason < 0) {
+            cv_work.wait_until(lk, front.t + max_wait);
+            continue;
+        }
+        // take up to 8 batches' worth: under a backlog one larger call beats several small ones
+        std::vector<std::unique_ptr<Item>> batch;
+        const auto com_b = pending.front()->com;
+        while (!pending.empty() && batch.size() < 8 * max_batch && pending.front()->com == com_b) {
+            batch.push_back(std::move(pending.front()));
+            pending.pop_front();
+        }
+        if (!pending.empty()) cv_work.notify_one();  // the rest may be another flusher's
+        lk.unlock();
+        std::vector<nwv_header> H;
+        std::vector<nwv_vote> V;
+        std::vector<nwv_certificate> C;
+        for (auto& it : batch) {
+            if (it->kind == HEADER) H.push_back(it->h);
+            else if (it->kind == VOTE) V.push_back(it->v);
+            else C.push_back(it->c);
+        }
+        std::vector<int32_t> rh(H.size()), rv(V.size()), rc(C.size());
+        const int rc_call = nwv_verify_mixed_many(ctx, &com_b->view, H.size(), H.data(), rh.data(), V.size(),
+                                                  V.data(), rv.data(), C.size(), C.data(), rc.data());
+        size_t ih = 0, iv = 0, ic = 0;
+        for (auto& it : batch) {
+            int32_t r = rc_call;
+            if (rc_call == 0) r = it->kind == HEADER ? rh[ih++] : it->kind == VOTE ? rv[iv++] : rc[ic++];
+            if (it->done) it->done(it->user, r);
+        }
+        lk.lock();
+        for (auto& it : batch) open.erase(it->seq);
+        stats[0]++;
+        stats[1] += batch.size();
+        stats[2] = std::max<uint64_t>(stats[2], batch.size());
+        stats[reason]++;
+        cv_done.notify_all();
+    }
+}
+
+int nwv_service::submit(std::unique_ptr<Item> it, nwv_done_fn done, void* user) {
+    it->done = done;
+    it->user = user;
+    std::lock_guard<std::mutex> g(mu);
+    if (stop) return NWV_ERR_ARG;
+    it->com = com;
+    it->seq = next_seq++;
+    it->t = Clock::now();
+    open.insert(it->seq);
+    pending.push_back(std::move(it));
+    if (pending.size() == 1 || pending.size() >= max_batch) cv_work.notify_one();
+    return NWV_OK;
+}
+
+extern "C" {
+
+int nwv_service_create(nwv_ctx* ctx, const nwv_committee* committee, size_t max_batch, uint32_t max_wait_us,
+                       nwv_service** out) {
+    if (!out) return NWV_ERR_ARG;
+    *out = nullptr;
+    if (!ctx || !committee || !committee->keys || !committee->stakes || max_batch == 0) return NWV_ERR_ARG;
+    auto* s = new (std::nothrow) nwv_service;
+    if (!s) return NWV_ERR_OOM;
+    try {
+        s->ctx = ctx;
+        s->max_batch = max_batch;
+        s->max_wait = std::chrono::microseconds(max_wait_us);
+        s->com = std::make_shared<const OwnedCommittee>(*committee);
+        // two flushers: one builds and verifies a batch while the other's is on the GPU (the
+        // engine's per-device lanes let the calls overlap)
+        for (int k = 0; k < 2; k++) s->workers.emplace_back([s] { s->run(); });
+    } catch (...) {
+        {
+            std::lock_guard<std::mutex> g(s->mu);
+            s->stop = true;
+        }
+        s->cv_work.notify_all();
+        for (auto& t : s->workers) t.join();
+        delete s;
+        return NWV_ERR_OOM;
+    }
+    *out = s;
+    return NWV_OK;
+}
+
+int nwv_service_set_committee(nwv_service* svc, const nwv_committee* committee) {
+    if (!svc || !committee || !committee->keys || !committee->stakes) return NWV_ERR_ARG;
+    try {
+        auto c = std::make_shared<const OwnedCommittee>(*committee);
+        std::lock_guard<std::mutex> g(svc->mu);
+        svc->com = std::move(c);
+    } catch (...) {
+        return NWV_ERR_OOM;
+    }
+    return NWV_OK;
+}
+
+int nwv_service_submit_header(nwv_service* svc, const nwv_header* h, nwv_done_fn done, void* user) {
+    if (!svc || !header_ok(h)) return NWV_ERR_ARG;
+    try {
+        auto it = std::make_unique<Item>();
+        it->kind = HEADER;
+        it->bytes.resize(header_bytes(*h));
+        it->words.resize(h->n_payload);
+        copy_header(it.get(), *h, 0, 0, it->h);
+        return svc->submit(std::move(it), done, user);
+    } catch (...) {
+        return NWV_ERR_OOM;
+    }
+}
+
+int nwv_service_submit_vote(nwv_service* svc, const nwv_vote* v, nwv_done_fn done, void* user) {
+    if (!svc || !v || !v->id || !v->origin || !v->author || !v->signature) return NWV_ERR_ARG;
+    try {
+        auto it = std::make_unique<Item>();
+        it->kind = VOTE;
+        it->bytes.resize(32 * 3 + 64);
+        uint8_t* b = it->bytes.data();
+        std::memcpy(b, v->id, 32);
+        std::memcpy(b + 32, v->origin, 32);
+        std::memcpy(b + 64, v->author, 32);
+        std::memcpy(b + 96, v->signature, 64);
+        it->v = nwv_vote{b, v->round, v->epoch, b + 32, b + 64, b + 96};
+        return svc->submit(std::move(it), done, user);
+    } catch (...) {
+        return NWV_ERR_OOM;
+    }
+}
+
+int nwv_service_submit_certificate(nwv_service* svc, const nwv_certificate* c, nwv_done_fn done, void* user) {
+    if (!svc || !c || !header_ok(&c->header) || (c->n_signed && !c->signed_authorities) ||
+        (c->n_sigs && !c->aggregated_signature))
+        return NWV_ERR_ARG;
+    try {
+        auto it = std::make_unique<Item>();
+        it->kind = CERT;
+        const size_t hb = header_bytes(c->header);
+        it->bytes.resize(hb + 64 * c->n_sigs);
+        it->words.resize(c->header.n_payload + c->n_signed);
+        copy_header(it.get(), c->header, 0, 0, it->c.header);
+        uint32_t* sa = it->words.data() + c->header.n_payload;
+        if (c->n_signed) std::memcpy(sa, c->signed_authorities, 4 * c->n_signed);
+        uint8_t* sg = it->bytes.data() + hb;
+        if (c->n_sigs) std::memcpy(sg, c->aggregated_signature, 64 * c->n_sigs);
+        it->c.n_signed = c->n_signed;
+        it->c.signed_authorities = c->n_signed ? sa : nullptr;
+        it->c.n_sigs = c->n_sigs;
+        it->c.aggregated_signature = c->n_sigs ? sg : nullptr;
+        return svc->submit(std::move(it), done, user);
+    } catch (...) {
+        return NWV_ERR_OOM;
+    }
+}
+
+int nwv_service_verify_header(nwv_service* svc, const nwv_header* h, int32_t* result) {
+    return verify_blocking([&](Waiter* w) { return nwv_service_submit_header(svc, h, waiter_done, w); }, result);
+}
+int nwv_service_verify_vote(nwv_service* svc, const nwv_vote* v, int32_t* result) {
+    return verify_blocking([&](Waiter* w) { return nwv_service_submit_vote(svc, v, waiter_done, w); }, result);
+}
+int nwv_service_verify_certificate(nwv_service* svc, const nwv_certificate* c, int32_t* result) {
+    return verify_blocking([&](Waiter* w) { return nwv_service_submit_certificate(svc, c, waiter_done, w); },
+                           result);
+}
+
+int nwv_service_flush(nwv_service* svc) {
+    if (!svc) return NWV_ERR_ARG;
+    std::unique_lock<std::mutex> lk(svc->mu);
+    const uint64_t upto = svc->next_seq;
+    svc->flush_upto = std::max(svc->flush_upto, upto);
+    svc->cv_work.notify_all();
+    svc->cv_done.wait(lk, [&] { return svc->open.empty() || *svc->open.begin() >= upto; });
+    return NWV_OK;
+}
+
+int nwv_service_stats(nwv_service* svc, uint64_t out[6]) {
+    if (!svc || !out) return NWV_ERR_ARG;
+    std::lock_guard<std::mutex> g(svc->mu);
+    std::memcpy(out, svc->stats, sizeof(svc->stats));
+    return NWV_OK;
+}
+
+void nwv_service_free(nwv_service* svc) {
+    if (!svc) return;
+    {
+        std::lock_guard<std::mutex> g(svc->mu);
+        svc->stop = true;
+    }
+    svc->cv_work.notify_all();
+    for (auto& t : svc->workers) t.join();
+    delete svc;
+}
+
+}  // extern "C"

@@ -1,0 +1,138 @@
+"""Batching verification service (include/nwv_service.h) over ctypes.
+
+Python view of the in-library coalescer in front of Core::sanitize_header / sanitize_vote /
+sanitize_certificate (primary/src/core.rs:497-573): threads call verify_header / verify_vote /
+verify_certificate (blocking; the GIL is released while waiting) or submit_* with a callback; the
+library's flusher threads verify whatever is pending as ONE nwv_verify_mixed_many call and hand
+each caller its own DagError code (0 = Ok, types/src/error.rs), exactly what Header::verify,
+Vote::verify and Certificate::verify (types/src/primary.rs:150-183, :307-328, :487-537) return.
+"""
+import ctypes
+import itertools
+
+import numpy as np
+
+from . import _lib
+from . import types as T
+
+DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int32)
+
+_SIGS = {
+    "nwv_service_create": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
+                            ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "nwv_service_set_committee": ([ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "nwv_service_submit_header": ([ctypes.c_void_p, ctypes.c_void_p, DONE_FN, ctypes.c_void_p], ctypes.c_int),
+    "nwv_service_submit_vote": ([ctypes.c_void_p, ctypes.c_void_p, DONE_FN, ctypes.c_void_p], ctypes.c_int),
+    "nwv_service_submit_certificate": ([ctypes.c_void_p, ctypes.c_void_p, DONE_FN, ctypes.c_void_p], ctypes.c_int),
+    "nwv_service_verify_header": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+    "nwv_service_verify_vote": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+    "nwv_service_verify_certificate": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)],
+                                       ctypes.c_int),
+    "nwv_service_flush": ([ctypes.c_void_p], ctypes.c_int),
+    "nwv_service_stats": ([ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "nwv_service_free": ([ctypes.c_void_p], None),
+}
+
+
+def bind(lib):
+    """declare the service entry points on a loaded library (libnwv.so, or the CPU test stub)"""
+    if not getattr(lib, "_service_bound", False):
+        for name, (args, res) in _SIGS.items():
+            f = getattr(lib, name)
+            f.argtypes = args
+            f.restype = res
+        lib._service_bound = True
+    return lib
+
+
+class Service:
+    """One batching service over an Engine's context (or any nwv_ctx handle with lib)."""
+
+    def __init__(self, engine, committee, max_batch=256, max_wait_us=200, lib=None, ctx=None):
+        self.lib = bind(lib if lib is not None else _lib.load())
+        self._keep = T._Keep()
+        cc = committee._c(self._keep)
+        h = ctypes.c_void_p()
+        rc = self.lib.nwv_service_create(ctx if ctx is not None else engine._h, ctypes.byref(cc), max_batch,
+                                         max_wait_us, ctypes.byref(h))
+        if rc:
+            raise _lib.NwvError(rc, "nwv_service_create")
+        self._h = h
+        self._callbacks = {}
+        self._keys = itertools.count()
+
+    def close(self):
+        if self._h:
+            self.lib.nwv_service_free(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_committee(self, committee):
+        keep = T._Keep()
+        cc = committee._c(keep)
+        rc = self.lib.nwv_service_set_committee(self._h, ctypes.byref(cc))
+        if rc:
+            raise _lib.NwvError(rc, "nwv_service_set_committee")
+
+    # blocking forms: the DagError code of the item (the structs are copied by the library)
+    def _verify(self, fn, st):
+        r = ctypes.c_int32(0)
+        rc = fn(self._h, ctypes.byref(st), ctypes.byref(r))
+        if rc < 0:
+            raise _lib.NwvError(rc, "service verify")
+        return r.value
+
+    def verify_header(self, header):
+        keep = T._Keep()
+        return self._verify(self.lib.nwv_service_verify_header, header._c(keep))
+
+    def verify_vote(self, vote):
+        keep = T._Keep()
+        return self._verify(self.lib.nwv_service_verify_vote, vote._c(keep))
+
+    def verify_certificate(self, cert):
+        keep = T._Keep()
+        return self._verify(self.lib.nwv_service_verify_certificate, cert._c(keep))
+
+    # asynchronous forms: done(code) runs on a service thread
+    def _submit(self, fn, st, done):
+        key = next(self._keys)
+
+        def cb(_user, code, key=key):
+            f = self._callbacks.pop(key)
+            done(code)
+            del f
+
+        c = DONE_FN(cb)
+        self._callbacks[key] = c
+        rc = fn(self._h, ctypes.byref(st), c, None)
+        if rc:
+            self._callbacks.pop(key, None)
+            raise _lib.NwvError(rc, "service submit")
+
+    def submit_header(self, header, done):
+        keep = T._Keep()
+        self._submit(self.lib.nwv_service_submit_header, header._c(keep), done)
+
+    def submit_vote(self, vote, done):
+        keep = T._Keep()
+        self._submit(self.lib.nwv_service_submit_vote, vote._c(keep), done)
+
+    def submit_certificate(self, cert, done):
+        keep = T._Keep()
+        self._submit(self.lib.nwv_service_submit_certificate, cert._c(keep), done)
+
+    def flush(self):
+        _lib._check(self.lib.nwv_service_flush(self._h))
+
+    def stats(self):
+        out = np.zeros(6, dtype=np.uint64)
+        _lib._check(self.lib.nwv_service_stats(self._h, out.ctypes.data))
+        keys = ("calls", "items", "max_batch", "by_count", "by_deadline", "by_flush")
+        return {k: int(v) for k, v in zip(keys, out)}
+

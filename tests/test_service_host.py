@@ -1,0 +1,182 @@
+"""The batching service's host logic (narwhal_amd/csrc/nwv_service.cpp) on the
+CPU, over a stand-in engine (tests/hostemu/service_stub.cpp: epoch mismatch -> InvalidEpoch,
+signature byte 0 = 0xFF -> InvalidSignature, else Ok).  Checks that concurrent submitters each
+get their own item's code, that items are coalesced into few engine calls, the max_batch /
+max_wait_us / flush triggers, committee replacement (items keep the committee current at their
+submission), engine errors reaching every submitter, and draining on free."""
+import ctypes
+import os
+import random
+import threading
+import time
+
+import pytest
+
+from narwhal_amd import service as S
+from narwhal_amd import types as T
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    path = os.path.join(ROOT, "tests", "_build", "libsvcstub.so")
+    if not os.path.exists(path):
+        import subprocess
+        subprocess.run(["make", "-C", ROOT, "tests/_build/libsvcstub.so"], check=True)
+    lib_ = ctypes.CDLL(path)
+    lib_.stub_reset.argtypes = [ctypes.c_long, ctypes.c_long]
+    lib_.stub_counts.argtypes = [ctypes.c_void_p]
+    return S.bind(lib_)
+
+
+def _committee(epoch=0, n=4):
+    keys = sorted(bytes([i + 1]) * 32 for i in range(n))
+    return T.Committee(keys, [1] * n, epoch, [[0, 1]] * n)
+
+
+def _header(rnd, epoch, bad):
+    sig = bytes([0xFF if bad else 1]) + rnd.randbytes(63)
+    return T.Header(rnd.randbytes(32), 1, epoch, [(rnd.randbytes(32), 0)], [rnd.randbytes(32) for _ in range(3)],
+                    rnd.randbytes(32), sig)
+
+
+def _vote(rnd, epoch, bad):
+    sig = bytes([0xFF if bad else 2]) + rnd.randbytes(63)
+    return T.Vote(rnd.randbytes(32), 1, epoch, rnd.randbytes(32), rnd.randbytes(32), sig)
+
+
+def _cert(rnd, epoch, bad):
+    c = T.Certificate(_header(rnd, epoch, bad))
+    c.signed_authorities = [0, 1, 2]
+    c.aggregated_signature = [rnd.randbytes(64) for _ in range(3)]
+    return c
+
+
+def _counts(lib):
+    import numpy as np
+    out = np.zeros(3, dtype=np.int64)
+    lib.stub_counts(out.ctypes.data)
+    return [int(x) for x in out]
+
+
+def _expect(item, epoch):
+    sig = item.header.signature if isinstance(item, T.Certificate) else item.signature
+    ep = item.header.epoch if isinstance(item, T.Certificate) else item.epoch
+    if ep != epoch:
+        return T.InvalidEpoch.code
+    return T.InvalidSignature.code if sig[0] == 0xFF else 0
+
+
+def _verify(svc, item):
+    if isinstance(item, T.Header):
+        return svc.verify_header(item)
+    if isinstance(item, T.Vote):
+        return svc.verify_vote(item)
+    return svc.verify_certificate(item)
+
+
+def test_concurrent_submitters_get_their_own_codes_and_are_coalesced(lib):
+    lib.stub_reset(2000, 0)  # each engine call takes 2 ms: submitters pile up behind it
+    rnd = random.Random(1)
+    items = []
+    for k in range(600):
+        make = (_header, _vote, _cert)[k % 3]
+        items.append(make(rnd, 0 if k % 7 else 1, k % 5 == 0))
+    got = [None] * len(items)
+    svc = S.Service(None, _committee(0), max_batch=64, max_wait_us=500, lib=lib, ctx=ctypes.c_void_p(1))
+    try:
+        def worker(t):
+            for i in range(t, len(items), 12):
+                got[i] = _verify(svc, items[i])
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(12)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        st = svc.stats()
+    finally:
+        svc.close()
+    assert got == [_expect(it, 0) for it in items]
+    calls, n_items, largest = _counts(lib)
+    assert n_items == len(items) == st["items"]
+    # 12 blocking submitters keep at most 12 items pending: coalesced about 4-12 per engine call
+    assert calls == st["calls"] < len(items) // 2, (calls, st)
+    assert largest > 1
+
+
+def test_max_batch_and_deadline_triggers(lib):
+    lib.stub_reset(0, 0)
+    rnd = random.Random(2)
+    svc = S.Service(None, _committee(0), max_batch=8, max_wait_us=50_000, lib=lib, ctx=ctypes.c_void_p(1))
+    try:
+        done = []
+        ev = threading.Event()
+
+        def cb(code):
+            done.append(code)
+            if len(done) == 8:
+                ev.set()
+
+        t0 = time.perf_counter()
+        for _ in range(8):
+            svc.submit_vote(_vote(rnd, 0, False), cb)
+        assert ev.wait(5) and time.perf_counter() - t0 < 0.04  # a full batch goes at once
+        assert svc.stats()["by_count"] >= 1
+        one = threading.Event()
+        t0 = time.perf_counter()
+        svc.submit_header(_header(rnd, 0, True), lambda c: (done.append(c), one.set()))
+        assert one.wait(5)
+        waited = time.perf_counter() - t0
+        assert 0.04 < waited < 2.0  # a lone item waits for its deadline
+        assert done[-1] == T.InvalidSignature.code
+        assert svc.stats()["by_deadline"] >= 1
+    finally:
+        svc.close()
+
+
+def test_flush_completes_everything_submitted_before(lib):
+    lib.stub_reset(0, 0)
+    rnd = random.Random(3)
+    svc = S.Service(None, _committee(0), max_batch=1000, max_wait_us=10_000_000, lib=lib, ctx=ctypes.c_void_p(1))
+    try:
+        codes = []
+        for k in range(10):
+            svc.submit_certificate(_cert(rnd, 0, k == 3), codes.append)
+        svc.flush()
+        assert sorted(codes) == [0] * 9 + [T.InvalidSignature.code]
+        assert svc.stats()["by_flush"] >= 1
+    finally:
+        svc.close()
+
+
+def test_committee_change_applies_to_later_submissions(lib):
+    lib.stub_reset(0, 0)
+    rnd = random.Random(4)
+    svc = S.Service(None, _committee(0), max_batch=1000, max_wait_us=10_000_000, lib=lib, ctx=ctypes.c_void_p(1))
+    try:
+        a, b = [], []
+        for _ in range(5):
+            svc.submit_vote(_vote(rnd, 1, False), a.append)  # epoch 1 under the epoch-0 committee
+        svc.set_committee(_committee(1))
+        for _ in range(5):
+            svc.submit_vote(_vote(rnd, 1, False), b.append)
+        svc.flush()
+        assert a == [T.InvalidEpoch.code] * 5 and b == [0] * 5
+    finally:
+        svc.close()
+
+
+def test_engine_error_reaches_every_submitter_and_free_drains(lib):
+    lib.stub_reset(0, 1)  # the engine call fails
+    rnd = random.Random(5)
+    svc = S.Service(None, _committee(0), max_batch=4, max_wait_us=1000, lib=lib, ctx=ctypes.c_void_p(1))
+    codes = []
+    for _ in range(3):
+        svc.submit_header(_header(rnd, 0, False), codes.append)
+    with pytest.raises(Exception):
+        svc.verify_vote(_vote(rnd, 0, False))
+    lib.stub_reset(0, 0)
+    svc.submit_vote(_vote(rnd, 0, False), codes.append)
+    svc.close()  # drains the pending item first
+    assert codes[:3] == [-2] * 3 and codes[3] == 0

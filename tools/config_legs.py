@@ -218,6 +218,117 @@ def leg_c4(eng, reps=5):
             "sigs_per_s": n / med}, {"items": items, "pos": pos, "bits": bits}
 
 
+def leg_c5_service(eng, com, cc, harr, varr, carr, nsig, threads=16, rounds=20):
+    """C5 through the batching service (include/nwv_service.h): `threads` submitter
+    threads each verify 1/threads of a round's 299 messages one message at a time (as Core's
+    sanitize_* calls would), blocking per message, for `rounds` rounds; the service coalesces
+    them.  Reports per-message latency (submit -> own result) and the round rate, beside the same
+    messages verified one engine call per message on one thread."""
+    import threading
+    from narwhal_amd import service as S
+    lib = S.bind(T.lib())
+    msgs = [(lib.nwv_service_verify_header, harr[i]) for i in range(len(harr))] + \
+           [(lib.nwv_service_verify_vote, varr[i]) for i in range(len(varr))] + \
+           [(lib.nwv_service_verify_certificate, carr[i]) for i in range(len(carr))]
+    out = {"threads": threads, "rounds": rounds, "messages_per_round": len(msgs)}
+    h = ctypes.c_void_p()
+    _lib._check(lib.nwv_service_create(eng._h, ctypes.byref(cc), 256, 200, ctypes.byref(h)))
+    lat = [[] for _ in range(threads)]
+    bad = []
+
+    def worker(t):
+        r = ctypes.c_int32(0)
+        for _ in range(rounds):
+            for fn, st in msgs[t::threads]:
+                t0 = time.perf_counter()
+                rc = fn(h, ctypes.byref(st), ctypes.byref(r))
+                lat[t].append(time.perf_counter() - t0)
+                if rc or r.value:
+                    bad.append((rc, r.value))
+
+    try:
+        worker(0)  # warm up
+        lat[0].clear()
+        t0 = time.perf_counter()
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        dt = time.perf_counter() - t0
+        stats = np.zeros(6, dtype=np.uint64)
+        lib.nwv_service_stats(h, stats.ctypes.data)
+    finally:
+        lib.nwv_service_free(h)
+    assert not bad, bad[:5]
+    a = np.concatenate([np.array(x) for x in lat]) * 1e3
+    out.update({"latency_ms_p50": float(np.percentile(a, 50)), "latency_ms_p99": float(np.percentile(a, 99)),
+                "ms_per_round": dt / rounds * 1e3, "sigs_per_s": nsig * rounds / dt,
+                "engine_calls": int(stats[0]), "items": int(stats[1]), "largest_batch": int(stats[2])})
+    # asynchronous submission: one thread submits a whole round's messages (a Core loop that
+    # hands every message to the service instead of verifying it inline), each completion
+    # callback records its latency; the service coalesces the round into one or two engine calls
+    h2 = ctypes.c_void_p()
+    _lib._check(lib.nwv_service_create(eng._h, ctypes.byref(cc), 512, 200, ctypes.byref(h2)))
+    sub_fns = [lib.nwv_service_submit_header] * len(harr) + [lib.nwv_service_submit_vote] * len(varr) + \
+              [lib.nwv_service_submit_certificate] * len(carr)
+    structs = [harr[i] for i in range(len(harr))] + [varr[i] for i in range(len(varr))] + \
+              [carr[i] for i in range(len(carr))]
+    t_sub = np.zeros(len(structs))
+    t_done = np.zeros(len(structs))
+    codes = np.zeros(len(structs), dtype=np.int32)
+    ev = threading.Event()
+    left = [0]
+    lk = threading.Lock()
+
+    def on_done(user, code):
+        i = user or 0
+        t_done[i] = time.perf_counter()
+        codes[i] = code
+        with lk:
+            left[0] -= 1
+            if left[0] == 0:
+                ev.set()
+
+    cb = S.DONE_FN(on_done)
+    lat2, rtimes = [], []
+    try:
+        for r in range(rounds + 1):
+            ev.clear()
+            left[0] = len(structs)
+            t0 = time.perf_counter()
+            for i, (fn, st) in enumerate(zip(sub_fns, structs)):
+                t_sub[i] = time.perf_counter()
+                _lib._check(fn(h2, ctypes.byref(st), cb, ctypes.c_void_p(i)))
+            ev.wait(30)
+            if r:  # the first round warms up
+                rtimes.append(time.perf_counter() - t0)
+                lat2.append(t_done - t_sub)
+            assert not codes.any()
+        stats2 = np.zeros(6, dtype=np.uint64)
+        lib.nwv_service_stats(h2, stats2.ctypes.data)
+    finally:
+        lib.nwv_service_free(h2)
+    a2 = np.concatenate(lat2) * 1e3
+    out["async_submit"] = {"latency_ms_p50": float(np.percentile(a2, 50)), "latency_ms_p99": float(np.percentile(a2, 99)),
+                           "ms_per_round": float(np.median(rtimes)) * 1e3,
+                           "sigs_per_s": nsig / float(np.median(rtimes)),
+                           "engine_calls": int(stats2[0]), "items": int(stats2[1]), "largest_batch": int(stats2[2])}
+    # the same messages, one engine call per message, serially (the reference's Core loop shape)
+    tl = T.lib()
+    one = []
+    r = ctypes.c_int32(0)
+    for fn_many, arr in ((tl.nwv_header_verify_many, harr), (tl.nwv_vote_verify_many, varr),
+                         (tl.nwv_certificate_verify_many, carr)):
+        for i in range(len(arr)):
+            t1 = time.perf_counter()
+            assert fn_many(eng._h, ctypes.byref(cc), 1, ctypes.byref(arr[i]), ctypes.byref(r)) == 0 and r.value == 0
+            one.append(time.perf_counter() - t1)
+    out["one_call_per_message"] = {"latency_ms_p50": float(np.median(one)) * 1e3,
+                                   "ms_per_round": float(np.sum(one)) * 1e3}
+    return out
+
+
 def leg_c5(eng, rounds=50):
     seeds, keys, com = committee_fixture(eng, 100, b"nwv-bench-c5")
     batches = [worker_batch(a) for a in range(100)]
@@ -268,12 +379,14 @@ def leg_c5(eng, rounds=50):
             t_dig.append(t2 - t1)
             t_mix.append(t4 - t3)
     nsig = sum(1 + len(c.aggregated_signature) for c in certs) + len(headers) + len(vsample)
+    svc = leg_c5_service(eng, com, cc, harr, varr, carr, nsig)
     ms = float(np.median(t_sig)) * 1e3
     return {"rounds": rounds, "signatures_per_round": nsig,
             "verify_ms_per_round": ms, "verify_sigs_per_s": nsig / (ms * 1e-3),
             "verify_coalesced_ms_per_round": float(np.median(t_mix)) * 1e3,
             "verify_coalesced_sigs_per_s": nsig / float(np.median(t_mix)),
             "worker_batch_digests_ms_per_round": float(np.median(t_dig)) * 1e3,
+            "service": svc,
             "note": "one round = validate_certificates(100 certs x (1 + 67) sigs) + 100 Header::verify + "
                     "99 Vote::verify (three C calls on prepared structs, host -> host; 'coalesced': the same round as one "
                     "nwv_verify_mixed_many call) and BLAKE2b-256 of 100 x 500,224 B "
