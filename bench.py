@@ -686,8 +686,15 @@ def main():
     if args.mode == 1:
         na = args.keys or args.n
         per = kernel_rooflines(kt, stats, args.n, na, peak)
-        dom = max(per, key=lambda k: per[k]["kernel_ms"])
-        roof = dict(per[dom], kernel=dom,
+        # the dominant kernel of the THROUGHPUT regime: the most VALU work (issue floor) -- with
+        # batches in flight the latency-bound tail overlaps other batches' work; by single-stream
+        # time when no PMC pass is committed for this size
+        floors = {k: (v.get("issue_floor") or {}).get("floor_ms") for k, v in per.items() if v["bound"] == "valu"}
+        if all(f is not None for f in floors.values()):
+            dom, how = max(floors, key=floors.get), "largest VALU issue floor (committed PMC pass)"
+        else:
+            dom, how = max(per, key=lambda k: per[k]["kernel_ms"]), "longest single-stream kernel time"
+        roof = dict(per[dom], kernel=dom, selected_by=how,
                     kernel_share=per[dom]["kernel_ms"] / sum(kt.values()))
     else:
         kms = kt.get("k_ed_straus", 0.0)
