@@ -160,6 +160,48 @@ NWV_HD bool msm_make_layout2(int c_lo, int c_hi, MsmLayout& L) {
 }
 NWV_HD bool msm_make_layout(int c, MsmLayout& L) { return msm_make_layout2(c, c, L); }
 
+// chunks of chunk_pts points in window w (all na + 1 + n points below nw_z, else na + 1)
+NWV_HD uint32_t msm_window_chunks(uint64_t n, uint64_t na, int w, int nw_z, uint32_t chunk_pts) {
+    const uint64_t cnt = w < nw_z ? na + 1 + n : na + 1;
+    return (uint32_t)((cnt + chunk_pts - 1) / chunk_pts);
+}
+
+// k_msm_scatter's XCD grouping.  Workgroups b and b + 8 share an XCD (MI355X_MICROARCH.md,
+// "Workgroup dispatch"), so group g = blockIdx.x % 8 runs every chunk of the windows win[g][..]:
+// all (bucket, chunk) slices of one window are then written through ONE XCD's L2, which
+// assembles whole lines, instead of up to eight partial write-backs of each line.
+static constexpr int MSM_XCD_GROUPS = 8, MSM_XCD_WIN = 8;
+struct MsmXcdMap {
+    uint32_t slots;  // workgroups per group: grid = MSM_XCD_GROUPS x slots
+    uint8_t nwin[MSM_XCD_GROUPS];
+    uint8_t win[MSM_XCD_GROUPS][MSM_XCD_WIN];
+};
+
+// windows -> groups, largest first onto the least-loaded group (load = chunks)
+NWV_HD void msm_xcd_map(const MsmLayout& L, uint64_t n, uint64_t na, uint32_t chunk_pts, MsmXcdMap& m) {
+    uint32_t load[MSM_XCD_GROUPS];
+    bool done[MSM_MAX_WINDOWS];
+    for (int g = 0; g < MSM_XCD_GROUPS; g++) load[g] = 0, m.nwin[g] = 0;
+    for (int w = 0; w < L.nw; w++) done[w] = false;
+    m.slots = 0;
+    for (int it = 0; it < L.nw; it++) {
+        int wb = -1;
+        uint32_t cb = 0;
+        for (int w = 0; w < L.nw; w++) {
+            const uint32_t c = msm_window_chunks(n, na, w, L.nw_z, chunk_pts);
+            if (!done[w] && (wb < 0 || c > cb)) wb = w, cb = c;
+        }
+        int gb = -1;  // MSM_MAX_WINDOWS <= MSM_XCD_GROUPS * MSM_XCD_WIN: some group has room
+        for (int g = 0; g < MSM_XCD_GROUPS; g++)
+            if (m.nwin[g] < MSM_XCD_WIN && (gb < 0 || load[g] < load[gb])) gb = g;
+        done[wb] = true;
+        m.win[gb][m.nwin[gb]++] = (uint8_t)wb;
+        load[gb] += cb;
+        m.slots = load[gb] > m.slots ? load[gb] : m.slots;
+    }
+}
+static_assert(MSM_MAX_WINDOWS <= MSM_XCD_GROUPS * MSM_XCD_WIN, "every window needs a group slot");
+
 // raw bits [pos, pos + width) of a 256-bit little-endian scalar (width <= 16)
 NWV_HD uint32_t msm_window_bits(const uint32_t s[8], int pos, int width) {
     uint64_t v = 0;

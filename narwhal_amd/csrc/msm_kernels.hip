@@ -321,12 +321,28 @@ extern "C" __global__ void __launch_bounds__(256) k_cnt_offsets(MsmLayout lay, u
     }
 }
 
+// grid MSM_XCD_GROUPS x xm.slots: workgroup b runs chunk s of the windows of group b % 8 (msm.h
+// MsmXcdMap), s counted over those windows in order; chunks = the plan's chunks per window
+// (the stride of the offsets)
 extern "C" __global__ void __launch_bounds__(256) k_msm_scatter(
-    uint64_t n, uint64_t na, MsmLayout lay, uint32_t chunk_pts, const int16_t* __restrict__ digits,
-    const uint32_t* __restrict__ off, uint32_t* __restrict__ entries) {
+    uint64_t n, uint64_t na, MsmLayout lay, MsmXcdMap xm, uint32_t chunks, uint32_t chunk_pts,
+    const int16_t* __restrict__ digits, const uint32_t* __restrict__ off, uint32_t* __restrict__ entries) {
     extern __shared__ uint32_t cur[];
-    const int w = blockIdx.y, nw_z = lay.nw_z, nb = 1 << (lay.width[w] - 1);
-    const uint32_t chunks = gridDim.x, chunk = blockIdx.x;
+    const uint32_t g = blockIdx.x % MSM_XCD_GROUPS;
+    uint32_t s = blockIdx.x / MSM_XCD_GROUPS;
+    int w = -1;
+    for (int k = 0; k < xm.nwin[g]; k++) {
+        const int wk = xm.win[g][k];
+        const uint32_t c = msm_window_chunks(n, na, wk, lay.nw_z, chunk_pts);
+        if (s < c) {
+            w = wk;
+            break;
+        }
+        s -= c;
+    }
+    if (w < 0) return;  // uniform over the workgroup: no barrier reached
+    const int nw_z = lay.nw_z, nb = 1 << (lay.width[w] - 1);
+    const uint32_t chunk = s;
     const uint32_t* mine = off + (uint64_t)lay.kbase[w] * chunks + (uint64_t)chunk * nb;
     for (int b = threadIdx.x; b < nb; b += blockDim.x) cur[b] = mine[b];
     __syncthreads();

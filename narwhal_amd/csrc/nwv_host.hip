@@ -342,6 +342,7 @@ int ed_launch(Lane& d, EdBuffers& b, size_t n, hipStream_t stream, hipEvent_t* e
 // points: n, or the m distinct keys of a keyed batch).
 struct MsmPlan {
     MsmLayout lay{};
+    MsmXcdMap xm{};  // k_msm_scatter's windows per XCD group
     uint32_t chunk_pts = 0, chunks = 0, nkeys = 0, ntiles = 0;
     uint32_t seg = 0;  // entries per k_msm_bucket lane
     uint32_t tail_S = 1;  // k_msm_tail: bucket chunks per window
@@ -371,6 +372,7 @@ MsmPlan msm_plan(size_t n, size_t na) {
         }
     p.chunk_pts = (uint32_t)std::max<uint64_t>(8192, (p.np + 63) / 64);
     p.chunks = (uint32_t)((p.np + p.chunk_pts - 1) / p.chunk_pts);
+    msm_xcd_map(p.lay, n, na, p.chunk_pts, p.xm);
     p.nkeys = p.lay.kbase[p.lay.nw];
     p.cnt_len = (uint64_t)p.nkeys * p.chunks;
     p.ntiles = (uint32_t)((p.nkeys + 4095) / 4096);  // the scan runs over the bucket totals
@@ -488,8 +490,8 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     }
     hipLaunchKernelGGL(k_cnt_offsets, dim3(kgrid), dim3(256), 0, stream, p.lay, p.chunks, cnt, kst);
     if ((rc = mark(5))) return rc;
-    hipLaunchKernelGGL(k_msm_scatter, gsort, dim3(256), lds_nb, stream, (uint64_t)n, (uint64_t)na, p.lay,
-                       p.chunk_pts, digits, cnt, b.m_entries.as<uint32_t>());
+    hipLaunchKernelGGL(k_msm_scatter, dim3(MSM_XCD_GROUPS * p.xm.slots), dim3(256), lds_nb, stream, (uint64_t)n,
+                       (uint64_t)na, p.lay, p.xm, p.chunks, p.chunk_pts, digits, cnt, b.m_entries.as<uint32_t>());
     if ((rc = mark(6))) return rc;
     hipLaunchKernelGGL(k_msm_bucket, dim3((unsigned)((p.nseg + 255) / 256)), dim3(256), 0, stream, p.seg,
                        p.nkeys, tiles + p.ntiles, b.m_entries.as<uint32_t>(), b.m_kstart.as<uint32_t>(),

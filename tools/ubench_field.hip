@@ -1,50 +1,242 @@
-// ubench_field.hip -- throughput of the field squaring / multiplication (fe25519.h) as a function
-// of waves per SIMD and independent chains per lane: how much latency hiding the VALU-bound
-// kernels need (k_msm_points runs 2 waves per SIMD with one chain per lane at 65,536 signatures).
+// ubench_field.hip -- field squaring / multiplication throughput: the 10-limb radix 2^25.5 form
+// the kernels use (fe25519.h) against an 8 x 32-bit-limb form (radix 2^32, x38 fold), as a
+// function of waves per SIMD and independent chains per lane.  VERDICT r1 item 6 / SURVEY.md §7
+// hard part 2: the radix is chosen by this measurement.
+//
+// Radix 2^32 forms measured:
+//   sq8_ps / mul8_ps  product scanning: each column accumulates its 32x32 products in a 96-bit
+//                     (lo64, hi32) register group with v_mad_u64_u32's carry-out added into the
+//                     high word (v_addc_co_u32), squaring doubles the cross-term column once
+//   sq8_os            operand scanning in plain C (x = a_i a_j + t + c fits 64 bits), the form the
+//                     compiler schedules by itself
+// Both reduce the 512-bit product by 2^256 = 38 (mod p) into 8 limbs < 2^32 (value < 2^256,
+// not canonical: the same lazy form the 10-limb code keeps).
+// Output: one JSON line per occupancy, plus {"check": ...} comparing every form's result of a
+// 64-squaring chain with the 10-limb result, canonically.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include "../narwhal_amd/csrc/fe25519.h"
 
 using namespace nwv;
 
-template <int ILP>
-__global__ void __launch_bounds__(256) k_sq(uint32_t* out, int iters) {
-    fe f[ILP];
-#pragma unroll
-    for (int c = 0; c < ILP; c++)
-        for (int i = 0; i < 10; i++) f[c].v[i] = (threadIdx.x * 7 + i * 13 + c) & M25;
-#pragma unroll 1
-    for (int it = 0; it < iters; it++) {
-#pragma unroll
-        for (int c = 0; c < ILP; c++) fe_pin(f[c]);
-#pragma unroll
-        for (int c = 0; c < ILP; c++) f[c] = fe_sq(f[c]);
-    }
-    uint32_t s = 0;
-#pragma unroll
-    for (int c = 0; c < ILP; c++)
-        for (int i = 0; i < 10; i++) s ^= f[c].v[i];
-    if (s == 0x12345u) out[0] = s;
+struct fe8 {
+    uint32_t v[8];
+};
+
+// 96-bit column accumulator (lo, hi) += a * b
+__device__ __forceinline__ void madc(uint64_t& lo, uint32_t& hi, uint32_t a, uint32_t b) {
+    uint64_t nlo;
+    uint32_t nhi;
+    asm("v_mad_u64_u32 %0, vcc, %2, %3, %4\n\t"
+        "v_addc_co_u32 %1, vcc, 0, %5, vcc"
+        : "=&v"(nlo), "=v"(nhi)
+        : "v"(a), "v"(b), "v"(lo), "v"(hi)
+        : "vcc");
+    lo = nlo;
+    hi = nhi;
 }
-template <int ILP>
-__global__ void __launch_bounds__(256) k_mul(uint32_t* out, int iters) {
-    fe f[ILP], g;
-    for (int i = 0; i < 10; i++) g.v[i] = (threadIdx.x * 5 + i * 11) & M25;
+
+// 512-bit t -> 8 limbs of t mod p (value < 2^256)
+__device__ __forceinline__ fe8 fe8_reduce(const uint32_t t[16]) {
+    fe8 r;
+    uint64_t c = 0;
 #pragma unroll
-    for (int c = 0; c < ILP; c++)
-        for (int i = 0; i < 10; i++) f[c].v[i] = (threadIdx.x * 7 + i * 13 + c) & M25;
-#pragma unroll 1
-    for (int it = 0; it < iters; it++) {
-#pragma unroll
-        for (int c = 0; c < ILP; c++) fe_pin(f[c]);
-#pragma unroll
-        for (int c = 0; c < ILP; c++) f[c] = fe_mul(f[c], g);
+    for (int k = 0; k < 8; k++) {
+        const uint64_t x = (uint64_t)t[k + 8] * 38u + t[k] + c;
+        r.v[k] = (uint32_t)x;
+        c = x >> 32;  // < 39
     }
-    uint32_t s = 0;
+    uint64_t x = c * 38u + r.v[0];
+    r.v[0] = (uint32_t)x;
+    c = x >> 32;
 #pragma unroll
-    for (int c = 0; c < ILP; c++)
-        for (int i = 0; i < 10; i++) s ^= f[c].v[i];
-    if (s == 0x12345u) out[0] = s;
+    for (int k = 1; k < 8; k++) {
+        x = (uint64_t)r.v[k] + c;
+        r.v[k] = (uint32_t)x;
+        c = x >> 32;
+    }
+    r.v[0] += (uint32_t)c * 38u;  // c = 1 only after a wrap, when r is tiny: no overflow
+    return r;
+}
+
+__device__ __forceinline__ fe8 fe8_sq_ps(const fe8& a) {
+    uint32_t t[16];
+    uint64_t acc = 0;
+    uint32_t acch = 0;
+#pragma unroll
+    for (int k = 0; k < 15; k++) {
+        uint64_t x = 0;
+        uint32_t xh = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int j = k - i;
+            if (j > i && j < 8) madc(x, xh, a.v[i], a.v[j]);
+        }
+        xh = (xh << 1) | (uint32_t)(x >> 63);
+        x <<= 1;
+        if ((k & 1) == 0 && k / 2 < 8) madc(x, xh, a.v[k / 2], a.v[k / 2]);
+        // acc += (x, xh)
+        const uint64_t s = acc + x;
+        acch += xh + (s < x ? 1u : 0u);
+        t[k] = (uint32_t)s;
+        acc = (s >> 32) | ((uint64_t)acch << 32);
+        acch = 0;
+    }
+    t[15] = (uint32_t)acc;
+    return fe8_reduce(t);
+}
+
+__device__ __forceinline__ fe8 fe8_mul_ps(const fe8& a, const fe8& b) {
+    uint32_t t[16];
+    uint64_t acc = 0;
+    uint32_t acch = 0;
+#pragma unroll
+    for (int k = 0; k < 15; k++) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int j = k - i;
+            if (j >= 0 && j < 8) madc(acc, acch, a.v[i], b.v[j]);
+        }
+        t[k] = (uint32_t)acc;
+        acc = (acc >> 32) | ((uint64_t)acch << 32);
+        acch = 0;
+    }
+    t[15] = (uint32_t)acc;
+    return fe8_reduce(t);
+}
+
+__device__ __forceinline__ fe8 fe8_sq_os(const fe8& a) {
+    uint32_t t[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) t[k] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int j = i + 1; j < 8; j++) {
+            const uint64_t x = (uint64_t)a.v[i] * a.v[j] + t[i + j] + c;
+            t[i + j] = (uint32_t)x;
+            c = (uint32_t)(x >> 32);
+        }
+        t[i + 8] = c;
+    }
+#pragma unroll
+    for (int k = 15; k > 0; k--) t[k] = (t[k] << 1) | (t[k - 1] >> 31);
+    t[0] <<= 1;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint64_t x = (uint64_t)a.v[i] * a.v[i] + t[2 * i] + c;
+        t[2 * i] = (uint32_t)x;
+        x = (uint64_t)t[2 * i + 1] + (x >> 32);
+        t[2 * i + 1] = (uint32_t)x;
+        c = (uint32_t)(x >> 32);
+    }
+    return fe8_reduce(t);
+}
+
+__device__ __forceinline__ void fe8_pin(fe8& a) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) asm volatile("" : "+v"(a.v[i]));
+}
+
+// canonical words of a radix-2^32 element (value < 2^256)
+__device__ void fe8_freeze(const fe8& a, uint32_t w[8]) {
+    uint32_t r[8];
+    // fold bit 255: r = a mod 2^255 + 19 * (a >> 255)
+    uint64_t c = (uint64_t)(a.v[7] >> 31) * 19u;
+    for (int k = 0; k < 8; k++) {
+        const uint64_t x = (uint64_t)(k == 7 ? (a.v[7] & 0x7fffffffu) : a.v[k]) + c;
+        r[k] = (uint32_t)x;
+        c = x >> 32;
+    }
+    // now r < 2^255 + 19: subtract p once if r >= p
+    uint32_t s[8];
+    int64_t br = 19;
+    for (int k = 0; k < 8; k++) {
+        const int64_t x = (int64_t)r[k] + br;
+        s[k] = (uint32_t)x;
+        br = x >> 32;
+    }
+    const bool ge = (s[7] >> 31) != 0;  // r + 19 >= 2^255 <=> r >= p
+    for (int k = 0; k < 8; k++) w[k] = ge ? (k == 7 ? s[7] & 0x7fffffffu : s[k]) : r[k];
+}
+
+enum { F10_SQ, F10_MUL, F8_SQ_PS, F8_SQ_OS, F8_MUL_PS };
+
+template <int OP, int ILP>
+__global__ void __launch_bounds__(256) k_bench(uint32_t* out, int iters) {
+    if constexpr (OP == F10_SQ || OP == F10_MUL) {
+        fe f[ILP], g;
+        for (int i = 0; i < 10; i++) g.v[i] = (threadIdx.x * 5 + i * 11) & M25;
+#pragma unroll
+        for (int c = 0; c < ILP; c++)
+            for (int i = 0; i < 10; i++) f[c].v[i] = (threadIdx.x * 7 + i * 13 + c) & M25;
+#pragma unroll 1
+        for (int it = 0; it < iters; it++) {
+#pragma unroll
+            for (int c = 0; c < ILP; c++) fe_pin(f[c]);
+#pragma unroll
+            for (int c = 0; c < ILP; c++) f[c] = OP == F10_SQ ? fe_sq(f[c]) : fe_mul(f[c], g);
+        }
+        uint32_t s = 0;
+#pragma unroll
+        for (int c = 0; c < ILP; c++)
+            for (int i = 0; i < 10; i++) s ^= f[c].v[i];
+        if (s == 0x12345u) out[0] = s;
+    } else {
+        fe8 f[ILP], g;
+        for (int i = 0; i < 8; i++) g.v[i] = threadIdx.x * 0x9e3779b9u + i * 0x85ebca6bu;
+#pragma unroll
+        for (int c = 0; c < ILP; c++)
+            for (int i = 0; i < 8; i++) f[c].v[i] = threadIdx.x * 0x27d4eb2fu + i * 0x165667b1u + c;
+#pragma unroll 1
+        for (int it = 0; it < iters; it++) {
+#pragma unroll
+            for (int c = 0; c < ILP; c++) fe8_pin(f[c]);
+#pragma unroll
+            for (int c = 0; c < ILP; c++)
+                f[c] = OP == F8_SQ_PS ? fe8_sq_ps(f[c]) : OP == F8_SQ_OS ? fe8_sq_os(f[c]) : fe8_mul_ps(f[c], g);
+        }
+        uint32_t s = 0;
+#pragma unroll
+        for (int c = 0; c < ILP; c++)
+            for (int i = 0; i < 8; i++) s ^= f[c].v[i];
+        if (s == 0x12345u) out[0] = s;
+    }
+}
+
+// lane t: x = (t + 1) * 0x9e3779b97f4a7c15-derived 255-bit element; 64 squarings and 8
+// multiplications by a second element in each form; canonical words of each result -> out
+__global__ void k_check(uint32_t* out) {
+    const uint32_t t = threadIdx.x;
+    uint32_t w[8], u[8];
+    for (int i = 0; i < 8; i++) {
+        w[i] = (t + 1) * 0x9e3779b9u ^ (i * 0x7f4a7c15u);
+        u[i] = (t + 3) * 0x85ebca6bu ^ (i * 0xc2b2ae35u);
+    }
+    w[7] &= 0x7fffffffu;
+    u[7] &= 0x7fffffffu;
+    fe f = fe_from_words(w), g = fe_from_words(u);
+    fe8 a, b, c, d;
+    for (int i = 0; i < 8; i++) a.v[i] = c.v[i] = w[i], b.v[i] = u[i];
+    for (int r = 0; r < 8; r++) {
+        for (int s = 0; s < 8; s++) {
+            f = fe_sq(f);
+            a = fe8_sq_ps(a);
+            c = fe8_sq_os(c);
+        }
+        f = fe_mul(f, g);
+        a = fe8_mul_ps(a, b);
+        c = fe8_mul_ps(c, b);
+    }
+    uint32_t o10[8], o8a[8], o8c[8];
+    fe_freeze(f, o10);
+    fe8_freeze(a, o8a);
+    fe8_freeze(c, o8c);
+    uint32_t bad = 0;
+    for (int i = 0; i < 8; i++) bad |= (o10[i] != o8a[i]) | ((o10[i] != o8c[i]) << 1);
+    atomicOr(out + 1, bad);
 }
 
 template <class K>
@@ -64,21 +256,35 @@ double rate(K kern, uint32_t* out, int iters, int blocks, int ilp) {
         hipEventElapsedTime(&ms, e0, e1);
         best = ms < best ? ms : best;
     }
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
     return (double)blocks * 256 * iters * ilp / (best * 1e-3);
 }
 
 int main() {
     uint32_t* out;
     hipMalloc(&out, 64);
+    hipMemset(out, 0, 64);
+    hipLaunchKernelGGL(k_check, dim3(1), dim3(256), 0, 0, out);
+    uint32_t h[2] = {0, 0};
+    hipMemcpy(h, out, 8, hipMemcpyDeviceToHost);
+    printf("{\"check\": {\"sq8_ps_mul8_ps_equal_10limb\": %s, \"sq8_os_equal_10limb\": %s, \"lanes\": 256, "
+           "\"chain\": \"8 x (8 squarings + 1 multiplication)\"}}\n",
+           (h[1] & 1) ? "false" : "true", (h[1] & 2) ? "false" : "true");
     hipDeviceProp_t p;
     hipGetDeviceProperties(&p, 0);
     const int cus = p.multiProcessorCount;
     const int iters = 4096;
     for (int w : {1, 2, 3, 4, 6, 8}) {
         const int blocks = cus * w;  // 256-thread blocks: one wave per SIMD per block
-        printf("{\"waves_per_simd\": %d, \"sq_ilp1\": %.4e, \"sq_ilp2\": %.4e, \"mul_ilp1\": %.4e, \"mul_ilp2\": %.4e}\n", w,
-               rate(k_sq<1>, out, iters, blocks, 1), rate(k_sq<2>, out, iters, blocks, 2),
-               rate(k_mul<1>, out, iters, blocks, 1), rate(k_mul<2>, out, iters, blocks, 2));
+        printf("{\"waves_per_simd\": %d, \"sq_ilp1\": %.4e, \"sq_ilp2\": %.4e, \"mul_ilp1\": %.4e, "
+               "\"mul_ilp2\": %.4e, \"sq8_ps_ilp1\": %.4e, \"sq8_ps_ilp2\": %.4e, \"sq8_os_ilp1\": %.4e, "
+               "\"mul8_ps_ilp1\": %.4e, \"mul8_ps_ilp2\": %.4e}\n",
+               w, rate(k_bench<F10_SQ, 1>, out, iters, blocks, 1), rate(k_bench<F10_SQ, 2>, out, iters, blocks, 2),
+               rate(k_bench<F10_MUL, 1>, out, iters, blocks, 1), rate(k_bench<F10_MUL, 2>, out, iters, blocks, 2),
+               rate(k_bench<F8_SQ_PS, 1>, out, iters, blocks, 1), rate(k_bench<F8_SQ_PS, 2>, out, iters, blocks, 2),
+               rate(k_bench<F8_SQ_OS, 1>, out, iters, blocks, 1), rate(k_bench<F8_MUL_PS, 1>, out, iters, blocks, 1),
+               rate(k_bench<F8_MUL_PS, 2>, out, iters, blocks, 2));
         fflush(stdout);
     }
     return 0;
