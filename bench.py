@@ -316,7 +316,8 @@ def kernel_rooflines(kt, stats, n, na, peak):
          "(R_i and the A points); the SHA-512 hashing in the same grid is not counted (a lower bound)")
     mem("k_msm_hist", ["k_msm_hist"], 2 * digit_slots + 4 * cnt_len,
         f"read the i16 digit rows ({digit_slots} slots), write {cnt_len} u32 counts")
-    mem("k_scan", ["k_scan_tile", "k_scan_tiles", "k_scan_add"], 8 * cnt_len, f"read + write {cnt_len} u32 counts")
+    mem("k_msm_wscan", ["k_msm_wscan"], 12 * cnt_len,
+        f"read the {cnt_len} counts twice (totals, then offsets) and write them back as offsets")
     mem("k_msm_scatter", ["k_msm_scatter"], 2 * digit_slots + 4 * cnt_len + 4 * E,
         f"read the digit rows and the {cnt_len} bucket offsets, write {E} u32 entries")
     valu("k_msm_bucket+fixup", ["k_msm_bucket", "k_msm_fixup"], MADS_MIXED_ADD * E,

@@ -9,9 +9,10 @@
 //   k_msm_points    2 lanes per signature (wave-uniform R / A roles): decompress, store the
 //                   128-byte affine Niels record of each point
 //   k_msm_hist      workgroup (chunk, window): LDS histogram of the window's bucket ids
-//   k_cnt_colsum    bucket totals over the chunks; k_scan_* their exclusive scan (bucket starts);
-//   k_cnt_offsets   the (bucket, chunk) slice offsets
-//   k_msm_scatter   workgroup (chunk, window): LDS cursors place j|sign into bucket order
+//   k_msm_wscan     workgroup per window: its entry base, bucket totals, their scan, the
+//                   (bucket, chunk) slice offsets
+//   k_msm_scatter   workgroup (chunk, window), XCD-grouped: LDS cursors place j|sign into bucket
+//                   order  (one-chunk batches: k_msm_sort1 does hist + scan + scatter per window)
 //   k_msm_bucket    lane per fixed-size chunk of the sorted entries: key-segment sums (mixed
 //                   additions, affine Niels), balanced whatever the bucket sizes
 //   k_msm_fixup     lane per bucket: joins the pieces of buckets that span chunks
@@ -255,69 +256,197 @@ __device__ __forceinline__ uint64_t msm_window_points(uint64_t n, uint64_t na, i
 }
 
 // grid (chunks, windows); counts laid out window by window, chunk-major inside a window:
-// cnt[kbase[w] * chunks + chunk * nb_w + b], so every workgroup stores one contiguous run
+// cnt[kbase[w] * chunks + chunk * nb_w + b], so every workgroup stores one contiguous run; the
+// workgroup's nonzero digits -> nzc[w * chunks + chunk] (the windows' entry bases, k_msm_wscan)
 extern "C" __global__ void __launch_bounds__(256) k_msm_hist(
     uint64_t n, uint64_t na, MsmLayout lay, uint32_t chunk_pts, const int16_t* __restrict__ digits,
-    uint32_t* __restrict__ cnt) {
+    uint32_t* __restrict__ cnt, uint32_t* __restrict__ nzc) {
     extern __shared__ uint32_t hist[];
+    __shared__ uint32_t nz;
     const int w = blockIdx.y, nw_z = lay.nw_z, nb = 1 << (lay.width[w] - 1);
     const uint32_t chunks = gridDim.x, chunk = blockIdx.x;
     for (int b = threadIdx.x; b < nb; b += blockDim.x) hist[b] = 0;
+    if (threadIdx.x == 0) nz = 0;
     __syncthreads();
     const uint64_t np = na + 1 + n, cnt_w = msm_window_points(n, na, w, nw_z);
     const uint64_t lo = (uint64_t)chunk * chunk_pts;
     const uint64_t hi = lo + chunk_pts < cnt_w ? lo + chunk_pts : cnt_w;
     const int16_t* dw = digits + (uint64_t)w * np;
+    uint32_t mine = 0;
     for (uint64_t j = lo + threadIdx.x; j < hi; j += blockDim.x) {
         const int d = dw[j];
-        if (d) atomicAdd(&hist[(d < 0 ? -d : d) - 1], 1u);
+        if (d) {
+            atomicAdd(&hist[(d < 0 ? -d : d) - 1], 1u);
+            mine++;
+        }
     }
+    atomicAdd(&nz, mine);
     __syncthreads();
     uint32_t* out = cnt + (uint64_t)lay.kbase[w] * chunks + (uint64_t)chunk * nb;
     for (int b = threadIdx.x; b < nb; b += blockDim.x) out[b] = hist[b];
+    if (threadIdx.x == 0) nzc[(uint64_t)w * chunks + chunk] = nz;
 }
 
-// window of bucket key k (kbase ascending, at most MSM_MAX_WINDOWS windows)
-__device__ __forceinline__ int msm_key_window(const MsmLayout& lay, uint32_t k) {
-    int lo = 0, hi = lay.nw;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (lay.kbase[mid] <= k) lo = mid;
-        else hi = mid;
+// ---- per-window scans: window w's entries start at ebase_w = the nonzero digits of the windows
+// before it, so the windows sort independently and the entries stay packed ----------------------
+// exclusive scan of one value per thread over the workgroup (wave prefix sums by shuffles, one
+// LDS word per wave); every thread gets its prefix and the workgroup total
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
+    const int t = threadIdx.x, wid = t >> 6, lane = t & 63, nwaves = blockDim.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += u;
     }
-    return lo;
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+    for (int k = 0; k < nwaves; k++) {
+        const uint32_t s = wsum[k];
+        pre += k < wid ? s : 0u;
+        tot += s;
+    }
+    __syncthreads();  // wsum may be rewritten by the next call
+    total = tot;
+    return pre + inc - v;
 }
 
-// lane per bucket key: tot[k] = entries of bucket k over all chunks (coalesced: consecutive
-// keys of a window are consecutive words of every chunk's run)
-extern "C" __global__ void __launch_bounds__(256) k_cnt_colsum(MsmLayout lay, uint32_t chunks,
-                                                                const uint32_t* __restrict__ cnt,
-                                                                uint32_t* __restrict__ tot) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= lay.kbase[lay.nw]) return;
-    const int w = msm_key_window(lay, k);
-    const uint32_t nb = 1u << (lay.width[w] - 1), b = k - lay.kbase[w];
-    const uint32_t* c = cnt + (uint64_t)lay.kbase[w] * chunks + b;
-    uint32_t s = 0;
-    for (uint32_t ch = 0; ch < chunks; ch++) s += c[(uint64_t)ch * nb];
-    tot[k] = s;
+// sum of one value per thread over the workgroup
+__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* wsum) {
+    uint32_t total;
+    (void)block_excl_scan(v, wsum, total);
+    return total;
 }
 
-// lane per bucket key: the counts become the start offsets of every (bucket, chunk) slice:
-// kstart[k] (the scanned totals) plus the counts of the earlier chunks
-extern "C" __global__ void __launch_bounds__(256) k_cnt_offsets(MsmLayout lay, uint32_t chunks,
-                                                                 uint32_t* __restrict__ cnt,
-                                                                 const uint32_t* __restrict__ kstart) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= lay.kbase[lay.nw]) return;
-    const int w = msm_key_window(lay, k);
-    const uint32_t nb = 1u << (lay.width[w] - 1), b = k - lay.kbase[w];
-    uint32_t* c = cnt + (uint64_t)lay.kbase[w] * chunks + b;
-    uint32_t o = kstart[k];
-    for (uint32_t ch = 0; ch < chunks; ch++) {
-        const uint32_t v = c[(uint64_t)ch * nb];
-        c[(uint64_t)ch * nb] = o;
-        o += v;
+// grid (nw), 1024 threads: the window's entry base (nonzero digits of the windows before it, from
+// k_msm_hist's per-chunk counts), its bucket totals over the chunks and their exclusive scan
+// (1024 buckets per step); the counts become absolute slice offsets in place:
+// cnt[(b, ch)] = ebase + (entries of buckets < b) + (entries of bucket b in chunks < ch);
+// kstart[key] = the bucket's first entry.  The last window stores the total (tot[nw]) and
+// every window its own count (tot[w]).
+extern "C" __global__ void __launch_bounds__(1024) k_msm_wscan(
+    MsmLayout lay, uint32_t chunks, uint32_t* __restrict__ cnt, const uint32_t* __restrict__ nzc,
+    uint32_t* __restrict__ kstart, uint32_t* __restrict__ tot_out) {
+    __shared__ uint32_t wsum[16];
+    const int w = blockIdx.x, nb = 1 << (lay.width[w] - 1);
+    uint32_t before = 0;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)w * chunks; i += blockDim.x) before += nzc[i];
+    const uint32_t ebase = block_sum(before, wsum);
+    uint32_t* c = cnt + (uint64_t)lay.kbase[w] * chunks;
+    uint32_t carry = 0;
+    for (int b0 = 0; b0 < nb; b0 += (int)blockDim.x) {
+        const int b = b0 + (int)threadIdx.x;
+        uint32_t tot = 0;
+        if (b < nb) {
+            // eight independent loads in flight per step (a sequential chain of loads per lane
+            // was latency-bound)
+            uint32_t ch = 0;
+            for (; ch + 8 <= chunks; ch += 8) {
+                uint32_t v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) v[u] = c[(uint64_t)(ch + u) * nb + b];
+#pragma unroll
+                for (int u = 0; u < 8; u++) tot += v[u];
+            }
+            for (; ch < chunks; ch++) tot += c[(uint64_t)ch * nb + b];
+        }
+        uint32_t step;
+        const uint32_t ex = block_excl_scan(tot, wsum, step);
+        if (b < nb) {
+            uint32_t o = ebase + carry + ex;
+            kstart[lay.kbase[w] + b] = o;
+            uint32_t ch = 0;
+            for (; ch + 8 <= chunks; ch += 8) {
+                uint32_t v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) v[u] = c[(uint64_t)(ch + u) * nb + b];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    c[(uint64_t)(ch + u) * nb + b] = o;
+                    o += v[u];
+                }
+            }
+            for (; ch < chunks; ch++) {
+                const uint32_t v = c[(uint64_t)ch * nb + b];
+                c[(uint64_t)ch * nb + b] = o;
+                o += v;
+            }
+        }
+        carry += step;
+    }
+    if (threadIdx.x == 0) {
+        tot_out[w] = carry;
+        if (w == lay.nw - 1) tot_out[MSM_MAX_WINDOWS] = ebase + carry;
+    }
+}
+
+// Small batches (one chunk per window): the whole sort of window w in ONE workgroup of 1024 --
+// its entry base (the nonzero digits of the earlier windows, counted here from their digit
+// rows: at most 8,192 points each), LDS histogram, scan, kstart, LDS cursors, scatter
+// (replaces hist + scan + scatter)
+extern "C" __global__ void __launch_bounds__(1024) k_msm_sort1(
+    uint64_t n, uint64_t na, MsmLayout lay, const int16_t* __restrict__ digits, uint32_t* __restrict__ kstart,
+    uint32_t* __restrict__ tot_out, uint32_t* __restrict__ entries) {
+    extern __shared__ uint32_t cur[];
+    __shared__ uint32_t wsum[16];
+    const int w = blockIdx.x, nb = 1 << (lay.width[w] - 1);
+    const uint64_t np = na + 1 + n;
+    // nonzero digits of the earlier windows: full rows below nw_z are one contiguous run
+    // (16-byte loads, eight digits each), the rows above it hold na + 1 digits each
+    uint32_t before = 0;
+    {
+        const uint64_t run = (uint64_t)(w < lay.nw_z ? w : lay.nw_z) * np;
+        const uint4* q = reinterpret_cast<const uint4*>(digits);
+        const uint64_t nq = run / 8;
+        auto nz2 = [](uint32_t x) { return ((x & 0xFFFFu) != 0u) + ((x >> 16) != 0u); };
+#pragma unroll 4
+        for (uint64_t i = threadIdx.x; i < nq; i += blockDim.x) {
+            const uint4 v = q[i];
+            before += nz2(v.x) + nz2(v.y) + nz2(v.z) + nz2(v.w);
+        }
+        for (uint64_t j = 8 * nq + threadIdx.x; j < run; j += blockDim.x) before += digits[j] != 0;
+        const uint64_t upper = w > lay.nw_z ? (uint64_t)(w - lay.nw_z) * (na + 1) : 0;
+#pragma unroll 4
+        for (uint64_t i = threadIdx.x; i < upper; i += blockDim.x) {
+            const uint64_t v = lay.nw_z + i / (na + 1), j = i % (na + 1);
+            before += digits[v * np + j] != 0;
+        }
+    }
+    const uint32_t ebase = block_sum(before, wsum);
+    const uint64_t cap = msm_window_points(n, na, w, lay.nw_z);
+    const int16_t* dw = digits + (uint64_t)w * np;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) cur[b] = 0;
+    __syncthreads();
+    for (uint64_t j = threadIdx.x; j < cap; j += blockDim.x) {
+        const int d = dw[j];
+        if (d) atomicAdd(&cur[(d < 0 ? -d : d) - 1], 1u);
+    }
+    __syncthreads();
+    uint32_t carry = 0;
+    for (int b0 = 0; b0 < nb; b0 += (int)blockDim.x) {
+        const int b = b0 + (int)threadIdx.x;
+        const uint32_t v = b < nb ? cur[b] : 0u;
+        uint32_t step;
+        const uint32_t ex = block_excl_scan(v, wsum, step);
+        if (b < nb) {
+            const uint32_t o = ebase + carry + ex;
+            cur[b] = o;
+            kstart[lay.kbase[w] + b] = o;
+        }
+        carry += step;
+    }
+    __syncthreads();
+    for (uint64_t j = threadIdx.x; j < cap; j += blockDim.x) {
+        const int d = dw[j];
+        if (d) {
+            const uint32_t slot = atomicAdd(&cur[(d < 0 ? -d : d) - 1], 1u);
+            entries[slot] = (uint32_t)j | (d < 0 ? MSM_NEG : 0u);
+        }
+    }
+    if (threadIdx.x == 0) {
+        tot_out[w] = carry;
+        if (w == lay.nw - 1) tot_out[MSM_MAX_WINDOWS] = ebase + carry;
     }
 }
 
@@ -357,86 +486,6 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_scatter(
             const uint32_t slot = atomicAdd(&cur[b], 1u);
             entries[slot] = (uint32_t)j | (d < 0 ? MSM_NEG : 0u);
         }
-    }
-}
-
-// ---- exclusive scan of u32 counts (tiles of 4096: 256 threads x 16) ----------------------
-// kstart != null: the whole array is one tile (small batches), so this launch also finishes the
-// scan: kstart[key] = a[key * chunks], tile_sum[0] = 0 and tile_sum[1] = total, i.e. what
-// k_scan_tiles and k_scan_add produce for several tiles
-// (a and kstart may be the same array: the scan of the bucket totals runs in place)
-extern "C" __global__ void __launch_bounds__(256) k_scan_tile(uint64_t len, uint32_t* a,
-                                                              uint32_t* __restrict__ tile_sum, uint32_t chunks,
-                                                              uint32_t* kstart) {
-    __shared__ uint32_t sh[256];
-    const uint64_t base = (uint64_t)blockIdx.x * 4096 + threadIdx.x * 16;
-    uint32_t v[16], s = 0;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        v[k] = base + k < len ? a[base + k] : 0u;
-        s += v[k];
-    }
-    sh[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = 1; o < 256; o <<= 1) {
-        const uint32_t x = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0u;
-        __syncthreads();
-        sh[threadIdx.x] += x;
-        __syncthreads();
-    }
-    uint32_t run = sh[threadIdx.x] - s;  // exclusive prefix of this thread
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        if (base + k < len) {
-            a[base + k] = run;
-            if (kstart && (base + k) % chunks == 0) kstart[(base + k) / chunks] = run;
-        }
-        run += v[k];
-    }
-    if (threadIdx.x == 255) {
-        if (kstart) {
-            tile_sum[0] = 0;
-            tile_sum[1] = sh[255];
-        } else {
-            tile_sum[blockIdx.x] = sh[255];
-        }
-    }
-}
-
-// one workgroup: exclusive scan of the tile sums in place; tile_sum[ntiles] = total
-extern "C" __global__ void __launch_bounds__(1024) k_scan_tiles(uint32_t ntiles, uint32_t* __restrict__ t) {
-    __shared__ uint32_t sh[1024];
-    __shared__ uint32_t carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (uint32_t b0 = 0; b0 < ntiles; b0 += 1024) {
-        const uint32_t idx = b0 + threadIdx.x;
-        const uint32_t v = idx < ntiles ? t[idx] : 0u;
-        sh[threadIdx.x] = v;
-        __syncthreads();
-        for (int o = 1; o < 1024; o <<= 1) {
-            const uint32_t x = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0u;
-            __syncthreads();
-            sh[threadIdx.x] += x;
-            __syncthreads();
-        }
-        if (idx < ntiles) t[idx] = carry + sh[threadIdx.x] - v;
-        __syncthreads();
-        if (threadIdx.x == 1023) carry += sh[1023];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) t[ntiles] = carry;
-}
-
-// adds the tile offsets; also gathers kstart[key] = a[key * chunks] (first entry of each key)
-extern "C" __global__ void __launch_bounds__(256) k_scan_add(uint64_t len, uint32_t* a,
-                                                             const uint32_t* __restrict__ tile_sum,
-                                                             uint32_t chunks, uint32_t* kstart) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < len) {
-        const uint32_t v = a[i] + tile_sum[i >> 12];
-        a[i] = v;
-        if (i % chunks == 0) kstart[i / chunks] = v;
     }
 }
 
@@ -501,8 +550,14 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_bucket(
             if (k + 1 < k1) {
                 kend = key + 2 < nkeys ? pf_val : E;
                 key++;
-                while (kend <= k + 1) {  // empty keys (sparse batches)
-                    key++;
+                if (kend <= k + 1) {  // empty keys follow: bisect for the key holding entry k + 1
+                    uint32_t lo = key, hi = nkeys;  // kstart[lo] <= k + 1
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (kstart[mid] <= k + 1) lo = mid;
+                        else hi = mid;
+                    }
+                    key = lo;
                     kend = key + 1 < nkeys ? kstart[key + 1] : E;
                 }
             }

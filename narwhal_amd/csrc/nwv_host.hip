@@ -343,7 +343,7 @@ int ed_launch(Lane& d, EdBuffers& b, size_t n, hipStream_t stream, hipEvent_t* e
 struct MsmPlan {
     MsmLayout lay{};
     MsmXcdMap xm{};  // k_msm_scatter's windows per XCD group
-    uint32_t chunk_pts = 0, chunks = 0, nkeys = 0, ntiles = 0;
+    uint32_t chunk_pts = 0, chunks = 0, nkeys = 0;
     uint32_t seg = 0;  // entries per k_msm_bucket lane
     uint32_t tail_S = 1;  // k_msm_tail: bucket chunks per window
     uint64_t np = 0, na = 0, cnt_len = 0, max_entries = 0, nseg = 0;
@@ -375,7 +375,6 @@ MsmPlan msm_plan(size_t n, size_t na) {
     msm_xcd_map(p.lay, n, na, p.chunk_pts, p.xm);
     p.nkeys = p.lay.kbase[p.lay.nw];
     p.cnt_len = (uint64_t)p.nkeys * p.chunks;
-    p.ntiles = (uint32_t)((p.nkeys + 4095) / 4096);  // the scan runs over the bucket totals
     p.max_entries = (uint64_t)(na + 1) * p.lay.nw + (uint64_t)n * p.lay.nw_z;
     // ~2 waves per SIMD of bucket lanes (256 CUs x 4 SIMDs x 2 x 64), 8..64 entries each
     p.seg = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, p.max_entries / (256 * 4 * 2 * 64)));
@@ -400,8 +399,8 @@ int msm_alloc(EdBuffers& b, const MsmPlan& p, size_t n) {
         (rc = b.m_state.ensure(128)) ||
         (rc = b.m_pts.ensure((size_t)4 * MSM_PT_WORDS * p.np + 64)) ||
         (rc = b.m_digits.ensure((size_t)2 * p.lay.nw * p.np + 64)) ||
-        (rc = b.m_cnt.ensure((size_t)4 * p.cnt_len + 64)) ||
-        (rc = b.m_tiles.ensure((size_t)4 * (p.ntiles + 1) + 64)) ||
+        (p.chunks > 1 && (rc = b.m_cnt.ensure((size_t)4 * (p.cnt_len + (size_t)p.lay.nw * p.chunks) + 64))) ||
+        (rc = b.m_tiles.ensure((size_t)4 * (MSM_MAX_WINDOWS + 1) + 64)) ||
         (rc = b.m_entries.ensure((size_t)4 * p.max_entries + 64)) ||
         (rc = b.m_kstart.ensure((size_t)4 * p.nkeys + 64)) ||
         (rc = b.m_hpart.ensure((size_t)4 * P3_WORDS * p.nseg + 64)) ||
@@ -417,10 +416,10 @@ static const char* const ED_KERNEL_NAMES[] = {"k_ed_hash", "k_ed_points", "k_ed_
 // event slots of one batch MSM; nullptr = no kernel in that slot (k_msm_prep runs the hash and
 // the decompression as one grid unless NWV_FLAG_MSM_SPLIT_PREP)
 static const char* const MSM_KERNEL_NAMES[] = {
-    "k_msm_prep", "k_msm_bscalar", nullptr, "k_msm_hist", "k_scan",
+    "k_msm_prep", "k_msm_bscalar", nullptr, "k_msm_hist", "k_msm_wscan",
     "k_msm_scatter", "k_msm_bucket+fixup", "k_msm_tail", nullptr};
 static const char* const MSM_KERNEL_NAMES_SPLIT[] = {
-    "k_msm_scalars", "k_msm_bscalar", "k_msm_points", "k_msm_hist", "k_scan",
+    "k_msm_scalars", "k_msm_bscalar", "k_msm_points", "k_msm_hist", "k_msm_wscan",
     "k_msm_scatter", "k_msm_bucket+fixup", "k_msm_tail", nullptr};
 constexpr int MSM_NKERNELS = 9;
 constexpr int MSM_NEVENTS = MSM_NKERNELS + 1;  // one event before each kernel, one after the last
@@ -468,36 +467,37 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     if ((rc = mark(2))) return rc;
     if (!fused) hipLaunchKernelGGL(k_msm_points, dim3(pblk), dim3(256), 0, stream, gp);
     if ((rc = mark(3))) return rc;
-    const dim3 gsort(p.chunks, (unsigned)p.lay.nw);
     const size_t lds_nb = (size_t)4 << (p.lay.cmax - 1);
-    uint32_t* cnt = b.m_cnt.as<uint32_t>();
-    uint32_t* tiles = b.m_tiles.as<uint32_t>();
-    hipLaunchKernelGGL(k_msm_hist, gsort, dim3(256), lds_nb, stream, (uint64_t)n, (uint64_t)na, p.lay, p.chunk_pts,
-                       digits, cnt);
-    if ((rc = mark(4))) return rc;
-    // bucket totals -> their exclusive scan in place (kstart: bucket starts, tiles[ntiles] = total
-    // entries) -> slice offsets of every (bucket, chunk) in place of the counts
     uint32_t* kst = b.m_kstart.as<uint32_t>();
-    const unsigned kgrid = (unsigned)((p.nkeys + 255) / 256);
-    hipLaunchKernelGGL(k_cnt_colsum, dim3(kgrid), dim3(256), 0, stream, p.lay, p.chunks, cnt, kst);
-    if (p.ntiles == 1) {  // one tile: the tile scan finishes the whole scan (two launches fewer)
-        hipLaunchKernelGGL(k_scan_tile, dim3(1), dim3(256), 0, stream, (uint64_t)p.nkeys, kst, tiles, 1u, kst);
+    uint32_t* tot = b.m_tiles.as<uint32_t>();  // [nw] entries per window, [MSM_MAX_WINDOWS] all
+    uint32_t* ent = b.m_entries.as<uint32_t>();
+    if (p.chunks == 1) {
+        // one chunk per window: the whole counting sort of a window in one workgroup (timed in
+        // the k_msm_hist slot)
+        hipLaunchKernelGGL(k_msm_sort1, dim3((unsigned)p.lay.nw), dim3(1024), lds_nb, stream, (uint64_t)n,
+                           (uint64_t)na, p.lay, digits, kst, tot, ent);
+        if ((rc = mark(4))) return rc;
+        if ((rc = mark(5))) return rc;
     } else {
-        hipLaunchKernelGGL(k_scan_tile, dim3(p.ntiles), dim3(256), 0, stream, (uint64_t)p.nkeys, kst, tiles, 1u,
-                           (uint32_t*)nullptr);
-        hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, stream, p.ntiles, tiles);
-        hipLaunchKernelGGL(k_scan_add, dim3(kgrid), dim3(256), 0, stream, (uint64_t)p.nkeys, kst, tiles, 1u, kst);
+        uint32_t* cnt = b.m_cnt.as<uint32_t>();
+        uint32_t* nzc = cnt + p.cnt_len;  // [nw][chunks] nonzero digits per histogram workgroup
+        hipLaunchKernelGGL(k_msm_hist, dim3(p.chunks, (unsigned)p.lay.nw), dim3(256), lds_nb, stream, (uint64_t)n,
+                           (uint64_t)na, p.lay, p.chunk_pts, digits, cnt, nzc);
+        if ((rc = mark(4))) return rc;
+        // per window: entry base, bucket totals -> scan -> absolute (bucket, chunk) slice offsets
+        hipLaunchKernelGGL(k_msm_wscan, dim3((unsigned)p.lay.nw), dim3(1024), 0, stream, p.lay, p.chunks, cnt, nzc,
+                           kst, tot);
+        if ((rc = mark(5))) return rc;
+        hipLaunchKernelGGL(k_msm_scatter, dim3(MSM_XCD_GROUPS * p.xm.slots), dim3(256), lds_nb, stream, (uint64_t)n,
+                           (uint64_t)na, p.lay, p.xm, p.chunks, p.chunk_pts, digits, cnt, ent);
     }
-    hipLaunchKernelGGL(k_cnt_offsets, dim3(kgrid), dim3(256), 0, stream, p.lay, p.chunks, cnt, kst);
-    if ((rc = mark(5))) return rc;
-    hipLaunchKernelGGL(k_msm_scatter, dim3(MSM_XCD_GROUPS * p.xm.slots), dim3(256), lds_nb, stream, (uint64_t)n,
-                       (uint64_t)na, p.lay, p.xm, p.chunks, p.chunk_pts, digits, cnt, b.m_entries.as<uint32_t>());
     if ((rc = mark(6))) return rc;
+    const uint32_t* E = tot + MSM_MAX_WINDOWS;
     hipLaunchKernelGGL(k_msm_bucket, dim3((unsigned)((p.nseg + 255) / 256)), dim3(256), 0, stream, p.seg,
-                       p.nkeys, tiles + p.ntiles, b.m_entries.as<uint32_t>(), b.m_kstart.as<uint32_t>(),
-                       b.m_pts.as<uint32_t>(), b.m_bsum.as<uint32_t>(), b.m_hpart.as<uint32_t>());
+                       p.nkeys, E, ent, kst, b.m_pts.as<uint32_t>(), b.m_bsum.as<uint32_t>(),
+                       b.m_hpart.as<uint32_t>());
     hipLaunchKernelGGL(k_msm_fixup, dim3((p.nkeys + 255) / 256), dim3(256), 0, stream, p.nkeys,
-                       p.seg, kst, tiles + p.ntiles, b.m_hpart.as<uint32_t>(), b.m_bsum.as<uint32_t>());
+                       p.seg, kst, E, b.m_hpart.as<uint32_t>(), b.m_bsum.as<uint32_t>());
     if ((rc = mark(7))) return rc;
     // window sums, their scaling and the verdict: one launch (its arrival counters are zeroed by
     // a memset node first, graph replays included)
@@ -1382,9 +1382,9 @@ int nwv_staged_msm_stats(nwv_staged* st, uint64_t out[8]) {
     out[5] = p.chunks;
     out[6] = p.seg;
     out[7] = na;
-    if (st->buf.m_tiles.p && st->buf.m_tiles.cap >= 4 * ((size_t)p.ntiles + 1)) {
-        uint32_t total = 0;
-        NWV_HIP(hipMemcpyAsync(&total, st->buf.m_tiles.as<uint32_t>() + p.ntiles, 4, hipMemcpyDeviceToHost,
+    if (st->buf.m_tiles.p && st->buf.m_tiles.cap >= 4 * ((size_t)MSM_MAX_WINDOWS + 1)) {
+        uint32_t total = 0;  // entries = nonzero digits over all windows
+        NWV_HIP(hipMemcpyAsync(&total, st->buf.m_tiles.as<uint32_t>() + MSM_MAX_WINDOWS, 4, hipMemcpyDeviceToHost,
                                st->stream));
         NWV_HIP(hipStreamSynchronize(st->stream));
         out[4] = total;
