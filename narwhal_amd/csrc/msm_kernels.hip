@@ -682,7 +682,11 @@ __device__ __forceinline__ bool tail_arrive(uint32_t* ctr, uint32_t expect, uint
         if (a.stamps && t == 0) a.stamps[8 * w + (slot)] = __builtin_amdgcn_s_memrealtime();       \
     } while (0)
 
-extern "C" __global__ void __launch_bounds__(256) k_msm_tail(MsmLayout lay, MsmTailArgs a) {
+// PER: combine items per thread (1 when every window's (lg C + 1) x S_w <= 256, else 3).  The
+// variant with one item needs 163 VGPRs instead of 216; fewer registers held by the tail's
+// long-lived waves leave room for other batches' waves on the same SIMDs.
+template <int PER>
+__device__ __forceinline__ void msm_tail_body(const MsmLayout& lay, const MsmTailArgs& a) {
     // 256 point slots of P3_WORDS; row-limb planes reuse the front once the slots are done;
     // the flag word sits behind the slots
     extern __shared__ uint32_t lds[];
@@ -712,10 +716,10 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_tail(MsmLayout lay, MsmT
     NWV_TAIL_STAMP(1);
     // ---- last chunk of window w: per plane, a butterfly over the Sw chunks.  Item j = q * Sw + s:
     // plane group q < lgC sums T_{s,q}; group lgC is the butterfly of the R_s.
-    const int items = (lgC + 1) * Sw, per = (items + 255) / 256;  // items per thread (<= 3)
-    ge_p3 v[3];
+    const int items = (lgC + 1) * Sw, per = (items + 255) / 256;  // items per thread (<= PER)
+    ge_p3 v[PER];
 #pragma unroll
-    for (int r = 0; r < 3; r++) {
+    for (int r = 0; r < PER; r++) {
         const int j = t + 256 * r;
         v[r] = ge_p3_identity();
         if (r < per && j < items) {
@@ -726,7 +730,7 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_tail(MsmLayout lay, MsmT
     }
     for (int o = 1; o < Sw; o <<= 1) {
 #pragma unroll
-        for (int r = 0; r < 3; r++) {
+        for (int r = 0; r < PER; r++) {
             if (r >= per) break;
             const int j = t + 256 * r;
             __syncthreads();
@@ -739,7 +743,7 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_tail(MsmLayout lay, MsmT
     // lgC * Sw + 2^i; U at item lgC * Sw.  Slot order: T_0 .. T_{m-1}, U  (m = lgC + lgS).
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 3; r++) {
+    for (int r = 0; r < PER; r++) {
         const int j = t + 256 * r;
         if (r >= per || j >= items) continue;
         const int q = j / Sw, sj = j % Sw;
@@ -805,4 +809,9 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_tail(MsmLayout lay, MsmT
         *a.verdict = ok ? 1u : 0u;
     }
     NWV_TAIL_STAMP(6);
+}
+
+extern "C" __global__ void __launch_bounds__(256) k_msm_tail(MsmLayout lay, MsmTailArgs a) { msm_tail_body<1>(lay, a); }
+extern "C" __global__ void __launch_bounds__(256) k_msm_tail_wide(MsmLayout lay, MsmTailArgs a) {
+    msm_tail_body<3>(lay, a);
 }

@@ -511,8 +511,20 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     }
     const MsmTailArgs ta{b.m_bsum.as<uint32_t>(), b.m_tpart.as<uint32_t>(), b.m_wsum.as<uint32_t>(),
                          b.m_ctr.as<uint32_t>(), state, state + 1, p.tail_S, st_buf};
-    hipLaunchKernelGGL(k_msm_tail, dim3(p.tail_S, (unsigned)p.lay.nw), dim3(256), (size_t)4 * (256 * P3_WORDS + 4),
-                       stream, p.lay, ta);
+    // combine items per thread: (lg C + 1) x S_w over the windows (C = nb / S_w buckets per chunk)
+    int items = 0;
+    for (int w = 0; w < p.lay.nw; w++) {
+        const int nb = 1 << (p.lay.width[w] - 1), Sw = (int)p.tail_S < nb ? (int)p.tail_S : nb;
+        int lgC = 0;
+        while ((1 << lgC) < nb / Sw) lgC++;
+        items = std::max(items, (lgC + 1) * Sw);
+    }
+    if (items <= 256)
+        hipLaunchKernelGGL(k_msm_tail, dim3(p.tail_S, (unsigned)p.lay.nw), dim3(256), (size_t)4 * (256 * P3_WORDS + 4),
+                           stream, p.lay, ta);
+    else
+        hipLaunchKernelGGL(k_msm_tail_wide, dim3(p.tail_S, (unsigned)p.lay.nw), dim3(256),
+                           (size_t)4 * (256 * P3_WORDS + 4), stream, p.lay, ta);
     if ((rc = mark(8))) return rc;
     if ((rc = mark(9))) return rc;
     NWV_HIP(hipGetLastError());
