@@ -368,6 +368,15 @@ def run_headline(args, eng, rank, world, dist):
     if dist is not None:
         dist.barrier()
     check_all("timed region: last run of every stage")
+    if args.mode == 1:
+        # every run's batch verdict, graph replays included, as tallied on the device by the runs
+        runs = len(stages) + args.warmup + args.steps
+        acc = rej = 0
+        for s_ in stages:
+            a_, r_ = s_.run_tally()
+            acc, rej = acc + a_, rej + r_
+        if rej or acc != runs:
+            raise SystemExit(f"batch verdicts over the bench: {acc} accepted, {rej} rejected of {runs} runs")
     # single-stream pass: step latency and per-kernel device times without overlap
     st = stages[0]
     st.kernel_times(args.mode, reset=True)

@@ -44,6 +44,12 @@ typedef struct nwv_ctx nwv_ctx;
 /* diagnostic: launch the MSM's hashing (k_msm_scalars) and decompression (k_msm_points) as two
  * kernels instead of one k_msm_prep grid (per-kernel timing of the decompression alone) */
 #define NWV_FLAG_MSM_SPLIT_PREP 4u
+/* keyed calls (nwv_ed25519_verify_batch_keyed[_digests], the types layer) keep each key's
+ * decompressed point and its 2^128 multiple in a per-device cache, so their MSM scalars are
+ * 128-bit (half the windows and doublings); this flag turns the cache off (every keyed call
+ * decompresses its keys, full-width scalars).  Env NWV_KEYCACHE_MAX_KEYS (default 4096): keyed
+ * calls with more distinct keys than this go uncached. */
+#define NWV_FLAG_NO_KEYCACHE 8u
 
 /* ------------------------------------------------------------------ lifecycle ----- */
 /* Process-wide context creation (created once, in Primary::spawn).
@@ -180,6 +186,9 @@ int nwv_staged_kernel_times(nwv_staged* st, int mode, int cap, const char** name
  * [3] buckets over all windows, [4] bucket entries of the last mode-1 run (0 before one),
  * [5] sort chunks, [6] entries per k_msm_bucket lane, [7] A points (n, or the distinct keys) */
 int nwv_staged_msm_stats(nwv_staged* st, uint64_t out[8]);
+/* batch verdicts of every mode-1 run since staging, counted on the device by the run itself
+ * (graph replays included): out[0] accepted runs, out[1] rejected runs.  Waits for the stream. */
+int nwv_staged_run_tally(nwv_staged* st, uint64_t out[2]);
 void nwv_staged_free(nwv_staged* st);
 
 /* ------------------------------------------------------------------ synthetic data ----- */

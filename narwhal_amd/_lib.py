@@ -25,6 +25,7 @@ NWV_ERR_LENGTH = -6
 NWV_FLAG_MSM_ALWAYS = 1
 NWV_FLAG_MSM_NEVER = 2
 NWV_FLAG_MSM_SPLIT_PREP = 4
+NWV_FLAG_NO_KEYCACHE = 8
 NWV_RUN_TIMED = 0x100
 
 
@@ -75,6 +76,7 @@ def load():
         "nwv_staged_kernel_times": ([_vp, _i32, _i32, _vp, _vp, _i32], _i32),
         "nwv_staged_free": ([_vp], None),
         "nwv_staged_msm_stats": ([_vp, _vp], _i32),
+        "nwv_staged_run_tally": ([_vp, _vp], _i32),
         "nwv_ed25519_sign_many": ([_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp], _i32),
     }
     for name, (args, res) in sig.items():
@@ -316,6 +318,13 @@ class Staged:
         _check(self.eng.lib.nwv_staged_msm_stats(self._h, _ptr(out)))
         keys = ("points", "windows", "windows_z", "buckets", "entries", "chunks", "seg", "a_points")
         return {k: int(v) for k, v in zip(keys, out)}
+
+    def run_tally(self):
+        """(accepted, rejected) batch verdicts of every mode-1 run since staging, counted on the
+        device by each run (graph replays included)"""
+        out = np.zeros(2, dtype=np.uint64)
+        _check(self.eng.lib.nwv_staged_run_tally(self._h, _ptr(out)))
+        return int(out[0]), int(out[1])
 
     def free(self):
         if self._h:

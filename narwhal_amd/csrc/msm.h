@@ -159,6 +159,39 @@ NWV_HD bool msm_make_layout2(int c_lo, int c_hi, MsmLayout& L) {
     return true;
 }
 NWV_HD bool msm_make_layout(int c, MsmLayout& L) { return msm_make_layout2(c, c, L); }
+// z range only (nw == nw_z): every scalar < 2^128, as in a keyed batch over the key cache
+// (split scalars, msm_split128)
+NWV_HD bool msm_make_layout_z(int c, MsmLayout& L) {
+    const int nz = (MSM_BITS_Z + 1 + c - 1) / c;
+    if (nz > MSM_MAX_WINDOWS) return false;
+    L.nw = nz;
+    L.nw_z = nz;
+    msm_split(L, 0, nz, MSM_BITS_Z + 1);
+    int pos = 0, cm = 0;
+    uint32_t kb = 0;
+    for (int w = 0; w < L.nw; w++) {
+        L.pos[w] = (uint16_t)pos;
+        L.kbase[w] = kb;
+        pos += L.width[w];
+        kb += 1u << (L.width[w] - 1);
+        cm = L.width[w] > cm ? L.width[w] : cm;
+    }
+    L.kbase[L.nw] = kb;
+    L.cmax = cm;
+    L.pad = 0;
+    return true;
+}
+// s = lo + 2^128 hi (both < 2^128)
+NWV_HD void msm_split128(const uint32_t s[8], uint32_t lo[8], uint32_t hi[8]) {
+    for (int k = 0; k < 8; k++) {
+        lo[k] = k < 4 ? s[k] : 0u;
+        hi[k] = k < 4 ? s[k + 4] : 0u;
+    }
+}
+
+// Committee key cache slot: A's point record, then 2^128 A's (msm_store_point layout); word
+// MSM_PT_WORDS - 1 of the first record is 1 when A failed to decode.  Slot 0 holds B.
+static constexpr int KC_SLOT_WORDS = 64;
 
 // chunks of chunk_pts points in window w (all na + 1 + n points below nw_z, else na + 1)
 NWV_HD uint32_t msm_window_chunks(uint64_t n, uint64_t na, int w, int nw_z, uint32_t chunk_pts) {

@@ -63,6 +63,7 @@ struct MsmScalarArgs {
 };
 struct MsmPointArgs {
     uint64_t n, na;
+    uint64_t ndec;  // A points to decompress into [0, ndec): na, or 0 when they come from the key cache
     const uint8_t* apk;
     const uint8_t* sig;
     uint32_t* pts;
@@ -128,11 +129,24 @@ __device__ __forceinline__ void msm_scalars_block(uint32_t blk, const MsmScalarA
 // Keyed batches (ed25519_consensus groups batch entries by verification key): one workgroup per
 // distinct key sums z_i k_i over its signatures (CSR: key_off[m+1], key_sig[n]), reduces mod l
 // and writes the key point's digits (row entry = key index).
+//
+// Split form (kc != null, committee key cache): the key's record and its 2^128 multiple's come
+// from cache slot kslot[key] and go to points key and m + key, with the 128-bit halves of the
+// key's scalar (K = lo + 2^128 hi), so every scalar of the MSM fits the z range (layout with
+// nw == nw_z: half the windows and half the final doubling chain).
 extern "C" __global__ void __launch_bounds__(256) k_msm_keysum(
     uint64_t n, uint64_t na, MsmLayout lay, const uint32_t* __restrict__ key_off,
-    const uint32_t* __restrict__ key_sig, const uint32_t* __restrict__ ascal, int16_t* __restrict__ digits) {
+    const uint32_t* __restrict__ key_sig, const uint32_t* __restrict__ ascal, int16_t* __restrict__ digits,
+    uint32_t m, const uint32_t* __restrict__ kslot, const uint32_t* __restrict__ kc, uint32_t* __restrict__ pts,
+    uint32_t* __restrict__ fail) {
     __shared__ unsigned long long col[256 * 9];
     const uint32_t key = blockIdx.x;
+    if (kc && threadIdx.x < 2 * MSM_PT_WORDS) {
+        const uint32_t* src = kc + (size_t)KC_SLOT_WORDS * kslot[key];
+        const uint32_t t = threadIdx.x;
+        pts[(size_t)MSM_PT_WORDS * (t < MSM_PT_WORDS ? key : m + key) + (t % MSM_PT_WORDS)] = src[t];
+        if (t == MSM_PT_WORDS - 1 && src[t]) atomicOr(fail, 2u);  // the key did not decode
+    }
     unsigned long long s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (uint32_t t = key_off[key] + threadIdx.x; t < key_off[key + 1]; t += 256) {
         const uint32_t* a = ascal + 8 * (size_t)key_sig[t];
@@ -165,16 +179,25 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_keysum(
         uint32_t r[8];
         sc_reduce512(x, r);
         const uint64_t np = na + 1 + n;
-        msm_recode(r, lay, lay.nw, [&](int w, int d) { digits[(uint64_t)w * np + key] = (int16_t)d; });
+        if (kc) {
+            uint32_t lo[8], hi[8];
+            msm_split128(r, lo, hi);
+            msm_recode(lo, lay, lay.nw_z, [&](int w, int d) { digits[(uint64_t)w * np + key] = (int16_t)d; });
+            msm_recode(hi, lay, lay.nw_z, [&](int w, int d) { digits[(uint64_t)w * np + m + key] = (int16_t)d; });
+        } else {
+            msm_recode(r, lay, lay.nw, [&](int w, int d) { digits[(uint64_t)w * np + key] = (int16_t)d; });
+        }
     }
 }
 
 // One workgroup of 256: b = -(sum of the partials) mod l -> scal[0..8), digits of point na;
 // B's record -> pts[na]
+// Split form (b128 != null: a keyed batch over the key cache): b = lo + 2^128 hi, lo on B (point
+// na), hi on 2^128 B (point na - 1, record b128) -- every scalar in the z range.
 extern "C" __global__ void __launch_bounds__(256) k_msm_bscalar(
     uint64_t n, uint64_t na, uint32_t nparts, MsmLayout lay, const uint32_t* __restrict__ partial,
     const uint32_t* __restrict__ btab, uint32_t* __restrict__ scal, int16_t* __restrict__ digits,
-    uint32_t* __restrict__ pts) {
+    uint32_t* __restrict__ pts, const uint32_t* __restrict__ b128) {
     __shared__ unsigned long long col[256 * 9];
     unsigned long long s[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (uint32_t p = threadIdx.x; p < nparts; p += 256)
@@ -210,11 +233,43 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_bscalar(
         }
         for (int k = 0; k < 8; k++) scal[k] = b[k];
         const uint64_t np = na + 1 + n;
-        msm_recode(b, lay, lay.nw, [&](int w, int d) { digits[(uint64_t)w * np + na] = (int16_t)d; });
+        if (b128) {
+            uint32_t lo[8], hi[8];
+            msm_split128(b, lo, hi);
+            msm_recode(lo, lay, lay.nw_z, [&](int w, int d) { digits[(uint64_t)w * np + na] = (int16_t)d; });
+            msm_recode(hi, lay, lay.nw_z, [&](int w, int d) { digits[(uint64_t)w * np + na - 1] = (int16_t)d; });
+        } else {
+            msm_recode(b, lay, lay.nw, [&](int w, int d) { digits[(uint64_t)w * np + na] = (int16_t)d; });
+        }
     }
     if (threadIdx.x < MSM_PT_WORDS)  // B's record from the basepoint table's entry 1 (= 1*B)
         pts[(size_t)MSM_PT_WORDS * na + threadIdx.x] =
             threadIdx.x < 30 ? btab[PRECOMP_ENTRY_WORDS + threadIdx.x] : 0u;
+    if (b128 && threadIdx.x >= 64 && threadIdx.x < 64 + MSM_PT_WORDS)
+        pts[(size_t)MSM_PT_WORDS * (na - 1) + threadIdx.x - 64] = b128[threadIdx.x - 64];
+}
+
+// Committee key cache fill: lane i decompresses keys[i] into slot slots[i] = { A's MSM point
+// record | 2^128 A's record }, word 31 = 1 when A does not decode (checked by k_msm_keysum).
+// 2^128 A: 128 doublings, then one inversion to the affine record.  Runs once per new key.
+extern "C" __global__ void __launch_bounds__(64) k_keycache_fill(uint32_t cnt, const uint8_t* __restrict__ keys,
+                                                                 const uint32_t* __restrict__ slots,
+                                                                 uint32_t* __restrict__ cache) {
+    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= cnt) return;
+    uint32_t w[8];
+    msm_load8(keys + 32 * (size_t)i, w);
+    ge_p3 P;
+    const bool ok = ge_decompress(w, P);
+    uint32_t* e = cache + (size_t)KC_SLOT_WORDS * slots[i];
+    msm_store_point(e, P);
+    e[MSM_PT_WORDS - 1] = ok ? 0u : 1u;
+    const ge_precomp q = ge_p3_to_precomp(p3_dbl_n(P, 128));
+    store_fe(e + MSM_PT_WORDS, q.ypx);
+    store_fe(e + MSM_PT_WORDS + 10, q.ymx);
+    store_fe(e + MSM_PT_WORDS + 20, q.xy2d);
+    e[MSM_PT_WORDS + 30] = 0u;
+    e[MSM_PT_WORDS + 31] = 0u;
 }
 
 // Decompression, wave-uniform roles: waves [0, ceil(n/64)) decompress R_i into point na+1+i,
@@ -226,7 +281,7 @@ __device__ __forceinline__ void msm_points_block(uint32_t blk, const MsmPointArg
     const uint64_t rwaves = (n + 63) / 64;
     const bool is_r = (t >> 6) < rwaves;
     const uint64_t i = is_r ? t : t - 64 * rwaves;
-    if (i >= (is_r ? n : na)) return;
+    if (i >= (is_r ? n : g.ndec)) return;
     uint32_t w[8];
     msm_load8(is_r ? g.sig + 64 * i : g.apk + 32 * i, w);
     ge_p3 P;
@@ -641,6 +696,7 @@ struct MsmTailArgs {
     uint32_t* ctr;         // [nw + 1] arrival counters
     const uint32_t* fail;
     uint32_t* verdict;
+    uint32_t* runs;  // [2] accepted / rejected runs since staging (never reset by a run), or null
     uint32_t S;
     unsigned long long* stamps;  // diagnostics (NWV_TAIL_STAMPS): [nw][8] s_memrealtime, or null
 };
@@ -807,6 +863,8 @@ __device__ __forceinline__ void msm_tail_body(const MsmLayout& lay, const MsmTai
         const fe X = fe_from_limbs16(part4), Y = fe_from_limbs16(part4 + 16), Z = fe_from_limbs16(part4 + 32);
         const bool ok = fe_is_zero(X) && fe_eq(Y, Z) && *a.fail == 0;
         *a.verdict = ok ? 1u : 0u;
+        // per-run tally (runs of one batch are ordered on its stream: a plain increment)
+        if (a.runs) a.runs[ok ? 0 : 1] += 1u;
     }
     NWV_TAIL_STAMP(6);
 }

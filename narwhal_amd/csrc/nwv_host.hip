@@ -15,6 +15,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/nwv.h"
@@ -122,15 +123,18 @@ struct EdBuffers {
         m_bsum, m_wsum, m_tpart, m_ctr, m_stamps;
     // keyed batches: distinct keys (m x 32), CSR of signatures by key, per-signature z_i k_i
     DevBuf keys, koff, ksig, m_ascal;
+    DevBuf kslot;  // keyed batches over the key cache: each distinct key's cache slot
     DevBuf in;  // staging arena: pk, sig, off, len, m_state and msg are views into it
     size_t nkeys_distinct = 0;  // 0: every signature is its own A point
+    bool kc_split = false;      // keyed batch whose keys are all in the device's key cache
     void release() {
         for (DevBuf* b : {&pk, &sig, &msg, &off, &len, &kbuf, &flags, &tables, &verdict, &m_scal,
                           &m_partial, &m_state, &m_pts, &m_digits, &m_cnt, &m_tiles, &m_entries,
                           &m_kstart, &m_hpart, &m_bsum, &m_wsum, &m_tpart, &m_ctr, &m_stamps, &keys, &koff, &ksig, &m_ascal,
-                          &in})
+                          &kslot, &in})
             b->release();
         nkeys_distinct = 0;
+        kc_split = false;
     }
 };
 
@@ -156,12 +160,41 @@ struct Lane {
     hipEvent_t b2stage_ev = nullptr;
 };
 
-// One device of a context: the basepoint table and the pool of lanes (created on demand, up to
-// max_lanes; env NWV_LANES, default 4).
+// Committee key cache of a device.  fastcrypto decompresses a public key once, when it is
+// deserialized; keyed calls (the types layer, nwv_ed25519_verify_batch_keyed) name their keys,
+// so each key's point record and that of 2^128 A are computed once (k_keycache_fill) and kept
+// in HBM.  A keyed batch whose keys are all cached then carries every MSM scalar in 128 bits
+// (K = lo + 2^128 hi on A and 2^128 A, the same for B): half the windows and half the final
+// doubling chain, and no key decompression in k_msm_prep.  Slots are append-only (a slot in
+// use by an in-flight or captured batch is never rewritten); when the cache is full a call
+// uses the uncached form.  Slot 0 holds B.
+struct Key32 {
+    uint8_t b[32];
+    bool operator==(const Key32& o) const { return std::memcmp(b, o.b, 32) == 0; }
+};
+struct Key32Hash {
+    size_t operator()(const Key32& k) const {
+        uint64_t h;
+        std::memcpy(&h, k.b, 8);
+        return (size_t)(h ^ (h >> 29));
+    }
+};
+struct KeyCache {
+    std::mutex mu;
+    std::unordered_map<Key32, uint32_t, Key32Hash> slot;
+    DevBuf recs;  // cap x KC_SLOT_WORDS words
+    uint32_t used = 0, cap = 0;
+    bool broken = false;  // allocation or fill failed once: stay uncached
+    bool b_ready = false;  // slot 0 (B) filled
+};
+
+// One device of a context: the basepoint table, the key cache and the pool of lanes (created on
+// demand, up to max_lanes; env NWV_LANES, default 4).
 struct Gpu {
     int ordinal = -1;
     uint32_t flags = 0;
     DevBuf btab;
+    KeyCache kc;
     std::mutex mu;  // guards the pool
     std::condition_variable cv;
     std::vector<Lane*> lanes, idle;
@@ -294,6 +327,7 @@ void gpu_close(Gpu& g) {
     g.lanes.clear();
     g.idle.clear();
     g.btab.release();
+    g.kc.recs.release();
 }
 
 // --------------------------------------------------------------- Ed25519 pipeline ------
@@ -352,7 +386,9 @@ struct MsmPlan {
 // Base width c minimises  7 Fmul x entries + 18 Fmul x buckets  (SURVEY.md §8d K5 cost model:
 // one mixed addition per nonzero digit, two full additions per bucket in the running-sum
 // reduction).
-MsmPlan msm_plan(size_t n, size_t na) {
+// split: a keyed batch over the key cache (na = 2m + 1 points before B, every scalar < 2^128):
+// only the z range, nw == nw_z.
+MsmPlan msm_plan(size_t n, size_t na, bool split = false) {
     MsmPlan p;
     p.na = na;
     p.np = (uint64_t)na + 1 + n;
@@ -361,8 +397,9 @@ MsmPlan msm_plan(size_t n, size_t na) {
     // chosen separately for the z range (all na + 1 + n points) and the range above it (na + 1)
     for (int c_lo = 6; c_lo <= 15; c_lo++)
         for (int c_hi = 3; c_hi <= 15; c_hi++) {
+            if (split && c_hi > 3) break;
             MsmLayout L;
-            if (!msm_make_layout2(c_lo, c_hi, L)) continue;
+            if (!(split ? msm_make_layout_z(c_lo, L) : msm_make_layout2(c_lo, c_hi, L))) continue;
             const double entries = (double)(na + 1) * L.nw + (double)n * L.nw_z;
             const double cost = 7.0 * entries + 18.0 * L.kbase[L.nw];
             if (cost < best) {
@@ -388,6 +425,13 @@ MsmPlan msm_plan(size_t n, size_t na) {
         while (p.tail_S < 64 && (long)(p.tail_S << 1) <= v) p.tail_S <<= 1;
     }
     return p;
+}
+
+// points before B: the A points (n, or the m distinct keys), or A and 2^128 A per cached key
+// and 2^128 B (split form)
+size_t msm_na(const EdBuffers& b, size_t n) {
+    if (!b.nkeys_distinct) return n;
+    return b.kc_split ? 2 * b.nkeys_distinct + 1 : b.nkeys_distinct;
 }
 
 constexpr size_t MSM_CTR_BYTES = 256;  // k_msm_tail arrival counters (nw + 1 <= 49 words)
@@ -429,11 +473,12 @@ constexpr int MSM_NEVENTS = MSM_NKERNELS + 1;  // one event before each kernel, 
 int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStream_t stream,
                hipEvent_t* ev, bool state_ready) {
     if (n == 0) return NWV_OK;
-    const size_t na = b.nkeys_distinct ? b.nkeys_distinct : n;
-    const MsmPlan p = msm_plan(n, na);
+    const size_t na = msm_na(b, n);
+    const MsmPlan p = msm_plan(n, na, b.kc_split);
     int rc = msm_alloc(b, p, n);
     if (rc) return rc;
-    uint32_t* state = b.m_state.as<uint32_t>();  // [0] fail flags, [1] verdict, [8..16) seed
+    // [0] fail flags, [1] verdict, [2..4) accepted / rejected run tally, [8..16) seed
+    uint32_t* state = b.m_state.as<uint32_t>();
     if (seed32 && !state_ready) NWV_HIP(hipMemcpyAsync(state + 8, seed32, 32, hipMemcpyHostToDevice, stream));
     const unsigned nblk = (unsigned)((n + 255) / 256);
     auto mark = [&](int k) -> int {
@@ -447,7 +492,8 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     const MsmScalarArgs gs{(uint64_t)n, (uint64_t)na, keyed, b.pk.as<uint8_t>(), b.sig.as<uint8_t>(),
                            b.msg.as<uint8_t>(), b.off.as<uint64_t>(), b.len.as<uint32_t>(), state + 8,
                            b.m_ascal.as<uint32_t>(), digits, b.m_partial.as<uint32_t>(), state};
-    const MsmPointArgs gp{(uint64_t)n, (uint64_t)na, keyed ? b.keys.as<uint8_t>() : b.pk.as<uint8_t>(),
+    const MsmPointArgs gp{(uint64_t)n, (uint64_t)na, b.kc_split ? 0 : (uint64_t)na,
+                          keyed ? b.keys.as<uint8_t>() : b.pk.as<uint8_t>(),
                           b.sig.as<uint8_t>(), b.m_pts.as<uint32_t>(), state};
     const size_t waves = (n + 63) / 64 + (na + 63) / 64;
     const unsigned pblk = (unsigned)((64 * waves + 255) / 256);
@@ -456,14 +502,17 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
         hipLaunchKernelGGL(k_msm_prep, dim3(nblk + pblk), dim3(256), 0, stream, gs, p.lay, gp, nblk);
     else
         hipLaunchKernelGGL(k_msm_scalars, dim3(nblk), dim3(256), 0, stream, gs, p.lay);
+    const uint32_t* kc = b.kc_split ? d.gpu->kc.recs.as<uint32_t>() : nullptr;
     if (keyed)
-        hipLaunchKernelGGL(k_msm_keysum, dim3((unsigned)na), dim3(256), 0, stream, (uint64_t)n, (uint64_t)na,
-                           p.lay, b.koff.as<uint32_t>(), b.ksig.as<uint32_t>(), b.m_ascal.as<uint32_t>(), digits);
+        hipLaunchKernelGGL(k_msm_keysum, dim3((unsigned)b.nkeys_distinct), dim3(256), 0, stream, (uint64_t)n,
+                           (uint64_t)na, p.lay, b.koff.as<uint32_t>(), b.ksig.as<uint32_t>(), b.m_ascal.as<uint32_t>(),
+                           digits, (uint32_t)b.nkeys_distinct, b.kslot.as<uint32_t>(), kc, b.m_pts.as<uint32_t>(),
+                           state);
     if ((rc = mark(1))) return rc;
     hipLaunchKernelGGL(k_msm_bscalar, dim3(1), dim3(256), 0, stream, (uint64_t)n, (uint64_t)na, (uint32_t)nblk,
                        p.lay,
                        b.m_partial.as<uint32_t>(), d.btab().as<uint32_t>(), b.m_scal.as<uint32_t>(), digits,
-                       b.m_pts.as<uint32_t>());
+                       b.m_pts.as<uint32_t>(), kc ? kc + MSM_PT_WORDS : nullptr);
     if ((rc = mark(2))) return rc;
     if (!fused) hipLaunchKernelGGL(k_msm_points, dim3(pblk), dim3(256), 0, stream, gp);
     if ((rc = mark(3))) return rc;
@@ -510,7 +559,7 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
         NWV_HIP(hipMemsetAsync(st_buf, 0, 8 * 8 * (size_t)MSM_MAX_WINDOWS, stream));
     }
     const MsmTailArgs ta{b.m_bsum.as<uint32_t>(), b.m_tpart.as<uint32_t>(), b.m_wsum.as<uint32_t>(),
-                         b.m_ctr.as<uint32_t>(), state, state + 1, p.tail_S, st_buf};
+                         b.m_ctr.as<uint32_t>(), state, state + 1, state + 2, p.tail_S, st_buf};
     // combine items per thread: (lg C + 1) x S_w over the windows (C = nb / S_w buckets per chunk)
     int items = 0;
     for (int w = 0; w < p.lay.nw; w++) {
@@ -615,6 +664,7 @@ struct KeyedTail {
     size_t m;
     const uint32_t* koff;  // m + 1
     const uint32_t* ksig;  // n
+    const uint32_t* kslot;  // m key cache slots, or null (uncached)
 };
 
 int ed_stage(Lane& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, const uint8_t* sig,
@@ -641,7 +691,8 @@ int ed_stage(Lane& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, con
     const size_t o_state = o_len + up(4 * n + 4), o_msg = o_state + 256, o_keys = up(o_msg + mbytes + MSG_PAD);
     const size_t m = kt ? kt->m : 0;
     const size_t o_koff = o_keys + (kt ? up(32 * m + 32) : 0), o_ksig = o_koff + (kt ? up(4 * m + 8) : 0);
-    const size_t total = o_ksig + (kt ? up(4 * n + 8) : 0);
+    const size_t o_kslot = o_ksig + (kt ? up(4 * n + 8) : 0);
+    const size_t total = o_kslot + (kt && kt->kslot ? up(4 * m + 8) : 0);
     int rc;
     if ((rc = b.in.ensure(total))) return rc;
     // views into the arena are stale once it may have moved: drop the ones not re-pointed below
@@ -651,6 +702,7 @@ int ed_stage(Lane& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, con
     if (!kt)
         for (DevBuf* v : {&b.keys, &b.koff, &b.ksig})
             if (v->view) v->release();
+    if ((!kt || !kt->kslot) && b.kslot.view) b.kslot.release();
     if (!inputs && ((rc = b.pk.ensure(32 * n + 16)) || (rc = b.sig.ensure(64 * n + 16)))) return rc;
     // the previous call's copy must have left the pinned buffer before it is rewritten
     htrace("stage:ensure");
@@ -675,6 +727,7 @@ int ed_stage(Lane& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, con
         if (m) std::memcpy(h + o_keys, kt->keys, 32 * m);
         std::memcpy(h + o_koff, kt->koff, 4 * (m + 1));
         if (n) std::memcpy(h + o_ksig, kt->ksig, 4 * n);
+        if (kt->kslot) std::memcpy(h + o_kslot, kt->kslot, 4 * m);
     }
     htrace("stage:packed");
     if (piped) {
@@ -715,8 +768,99 @@ int ed_stage(Lane& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, con
         b.keys.set_view(g + o_keys, 32 * m + 32);
         b.koff.set_view(g + o_koff, 4 * m + 8);
         b.ksig.set_view(g + o_ksig, 4 * n + 8);
+        if (kt->kslot) b.kslot.set_view(g + o_kslot, 4 * m + 8);
     }
     b.nkeys_distinct = m;
+    b.kc_split = kt && kt->kslot && m;
+    return NWV_OK;
+}
+
+// Cache slots of m distinct keys on d's device (misses are filled first, on d.stream, under the
+// cache lock); out is left empty when the call should go uncached (cache disabled or full, or
+// more keys than NWV_KEYCACHE_MAX_KEYS: a batch of mostly fresh keys would pay 128 doublings
+// per key for nothing).
+int keycache_slots(Lane& d, const uint8_t* keys, size_t m, std::vector<uint32_t>& out) {
+    out.clear();
+    static const long max_keys = [] {
+        const char* e = std::getenv("NWV_KEYCACHE_MAX_KEYS");
+        return e ? std::strtol(e, nullptr, 10) : 4096L;
+    }();
+    if (m == 0 || (d.flags & NWV_FLAG_NO_KEYCACHE) || (long)m > max_keys) return NWV_OK;
+    KeyCache& kc = d.gpu->kc;
+    std::lock_guard<std::mutex> g(kc.mu);
+    if (kc.broken) return NWV_OK;
+    constexpr uint32_t kCap = 1u << 16;  // 16 MiB of records
+    if (!kc.cap) {
+        // allocated once at full size: captured graphs and in-flight batches hold its address
+        if (kc.recs.ensure((size_t)4 * KC_SLOT_WORDS * kCap)) {
+            kc.broken = true;
+            return NWV_OK;
+        }
+        kc.cap = kCap;
+        kc.used = 1;  // slot 0: B (filled with the first misses below)
+    }
+    out.resize(m);
+    thread_local std::vector<uint8_t> miss_keys;
+    thread_local std::vector<uint32_t> miss_slots;
+    miss_keys.clear();
+    miss_slots.clear();
+    if (!kc.b_ready) {  // first fill: B into slot 0
+        uint32_t bw[8];
+        ge_basepoint_words(bw);
+        miss_keys.insert(miss_keys.end(), (const uint8_t*)bw, (const uint8_t*)bw + 32);
+        miss_slots.push_back(0);
+    }
+    std::vector<Key32> fresh;
+    uint32_t next = kc.used;
+    for (size_t j = 0; j < m; j++) {
+        Key32 k;
+        std::memcpy(k.b, keys + 32 * j, 32);
+        auto it = kc.slot.find(k);
+        if (it != kc.slot.end()) {
+            out[j] = it->second;
+            continue;
+        }
+        // a key repeated inside one call gets one slot (keys are distinct per call, but be safe)
+        bool dup = false;
+        for (size_t f = 0; f < fresh.size() && !dup; f++)
+            if (fresh[f] == k) {
+                out[j] = miss_slots[miss_slots.size() - fresh.size() + f];
+                dup = true;
+            }
+        if (dup) continue;
+        if (next >= kc.cap) {  // full: this call goes uncached, nothing is published
+            out.clear();
+            return NWV_OK;
+        }
+        fresh.push_back(k);
+        miss_keys.insert(miss_keys.end(), keys + 32 * j, keys + 32 * j + 32);
+        miss_slots.push_back(next);
+        out[j] = next++;
+    }
+    if (!miss_slots.empty()) {
+        const size_t cnt = miss_slots.size();
+        DevBuf tmp;
+        auto fail = [&](int rc) {
+            tmp.release();
+            kc.broken = true;
+            out.clear();
+            return rc;
+        };
+        if (tmp.ensure(36 * cnt + 64)) return fail(NWV_OK);
+        uint8_t* tk = tmp.as<uint8_t>();
+        uint32_t* ts = reinterpret_cast<uint32_t*>(tk + 32 * cnt);
+        if (hipMemcpyAsync(tk, miss_keys.data(), 32 * cnt, hipMemcpyHostToDevice, d.stream) != hipSuccess ||
+            hipMemcpyAsync(ts, miss_slots.data(), 4 * cnt, hipMemcpyHostToDevice, d.stream) != hipSuccess)
+            return fail(set_err(NWV_ERR_HIP, "key cache upload"));
+        hipLaunchKernelGGL(k_keycache_fill, dim3((unsigned)((cnt + 63) / 64)), dim3(64), 0, d.stream, (uint32_t)cnt,
+                           tk, ts, kc.recs.as<uint32_t>());
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(d.stream) != hipSuccess)
+            return fail(set_err(NWV_ERR_HIP, "key cache fill"));
+        tmp.release();
+        for (size_t f = 0; f < fresh.size(); f++) kc.slot.emplace(fresh[f], miss_slots[miss_slots.size() - fresh.size() + f]);
+        kc.b_ready = true;
+        kc.used = next;
+    }
     return NWV_OK;
 }
 
@@ -754,7 +898,10 @@ int ed_stage_keyed(Lane& d, EdBuffers& b, size_t lo, size_t hi, size_t n_keys, c
     for (size_t k = 0; k < m; k++) koff[k + 1] = koff[k] + cnt[k];
     cur.assign(koff.begin(), koff.end() - 1);
     for (size_t i = 0; i < n; i++) ksig[cur[kid[i]]++] = (uint32_t)i;
-    const KeyedTail kt{klist.data(), m, koff.data(), ksig.data()};
+    thread_local std::vector<uint32_t> kslot;
+    int rc = keycache_slots(d, klist.data(), m, kslot);
+    if (rc) return rc;
+    const KeyedTail kt{klist.data(), m, koff.data(), ksig.data(), kslot.empty() ? nullptr : kslot.data()};
     return ed_stage(d, b, 0, n, pk.data(), sig + 64 * lo, msg_base, msg_off + lo, msg_len + lo, seed32, &kt,
                     dev_msg);
 }
@@ -807,6 +954,7 @@ struct nwv_staged {
     bool pending_timing = false;
     hipGraphExec_t graph = nullptr;  // captured batch MSM (mode 1)
     bool graph_failed = false;
+    bool tally_ready = false;  // m_state[2..4) zeroed before the first mode-1 run
     // per-run coefficient seeds go to the device from a ring of pinned slots, so a graph replay is
     // two truly asynchronous calls (a pageable copy may wait for the stream)
     static constexpr int SEED_SLOTS = 64;
@@ -1279,6 +1427,13 @@ int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]) {
     if (mode == 1) {
         uint8_t seed[32];
         fill_seed(seed32, seed);
+        if (!st->tally_ready && st->n) {
+            // the run tally (m_state[2..4)) starts at zero and no run ever resets it
+            const size_t na = msm_na(st->buf, st->n);
+            if ((rc = msm_alloc(st->buf, msm_plan(st->n, na, st->buf.kc_split), st->n))) return rc;
+            NWV_HIP(hipMemsetAsync(st->buf.m_state.as<uint32_t>() + 2, 0, 8, st->stream));
+            st->tally_ready = true;
+        }
         if (!timed && st->graph) {
             const int slot = (int)(st->seed_runs++ % nwv_staged::SEED_SLOTS);
             if ((rc = st->seeds.ensure(32 * nwv_staged::SEED_SLOTS))) return rc;
@@ -1378,6 +1533,21 @@ int nwv_staged_kernel_times(nwv_staged* st, int mode, int cap, const char** name
     return total;
 }
 
+int nwv_staged_run_tally(nwv_staged* st, uint64_t out[2]) {
+    if (!st || !out) return set_err(NWV_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> g(st->mu);
+    int rc = staged_sync_locked(st);
+    if (rc) return rc;
+    out[0] = out[1] = 0;
+    if (!st->tally_ready) return NWV_OK;
+    uint32_t w[2] = {0, 0};
+    NWV_HIP(hipMemcpyAsync(w, st->buf.m_state.as<uint32_t>() + 2, 8, hipMemcpyDeviceToHost, st->stream));
+    NWV_HIP(hipStreamSynchronize(st->stream));
+    out[0] = w[0];
+    out[1] = w[1];
+    return NWV_OK;
+}
+
 int nwv_staged_msm_stats(nwv_staged* st, uint64_t out[8]) {
     if (!st || !out) return set_err(NWV_ERR_ARG, "null argument");
     std::lock_guard<std::mutex> g(st->mu);
@@ -1385,8 +1555,8 @@ int nwv_staged_msm_stats(nwv_staged* st, uint64_t out[8]) {
     if (rc) return rc;
     std::memset(out, 0, 8 * sizeof(uint64_t));
     if (!st->n) return NWV_OK;
-    const size_t na = st->buf.nkeys_distinct ? st->buf.nkeys_distinct : st->n;
-    const MsmPlan p = msm_plan(st->n, na);
+    const size_t na = msm_na(st->buf, st->n);
+    const MsmPlan p = msm_plan(st->n, na, st->buf.kc_split);
     out[0] = p.np;
     out[1] = (uint64_t)p.lay.nw;
     out[2] = (uint64_t)p.lay.nw_z;

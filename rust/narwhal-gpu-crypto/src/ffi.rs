@@ -254,6 +254,7 @@ extern "C" {
         reset: c_int,
     ) -> c_int;
     pub fn nwv_staged_msm_stats(st: *mut NwvStaged, out: *mut u64) -> c_int;
+    pub fn nwv_staged_run_tally(st: *mut NwvStaged, out: *mut u64) -> c_int;
     pub fn nwv_staged_free(st: *mut NwvStaged);
     // ---- synthetic signing, for workloads and tests (include/nwv.h)
     pub fn nwv_ed25519_sign_many(

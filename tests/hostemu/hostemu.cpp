@@ -270,14 +270,20 @@ void he_sign(const uint8_t* seed, const uint8_t* msg, uint32_t len, uint8_t* pk_
 // Batch verification through the K5 MSM, sequentially on the host with the device arithmetic
 // (msm.h): same point layout, window layout, recoding, bucket rule, G-lane window reduction and
 // Horner as narwhal_amd/csrc/msm_kernels.hip, without the parallel sort.  Returns the verdict.
-int he_msm_batch(size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
-                 const uint32_t* len, const uint8_t* seed32, int c, int G, unsigned long long* counts) {
+//
+// split != 0: the key-cache form (k_keycache_fill / k_msm_keysum / k_msm_bscalar with a cache):
+// points [0, n) A_i with lo(z_i k_i), [n, 2n) 2^128 A_i with hi(z_i k_i), 2n = 2^128 B with hi(b),
+// 2n + 1 = B with lo(b), then the R_i; every scalar < 2^128, z-only layout (msm_make_layout_z).
+static int msm_batch_impl(size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
+                          const uint32_t* len, const uint8_t* seed32, int c, int G, unsigned long long* counts,
+                          bool split) {
     ensure_btab();
     MsmLayout lay;
-    if (!msm_make_layout(c, lay)) return -1;
+    if (!(split ? msm_make_layout_z(c, lay) : msm_make_layout(c, lay))) return -1;
     uint32_t seed[8];
     std::memcpy(seed, seed32, 32);
-    const size_t np = 2 * n + 1;
+    const size_t na = split ? 2 * n + 1 : n;  // points before B
+    const size_t np = na + 1 + n;
     std::vector<uint32_t> scal(8 * np, 0), pts(MSM_PT_WORDS * np);
     bool ok = true;
     unsigned long long col[9] = {0};
@@ -292,16 +298,27 @@ int he_msm_batch(size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t*
         msm_z(seed, i, z);
         sc_mul(z, k, a);
         sc_mul(z, Sw, zs);
+        uint32_t lo[8], hi[8];
+        msm_split128(a, lo, hi);
         for (int t = 0; t < 8; t++) {
-            scal[8 * i + t] = a[t];
-            scal[8 * (n + 1 + i) + t] = z[t];
+            scal[8 * i + t] = split ? lo[t] : a[t];
+            if (split) scal[8 * (n + i) + t] = hi[t];
+            scal[8 * (na + 1 + i) + t] = z[t];
             col[t] += zs[t];
         }
         ge_p3 P;
         ok &= ge_decompress(Aw, P);
         msm_store_point(pts.data() + MSM_PT_WORDS * i, P);
+        if (split) {  // the cache's second record, as k_keycache_fill builds it
+            const ge_precomp q = ge_p3_to_precomp(p3_dbl_n(P, 128));
+            uint32_t* e = pts.data() + MSM_PT_WORDS * (n + i);
+            store_fe(e, q.ypx);
+            store_fe(e + 10, q.ymx);
+            store_fe(e + 20, q.xy2d);
+            e[30] = e[31] = 0u;
+        }
         ok &= ge_decompress(Rw, P);
-        msm_store_point(pts.data() + MSM_PT_WORDS * (n + 1 + i), P);
+        msm_store_point(pts.data() + MSM_PT_WORDS * (na + 1 + i), P);
     }
     {
         uint32_t x[16];
@@ -316,18 +333,37 @@ int he_msm_batch(size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t*
         uint32_t nz = 0;
         for (int t = 0; t < 8; t++) nz |= r[t];
         long long br = 0;
+        uint32_t b[8];
         for (int t = 0; t < 8; t++) {
             long long d = (long long)sc_l(t) - r[t] + br;
-            scal[8 * n + t] = nz ? (uint32_t)d : 0u;
+            b[t] = nz ? (uint32_t)d : 0u;
             br = d >> 32;
         }
-        msm_point_from_precomp(pts.data() + MSM_PT_WORDS * n, g_btab.data() + PRECOMP_ENTRY_WORDS);
+        uint32_t lo[8], hi[8];
+        msm_split128(b, lo, hi);
+        for (int t = 0; t < 8; t++) {
+            scal[8 * na + t] = split ? lo[t] : b[t];
+            if (split) scal[8 * (na - 1) + t] = hi[t];
+        }
+        msm_point_from_precomp(pts.data() + MSM_PT_WORDS * na, g_btab.data() + PRECOMP_ENTRY_WORDS);
+        if (split) {
+            uint32_t bw[8];
+            ge_basepoint_words(bw);
+            ge_p3 Bp;
+            ge_decompress(bw, Bp);
+            const ge_precomp q = ge_p3_to_precomp(p3_dbl_n(Bp, 128));
+            uint32_t* e = pts.data() + MSM_PT_WORDS * (na - 1);
+            store_fe(e, q.ypx);
+            store_fe(e + 10, q.ymx);
+            store_fe(e + 20, q.xy2d);
+            e[30] = e[31] = 0u;
+        }
     }
     nwv_count_mul = nwv_count_sq = 0;
     const uint32_t nkeys = lay.kbase[lay.nw];
     std::vector<std::vector<uint32_t>> buckets(nkeys);
     for (size_t j = 0; j < np; j++) {
-        msm_recode(&scal[8 * j], lay, j <= n ? lay.nw : lay.nw_z, [&](int w, int d) {
+        msm_recode(&scal[8 * j], lay, j <= na ? lay.nw : lay.nw_z, [&](int w, int d) {
             if (d) buckets[lay.kbase[w] + (d < 0 ? -d : d) - 1].push_back((uint32_t)j | (d < 0 ? MSM_NEG : 0u));
         });
     }
@@ -373,6 +409,15 @@ int he_msm_batch(size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t*
         counts[1] = nwv_count_sq;
     }
     return (ok && eq) ? 1 : 0;
+}
+
+int he_msm_batch(size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
+                 const uint32_t* len, const uint8_t* seed32, int c, int G, unsigned long long* counts) {
+    return msm_batch_impl(n, pk, sig, msg, off, len, seed32, c, G, counts, false);
+}
+int he_msm_batch_split(size_t n, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
+                       const uint32_t* len, const uint8_t* seed32, int c, int G) {
+    return msm_batch_impl(n, pk, sig, msg, off, len, seed32, c, G, nullptr, true);
 }
 
 // signed digits of a 256-bit scalar over layout(c): z range (bits = 128) or full range (253);

@@ -21,6 +21,21 @@ def eng():
     e.close()
 
 
+@pytest.fixture(scope="module")
+def eng_nokc():
+    """keyed calls without the committee key cache (full-width scalars, keys decompressed per call)"""
+    import narwhal_amd
+    from narwhal_amd import _lib
+    e = narwhal_amd.Engine(device=0, flags=_lib.NWV_FLAG_MSM_ALWAYS | _lib.NWV_FLAG_NO_KEYCACHE)
+    yield e
+    e.close()
+
+
+@pytest.fixture(params=["keycache", "nokeycache"])
+def keng(request, eng, eng_nokc):
+    return eng if request.param == "keycache" else eng_nokc
+
+
 def _v(v):
     return bytes.fromhex(v["pk"]), bytes.fromhex(v["sig"]), bytes.fromhex(v["msg"])
 
@@ -139,6 +154,10 @@ def test_staged_graph_replay_valid_and_invalid(eng):
         st.run(mode=1, seed=bytes([r + 9]) * 32)
         allv, bits = st.fetch()
         assert allv and bits.all()
+    # back-to-back replays with no host read in between: the device-side tally sees every one
+    for r in range(7):
+        st.run(mode=1)
+    assert st.run_tally() == (12, 0)
     st.free()
     sg2 = sg.copy()
     sg2[64 * 1234 + 50] ^= 8
@@ -147,6 +166,7 @@ def test_staged_graph_replay_valid_and_invalid(eng):
         st.run(mode=1, seed=bytes([r + 1]) * 32)
         allv, bits = st.fetch()
         assert not allv and list(np.flatnonzero(~bits)) == [1234]
+    assert st.run_tally() == (0, 4)
     st.free()
 
 
@@ -162,9 +182,10 @@ def _keyed(items):
 
 
 @pytest.mark.parametrize("n,m", [(1, 1), (300, 4), (5000, 100), (20000, 7)])
-def test_keyed_batches_committee(eng, n, m):
+def test_keyed_batches_committee(keng, n, m):
     """one MSM point per distinct key (configs[1] m = 100 variant, committee batches): valid
     batches accept; one forged signature is pinpointed exactly"""
+    eng = keng
     rnd = np.random.default_rng(n + m)
     kseeds = [rnd.bytes(32) for _ in range(m)]
     msgs = [rnd.bytes(32) for _ in range(n)]
@@ -181,9 +202,15 @@ def test_keyed_batches_committee(eng, n, m):
     sigs[bad] = bytes(s)
     ok, bits = eng.verify_batch_keyed(keys, kidx, sigs, msgs)
     assert not ok and [i for i in range(n) if not bits[i]] == [bad]
+    # the same keys again (cache hits), in another order and with a subset of the committee
+    perm = list(range(m))[::-1]
+    keys2 = [keys[j] for j in perm]
+    kidx2 = [perm.index(k) for k in kidx]
+    ok, bits = eng.verify_batch_keyed(keys2, kidx2, [x[1] for x in items], msgs)
+    assert ok and all(bits)
 
 
-def test_keyed_golden_and_bad_keys(eng):
+def test_keyed_golden_and_bad_keys(keng):
     """golden / ZIP-215 vectors (small-order, non-canonical and undecodable keys) keyed by their
     raw key bytes: verdicts equal the oracle's, and an unused undecodable key changes nothing"""
     g = of.load_golden("ed25519_vectors.json")["vectors"]
@@ -191,6 +218,7 @@ def test_keyed_golden_and_bad_keys(eng):
     items = [_v(v) for v in g + z]
     keys, kidx = _keyed(items)
     want = [of.verify(*it) for it in items]
+    eng = keng
     ok, bits = eng.verify_batch_keyed(keys, kidx, [s for _, s, _ in items], [m for _, _, m in items])
     assert bits == want and ok == all(want)
     good = [it for it, w in zip(items, want) if w]
@@ -199,6 +227,12 @@ def test_keyed_golden_and_bad_keys(eng):
     assert not of.lib().or_point_decompress_ok(undecodable)
     ok, bits = eng.verify_batch_keyed(keys + [undecodable], kidx, [s for _, s, _ in good], [m for _, _, m in good])
     assert ok and all(bits)
+    # every signature valid but one signer's key undecodable (cached with its failure flag on the
+    # first call, a cache hit on the second): the batch rejects, the fallback pinpoints exactly it
+    for _ in range(2):
+        ok, bits = eng.verify_batch_keyed(keys + [undecodable], kidx + [len(keys)],
+                                          [s for _, s, _ in good] + [good[0][1]], [m for _, _, m in good] + [b"x"])
+        assert not ok and [i for i in range(len(bits)) if not bits[i]] == [len(good)]
 
 
 def test_staged_keyed_msm(eng):

@@ -26,13 +26,16 @@ def he():
     lib = ctypes.CDLL(HE_PATH)
     vp = ctypes.c_void_p
     lib.he_msm_batch.argtypes = [ctypes.c_size_t, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]
+    lib.he_msm_batch_split.argtypes = [ctypes.c_size_t, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int]
     lib.he_msm_recode.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, vp]
     lib.he_msm_layout.argtypes = [ctypes.c_int, vp]
     lib.he_msm_z.argtypes = [ctypes.c_char_p, ctypes.c_uint64, vp]
     return lib
 
 
-def msm_batch(he, items, c, G, seed=b"\x11" * 32, counts=None):
+def msm_batch(he, items, c, G, seed=b"\x11" * 32, counts=None, split=False):
+    """split: the key-cache form (every scalar split at 2^128 over A / 2^128 A and B / 2^128 B,
+    z-only window layout), as k_keycache_fill + k_msm_keysum + k_msm_bscalar run it"""
     pk = np.frombuffer(b"".join(p for p, _, _ in items) + b"\0" * 16, dtype=np.uint8)
     sg = np.frombuffer(b"".join(s for _, s, _ in items) + b"\0" * 16, dtype=np.uint8)
     msgs = [m for _, _, m in items]
@@ -43,6 +46,11 @@ def msm_batch(he, items, c, G, seed=b"\x11" * 32, counts=None):
     arena = np.frombuffer(b"".join(msgs) + b"\0" * 16, dtype=np.uint8)
     sd = np.frombuffer(seed, dtype=np.uint8)
     cp = counts.ctypes.data if counts is not None else None
+    if split:
+        r = he.he_msm_batch_split(len(items), pk.ctypes.data, sg.ctypes.data, arena.ctypes.data,
+                                  offs.ctypes.data, lens.ctypes.data, sd.ctypes.data, c, G)
+        assert r in (0, 1)
+        return bool(r)
     r = he.he_msm_batch(len(items), pk.ctypes.data, sg.ctypes.data, arena.ctypes.data, offs.ctypes.data,
                         lens.ctypes.data, sd.ctypes.data, c, G, cp)
     assert r in (0, 1)
@@ -222,6 +230,31 @@ def test_all_small_order_batch_accepts(he):
     z = of.load_golden("zip215_small_order.json")["vectors"]
     items = [(bytes.fromhex(v["pk"]), bytes.fromhex(v["sig"]), bytes.fromhex(v["msg"])) for v in z]
     assert msm_batch(he, items, 7, 64)
+
+
+@pytest.mark.parametrize("c,G", [(6, 8), (9, 64), (13, 256), (15, 64)])
+def test_split_form_valid_batches_accept(he, c, G):
+    rnd = random.Random(700 + c)
+    assert msm_batch(he, honest(rnd, 11, mlen=40), c, G, split=True)
+
+
+def test_split_form_invalid_and_zip215_match_oracle(he):
+    """key-cache form: one forged signature rejects; every golden / ZIP-215 vector inside a
+    batch gives the AND of the oracle's per-signature verdicts (small-order A included: its
+    2^128 multiple is the identity, and K A = lo A + hi 2^128 A holds for every group element)"""
+    rnd = random.Random(23)
+    items = honest(rnd, 6)
+    pk, sg, m = items[4]
+    items_bad = list(items)
+    items_bad[4] = (pk, sg[:40] + bytes([sg[40] ^ 2]) + sg[41:], m)
+    assert not msm_batch(he, items_bad, 8, 16, split=True)
+    g = of.load_golden("ed25519_vectors.json")["vectors"]
+    z = of.load_golden("zip215_small_order.json")["vectors"]
+    vecs = [(bytes.fromhex(v["pk"]), bytes.fromhex(v["sig"]), bytes.fromhex(v["msg"])) for v in g + z[::7]]
+    for k, v in enumerate(vecs):
+        batch = items[:2] + [v] + items[2:4]
+        want = all(of.verify(*it) for it in batch)
+        assert msm_batch(he, batch, 7 if k % 2 else 10, 16, split=True) == want, (k, v)
 
 
 def test_point_kernel_op_count_matches_bench(he):
