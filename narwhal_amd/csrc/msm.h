@@ -189,6 +189,49 @@ NWV_HD void msm_split128(const uint32_t s[8], uint32_t lo[8], uint32_t hi[8]) {
     }
 }
 
+// Fixed-base comb for the basepoint term.  B's scalar b = -sum z_i s_i is known only after every
+// signature is hashed, and as an MSM point B would put a full-width scalar (and a sort / bucket
+// dependency on b) into every window.  Instead [8 b]B = sum_j [d_j 16^j] B over the 64 signed
+// radix-16 digits d_j in [-8, 8] of c = 8 b mod l, from a per-device table of i 16^j B
+// (i = 1..8, affine Niels records), is summed by the last hash workgroup of k_msm_prep while
+// the other blocks still decompress, and joins the MSM tail's final sum.  (B has prime order l,
+// so [8]([b]B) = [8 b mod l]B.)
+static constexpr int COMB_TABLES = 64, COMB_ENTRIES = 8;
+
+// i 16^j B (1 <= i <= 8) as an MSM point record (affine Niels)
+NWV_HD void comb_entry(int j, int i, uint32_t* e) {
+    uint32_t bw[8];
+    ge_basepoint_words(bw);
+    ge_p3 B;
+    ge_decompress(bw, B);
+    ge_p3 Q = j ? p3_dbl_n(B, 4 * j) : B;
+    const ge_cached cq = ge_p3_to_cached(Q);
+    ge_p3 acc = ge_p3_identity();
+    for (int bit = 3; bit >= 0; bit--) {
+        acc = ge_p3_dbl(acc);
+        if ((i >> bit) & 1) acc = ge_p1p1_to_p3(ge_add(acc, cq));
+    }
+    const ge_precomp q = ge_p3_to_precomp(acc);
+    store_fe(e, q.ypx);
+    store_fe(e + 10, q.ymx);
+    store_fe(e + 20, q.xy2d);
+    e[30] = e[31] = 0u;
+}
+
+// signed radix-16 digits of c < 2^253: c = sum_{j < 64} d_j 16^j, d_j in [-8, 8)  (d_63 <= 2)
+NWV_HD void comb_digits(const uint32_t c[8], int d[COMB_TABLES]) {
+    int carry = 0;
+    for (int j = 0; j < COMB_TABLES; j++) {
+        int v = (int)((c[j >> 3] >> (4 * (j & 7))) & 15u) + carry;
+        carry = 0;
+        if (j + 1 < COMB_TABLES && v >= 8) {
+            v -= 16;
+            carry = 1;
+        }
+        d[j] = v;
+    }
+}
+
 // Committee key cache slot: A's point record, then 2^128 A's (msm_store_point layout); word
 // MSM_PT_WORDS - 1 of the first record is 1 when A failed to decode.  Slot 0 holds B.
 static constexpr int KC_SLOT_WORDS = 64;

@@ -4,8 +4,8 @@
 //   k_msm_scalars   lane i: k_i = SHA-512(R||A||M) mod l, s_i < l, z_i = PRF(seed, i),
 //                   scalars z_i k_i and z_i recoded to signed digits -> digits[w][.] (i16);
 //                   per-workgroup partial sums of z_i s_i
-//   k_msm_bscalar   one workgroup: b = -sum z_i s_i mod l (the basepoint's scalar), its digits,
-//                   B's point record
+//                   the last hash workgroup: b = -sum z_i s_i mod l and the basepoint term
+//                   [8 b]B from a fixed-base comb table (msm.h), off the MSM
 //   k_msm_points    2 lanes per signature (wave-uniform R / A roles): decompress, store the
 //                   128-byte affine Niels record of each point
 //   k_msm_hist      workgroup (chunk, window): LDS histogram of the window's bucket ids
@@ -42,6 +42,18 @@ __device__ __forceinline__ void msm_store8(uint32_t* p, const uint32_t w[8]) {
     q[1] = make_uint4(w[4], w[5], w[6], w[7]);
 }
 
+__device__ __forceinline__ ge_p3 shfl_down_p3(const ge_p3& p, int o) {
+    ge_p3 r;
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+        r.X.v[k] = (uint32_t)__shfl_down((int)p.X.v[k], o, 64);
+        r.Y.v[k] = (uint32_t)__shfl_down((int)p.Y.v[k], o, 64);
+        r.Z.v[k] = (uint32_t)__shfl_down((int)p.Z.v[k], o, 64);
+        r.T.v[k] = (uint32_t)__shfl_down((int)p.T.v[k], o, 64);
+    }
+    return r;
+}
+
 }  // namespace
 
 // digits: [window][na+1+n] signed digits of every point's scalar (A points at [0, na), B's
@@ -60,6 +72,9 @@ struct MsmScalarArgs {
     int16_t* digits;
     uint32_t* partial;
     uint32_t* fail;
+    // B is not an MSM point (its term comes from the fixed-base comb, k_msm_tail): workgroup 0
+    // zeroes its digit column (point na, and na - 1 = 2^128 B's column of the key-cache form)
+    uint32_t split;
 };
 struct MsmPointArgs {
     uint64_t n, na;
@@ -123,6 +138,11 @@ __device__ __forceinline__ void msm_scalars_block(uint32_t blk, const MsmScalarA
             c >>= 32;
         }
         out[8] = (uint32_t)c;
+    }
+    if (blk == 0 && threadIdx.x < (unsigned)lay.nw) {  // B's digit column(s) stay empty
+        const uint64_t np = na + 1 + n;
+        digits[(uint64_t)threadIdx.x * np + na] = 0;
+        if (g.split) digits[(uint64_t)threadIdx.x * np + na - 1] = 0;
     }
 }
 
@@ -190,63 +210,11 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_keysum(
     }
 }
 
-// One workgroup of 256: b = -(sum of the partials) mod l -> scal[0..8), digits of point na;
-// B's record -> pts[na]
-// Split form (b128 != null: a keyed batch over the key cache): b = lo + 2^128 hi, lo on B (point
-// na), hi on 2^128 B (point na - 1, record b128) -- every scalar in the z range.
-extern "C" __global__ void __launch_bounds__(256) k_msm_bscalar(
-    uint64_t n, uint64_t na, uint32_t nparts, MsmLayout lay, const uint32_t* __restrict__ partial,
-    const uint32_t* __restrict__ btab, uint32_t* __restrict__ scal, int16_t* __restrict__ digits,
-    uint32_t* __restrict__ pts, const uint32_t* __restrict__ b128) {
-    __shared__ unsigned long long col[256 * 9];
-    unsigned long long s[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t p = threadIdx.x; p < nparts; p += 256)
-#pragma unroll
-        for (int k = 0; k < 9; k++) s[k] += partial[9 * p + k];
-#pragma unroll
-    for (int k = 0; k < 9; k++) col[threadIdx.x * 9 + k] = s[k];
-    __syncthreads();
-    if (threadIdx.x < 9) {
-        unsigned long long t = 0;
-        for (int r = 0; r < 256; r++) t += col[r * 9 + threadIdx.x];  // < 2^(32+13+8)
-        col[threadIdx.x] = t;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t x[16];
-        unsigned long long c = 0;
-        for (int k = 0; k < 16; k++) {
-            if (k < 9) c += col[k];
-            x[k] = (uint32_t)c;
-            c >>= 32;
-        }
-        uint32_t r[8], b[8];
-        sc_reduce512(x, r);
-        // b = l - r (mod l)
-        uint32_t nz = 0;
-        for (int k = 0; k < 8; k++) nz |= r[k];
-        long long br = 0;
-        for (int k = 0; k < 8; k++) {
-            long long d = (long long)sc_l(k) - r[k] + br;
-            b[k] = nz ? (uint32_t)d : 0u;
-            br = d >> 32;
-        }
-        for (int k = 0; k < 8; k++) scal[k] = b[k];
-        const uint64_t np = na + 1 + n;
-        if (b128) {
-            uint32_t lo[8], hi[8];
-            msm_split128(b, lo, hi);
-            msm_recode(lo, lay, lay.nw_z, [&](int w, int d) { digits[(uint64_t)w * np + na] = (int16_t)d; });
-            msm_recode(hi, lay, lay.nw_z, [&](int w, int d) { digits[(uint64_t)w * np + na - 1] = (int16_t)d; });
-        } else {
-            msm_recode(b, lay, lay.nw, [&](int w, int d) { digits[(uint64_t)w * np + na] = (int16_t)d; });
-        }
-    }
-    if (threadIdx.x < MSM_PT_WORDS)  // B's record from the basepoint table's entry 1 (= 1*B)
-        pts[(size_t)MSM_PT_WORDS * na + threadIdx.x] =
-            threadIdx.x < 30 ? btab[PRECOMP_ENTRY_WORDS + threadIdx.x] : 0u;
-    if (b128 && threadIdx.x >= 64 && threadIdx.x < 64 + MSM_PT_WORDS)
-        pts[(size_t)MSM_PT_WORDS * (na - 1) + threadIdx.x - 64] = b128[threadIdx.x - 64];
+// One-time per device: the fixed-base comb table, entry 8 j + i - 1 = i 16^j B (msm.h)
+extern "C" __global__ void __launch_bounds__(64) k_comb_table(uint32_t* comb) {
+    const int e = blockIdx.x * 64 + threadIdx.x;
+    if (e >= COMB_TABLES * COMB_ENTRIES) return;
+    comb_entry(e / COMB_ENTRIES, e % COMB_ENTRIES + 1, comb + MSM_PT_WORDS * e);
 }
 
 // Committee key cache fill: lane i decompresses keys[i] into slot slots[i] = { A's MSM point
@@ -695,6 +663,10 @@ struct MsmTailArgs {
     uint32_t* wsc;         // [nw] scaled window sums (P3)
     uint32_t* ctr;         // [nw + 1] arrival counters
     const uint32_t* fail;
+    uint32_t* bpt;             // [8 b]B (P3): the basepoint term (workgroup row nw)
+    const uint32_t* partial;   // k_msm_prep's per-workgroup sums of z_i s_i (nblk x 9 words)
+    const uint32_t* comb;      // fixed-base comb table
+    uint32_t nblk;
     uint32_t* verdict;
     uint32_t* runs;  // [2] accepted / rejected runs since staging (never reset by a run), or null
     uint32_t S;
@@ -733,6 +705,66 @@ __device__ __forceinline__ bool tail_arrive(uint32_t* ctr, uint32_t expect, uint
 
 }  // namespace
 
+// The basepoint term (one extra workgroup of k_msm_tail, running beside the windows' bucket
+// sums): b = -(sum of k_msm_prep's per-workgroup partial sums of z_i s_i) mod l, c = 8 b mod l,
+// [c]B = sum of 64 comb entries (wave 0: one entry per lane, then a six-level butterfly of
+// additions) -> bpt.
+__device__ __forceinline__ void msm_bterm(const uint32_t* __restrict__ partial, uint32_t nblk,
+                                          const uint32_t* __restrict__ comb, uint32_t* __restrict__ bpt) {
+    __shared__ unsigned long long wcol[4][9];
+    __shared__ int dig[COMB_TABLES];
+    const int t = threadIdx.x, wid = t >> 6, lane = t & 63;
+    unsigned long long s[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t q = t; q < nblk; q += 256)
+#pragma unroll
+        for (int k = 0; k < 9; k++) s[k] += partial[9 * (size_t)q + k];  // < 2^32 each, < 2^16 of them
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        unsigned long long v = s[k];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (lane == 0) wcol[wid][k] = v;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t x[16];
+        unsigned long long c = 0;
+        for (int k = 0; k < 16; k++) {
+            if (k < 9) c += wcol[0][k] + wcol[1][k] + wcol[2][k] + wcol[3][k];
+            x[k] = (uint32_t)c;
+            c >>= 32;
+        }
+        uint32_t r[8], b[8], c8[8];
+        sc_reduce512(x, r);
+        uint32_t nz = 0;
+        for (int k = 0; k < 8; k++) nz |= r[k];
+        long long br = 0;
+        for (int k = 0; k < 8; k++) {  // b = l - r (mod l)
+            const long long d = (long long)sc_l(k) - r[k] + br;
+            b[k] = nz ? (uint32_t)d : 0u;
+            br = d >> 32;
+        }
+        const uint32_t eight[8] = {8u, 0, 0, 0, 0, 0, 0, 0};
+        sc_mul(b, eight, c8);
+        int d[COMB_TABLES];
+        comb_digits(c8, d);
+        for (int j = 0; j < COMB_TABLES; j++) dig[j] = d[j];
+    }
+    __syncthreads();
+    if (wid == 0) {  // (no early return: the caller's arrival barrier follows)
+        const int dj = dig[lane], a = dj < 0 ? -dj : dj;
+        ge_p3 P = ge_p3_identity();
+        if (a)
+            P = ge_p1p1_to_p3(ge_madd(P, msm_load_point(comb + MSM_PT_WORDS * (COMB_ENTRIES * lane + a - 1), dj < 0)));
+#pragma unroll 1
+        for (int o = 1; o < 64; o <<= 1) {
+            const ge_p3 Q = shfl_down_p3(P, o);
+            if (!(lane & (2 * o - 1))) P = p3_add(P, Q);
+        }
+        if (lane == 0) store_p3(bpt, P);
+    }
+}
+
 #define NWV_TAIL_STAMP(slot)                                                                       \
     do {                                                                                           \
         if (a.stamps && t == 0) a.stamps[8 * w + (slot)] = __builtin_amdgcn_s_memrealtime();       \
@@ -741,18 +773,17 @@ __device__ __forceinline__ bool tail_arrive(uint32_t* ctr, uint32_t expect, uint
 // PER: combine items per thread (1 when every window's (lg C + 1) x S_w <= 256, else 3).  The
 // variant with one item needs 163 VGPRs instead of 216; fewer registers held by the tail's
 // long-lived waves leave room for other batches' waves on the same SIMDs.
+// Workgroup (s, row) of a window row: chunk s of window w = nw - row.  Returns true (uniformly) in
+// the workgroup that arrives last at the final counter (windows and the basepoint term).
 template <int PER>
-__device__ __forceinline__ void msm_tail_body(const MsmLayout& lay, const MsmTailArgs& a) {
-    // 256 point slots of P3_WORDS; row-limb planes reuse the front once the slots are done;
-    // the flag word sits behind the slots
-    extern __shared__ uint32_t lds[];
-    uint32_t* flag = lds + 256 * P3_WORDS;
-    // top window first: its sum precedes the longest doubling chain, and workgroups are
+__device__ __forceinline__ bool msm_tail_window(const MsmLayout& lay, const MsmTailArgs& a, uint32_t* lds,
+                                                uint32_t* flag) {
+    // top window first (row 1): its sum precedes the longest doubling chain, and workgroups are
     // dispatched in blockIdx order (a grid larger than the chip runs in waves)
-    const int t = threadIdx.x, w = lay.nw - 1 - (int)blockIdx.y, s = blockIdx.x;
+    const int t = threadIdx.x, w = lay.nw - (int)blockIdx.y, s = blockIdx.x;
     const int nb = 1 << (lay.width[w] - 1);
     const int Sw = (int)a.S < nb ? (int)a.S : nb;
-    if (s >= Sw) return;  // whole workgroup
+    if (s >= Sw) return false;  // whole workgroup
     const int C = nb / Sw, lgC = tail_lg(C), lgS = tail_lg(Sw);
     if (s == 0) NWV_TAIL_STAMP(0);
     // ---- chunk butterfly: lane 0 -> R_s, lane 2^k -> T_{s,k}
@@ -768,7 +799,7 @@ __device__ __forceinline__ void msm_tail_body(const MsmLayout& lay, const MsmTai
     uint32_t* mypart = a.part + (size_t)P3_WORDS * TAIL_PART_SLOTS * ((size_t)w * a.S + s);
     if (t == 0) store_p3(mypart, p);
     if (t < C && t && !(t & (t - 1))) store_p3(mypart + P3_WORDS * (1 + tail_lg(t)), p);
-    if (!tail_arrive(a.ctr + w, (uint32_t)Sw, flag)) return;
+    if (!tail_arrive(a.ctr + w, (uint32_t)Sw, flag)) return false;
     NWV_TAIL_STAMP(1);
     // ---- last chunk of window w: per plane, a butterfly over the Sw chunks.  Item j = q * Sw + s:
     // plane group q < lgC sums T_{s,q}; group lgC is the butterfly of the R_s.
@@ -827,17 +858,36 @@ __device__ __forceinline__ void msm_tail_body(const MsmLayout& lay, const MsmTai
     __syncthreads();
     NWV_TAIL_STAMP(4);
     if (t < 4) store_fe(a.wsc + (size_t)P3_WORDS * w + 10 * t, fe_from_limbs16(out + 16 * t));
-    if (!tail_arrive(a.ctr + lay.nw, (uint32_t)lay.nw, flag)) return;
+    return tail_arrive(a.ctr + lay.nw, (uint32_t)lay.nw + 1, flag);
+}
+
+template <int PER>
+__device__ __forceinline__ void msm_tail_body(const MsmLayout& lay, const MsmTailArgs& a) {
+    // 256 point slots of P3_WORDS; row-limb planes reuse the front once the slots are done;
+    // the flag word sits behind the slots
+    extern __shared__ uint32_t lds[];
+    uint32_t* flag = lds + 256 * P3_WORDS;
+    const int t = threadIdx.x;
+    if (blockIdx.y == 0) {
+        // row 0: the basepoint term, one workgroup beside the windows
+        if (blockIdx.x != 0) return;
+        msm_bterm(a.partial, a.nblk, a.comb, a.bpt);
+        if (!tail_arrive(a.ctr + lay.nw, (uint32_t)lay.nw + 1, flag)) return;
+    } else if (!msm_tail_window<PER>(lay, a, lds, flag)) {
+        return;
+    }
+    const int w = blockIdx.y ? lay.nw - (int)blockIdx.y : lay.nw - 1;  // stamp slot of the last arrival
     NWV_TAIL_STAMP(5);
-    // ---- last window: sum of the nw scaled windows on 16-lane rows (wave q adds the windows
-    // w = q mod 4, then wave 0 adds the other three partial sums), identity test
-    uint32_t* cq = lds;                          // [nw][64] cached row limbs
-    uint32_t* part4 = lds + 64 * MSM_MAX_WINDOWS;  // [4][64] partial sums X | Y | Z | T
-    uint32_t* cq4 = part4 + 256;                 // [3][64] cached row limbs of partials 1..3
-    uint32_t* sc = cq4 + 192;                    // [4][192] multiply scratch, one per wave
-    const int nw = lay.nw;
+    // ---- last window: sum of the nw scaled windows and the basepoint term on 16-lane rows (wave
+    // q adds the items i = q mod 4, then wave 0 adds the other three partial sums), identity test
+    uint32_t* cq = lds;                                // [nw + 1][64] cached row limbs
+    uint32_t* part4 = lds + 64 * (MSM_MAX_WINDOWS + 1);  // [4][64] partial sums X | Y | Z | T
+    uint32_t* cq4 = part4 + 256;                       // [3][64] cached row limbs of partials 1..3
+    uint32_t* sc = cq4 + 192;                          // [4][192] multiply scratch, one per wave
+    const int nw = lay.nw + 1;                         // items: the windows, then [8 b]B
     if (t < 4 * nw) {
-        const ge_p3 x = load_p3(a.wsc + (size_t)P3_WORDS * (t >> 2));
+        const int it = t >> 2;
+        const ge_p3 x = load_p3(it < lay.nw ? a.wsc + (size_t)P3_WORDS * it : a.bpt);
         const int c = t & 3;
         fe v = c == 0 ? fe_add(x.Y, x.X) : c == 1 ? fe_sub(x.Y, x.X) : c == 2 ? fe_mul(x.T, fe_d2()) : fe_add(x.Z, x.Z);
         fe_to_limbs16(fe_carry(v), cq + 64 * (t >> 2) + 16 * c);

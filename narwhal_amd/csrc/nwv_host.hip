@@ -120,7 +120,7 @@ struct PinnedBuf {
 struct EdBuffers {
     DevBuf pk, sig, msg, off, len, kbuf, flags, tables, verdict;
     DevBuf m_scal, m_partial, m_state, m_pts, m_digits, m_cnt, m_tiles, m_entries, m_kstart, m_hpart,
-        m_bsum, m_wsum, m_tpart, m_ctr, m_stamps;
+        m_bsum, m_wsum, m_tpart, m_ctr, m_stamps, m_bpt;
     // keyed batches: distinct keys (m x 32), CSR of signatures by key, per-signature z_i k_i
     DevBuf keys, koff, ksig, m_ascal;
     DevBuf kslot;  // keyed batches over the key cache: each distinct key's cache slot
@@ -130,7 +130,7 @@ struct EdBuffers {
     void release() {
         for (DevBuf* b : {&pk, &sig, &msg, &off, &len, &kbuf, &flags, &tables, &verdict, &m_scal,
                           &m_partial, &m_state, &m_pts, &m_digits, &m_cnt, &m_tiles, &m_entries,
-                          &m_kstart, &m_hpart, &m_bsum, &m_wsum, &m_tpart, &m_ctr, &m_stamps, &keys, &koff, &ksig, &m_ascal,
+                          &m_kstart, &m_hpart, &m_bsum, &m_wsum, &m_tpart, &m_ctr, &m_stamps, &m_bpt, &keys, &koff, &ksig, &m_ascal,
                           &kslot, &in})
             b->release();
         nkeys_distinct = 0;
@@ -194,6 +194,7 @@ struct Gpu {
     int ordinal = -1;
     uint32_t flags = 0;
     DevBuf btab;
+    DevBuf comb;  // fixed-base comb table of the MSM's basepoint term (msm.h)
     KeyCache kc;
     std::mutex mu;  // guards the pool
     std::condition_variable cv;
@@ -312,6 +313,9 @@ int gpu_open(Gpu& g, int ordinal, uint32_t flags) {
     g.idle.push_back(l);
     hipLaunchKernelGGL(k_base_table, dim3((BASE_TABLE_ENTRIES + 63) / 64), dim3(64), 0, l->stream,
                        g.btab.as<uint32_t>());
+    if ((rc = g.comb.ensure((size_t)4 * MSM_PT_WORDS * COMB_TABLES * COMB_ENTRIES))) return rc;
+    hipLaunchKernelGGL(k_comb_table, dim3((COMB_TABLES * COMB_ENTRIES + 63) / 64), dim3(64), 0, l->stream,
+                       g.comb.as<uint32_t>());
     NWV_HIP(hipGetLastError());
     NWV_HIP(hipStreamSynchronize(l->stream));
     return NWV_OK;
@@ -327,6 +331,7 @@ void gpu_close(Gpu& g) {
     g.lanes.clear();
     g.idle.clear();
     g.btab.release();
+    g.comb.release();
     g.kc.recs.release();
 }
 
@@ -439,7 +444,7 @@ constexpr size_t MSM_CTR_BYTES = 256;  // k_msm_tail arrival counters (nw + 1 <=
 int msm_alloc(EdBuffers& b, const MsmPlan& p, size_t n) {
     const size_t nblk = (n + 255) / 256;
     int rc;
-    if ((rc = b.m_scal.ensure(64)) || (b.nkeys_distinct && (rc = b.m_ascal.ensure(32 * n + 32))) || (rc = b.m_partial.ensure(36 * nblk + 36)) ||
+    if ((b.nkeys_distinct && (rc = b.m_ascal.ensure(32 * n + 32))) || (rc = b.m_partial.ensure(36 * nblk + 36)) ||
         (rc = b.m_state.ensure(128)) ||
         (rc = b.m_pts.ensure((size_t)4 * MSM_PT_WORDS * p.np + 64)) ||
         (rc = b.m_digits.ensure((size_t)2 * p.lay.nw * p.np + 64)) ||
@@ -451,7 +456,7 @@ int msm_alloc(EdBuffers& b, const MsmPlan& p, size_t n) {
         (rc = b.m_bsum.ensure((size_t)4 * P3_WORDS * p.nkeys + 64)) ||
         (rc = b.m_wsum.ensure((size_t)4 * P3_WORDS * p.lay.nw + 64)) ||
         (rc = b.m_tpart.ensure((size_t)4 * P3_WORDS * TAIL_PART_SLOTS * p.lay.nw * p.tail_S + 64)) ||
-        (rc = b.m_ctr.ensure(MSM_CTR_BYTES)))
+        (rc = b.m_ctr.ensure(MSM_CTR_BYTES)) || (rc = b.m_bpt.ensure(4 * P3_WORDS + 64)))
         return rc;
     return NWV_OK;
 }
@@ -460,10 +465,10 @@ static const char* const ED_KERNEL_NAMES[] = {"k_ed_hash", "k_ed_points", "k_ed_
 // event slots of one batch MSM; nullptr = no kernel in that slot (k_msm_prep runs the hash and
 // the decompression as one grid unless NWV_FLAG_MSM_SPLIT_PREP)
 static const char* const MSM_KERNEL_NAMES[] = {
-    "k_msm_prep", "k_msm_bscalar", nullptr, "k_msm_hist", "k_msm_wscan",
+    "k_msm_prep", nullptr, nullptr, "k_msm_hist", "k_msm_wscan",
     "k_msm_scatter", "k_msm_bucket+fixup", "k_msm_tail", nullptr};
 static const char* const MSM_KERNEL_NAMES_SPLIT[] = {
-    "k_msm_scalars", "k_msm_bscalar", "k_msm_points", "k_msm_hist", "k_msm_wscan",
+    "k_msm_scalars", nullptr, "k_msm_points", "k_msm_hist", "k_msm_wscan",
     "k_msm_scatter", "k_msm_bucket+fixup", "k_msm_tail", nullptr};
 constexpr int MSM_NKERNELS = 9;
 constexpr int MSM_NEVENTS = MSM_NKERNELS + 1;  // one event before each kernel, one after the last
@@ -491,7 +496,8 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     const int keyed = b.nkeys_distinct ? 1 : 0;
     const MsmScalarArgs gs{(uint64_t)n, (uint64_t)na, keyed, b.pk.as<uint8_t>(), b.sig.as<uint8_t>(),
                            b.msg.as<uint8_t>(), b.off.as<uint64_t>(), b.len.as<uint32_t>(), state + 8,
-                           b.m_ascal.as<uint32_t>(), digits, b.m_partial.as<uint32_t>(), state};
+                           b.m_ascal.as<uint32_t>(), digits, b.m_partial.as<uint32_t>(), state,
+                           b.kc_split ? 1u : 0u};
     const MsmPointArgs gp{(uint64_t)n, (uint64_t)na, b.kc_split ? 0 : (uint64_t)na,
                           keyed ? b.keys.as<uint8_t>() : b.pk.as<uint8_t>(),
                           b.sig.as<uint8_t>(), b.m_pts.as<uint32_t>(), state};
@@ -509,10 +515,6 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
                            digits, (uint32_t)b.nkeys_distinct, b.kslot.as<uint32_t>(), kc, b.m_pts.as<uint32_t>(),
                            state);
     if ((rc = mark(1))) return rc;
-    hipLaunchKernelGGL(k_msm_bscalar, dim3(1), dim3(256), 0, stream, (uint64_t)n, (uint64_t)na, (uint32_t)nblk,
-                       p.lay,
-                       b.m_partial.as<uint32_t>(), d.btab().as<uint32_t>(), b.m_scal.as<uint32_t>(), digits,
-                       b.m_pts.as<uint32_t>(), kc ? kc + MSM_PT_WORDS : nullptr);
     if ((rc = mark(2))) return rc;
     if (!fused) hipLaunchKernelGGL(k_msm_points, dim3(pblk), dim3(256), 0, stream, gp);
     if ((rc = mark(3))) return rc;
@@ -548,8 +550,8 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     hipLaunchKernelGGL(k_msm_fixup, dim3((p.nkeys + 255) / 256), dim3(256), 0, stream, p.nkeys,
                        p.seg, kst, E, b.m_hpart.as<uint32_t>(), b.m_bsum.as<uint32_t>());
     if ((rc = mark(7))) return rc;
-    // window sums, their scaling and the verdict: one launch (its arrival counters are zeroed by
-    // a memset node first, graph replays included)
+    // window sums, their scaling, the basepoint term and the verdict: one launch (its arrival
+    // counters are zeroed by a memset node first, graph replays included)
     NWV_HIP(hipMemsetAsync(b.m_ctr.p, 0, MSM_CTR_BYTES, stream));
     static const bool stamps = std::getenv("NWV_TAIL_STAMPS") != nullptr;  // diagnostics only
     unsigned long long* st_buf = nullptr;
@@ -559,7 +561,8 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
         NWV_HIP(hipMemsetAsync(st_buf, 0, 8 * 8 * (size_t)MSM_MAX_WINDOWS, stream));
     }
     const MsmTailArgs ta{b.m_bsum.as<uint32_t>(), b.m_tpart.as<uint32_t>(), b.m_wsum.as<uint32_t>(),
-                         b.m_ctr.as<uint32_t>(), state, state + 1, state + 2, p.tail_S, st_buf};
+                         b.m_ctr.as<uint32_t>(), state, b.m_bpt.as<uint32_t>(), b.m_partial.as<uint32_t>(),
+                         d.gpu->comb.as<uint32_t>(), nblk, state + 1, state + 2, p.tail_S, st_buf};
     // combine items per thread: (lg C + 1) x S_w over the windows (C = nb / S_w buckets per chunk)
     int items = 0;
     for (int w = 0; w < p.lay.nw; w++) {
@@ -569,10 +572,10 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
         items = std::max(items, (lgC + 1) * Sw);
     }
     if (items <= 256)
-        hipLaunchKernelGGL(k_msm_tail, dim3(p.tail_S, (unsigned)p.lay.nw), dim3(256), (size_t)4 * (256 * P3_WORDS + 4),
+        hipLaunchKernelGGL(k_msm_tail, dim3(p.tail_S, (unsigned)p.lay.nw + 1), dim3(256), (size_t)4 * (256 * P3_WORDS + 4),
                            stream, p.lay, ta);
     else
-        hipLaunchKernelGGL(k_msm_tail_wide, dim3(p.tail_S, (unsigned)p.lay.nw), dim3(256),
+        hipLaunchKernelGGL(k_msm_tail_wide, dim3(p.tail_S, (unsigned)p.lay.nw + 1), dim3(256),
                            (size_t)4 * (256 * P3_WORDS + 4), stream, p.lay, ta);
     if ((rc = mark(8))) return rc;
     if ((rc = mark(9))) return rc;

@@ -420,6 +420,41 @@ int he_msm_batch_split(size_t n, const uint8_t* pk, const uint8_t* sig, const ui
     return msm_batch_impl(n, pk, sig, msg, off, len, seed32, c, G, nullptr, true);
 }
 
+// The MSM's basepoint term as k_msm_prep's last hash workgroup computes it: c = 8 b mod l, its 64
+// signed radix-16 digits, the sum of the comb entries i 16^j B (msm.h comb_entry), against
+// [8]([b]B) by plain double-and-add.  Returns 1 when the two points are equal.
+int he_comb_check(const uint8_t* b32) {
+    uint32_t b[8], c[8];
+    words(b32, b);
+    const uint32_t eight[8] = {8u, 0, 0, 0, 0, 0, 0, 0};
+    sc_mul(b, eight, c);
+    int d[COMB_TABLES];
+    comb_digits(c, d);
+    ge_p3 acc = ge_p3_identity();
+    std::vector<uint32_t> e(MSM_PT_WORDS);
+    for (int j = 0; j < COMB_TABLES; j++) {
+        if (d[j] < -8 || d[j] > 8) return -1;
+        if (!d[j]) continue;
+        comb_entry(j, d[j] < 0 ? -d[j] : d[j], e.data());
+        acc = ge_p1p1_to_p3(ge_madd(acc, msm_load_point(e.data(), d[j] < 0)));
+    }
+    uint32_t bw[8];
+    ge_basepoint_words(bw);
+    ge_p3 B;
+    ge_decompress(bw, B);
+    const ge_cached cb = ge_p3_to_cached(B);
+    ge_p3 ref = ge_p3_identity();
+    for (int bit = 255; bit >= 0; bit--) {
+        ref = ge_p3_dbl(ref);
+        if ((b[bit >> 5] >> (bit & 31)) & 1) ref = ge_p1p1_to_p3(ge_add(ref, cb));
+    }
+    ref = p3_dbl_n(ref, 3);
+    uint32_t w1[8], w2[8];
+    ge_compress(acc, w1);
+    ge_compress(ref, w2);
+    return std::memcmp(w1, w2, 32) == 0 ? 1 : 0;
+}
+
 // signed digits of a 256-bit scalar over layout(c): z range (bits = 128) or full range (253);
 // out: nw, then (pos, digit) pairs
 int he_msm_recode(const uint8_t* s32, int c, int bits, int* out) {

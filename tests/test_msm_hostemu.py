@@ -27,6 +27,7 @@ def he():
     vp = ctypes.c_void_p
     lib.he_msm_batch.argtypes = [ctypes.c_size_t, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]
     lib.he_msm_batch_split.argtypes = [ctypes.c_size_t, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int]
+    lib.he_comb_check.argtypes = [ctypes.c_char_p]
     lib.he_msm_recode.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, vp]
     lib.he_msm_layout.argtypes = [ctypes.c_int, vp]
     lib.he_msm_z.argtypes = [ctypes.c_char_p, ctypes.c_uint64, vp]
@@ -35,7 +36,7 @@ def he():
 
 def msm_batch(he, items, c, G, seed=b"\x11" * 32, counts=None, split=False):
     """split: the key-cache form (every scalar split at 2^128 over A / 2^128 A and B / 2^128 B,
-    z-only window layout), as k_keycache_fill + k_msm_keysum + k_msm_bscalar run it"""
+    z-only window layout), as k_keycache_fill + k_msm_keysum run it"""
     pk = np.frombuffer(b"".join(p for p, _, _ in items) + b"\0" * 16, dtype=np.uint8)
     sg = np.frombuffer(b"".join(s for _, s, _ in items) + b"\0" * 16, dtype=np.uint8)
     msgs = [m for _, _, m in items]
@@ -255,6 +256,14 @@ def test_split_form_invalid_and_zip215_match_oracle(he):
         batch = items[:2] + [v] + items[2:4]
         want = all(of.verify(*it) for it in batch)
         assert msm_batch(he, batch, 7 if k % 2 else 10, 16, split=True) == want, (k, v)
+
+
+def test_basepoint_comb_term(he):
+    """[8 b]B from the fixed-base comb (64 signed radix-16 digits of 8 b mod l over the table
+    i 16^j B) equals [8]([b]B), for b = 0, 1, l - 1, 2^252 and random scalars mod l"""
+    rnd = random.Random(99)
+    for b in [0, 1, 2, L - 1, 2**252, 2**128 - 1] + [rnd.randrange(L) for _ in range(12)]:
+        assert he.he_comb_check(b.to_bytes(32, "little")) == 1, b
 
 
 def test_point_kernel_op_count_matches_bench(he):
