@@ -31,6 +31,11 @@ pub const NWV_ERR_NODEV: c_int = -4;
 pub const NWV_ERR_EMPTY: c_int = -5;
 pub const NWV_ERR_LENGTH: c_int = -6;
 pub const NWV_ABI_VERSION: c_int = 1;
+// nwv_init flags
+pub const NWV_FLAG_MSM_ALWAYS: u32 = 1;
+pub const NWV_FLAG_MSM_NEVER: u32 = 2;
+pub const NWV_FLAG_MSM_SPLIT_PREP: u32 = 4;
+pub const NWV_FLAG_NO_KEYCACHE: u32 = 8;
 
 pub const NWV_DAG_OK: i32 = 0;
 pub const NWV_DAG_INVALID_EPOCH: i32 = 10;
