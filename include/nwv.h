@@ -50,6 +50,10 @@ typedef struct nwv_ctx nwv_ctx;
  * decompresses its keys, full-width scalars).  Env NWV_KEYCACHE_MAX_KEYS (default 4096): keyed
  * calls with more distinct keys than this go uncached. */
 #define NWV_FLAG_NO_KEYCACHE 8u
+/* diagnostic / tests: the batch MSM's two-level counting sort (coarse bins, then each bin in one
+ * workgroup) whenever the sort has more than one chunk; by default it is used for windows of
+ * NWV_MSM_SORT2_MIN_PTS points or more (env, default 2^20) */
+#define NWV_FLAG_MSM_SORT2 16u
 
 /* ------------------------------------------------------------------ lifecycle ----- */
 /* Process-wide context creation (created once, in Primary::spawn).

@@ -311,6 +311,23 @@ NWV_HD void msm_recode(const uint32_t s[8], const MsmLayout& L, int nw, Emit emi
 // Bucket entry encoding: point index | sign bit
 static constexpr uint32_t MSM_NEG = 0x80000000u;
 
+// Two-level counting sort of large batches.  A one-level scatter of a window with 2^14 buckets
+// and 64 chunks writes runs of ~4 entries per (bucket, chunk) slice: every line of the entry
+// array is written piecemeal by many workgroups, and once a window's entries (16 MB at 2M
+// signatures) exceed an XCD's 4 MB L2 the pieces are written back separately.  The first level
+// sorts by the top bits of the bucket (bin (|d| - 1) >> shift: runs of ~64 entries per slice),
+// packing the low bits into the entry; the second (k_msm_lsort) orders each coarse bin by its low
+// bits inside one workgroup.  Packed entry: sign (bit 31) | low bits (shift of them, below bit 31)
+// | point index (31 - shift bits).
+static constexpr int MSM_SORT2_MAX_SHIFT = 8;
+NWV_HD uint32_t msm_pack2(uint32_t j, uint32_t b, bool neg, int shift) {
+    return j | ((b & ((1u << shift) - 1u)) << (31 - shift)) | (neg ? MSM_NEG : 0u);
+}
+NWV_HD uint32_t msm_unpack2_low(uint32_t e, int shift) { return (e >> (31 - shift)) & ((1u << shift) - 1u); }
+NWV_HD uint32_t msm_unpack2_entry(uint32_t e, int shift) {
+    return (e & ((1u << (31 - shift)) - 1u)) | (e & MSM_NEG);
+}
+
 // MSM point record: affine Niels (y+x | y-x | 2dxy) of a decompressed point (Z = 1, T = xy),
 // padded to 32 words = 128 bytes so a bucket lane's random gather touches one cache line; a
 // negative digit swaps y+x / y-x and negates 2dxy on the fly.

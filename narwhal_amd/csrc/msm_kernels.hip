@@ -42,6 +42,19 @@ __device__ __forceinline__ void msm_store8(uint32_t* p, const uint32_t w[8]) {
     q[1] = make_uint4(w[4], w[5], w[6], w[7]);
 }
 
+__device__ __forceinline__ fe fe_quad_bcast(const fe& a, int k) {
+    fe r;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        switch (k) {
+            case 0: r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.v[i], 0x00, 0xF, 0xF, false); break;
+            case 1: r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.v[i], 0x55, 0xF, 0xF, false); break;
+            case 2: r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.v[i], 0xAA, 0xF, 0xF, false); break;
+            default: r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.v[i], 0xFF, 0xF, 0xF, false); break;
+        }
+    }
+    return r;
+}
 __device__ __forceinline__ ge_p3 shfl_down_p3(const ge_p3& p, int o) {
     ge_p3 r;
 #pragma unroll
@@ -75,6 +88,7 @@ struct MsmScalarArgs {
     // B is not an MSM point (its term comes from the fixed-base comb, k_msm_tail): workgroup 0
     // zeroes its digit column (point na, and na - 1 = 2^128 B's column of the key-cache form)
     uint32_t split;
+    uint32_t* tail_ctr;  // k_msm_tail's arrival counters (64 words), zeroed by workgroup 0
 };
 struct MsmPointArgs {
     uint64_t n, na;
@@ -144,6 +158,7 @@ __device__ __forceinline__ void msm_scalars_block(uint32_t blk, const MsmScalarA
         digits[(uint64_t)threadIdx.x * np + na] = 0;
         if (g.split) digits[(uint64_t)threadIdx.x * np + na - 1] = 0;
     }
+    if (blk == 0 && threadIdx.x < 64) g.tail_ctr[threadIdx.x] = 0u;  // (no memset launch)
 }
 
 // Keyed batches (ed25519_consensus groups batch entries by verification key): one workgroup per
@@ -281,9 +296,13 @@ __device__ __forceinline__ uint64_t msm_window_points(uint64_t n, uint64_t na, i
 // grid (chunks, windows); counts laid out window by window, chunk-major inside a window:
 // cnt[kbase[w] * chunks + chunk * nb_w + b], so every workgroup stores one contiguous run; the
 // workgroup's nonzero digits -> nzc[w * chunks + chunk] (the windows' entry bases, k_msm_wscan)
+//
+// Two-level sort (large batches, msm.h MsmSort2): lay is the coarse layout (widths reduced by
+// shift) and every digit counts in bin (|d| - 1) >> shift; k_msm_scatter then writes packed
+// entries (msm_pack2) that k_msm_lsort orders by the remaining low bits.
 extern "C" __global__ void __launch_bounds__(256) k_msm_hist(
     uint64_t n, uint64_t na, MsmLayout lay, uint32_t chunk_pts, const int16_t* __restrict__ digits,
-    uint32_t* __restrict__ cnt, uint32_t* __restrict__ nzc) {
+    uint32_t* __restrict__ cnt, uint32_t* __restrict__ nzc, int shift) {
     extern __shared__ uint32_t hist[];
     __shared__ uint32_t nz;
     const int w = blockIdx.y, nw_z = lay.nw_z, nb = 1 << (lay.width[w] - 1);
@@ -299,7 +318,7 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_hist(
     for (uint64_t j = lo + threadIdx.x; j < hi; j += blockDim.x) {
         const int d = dw[j];
         if (d) {
-            atomicAdd(&hist[(d < 0 ? -d : d) - 1], 1u);
+            atomicAdd(&hist[((d < 0 ? -d : d) - 1) >> shift], 1u);
             mine++;
         }
     }
@@ -478,7 +497,8 @@ extern "C" __global__ void __launch_bounds__(1024) k_msm_sort1(
 // (the stride of the offsets)
 extern "C" __global__ void __launch_bounds__(256) k_msm_scatter(
     uint64_t n, uint64_t na, MsmLayout lay, MsmXcdMap xm, uint32_t chunks, uint32_t chunk_pts,
-    const int16_t* __restrict__ digits, const uint32_t* __restrict__ off, uint32_t* __restrict__ entries) {
+    const int16_t* __restrict__ digits, const uint32_t* __restrict__ off, uint32_t* __restrict__ entries,
+    int shift) {
     extern __shared__ uint32_t cur[];
     const uint32_t g = blockIdx.x % MSM_XCD_GROUPS;
     uint32_t s = blockIdx.x / MSM_XCD_GROUPS;
@@ -506,9 +526,45 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_scatter(
         const int d = dw[j];
         if (d) {
             const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
-            const uint32_t slot = atomicAdd(&cur[b], 1u);
-            entries[slot] = (uint32_t)j | (d < 0 ? MSM_NEG : 0u);
+            const uint32_t slot = atomicAdd(&cur[b >> shift], 1u);
+            entries[slot] = shift ? msm_pack2((uint32_t)j, b, d < 0, shift) : ((uint32_t)j | (d < 0 ? MSM_NEG : 0u));
         }
+    }
+}
+
+// Second level of the two-level sort: workgroup (s, w) orders coarse bin s of window w -- the
+// entries of buckets [s << shift, (s + 1) << shift), contiguous in mid after the first level --
+// by their low bucket bits, writing the final entries (j | sign) into the same index range of
+// entries and the buckets' start offsets.  The whole range is written by one workgroup (LDS
+// cursors), so its lines are written whole.
+extern "C" __global__ void __launch_bounds__(256) k_msm_lsort(
+    MsmLayout lay, MsmLayout lay2, int shift, const uint32_t* __restrict__ mid, const uint32_t* __restrict__ kst2,
+    const uint32_t* __restrict__ tot, uint32_t* __restrict__ entries, uint32_t* __restrict__ kstart) {
+    __shared__ uint32_t cur[1 << MSM_SORT2_MAX_SHIFT];
+    __shared__ uint32_t wsum[4];
+    const int w = blockIdx.y, s = blockIdx.x;
+    const int nb2 = 1 << (lay2.width[w] - 1), nlo = 1 << shift;
+    if (s >= nb2) return;  // whole workgroup
+    const uint32_t key2 = lay2.kbase[w] + s;
+    const uint32_t lo = kst2[key2];
+    const uint32_t hi = key2 + 1 < lay2.kbase[lay2.nw] ? kst2[key2 + 1] : tot[MSM_MAX_WINDOWS];
+    const int t = threadIdx.x;
+    if (t < nlo) cur[t] = 0;
+    __syncthreads();
+    for (uint32_t k = lo + t; k < hi; k += 256) atomicAdd(&cur[msm_unpack2_low(mid[k], shift)], 1u);
+    __syncthreads();
+    uint32_t total;
+    const uint32_t v = t < nlo ? cur[t] : 0u;
+    const uint32_t ex = block_excl_scan(v, wsum, total);
+    if (t < nlo) {
+        cur[t] = lo + ex;
+        kstart[lay.kbase[w] + ((uint32_t)s << shift) + t] = lo + ex;
+    }
+    __syncthreads();
+    for (uint32_t k = lo + t; k < hi; k += 256) {
+        const uint32_t e = mid[k];
+        const uint32_t slot = atomicAdd(&cur[msm_unpack2_low(e, shift)], 1u);
+        entries[slot] = msm_unpack2_entry(e, shift);
     }
 }
 
@@ -613,6 +669,78 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_bucket(
     }
 }
 
+// k_msm_bucket on quads (latency-bound small batches): quad g adds the entries [gT, gT + T), lane
+// q holding coordinate q (X, Y, Z, T) of the running sum.  A mixed addition is ge_madd's field
+// operations on the same operands (so the same magnitudes) in two multiply latencies instead of
+// seven: step 1 MM (q0), PP (q1), T xy2d (q2), 2Z (q3); the four broadcast in the quad (DPP);
+// step 2 the four products of ge_p1p1_to_p3.  Segment bookkeeping is identical on the quad's lanes.
+extern "C" __global__ void __launch_bounds__(256) k_msm_bucket_q(
+    uint32_t T, uint32_t nkeys, const uint32_t* __restrict__ total, const uint32_t* __restrict__ entries,
+    const uint32_t* __restrict__ kstart, const uint32_t* __restrict__ pts, uint32_t* __restrict__ bsum,
+    uint32_t* __restrict__ hpart) {
+    const uint32_t E = *total;
+    const int q = threadIdx.x & 3;
+    const uint64_t k0 = ((uint64_t)blockIdx.x * (blockDim.x >> 2) + (threadIdx.x >> 2)) * T;
+    if (k0 >= E) return;  // whole quad
+    const uint32_t k1 = (uint32_t)(k0 + T < E ? k0 + T : E);
+    uint32_t lo = 0, hi = nkeys;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (kstart[mid] <= k0) lo = mid;
+        else hi = mid;
+    }
+    uint32_t key = lo;
+    uint32_t kend = key + 1 < nkeys ? kstart[key + 1] : E;
+    bool head = kstart[key] < k0;
+    const bool q0 = q == 0, q1 = q == 1, q2 = q == 2, q3 = q == 3;
+    const fe ident = (q1 || q2) ? fe_one() : fe_zero();  // (0 : 1 : 1 : 0)
+    fe acc = ident;
+    const uint32_t zero = 0u - (T >> 31);
+    uint32_t wcur[32], wnext[32];
+    uint32_t v = entries[k0];
+    msm_load_raw(pts, v, wcur);
+#pragma unroll 1
+    for (uint32_t k = (uint32_t)k0; k < k1; k++) {
+        const uint32_t vn = entries[k + 1 < k1 ? k + 1 : k];
+        msm_load_raw(pts, vn, wnext);
+        const ge_precomp P = msm_point_of(wcur, v, zero);
+        const fe X = fe_quad_bcast(acc, 0), Y = fe_quad_bcast(acc, 1), Z = fe_quad_bcast(acc, 2),
+                 Tt = fe_quad_bcast(acc, 3);
+        const fe a = fe_select(fe_select(fe_select(Z, Tt, q2), fe_add(Y, X), q1), fe_sub(Y, X), q0);
+        const fe b = fe_select(fe_select(fe_select(fe_one(), P.xy2d, q2), P.ypx, q1), P.ymx, q0);
+        fe r = fe_mul(a, b);
+        if (q3) r = fe_carry(fe_add(Z, Z));
+        const fe MM = fe_quad_bcast(r, 0), PP = fe_quad_bcast(r, 1), TX = fe_quad_bcast(r, 2), Z2 = fe_quad_bcast(r, 3);
+        const fe cX = fe_sub(PP, MM), cY = fe_add(PP, MM), cZ = fe_add(Z2, TX), cT = fe_sub(Z2, TX);
+        const fe u = fe_select(fe_select(cZ, cY, q1), cX, q0 || q3);
+        const fe w2 = fe_select(fe_select(cY, cZ, q1), cT, q0 || q2);
+        acc = fe_mul(u, w2);
+        if (k + 1 == k1 || k + 1 == kend) {
+            uint32_t* out = head ? hpart + (size_t)P3_WORDS * (k0 / T) : bsum + (size_t)P3_WORDS * key;
+            store_fe(out + 10 * q, acc);
+            acc = ident;
+            head = false;
+            if (k + 1 < k1) {
+                key++;
+                kend = key + 1 < nkeys ? kstart[key + 1] : E;
+                if (kend <= k + 1) {  // empty keys follow: bisect for the key holding entry k + 1
+                    uint32_t l2 = key, h2 = nkeys;
+                    while (h2 - l2 > 1) {
+                        const uint32_t mid = (l2 + h2) >> 1;
+                        if (kstart[mid] <= k + 1) l2 = mid;
+                        else h2 = mid;
+                    }
+                    key = l2;
+                    kend = key + 1 < nkeys ? kstart[key + 1] : E;
+                }
+            }
+        }
+        v = vn;
+#pragma unroll
+        for (int i = 0; i < 32; i++) wcur[i] = wnext[i];
+    }
+}
+
 // One lane per key: empty buckets become the identity; a key spanning chunks i0..i1 adds the
 // continuation pieces hpart[i0+1 .. i1] to its first piece.
 extern "C" __global__ void __launch_bounds__(256) k_msm_fixup(
@@ -667,6 +795,7 @@ struct MsmTailArgs {
     const uint32_t* partial;   // k_msm_prep's per-workgroup sums of z_i s_i (nblk x 9 words)
     const uint32_t* comb;      // fixed-base comb table
     uint32_t nblk;
+    uint32_t quad_max_c;  // chunk butterflies of at most this many buckets run on quads (0: never)
     uint32_t* verdict;
     uint32_t* runs;  // [2] accepted / rejected runs since staging (never reset by a run), or null
     uint32_t S;
@@ -765,6 +894,31 @@ __device__ __forceinline__ void msm_bterm(const uint32_t* __restrict__ partial, 
     }
 }
 
+// Extended addition of the P3 points in LDS slots i and i + o into slot i by the four lanes of a
+// quad, one coordinate each: the same field operations as p3_add (ge_p3_to_cached, ge_add,
+// ge_p1p1_to_p3) on the same operands, so the same magnitudes, but three multiply latencies
+// instead of nine.  Lane q: step 1 MM (q0), PP (q1), 2d T2 (q2), Z1 2Z2 (q3); step 2 TT2d = T1 2dT2
+// (q2); the four products are broadcast in the quad (DPP quad_perm); step 3 X3, Y3, Z3, T3.
+// Branch-free operand selection: every lane of the wave runs every multiply once.
+__device__ __forceinline__ void quad_p3_add(uint32_t* lds, int i, int o, int q) {
+    const uint32_t* L = lds + P3_WORDS * i;
+    const uint32_t* R = lds + P3_WORDS * (i + o);
+    const fe X1 = load_fe(L), Y1 = load_fe(L + 10), Z1 = load_fe(L + 20), T1 = load_fe(L + 30);
+    const fe X2 = load_fe(R), Y2 = load_fe(R + 10), Z2 = load_fe(R + 20), T2 = load_fe(R + 30);
+    const bool q0 = q == 0, q1 = q == 1, q2 = q == 2;
+    const fe a = fe_select(fe_select(fe_select(Z1, T2, q2), fe_add(Y1, X1), q1), fe_sub(Y1, X1), q0);
+    const fe b = fe_select(fe_select(fe_select(fe_carry(fe_add(Z2, Z2)), fe_d2(), q2), fe_carry(fe_add(Y2, X2)), q1),
+                           fe_carry(fe_sub(Y2, X2)), q0);
+    fe r = fe_mul(a, b);
+    if (q2) r = fe_mul(T1, r);
+    const fe MM = fe_quad_bcast(r, 0), PP = fe_quad_bcast(r, 1), TT2d = fe_quad_bcast(r, 2), ZZ2 = fe_quad_bcast(r, 3);
+    const fe cX = fe_sub(PP, MM), cY = fe_add(PP, MM), cZ = fe_add(ZZ2, TT2d), cT = fe_sub(ZZ2, TT2d);
+    const bool q3 = q == 3;
+    const fe u = fe_select(fe_select(cZ, cY, q1), cX, q0 || q3);
+    const fe v = fe_select(fe_select(cY, cZ, q1), cT, q0 || q2);
+    store_fe(lds + P3_WORDS * i + 10 * q, fe_mul(u, v));
+}
+
 #define NWV_TAIL_STAMP(slot)                                                                       \
     do {                                                                                           \
         if (a.stamps && t == 0) a.stamps[8 * w + (slot)] = __builtin_amdgcn_s_memrealtime();       \
@@ -790,11 +944,27 @@ __device__ __forceinline__ bool msm_tail_window(const MsmLayout& lay, const MsmT
     uint32_t* mine = lds + P3_WORDS * t;
     ge_p3 p = ge_p3_identity();
     if (t < C) p = load_p3(a.bsum + (size_t)P3_WORDS * ((size_t)lay.kbase[w] + (size_t)s * C + t));
-    for (int o = 1; o < C; o <<= 1) {
+    if ((uint32_t)C <= a.quad_max_c) {
+        // on quads (latency-bound small batches): every level's C / 2 additions (lanes i with bit
+        // o clear add lane i + o, in place) as 64 quads per pass
         if (t < C) store_p3(mine, p);
         __syncthreads();
-        if (t < C && !(t & o)) p = p3_add(p, load_p3(lds + P3_WORDS * (t + o)));
-        __syncthreads();
+        const int q = t & 3;
+        for (int o = 1, lg = 0; o < C; o <<= 1, lg++) {
+            for (int g = t >> 2; g < C / 2; g += 64) {
+                const int i = ((g >> lg) << (lg + 1)) | (g & (o - 1));
+                quad_p3_add(lds, i, o, q);
+            }
+            __syncthreads();
+        }
+        if (t < C) p = load_p3(mine);
+    } else {
+        for (int o = 1; o < C; o <<= 1) {
+            if (t < C) store_p3(mine, p);
+            __syncthreads();
+            if (t < C && !(t & o)) p = p3_add(p, load_p3(lds + P3_WORDS * (t + o)));
+            __syncthreads();
+        }
     }
     uint32_t* mypart = a.part + (size_t)P3_WORDS * TAIL_PART_SLOTS * ((size_t)w * a.S + s);
     if (t == 0) store_p3(mypart, p);

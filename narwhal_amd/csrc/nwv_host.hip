@@ -120,7 +120,7 @@ struct PinnedBuf {
 struct EdBuffers {
     DevBuf pk, sig, msg, off, len, kbuf, flags, tables, verdict;
     DevBuf m_scal, m_partial, m_state, m_pts, m_digits, m_cnt, m_tiles, m_entries, m_kstart, m_hpart,
-        m_bsum, m_wsum, m_tpart, m_ctr, m_stamps, m_bpt;
+        m_bsum, m_wsum, m_tpart, m_ctr, m_stamps, m_bpt, m_mid, m_kst2;
     // keyed batches: distinct keys (m x 32), CSR of signatures by key, per-signature z_i k_i
     DevBuf keys, koff, ksig, m_ascal;
     DevBuf kslot;  // keyed batches over the key cache: each distinct key's cache slot
@@ -130,7 +130,7 @@ struct EdBuffers {
     void release() {
         for (DevBuf* b : {&pk, &sig, &msg, &off, &len, &kbuf, &flags, &tables, &verdict, &m_scal,
                           &m_partial, &m_state, &m_pts, &m_digits, &m_cnt, &m_tiles, &m_entries,
-                          &m_kstart, &m_hpart, &m_bsum, &m_wsum, &m_tpart, &m_ctr, &m_stamps, &m_bpt, &keys, &koff, &ksig, &m_ascal,
+                          &m_kstart, &m_hpart, &m_bsum, &m_wsum, &m_tpart, &m_ctr, &m_stamps, &m_bpt, &m_mid, &m_kst2, &keys, &koff, &ksig, &m_ascal,
                           &kslot, &in})
             b->release();
         nkeys_distinct = 0;
@@ -386,6 +386,9 @@ struct MsmPlan {
     uint32_t seg = 0;  // entries per k_msm_bucket lane
     uint32_t tail_S = 1;  // k_msm_tail: bucket chunks per window
     uint64_t np = 0, na = 0, cnt_len = 0, max_entries = 0, nseg = 0;
+    // two-level counting sort (msm.h): coarse layout lay2 (widths reduced by shift)
+    int shift = 0;
+    MsmLayout lay2{};
 };
 
 // Base width c minimises  7 Fmul x entries + 18 Fmul x buckets  (SURVEY.md §8d K5 cost model:
@@ -393,7 +396,9 @@ struct MsmPlan {
 // reduction).
 // split: a keyed batch over the key cache (na = 2m + 1 points before B, every scalar < 2^128):
 // only the z range, nw == nw_z.
-MsmPlan msm_plan(size_t n, size_t na, bool split = false) {
+// sort2: 1 forces the two-level counting sort whenever the sort has more than one chunk (tests),
+// 0 lets the size decide (windows of at least NWV_MSM_SORT2_MIN_PTS points, default 2^20)
+MsmPlan msm_plan(size_t n, size_t na, bool split = false, int sort2 = 0) {
     MsmPlan p;
     p.na = na;
     p.np = (uint64_t)na + 1 + n;
@@ -417,6 +422,38 @@ MsmPlan msm_plan(size_t n, size_t na, bool split = false) {
     msm_xcd_map(p.lay, n, na, p.chunk_pts, p.xm);
     p.nkeys = p.lay.kbase[p.lay.nw];
     p.cnt_len = (uint64_t)p.nkeys * p.chunks;
+    // two-level sort: at most 128 coarse bins per window (bins of 2^shift buckets).  A scatter
+    // workgroup keeps one partly written line open per bin; with 128 bins the open lines of all
+    // the workgroups on an XCD stay well inside its 4 MB L2, so each line is written back whole
+    // (1,024 bins measured 6.3x the entry bytes written at 2M, from L2 evictions)
+    static const uint64_t sort2_min = [] {
+        const char* e = std::getenv("NWV_MSM_SORT2_MIN_PTS");
+        return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)1 << 20;
+    }();
+    if (p.chunks > 1 && (sort2 == 1 || p.np >= sort2_min)) {
+        int lgc = 0;
+        while (lgc < 7 && ((uint64_t)1 << (lgc + 1)) <= p.chunk_pts / 64) lgc++;
+        int cmin = 99;
+        for (int w = 0; w < p.lay.nw; w++) cmin = std::min(cmin, (int)p.lay.width[w]);
+        int sh = std::min(MSM_SORT2_MAX_SHIFT, std::max(0, (p.lay.cmax - 1) - lgc));
+        if (sort2 == 1) sh = std::max(sh, 2);
+        sh = std::min(sh, cmin - 1);
+        if (sh >= 2 && p.np < ((uint64_t)1 << (31 - sh))) {
+            p.shift = sh;
+            p.lay2 = p.lay;
+            uint32_t kb = 0;
+            int cm = 0;
+            for (int w = 0; w < p.lay.nw; w++) {
+                p.lay2.width[w] = (uint8_t)(p.lay.width[w] - sh);
+                p.lay2.kbase[w] = kb;
+                kb += 1u << (p.lay2.width[w] - 1);
+                cm = std::max(cm, (int)p.lay2.width[w]);
+            }
+            p.lay2.kbase[p.lay.nw] = kb;
+            p.lay2.cmax = cm;
+            p.cnt_len = (uint64_t)kb * p.chunks;
+        }
+    }
     p.max_entries = (uint64_t)(na + 1) * p.lay.nw + (uint64_t)n * p.lay.nw_z;
     // ~2 waves per SIMD of bucket lanes (256 CUs x 4 SIMDs x 2 x 64), 8..64 entries each
     p.seg = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, p.max_entries / (256 * 4 * 2 * 64)));
@@ -451,6 +488,8 @@ int msm_alloc(EdBuffers& b, const MsmPlan& p, size_t n) {
         (p.chunks > 1 && (rc = b.m_cnt.ensure((size_t)4 * (p.cnt_len + (size_t)p.lay.nw * p.chunks) + 64))) ||
         (rc = b.m_tiles.ensure((size_t)4 * (MSM_MAX_WINDOWS + 1) + 64)) ||
         (rc = b.m_entries.ensure((size_t)4 * p.max_entries + 64)) ||
+        (p.shift && (rc = b.m_mid.ensure((size_t)4 * p.max_entries + 64))) ||
+        (p.shift && (rc = b.m_kst2.ensure((size_t)4 * p.lay2.kbase[p.lay2.nw] + 64))) ||
         (rc = b.m_kstart.ensure((size_t)4 * p.nkeys + 64)) ||
         (rc = b.m_hpart.ensure((size_t)4 * P3_WORDS * p.nseg + 64)) ||
         (rc = b.m_bsum.ensure((size_t)4 * P3_WORDS * p.nkeys + 64)) ||
@@ -479,7 +518,7 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
                hipEvent_t* ev, bool state_ready) {
     if (n == 0) return NWV_OK;
     const size_t na = msm_na(b, n);
-    const MsmPlan p = msm_plan(n, na, b.kc_split);
+    const MsmPlan p = msm_plan(n, na, b.kc_split, (d.flags & NWV_FLAG_MSM_SORT2) ? 1 : 0);
     int rc = msm_alloc(b, p, n);
     if (rc) return rc;
     // [0] fail flags, [1] verdict, [2..4) accepted / rejected run tally, [8..16) seed
@@ -497,7 +536,7 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     const MsmScalarArgs gs{(uint64_t)n, (uint64_t)na, keyed, b.pk.as<uint8_t>(), b.sig.as<uint8_t>(),
                            b.msg.as<uint8_t>(), b.off.as<uint64_t>(), b.len.as<uint32_t>(), state + 8,
                            b.m_ascal.as<uint32_t>(), digits, b.m_partial.as<uint32_t>(), state,
-                           b.kc_split ? 1u : 0u};
+                           b.kc_split ? 1u : 0u, b.m_ctr.as<uint32_t>()};
     const MsmPointArgs gp{(uint64_t)n, (uint64_t)na, b.kc_split ? 0 : (uint64_t)na,
                           keyed ? b.keys.as<uint8_t>() : b.pk.as<uint8_t>(),
                           b.sig.as<uint8_t>(), b.m_pts.as<uint32_t>(), state};
@@ -532,27 +571,44 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     } else {
         uint32_t* cnt = b.m_cnt.as<uint32_t>();
         uint32_t* nzc = cnt + p.cnt_len;  // [nw][chunks] nonzero digits per histogram workgroup
-        hipLaunchKernelGGL(k_msm_hist, dim3(p.chunks, (unsigned)p.lay.nw), dim3(256), lds_nb, stream, (uint64_t)n,
-                           (uint64_t)na, p.lay, p.chunk_pts, digits, cnt, nzc);
+        // two-level form: the first level sorts coarse bins (lay2) into mid, k_msm_lsort the rest
+        const MsmLayout& l1 = p.shift ? p.lay2 : p.lay;
+        const size_t lds1 = (size_t)4 << (l1.cmax - 1);
+        uint32_t* kst1 = p.shift ? b.m_kst2.as<uint32_t>() : kst;
+        uint32_t* ent1 = p.shift ? b.m_mid.as<uint32_t>() : ent;
+        hipLaunchKernelGGL(k_msm_hist, dim3(p.chunks, (unsigned)p.lay.nw), dim3(256), lds1, stream, (uint64_t)n,
+                           (uint64_t)na, l1, p.chunk_pts, digits, cnt, nzc, p.shift);
         if ((rc = mark(4))) return rc;
         // per window: entry base, bucket totals -> scan -> absolute (bucket, chunk) slice offsets
-        hipLaunchKernelGGL(k_msm_wscan, dim3((unsigned)p.lay.nw), dim3(1024), 0, stream, p.lay, p.chunks, cnt, nzc,
-                           kst, tot);
+        hipLaunchKernelGGL(k_msm_wscan, dim3((unsigned)p.lay.nw), dim3(1024), 0, stream, l1, p.chunks, cnt, nzc,
+                           kst1, tot);
         if ((rc = mark(5))) return rc;
-        hipLaunchKernelGGL(k_msm_scatter, dim3(MSM_XCD_GROUPS * p.xm.slots), dim3(256), lds_nb, stream, (uint64_t)n,
-                           (uint64_t)na, p.lay, p.xm, p.chunks, p.chunk_pts, digits, cnt, ent);
+        hipLaunchKernelGGL(k_msm_scatter, dim3(MSM_XCD_GROUPS * p.xm.slots), dim3(256), lds1, stream, (uint64_t)n,
+                           (uint64_t)na, l1, p.xm, p.chunks, p.chunk_pts, digits, cnt, ent1, p.shift);
+        if (p.shift)  // timed with k_msm_scatter
+            hipLaunchKernelGGL(k_msm_lsort, dim3(1u << (p.lay2.cmax - 1), (unsigned)p.lay.nw), dim3(256), 0, stream,
+                               p.lay, p.lay2, p.shift, ent1, kst1, tot, ent, kst);
     }
     if ((rc = mark(6))) return rc;
     const uint32_t* E = tot + MSM_MAX_WINDOWS;
-    hipLaunchKernelGGL(k_msm_bucket, dim3((unsigned)((p.nseg + 255) / 256)), dim3(256), 0, stream, p.seg,
-                       p.nkeys, E, ent, kst, b.m_pts.as<uint32_t>(), b.m_bsum.as<uint32_t>(),
-                       b.m_hpart.as<uint32_t>());
+    // bucket sums on quads where they are latency-bound (small batches), else one lane per chunk
+    static const uint64_t bucket_quad_max_n = [] {
+        const char* e = std::getenv("NWV_BUCKET_QUAD_MAX_N");
+        return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)16384;
+    }();
+    if (n <= bucket_quad_max_n)
+        hipLaunchKernelGGL(k_msm_bucket_q, dim3((unsigned)((p.nseg + 63) / 64)), dim3(256), 0, stream, p.seg,
+                           p.nkeys, E, ent, kst, b.m_pts.as<uint32_t>(), b.m_bsum.as<uint32_t>(),
+                           b.m_hpart.as<uint32_t>());
+    else
+        hipLaunchKernelGGL(k_msm_bucket, dim3((unsigned)((p.nseg + 255) / 256)), dim3(256), 0, stream, p.seg,
+                           p.nkeys, E, ent, kst, b.m_pts.as<uint32_t>(), b.m_bsum.as<uint32_t>(),
+                           b.m_hpart.as<uint32_t>());
     hipLaunchKernelGGL(k_msm_fixup, dim3((p.nkeys + 255) / 256), dim3(256), 0, stream, p.nkeys,
                        p.seg, kst, E, b.m_hpart.as<uint32_t>(), b.m_bsum.as<uint32_t>());
     if ((rc = mark(7))) return rc;
     // window sums, their scaling, the basepoint term and the verdict: one launch (its arrival
-    // counters are zeroed by a memset node first, graph replays included)
-    NWV_HIP(hipMemsetAsync(b.m_ctr.p, 0, MSM_CTR_BYTES, stream));
+    // counters were zeroed by k_msm_prep's first workgroup, graph replays included)
     static const bool stamps = std::getenv("NWV_TAIL_STAMPS") != nullptr;  // diagnostics only
     unsigned long long* st_buf = nullptr;
     if (stamps && (rc = b.m_stamps.ensure(8 * 8 * (size_t)MSM_MAX_WINDOWS))) return rc;
@@ -560,9 +616,16 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
         st_buf = b.m_stamps.as<unsigned long long>();
         NWV_HIP(hipMemsetAsync(st_buf, 0, 8 * 8 * (size_t)MSM_MAX_WINDOWS, stream));
     }
+    // quad-lane butterflies where the tail is latency-bound (small batches); large batches keep the
+    // lane-local additions (fewer instructions while other batches fill the chip).  NWV_TAIL_QUAD_MAX_N
+    static const uint64_t quad_max_n = [] {
+        const char* e = std::getenv("NWV_TAIL_QUAD_MAX_N");
+        return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)16384;
+    }();
+    const uint32_t quad_max_c = n <= quad_max_n ? 256u : 0u;
     const MsmTailArgs ta{b.m_bsum.as<uint32_t>(), b.m_tpart.as<uint32_t>(), b.m_wsum.as<uint32_t>(),
                          b.m_ctr.as<uint32_t>(), state, b.m_bpt.as<uint32_t>(), b.m_partial.as<uint32_t>(),
-                         d.gpu->comb.as<uint32_t>(), nblk, state + 1, state + 2, p.tail_S, st_buf};
+                         d.gpu->comb.as<uint32_t>(), nblk, quad_max_c, state + 1, state + 2, p.tail_S, st_buf};
     // combine items per thread: (lg C + 1) x S_w over the windows (C = nb / S_w buckets per chunk)
     int items = 0;
     for (int w = 0; w < p.lay.nw; w++) {
@@ -1433,7 +1496,9 @@ int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]) {
         if (!st->tally_ready && st->n) {
             // the run tally (m_state[2..4)) starts at zero and no run ever resets it
             const size_t na = msm_na(st->buf, st->n);
-            if ((rc = msm_alloc(st->buf, msm_plan(st->n, na, st->buf.kc_split), st->n))) return rc;
+            if ((rc = msm_alloc(st->buf, msm_plan(st->n, na, st->buf.kc_split, (st->own.flags & NWV_FLAG_MSM_SORT2) ? 1 : 0),
+                                st->n)))
+                return rc;
             NWV_HIP(hipMemsetAsync(st->buf.m_state.as<uint32_t>() + 2, 0, 8, st->stream));
             st->tally_ready = true;
         }
@@ -1559,7 +1624,7 @@ int nwv_staged_msm_stats(nwv_staged* st, uint64_t out[8]) {
     std::memset(out, 0, 8 * sizeof(uint64_t));
     if (!st->n) return NWV_OK;
     const size_t na = msm_na(st->buf, st->n);
-    const MsmPlan p = msm_plan(st->n, na, st->buf.kc_split);
+    const MsmPlan p = msm_plan(st->n, na, st->buf.kc_split, (st->own.flags & NWV_FLAG_MSM_SORT2) ? 1 : 0);
     out[0] = p.np;
     out[1] = (uint64_t)p.lay.nw;
     out[2] = (uint64_t)p.lay.nw_z;

@@ -31,6 +31,42 @@ def eng_nokc():
     e.close()
 
 
+@pytest.fixture(scope="module")
+def eng_sort2():
+    """the two-level counting sort (coarse bins, then k_msm_lsort) forced whenever the sort has
+    more than one chunk; by default only windows of 2^20+ points use it"""
+    import narwhal_amd
+    from narwhal_amd import _lib
+    e = narwhal_amd.Engine(device=0, flags=_lib.NWV_FLAG_MSM_ALWAYS | _lib.NWV_FLAG_MSM_SORT2)
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("n", [5000, 40000])
+def test_two_level_sort(eng, eng_sort2, n):
+    """batches through the two-level sort: valid batches accept, three forged signatures are
+    pinpointed exactly, and every golden / ZIP-215 vector inside a batch gives the oracle's
+    verdict"""
+    items = _synthetic(eng, n, 32, seed=300 + n)
+    ok, bits = eng_sort2.verify_batch(items, seed=b"\x09" * 32)
+    assert ok and all(bits)
+    bad = [0, n // 3, n - 1]
+    forged = list(items)
+    for i in bad:
+        p, s_, m = forged[i]
+        forged[i] = (p, s_[:10] + bytes([s_[10] ^ 0x40]) + s_[11:], m)
+    ok, bits = eng_sort2.verify_batch(forged)
+    assert not ok and [i for i in range(n) if not bits[i]] == bad
+    if n == 5000:
+        g = of.load_golden("ed25519_vectors.json")["vectors"]
+        z = of.load_golden("zip215_small_order.json")["vectors"]
+        vecs = [_v(v) for v in g + z]
+        batch = items[:n - len(vecs)] + vecs
+        want = all(of.verify(*v) for v in vecs)
+        ok, _ = eng_sort2.verify_batch(batch)
+        assert ok == want
+
+
 @pytest.fixture(params=["keycache", "nokeycache"])
 def keng(request, eng, eng_nokc):
     return eng if request.param == "keycache" else eng_nokc
