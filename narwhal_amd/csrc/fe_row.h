@@ -326,7 +326,8 @@ NWV_HD RowP3 row_add_cached(const RowP3& p, V qc, const RowConsts& k) {
     return row_complete(sub(PP, MM, k), PP + MM, ZZ + TT, sub(ZZ, TT, k), k);
 }
 
-// Horner over the window sums of an MSM layout on one wave, then [8]:
+// Horner over the window sums of an MSM layout on one wave, then [8] (the round-1 final kernel's
+// chain; now the host-emulation tests' check of row_dbl / row_add_cached against the lane chain):
 //   d = W_{nw-1};  d = [2^width[w]] d + W_w  for w = nw-2 .. 0;  d = [8] d.
 // cq: [nw][4][16] row limbs of each window sum in cached form (Y+X | Y-X | 2dT | 2Z);
 // top: [4][16] row limbs of W_{nw-1} (X | Y | Z | T).  Row 0 writes d's X | Y | Z limbs to
@@ -371,40 +372,6 @@ NWV_HD void row_planes_chain(const uint32_t* planes, int m, int post, uint32_t* 
     d = row_add_cached(d, ld(planes, bc(64u * (uint32_t)m) + lane), k);
 #pragma unroll 1
     for (int i = 0; i < post; i++) d = row_dbl(d, k);
-    const M r0 = row_is(0);
-    st(out, limb, d.X, r0);
-    st(out, limb + bc(16), d.Y, r0);
-    st(out, limb + bc(32), d.Z, r0);
-    st(out, limb + bc(48), d.T, r0);
-}
-
-// Sum of cached points on one wave: d = sum_{i < count} pts[first + i * step] (each [4][16] row
-// limbs Y+X | Y-X | 2dT | 2Z, at pts + 64 * index); row 0 writes d's X | Y | Z | T limbs to out.
-NWV_HD void row_sum_cached(const uint32_t* pts, int first, int step, int count, uint32_t* out, uint32_t* sc = nullptr) {
-    RowConsts k = row_consts();
-    k.sc = sc;
-    const V lane = lane_id() & 63u;
-    const V limb = lane & 15u;
-    RowP3 d{bc(0), sel(limb_is(0), bc(0), bc(1)), sel(limb_is(0), bc(0), bc(1)), bc(0)};
-#pragma unroll 1
-    for (int i = 0; i < count; i++) d = row_add_cached(d, ld(pts, bc(64u * (uint32_t)(first + i * step)) + lane), k);
-    const M r0 = row_is(0);
-    st(out, limb, d.X, r0);
-    st(out, limb + bc(16), d.Y, r0);
-    st(out, limb + bc(32), d.Z, r0);
-    st(out, limb + bc(48), d.T, r0);
-}
-
-// d = p0 (X | Y | Z | T row limbs) + the n cached points at cq + 64 i; row 0 writes d's
-// X | Y | Z | T limbs to out (which may be p0)
-NWV_HD void row_add_cached_n(const uint32_t* p0, const uint32_t* cq, int n, uint32_t* out, uint32_t* sc = nullptr) {
-    RowConsts k = row_consts();
-    k.sc = sc;
-    const V lane = lane_id() & 63u;
-    const V limb = lane & 15u;
-    RowP3 d{ld(p0, limb), ld(p0, limb + bc(16)), ld(p0, limb + bc(32)), ld(p0, limb + bc(48))};
-#pragma unroll 1
-    for (int i = 0; i < n; i++) d = row_add_cached(d, ld(cq, bc(64u * (uint32_t)i) + lane), k);
     const M r0 = row_is(0);
     st(out, limb, d.X, r0);
     st(out, limb + bc(16), d.Y, r0);

@@ -1048,40 +1048,22 @@ __device__ __forceinline__ void msm_tail_body(const MsmLayout& lay, const MsmTai
     }
     const int w = blockIdx.y ? lay.nw - (int)blockIdx.y : lay.nw - 1;  // stamp slot of the last arrival
     NWV_TAIL_STAMP(5);
-    // ---- last window: sum of the nw scaled windows and the basepoint term on 16-lane rows (wave
-    // q adds the items i = q mod 4, then wave 0 adds the other three partial sums), identity test
-    uint32_t* cq = lds;                                // [nw + 1][64] cached row limbs
-    uint32_t* part4 = lds + 64 * (MSM_MAX_WINDOWS + 1);  // [4][64] partial sums X | Y | Z | T
-    uint32_t* cq4 = part4 + 256;                       // [3][64] cached row limbs of partials 1..3
-    uint32_t* sc = cq4 + 192;                          // [4][192] multiply scratch, one per wave
-    const int nw = lay.nw + 1;                         // items: the windows, then [8 b]B
-    if (t < 4 * nw) {
-        const int it = t >> 2;
-        const ge_p3 x = load_p3(it < lay.nw ? a.wsc + (size_t)P3_WORDS * it : a.bpt);
-        const int c = t & 3;
-        fe v = c == 0 ? fe_add(x.Y, x.X) : c == 1 ? fe_sub(x.Y, x.X) : c == 2 ? fe_mul(x.T, fe_d2()) : fe_add(x.Z, x.Z);
-        fe_to_limbs16(fe_carry(v), cq + 64 * (t >> 2) + 16 * c);
+    // ---- last arrival: the nw scaled windows and the basepoint term summed as a binary tree of
+    // quad-lane additions in LDS (P2 slots, identity padding), then the identity test
+    const int items = lay.nw + 1;
+    int P2 = 1;
+    while (P2 < items) P2 <<= 1;
+    for (int i = t; i < P2; i += 256)
+        store_p3(lds + P3_WORDS * i, i < lay.nw ? load_p3(a.wsc + (size_t)P3_WORDS * i)
+                                                : i == lay.nw ? load_p3(a.bpt) : ge_p3_identity());
+    __syncthreads();
+    for (int o = 1; o < P2; o <<= 1) {
+        for (int g = t >> 2; g < P2 / (2 * o); g += 64) quad_p3_add(lds, 2 * o * g, o, t & 3);
+        __syncthreads();
     }
-    __syncthreads();
-    {
-        const int q = t >> 6;  // wave
-        const int cnt = q < nw ? (nw - 1 - q) / 4 + 1 : 0;
-        rowf::row_sum_cached(cq, q, 4, cnt, part4 + 64 * q, sc + 192 * q);
-    }
-    __syncthreads();
-    if (t >= 4 && t < 16) {  // partials 1..3 -> cached row limbs (lane-local conversion)
-        const int q = t >> 2, c = t & 3;
-        const fe X = fe_from_limbs16(part4 + 64 * q), Y = fe_from_limbs16(part4 + 64 * q + 16),
-                 Z = fe_from_limbs16(part4 + 64 * q + 32), T = fe_from_limbs16(part4 + 64 * q + 48);
-        fe v = c == 0 ? fe_add(Y, X) : c == 1 ? fe_sub(Y, X) : c == 2 ? fe_mul(T, fe_d2()) : fe_add(Z, Z);
-        fe_to_limbs16(fe_carry(v), cq4 + 64 * (q - 1) + 16 * c);
-    }
-    __syncthreads();
-    if (t < 64) rowf::row_add_cached_n(part4, cq4, 3, part4, sc);  // partial 0 + partials 1..3
-    __syncthreads();
     if (t == 0) {
-        const fe X = fe_from_limbs16(part4), Y = fe_from_limbs16(part4 + 16), Z = fe_from_limbs16(part4 + 32);
-        const bool ok = fe_is_zero(X) && fe_eq(Y, Z) && *a.fail == 0;
+        const ge_p3 d = load_p3(lds);
+        const bool ok = fe_is_zero(d.X) && fe_eq(d.Y, d.Z) && *a.fail == 0;
         *a.verdict = ok ? 1u : 0u;
         // per-run tally (runs of one batch are ordered on its stream: a plain increment)
         if (a.runs) a.runs[ok ? 0 : 1] += 1u;

@@ -594,7 +594,7 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     // bucket sums on quads where they are latency-bound (small batches), else one lane per chunk
     static const uint64_t bucket_quad_max_n = [] {
         const char* e = std::getenv("NWV_BUCKET_QUAD_MAX_N");
-        return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)16384;
+        return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)4096;
     }();
     if (n <= bucket_quad_max_n)
         hipLaunchKernelGGL(k_msm_bucket_q, dim3((unsigned)((p.nseg + 63) / 64)), dim3(256), 0, stream, p.seg,

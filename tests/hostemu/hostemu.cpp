@@ -106,29 +106,17 @@ static bool tail_host(const MsmLayout& lay, const uint32_t* bs, uint32_t S) {
         scaled.push_back(ws);
         tot = p3_add(tot, ws);
     }
-    // the kernel's last step on rows: wave q sums windows q, q+4, ...; wave 0 adds the others
-    auto cached_limbs = [](const ge_p3& x, uint32_t* dst) {
-        fe_to_limbs16(fe_carry(fe_add(x.Y, x.X)), dst);
-        fe_to_limbs16(fe_carry(fe_sub(x.Y, x.X)), dst + 16);
-        fe_to_limbs16(fe_carry(fe_mul(x.T, fe_d2())), dst + 32);
-        fe_to_limbs16(fe_carry(fe_add(x.Z, x.Z)), dst + 48);
-    };
-    const int nw = lay.nw;
-    std::vector<uint32_t> cq(64 * nw), part4(256), cq4(192), sc(192);
-    for (int w = 0; w < nw; w++) cached_limbs(scaled[w], cq.data() + 64 * w);
-    for (int q = 0; q < 4; q++)
-        rowf::row_sum_cached(cq.data(), q, 4, q < nw ? (nw - 1 - q) / 4 + 1 : 0, part4.data() + 64 * q, sc.data());
-    for (int q = 1; q < 4; q++) {
-        const uint32_t* pq = part4.data() + 64 * q;
-        const ge_p3 x{fe_from_limbs16(pq), fe_from_limbs16(pq + 16), fe_from_limbs16(pq + 32), fe_from_limbs16(pq + 48)};
-        cached_limbs(x, cq4.data() + 64 * (q - 1));
-    }
-    rowf::row_add_cached_n(part4.data(), cq4.data(), 3, part4.data(), sc.data());
-    const fe X = fe_from_limbs16(part4.data()), Y = fe_from_limbs16(part4.data() + 16), Z = fe_from_limbs16(part4.data() + 32);
-    const bool rows_id = fe_is_zero(X) && fe_eq(Y, Z);
+    // the kernel's last step: a binary tree of additions over the windows, identity padded to a
+    // power of two (k_msm_tail adds [8 b]B as one more item; here B is inside the MSM)
+    size_t P2 = 1;
+    while (P2 < scaled.size()) P2 <<= 1;
+    scaled.resize(P2, ge_p3_identity());
+    for (size_t o = 1; o < P2; o <<= 1)
+        for (size_t i = 0; i + o < P2; i += 2 * o) scaled[i] = p3_add(scaled[i], scaled[i + o]);
+    const bool tree_id = fe_is_zero(scaled[0].X) && fe_eq(scaled[0].Y, scaled[0].Z);
     const bool lane_id = fe_is_zero(tot.X) && fe_eq(tot.Y, tot.Z);
-    if (rows_id != lane_id) abort();  // the row sum and the lane-local sum must agree
-    return rows_id;
+    if (tree_id != lane_id) abort();  // the tree sum and the sequential sum must agree
+    return tree_id;
 }
 
 extern "C" {
