@@ -469,14 +469,26 @@ def host_to_host(eng, data, threads, seconds):
                     "batch MSM, verdict D2H; PCIe Gen5 x16 (63 GB/s spec) bounds it"}
 
 
+def firehose_subshard(m):
+    """sub-shard size for a rank's m signatures: at most SUBSHARD (2M: the MSM's per-point cost
+    flattens out there), and at least 4 sub-shards per rank, so that consecutive passes overlap
+    one sub-shard's latency-bound tail with another's bulk kernels also at 8 GPUs (2M per rank).
+    Env NWV_FIREHOSE_SUBSHARD overrides."""
+    env = os.environ.get("NWV_FIREHOSE_SUBSHARD")
+    if env:
+        return max(64, int(env))
+    return max(64, min(SUBSHARD, -(-m // 4) + 63 & ~63))
+
+
 def firehose_pass(eng, lo, hi, reps, warm=1, dist=None):
-    """verify [lo, hi) of the firehose as resident sub-shards of <= SUBSHARD on their own streams:
-    returns (seconds for `reps` passes, data, stages' kernel times)"""
+    """verify [lo, hi) of the firehose as resident sub-shards (firehose_subshard) on their own
+    streams: returns (seconds for `reps` passes, data, stages' kernel times)"""
     pk, sg, msgs, offs, lens = firehose_shard_data(eng, lo, hi)
     m = hi - lo
     subs = []
-    for a in range(0, m, SUBSHARD):
-        b = min(m, a + SUBSHARD)
+    sub = firehose_subshard(m)
+    for a in range(0, m, sub):
+        b = min(m, a + sub)
         subs.append(eng.stage(pk[32 * a:32 * b], sg[64 * a:64 * b], msgs, offs[a:b], lens[a:b]))
     for st in subs:
         for _ in range(warm):
