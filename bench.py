@@ -718,6 +718,18 @@ def main():
             dom, how = max(per, key=lambda k: per[k]["kernel_ms"]), "longest single-stream kernel time"
         roof = dict(per[dom], kernel=dom, selected_by=how,
                     kernel_share=per[dom]["kernel_ms"] / sum(kt.values()))
+        # the whole step against the chip's VALU issue rate: every MSM kernel's committed PMC
+        # instruction counts (64-bit forms at the v_mad_u64_u32 rate, the rest at v_add_u32's)
+        # over the measured time per batch with batches in flight
+        msm_k = ["k_msm_prep", "k_msm_hist", "k_msm_wscan", "k_msm_scatter", "k_msm_lsort", "k_msm_sort1",
+                 "k_msm_bucket", "k_msm_bucket_q", "k_msm_fixup", "k_msm_tail", "k_msm_tail_wide", "k_msm_keysum"]
+        present = [k for k in msm_k if pmc_kernel(k, args.n)[0]]
+        fl = issue_floor(present, args.n, dt / args.steps * 1e3, peak) if present else None
+        if fl:
+            fl["kernels"] = present
+            fl["note"] = ("VALU issue floor of one whole batch (all MSM kernels) against the step time "
+                          "with batches in flight")
+        roof["batch_issue_floor"] = fl
     else:
         kms = kt.get("k_ed_straus", 0.0)
         m = (OPS_STRAUS[0] * MADS_PER_MUL + OPS_STRAUS[1] * MADS_PER_SQ) * args.n
