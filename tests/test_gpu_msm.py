@@ -246,6 +246,29 @@ def test_keyed_batches_committee(keng, n, m):
     assert ok and all(bits)
 
 
+def test_keyed_many_keys_bypass_cache(eng):
+    """a keyed call with more distinct keys than NWV_KEYCACHE_MAX_KEYS (4,096) goes uncached
+    (full-width scalars); the same keys in a call of 3,000 distinct keys go through the cache:
+    both give the oracle's verdicts, including one forged signature"""
+    n = 6000
+    items = _synthetic(eng, n, 32, seed=77)
+    keys, kidx = _keyed(items)
+    assert len(keys) == n
+    sigs = [s for _, s, _ in items]
+    msgs = [m for _, _, m in items]
+    ok, bits = eng.verify_batch_keyed(keys, kidx, sigs, msgs)
+    assert ok and all(bits)
+    s = bytearray(sigs[4321])
+    s[50] ^= 0x10
+    sigs[4321] = bytes(s)
+    ok, bits = eng.verify_batch_keyed(keys, kidx, sigs, msgs)
+    assert not ok and [i for i in range(n) if not bits[i]] == [4321]
+    sub = list(range(2000, 5000))  # 3,000 distinct keys: cached, including the forged signature
+    ok, bits = eng.verify_batch_keyed([keys[i] for i in sub], list(range(len(sub))), [sigs[i] for i in sub],
+                                      [msgs[i] for i in sub])
+    assert not ok and [sub[i] for i in range(len(sub)) if not bits[i]] == [4321]
+
+
 def test_keyed_golden_and_bad_keys(keng):
     """golden / ZIP-215 vectors (small-order, non-canonical and undecodable keys) keyed by their
     raw key bytes: verdicts equal the oracle's, and an unused undecodable key changes nothing"""
