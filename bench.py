@@ -514,6 +514,8 @@ def firehose_pass(eng, lo, hi, reps, warm=1, dist=None):
     subs[0].kernel_times(1, reset=True)
     subs[0].run(mode=1, timed=True)
     kt = subs[0].kernel_times(1, reset=True)
+    firehose_pass.last_stats = subs[0].msm_stats()  # MSM shape of one sub-shard (roofline)
+    firehose_pass.last_sub = subs[0].n
     for st in subs:
         st.free()
     return dt, (pk, sg, msgs, offs, lens), kt, len(subs)
@@ -556,6 +558,11 @@ def run_firehose(args, eng, rank, world, dist):
         raise SystemExit("firehose exact-bad-set check failed")
     if rank != 0:
         return None
+    # rank 0's sub-shard MSM against the integer roofline (event-timed kernels of one sub-shard)
+    sub_n = firehose_pass.last_sub
+    per = kernel_rooflines(kt, firehose_pass.last_stats, sub_n, sub_n, valu_peak())
+    roof = dict(per["k_msm_prep"], kernel="k_msm_prep", selected_by="largest VALU kernel of the bulk phase",
+                kernel_share=per["k_msm_prep"]["kernel_ms"] / sum(kt.values()), subshard_sigs=sub_n)
     return {
         "metric": "Ed25519 sigs verified/sec",
         "value": FIREHOSE_N * args.steps / dt,
@@ -575,6 +582,8 @@ def run_firehose(args, eng, rank, world, dist):
                    "sigs_total": FIREHOSE_N, "sigs_per_gpu": hi - lo, "subshards_per_gpu": nsub,
                    "msg_len": 32, "parallelism": f"signature-index shards x{world}, no collective"},
         "kernel_ms_rank0_subshard": kt,
+        "roofline": roof,
+        "roofline_per_kernel": per,
         "exact_bad_set": badset,
     }
 
