@@ -97,16 +97,20 @@ NWV_HD void chacha20_block(const uint32_t key[8], uint32_t counter, const uint32
     for (int k = 0; k < 16; k++) out[k] = x[k] + s[k];
 }
 
-// Per-signature random coefficient z_i in [0, 2^128): the first 16 bytes of the ChaCha20 block
+// Per-signature random coefficient z_i in [1, 2^128), odd: the first 16 bytes of the ChaCha20 block
 // keyed by the caller's 32-byte seed with counter = low word of i and nonce = (high word of i,
 // "nwv-", "z128").  ed25519-consensus draws z_i from the thread RNG (a ChaCha CSPRNG in rand);
 // here the caller's CSPRNG seed keys the stream so the kernels need no device RNG state.
+// The low bit is forced to 1 (127 random bits): z_i != 0, so a batch holding one invalid
+// signature fails deterministically -- a one-signature batch verdict is then exactly the
+// signature's ZIP-215 verdict (nwv_ed25519_pubkey_verify relies on it).
 NWV_HD void msm_z(const uint32_t seed[8], uint64_t i, uint32_t z[8]) {
     const uint32_t nonce[3] = {(uint32_t)(i >> 32), 0x2d76776eu /* "nwv-" */, 0x3832317au /* "z128" */};
     uint32_t blk[16];
     chacha20_block(seed, (uint32_t)i, nonce, blk);
 #pragma unroll
     for (int k = 0; k < 8; k++) z[k] = k < 4 ? blk[k] : 0u;
+    z[0] |= 1u;
 }
 
 // Window layout.  Windows have near-equal widths <= c chosen so that every window's bucket range

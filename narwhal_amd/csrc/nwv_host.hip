@@ -1209,6 +1209,14 @@ static int batch_on_device(Lane& d, EdBuffers& b, size_t n, const uint8_t seed[3
             }
             return NWV_OK;
         }
+        // a batch of valid signatures always passes (the cofactored equation holds for each term
+        // whatever z_i), so a rejection means some signature is invalid: callers that only want
+        // the batch verdict (fastcrypto's verify_batch / aggregate verify) get it without the
+        // per-signature pass, which only runs to name the bad signatures
+        if (!bits) {
+            *ok = 0;
+            return NWV_OK;
+        }
     }
     htrace("batch:fallback");
     if ((rc = ed_launch(d, b, n, stream, nullptr))) return rc;
@@ -1286,17 +1294,29 @@ int nwv_ed25519_verify_batch_keyed(nwv_ctx* ctx, size_t n_keys, const uint8_t* k
 }
 
 // ---- fastcrypto trait surface ---------------------------------------------------------
+// Verifier::verify: a one-signature keyed batch.  With z != 0 its MSM verdict is exactly the
+// signature's ZIP-215 verdict, the key goes through the committee key cache (128-bit scalars:
+// Narwhal verifies committee members' keys), and no per-signature pass is needed either way.
+// Contexts opened with NWV_FLAG_MSM_NEVER use the per-signature pipeline.
 int nwv_ed25519_pubkey_verify(nwv_ctx* ctx, const uint8_t pk[32], const uint8_t* msg,
                               size_t msg_len, const uint8_t sig[64]) {
-    if (!pk || !sig || (msg_len && !msg)) return set_err(NWV_ERR_ARG, "null argument");
+    if (!ctx || !pk || !sig || (msg_len && !msg)) return set_err(NWV_ERR_ARG, "null argument");
     if (msg_len > UINT32_MAX) return set_err(NWV_ERR_ARG, "message too long");
     const uint64_t off = 0;
     const uint32_t len = (uint32_t)msg_len;
-    uint64_t bits = 0;
     static const uint8_t empty[1] = {0};
-    int rc = nwv_ed25519_verify_each(ctx, 1, pk, sig, msg_len ? msg : empty, &off, &len, &bits);
+    if (ctx->devs.empty() || (ctx->devs[0]->flags & NWV_FLAG_MSM_NEVER)) {
+        uint64_t bits = 0;
+        int rc = nwv_ed25519_verify_each(ctx, 1, pk, sig, msg_len ? msg : empty, &off, &len, &bits);
+        if (rc) return rc;
+        return (bits & 1) ? NWV_OK : NWV_ERR_SIGNATURE;
+    }
+    const uint32_t kidx = 0;
+    int all = 0;
+    int rc = nwv_ed25519_verify_batch_keyed(ctx, 1, pk, 1, &kidx, sig, msg_len ? msg : empty, &off, &len, nullptr,
+                                            &all, nullptr);
     if (rc) return rc;
-    return (bits & 1) ? NWV_OK : NWV_ERR_SIGNATURE;
+    return all ? NWV_OK : NWV_ERR_SIGNATURE;
 }
 
 static int shared_msg_batch(nwv_ctx* ctx, size_t n, const uint8_t* pks, const uint8_t* sigs,

@@ -169,13 +169,14 @@ def test_chacha20_block(he):
 
 def test_z_prf(he):
     """z_i = first 16 bytes of ChaCha20(key = seed, counter = low word of i, nonce = high word of
-    i || "nwv-" || "z128")"""
+    i || "nwv-" || "z128"), low bit forced to 1 (z_i != 0)"""
     out = ctypes.create_string_buffer(32)
     seed = bytes(range(32))
     for i in (0, 1, 2**32 + 5, 123456789):
         he.he_msm_z(seed, i, out)
-        want = _chacha20_block_py(seed, i & 0xFFFFFFFF, struct.pack("<I", i >> 32) + b"nwv-z128")[:16]
-        assert out.raw == want + bytes(16)
+        want = bytearray(_chacha20_block_py(seed, i & 0xFFFFFFFF, struct.pack("<I", i >> 32) + b"nwv-z128")[:16])
+        want[0] |= 1
+        assert out.raw == bytes(want) + bytes(16)
 
 
 @pytest.mark.parametrize("c,G", [(6, 1), (6, 8), (8, 128), (13, 256), (13, 64)])
