@@ -14,7 +14,7 @@ sys.path.insert(0, ROOT)
 def main():
     import narwhal_amd
     sizes = [int(x) for x in (sys.argv[1:] or ["1024", "65536"])]
-    eng = narwhal_amd.Engine(device=0)
+    eng = narwhal_amd.Engine(device=0, flags=int(os.environ.get("NWV_SWEEP_FLAGS", "0")))
     for n in sizes:
         rng = np.random.default_rng(n)
         mlen = 32 if n < 65536 else 512
