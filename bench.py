@@ -320,12 +320,13 @@ def kernel_rooflines(kt, stats, n, na, peak):
         f"read the {cnt_len} counts twice (totals, then offsets) and write them back as offsets")
     mem("k_msm_scatter", ["k_msm_scatter"], 2 * digit_slots + 4 * cnt_len + 4 * E,
         f"read the digit rows and the {cnt_len} bucket offsets, write {E} u32 entries")
-    valu("k_msm_bucket+fixup", ["k_msm_bucket", "k_msm_fixup"], MADS_MIXED_ADD * E,
+    valu("k_msm_bucket", ["k_msm_bucket"], MADS_MIXED_ADD * E,
          f"{MADS_MIXED_ADD} multiply-adds per bucket entry (one mixed addition, 7 mul) x {E} entries")
     valu("k_msm_tail", ["k_msm_tail"], 2 * MADS_ADD * buckets + 256 * MADS_DBL * nw,
          f"window sums: two extended additions ({MADS_ADD} multiply-adds each) per bucket x {buckets} "
          f"buckets (running sums), then each of the {nw} windows scaled by up to ~256 doublings "
-         f"({MADS_DBL} multiply-adds each; the top window's chain is latency-bound by construction)")
+         f"({MADS_DBL} multiply-adds each; the top window's chain is latency-bound by construction); "
+         "the joins of buckets spanning bucket lanes (about one extended addition per bucket) are not counted")
     return out
 
 
@@ -428,7 +429,11 @@ def latency_1k(eng, data, reps):
             lat.append((time.perf_counter() - t) * 1e3)
         assert rc == 0 and allv.value == 1
     lat = np.array(lat)
-    return {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)), "reps": len(lat)}
+    mlen = int(lens[:n1].max()) if n1 <= len(lens) else None
+    return {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)), "reps": len(lat),
+            "msg_len": mlen,
+            "note": "the first 1,024 signatures of the headline batch (its message length); configs.C1."
+                    "verify_batch_1024_m32 is the same call on configs[0]'s 32 B messages"}
 
 
 def host_to_host(eng, data, threads, seconds):
@@ -731,7 +736,7 @@ def main():
         # instruction counts (64-bit forms at the v_mad_u64_u32 rate, the rest at v_add_u32's)
         # over the measured time per batch with batches in flight
         msm_k = ["k_msm_prep", "k_msm_hist", "k_msm_wscan", "k_msm_scatter", "k_msm_lsort", "k_msm_sort1",
-                 "k_msm_bucket", "k_msm_bucket_q", "k_msm_fixup", "k_msm_tail", "k_msm_tail_wide", "k_msm_keysum"]
+                 "k_msm_bucket", "k_msm_bucket_q", "k_msm_tail", "k_msm_tail_wide", "k_msm_keysum"]
         present = [k for k in msm_k if pmc_kernel(k, args.n)[0]]
         fl = issue_floor(present, args.n, dt / args.steps * 1e3, peak) if present else None
         if fl:

@@ -181,7 +181,7 @@ int nwv_staged_kernel_ms(nwv_staged* st, double avg_ms[3], int reset);
  * cap (name, ms) pairs in launch order (names point to static strings) and returns the number
  * of kernels in that pipeline (< 0 on error).  mode 1 (batch MSM, K5) kernels:
  * k_msm_prep (hash + decompression + the basepoint term), k_msm_hist, k_msm_wscan,
- * k_msm_scatter, k_msm_bucket+fixup, k_msm_tail; k_msm_keysum is timed with k_msm_prep, and
+ * k_msm_scatter, k_msm_bucket, k_msm_tail; k_msm_keysum is timed with k_msm_prep, and
  * batches whose counting sort fits one chunk per window time k_msm_sort1 as k_msm_hist with
  * zero-length k_msm_wscan / k_msm_scatter slots.  Under NWV_FLAG_MSM_SPLIT_PREP k_msm_prep is
  * split into k_msm_scalars and k_msm_points. */

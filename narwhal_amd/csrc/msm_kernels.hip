@@ -15,8 +15,7 @@
 //                   order  (one-chunk batches: k_msm_sort1 does hist + scan + scatter per window)
 //   k_msm_bucket    lane per fixed-size chunk of the sorted entries: key-segment sums (mixed
 //                   additions, affine Niels), balanced whatever the bucket sizes
-//   k_msm_fixup     lane per bucket: joins the pieces of buckets that span chunks
-//   k_msm_tail      window sums by bit-plane butterflies, each window scaled on 16-lane rows
+//   k_msm_tail      bucket pieces joined, window sums by bit-plane butterflies, each window scaled on 16-lane rows
 //                   (fe_row.h) as soon as its sum is known, the sum over windows, [8], identity
 //                   test -> batch verdict word (one launch)
 // The counting sort keeps every histogram / cursor atomic in LDS; the only global atomics are
@@ -572,7 +571,7 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_lsort(
 // Lane q adds the entries [qT, qT + T) (mixed additions of affine Niels points, the next point's
 // words loaded while the current one is added).  Each key segment that ends inside the chunk is
 // written out: to bsum[key] if the key starts in this chunk (complete, or the key's first piece),
-// else to hpart[q] (a continuation from earlier chunks, completed by k_msm_fixup).  Every lane
+// else to hpart[q] (a continuation from earlier chunks, joined by k_msm_tail).  Every lane
 // does the same number of additions whatever the bucket sizes.
 // one 128-byte record as eight 16-byte loads (affine Niels words 0..29, two padding words)
 __device__ __forceinline__ void msm_load_raw(const uint32_t* __restrict__ pts, uint32_t v, uint32_t w[32]) {
@@ -741,28 +740,6 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_bucket_q(
     }
 }
 
-// One lane per key: empty buckets become the identity; a key spanning chunks i0..i1 adds the
-// continuation pieces hpart[i0+1 .. i1] to its first piece.
-extern "C" __global__ void __launch_bounds__(256) k_msm_fixup(
-    uint32_t nkeys, uint32_t T, const uint32_t* __restrict__ kstart,
-    const uint32_t* __restrict__ total, const uint32_t* __restrict__ hpart, uint32_t* __restrict__ bsum) {
-    const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
-    if (key >= nkeys) return;
-    const uint32_t s = kstart[key];
-    const uint32_t e = key + 1 < nkeys ? kstart[key + 1] : *total;
-    uint32_t* out = bsum + (size_t)P3_WORDS * key;
-    if (s == e) {
-        store_p3(out, ge_p3_identity());
-        return;
-    }
-    const uint32_t i0 = s / T, i1 = (e - 1) / T;
-    if (i1 == i0) return;
-    ge_p3 acc = load_p3(out);
-#pragma unroll 1
-    for (uint32_t i = i0 + 1; i <= i1; i++) acc = p3_add(acc, load_p3(hpart + (size_t)P3_WORDS * i));
-    store_p3(out, acc);
-}
-
 // ---- fused tail: window sums, their scaling and the batch verdict in ONE launch ------------
 // The MSM total is  sum_w [2^pos_w] W_w  with  W_w = sum_{b'=0}^{nb-1} (b'+1) S_{w,b'}.  Instead
 // of a window kernel followed by a one-wave Horner (every window sum on the critical path, then
@@ -786,7 +763,11 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_fixup(
 // tests the identity: *verdict = 1 iff accepted and no failure flag is set.  ctr[0..nw] must be
 // zero at launch (a memset node precedes it).
 struct MsmTailArgs {
-    const uint32_t* bsum;  // [nkeys] bucket sums (P3)
+    const uint32_t* bsum;  // [nkeys] bucket sums (P3): a bucket's first piece (k_msm_bucket[_q])
+    const uint32_t* hpart;    // [nseg] continuation pieces of buckets spanning chunks
+    const uint32_t* kstart;   // [nkeys] first entry of each bucket
+    const uint32_t* total;    // entry count E
+    uint32_t nkeys, seg;      // seg: entries per bucket lane (T of k_msm_bucket[_q])
     uint32_t* part;        // [nw][S][TAIL_PART_SLOTS] chunk planes (P3): R_s, T_{s,0}, T_{s,1}, ...
     uint32_t* wsc;         // [nw] scaled window sums (P3)
     uint32_t* ctr;         // [nw + 1] arrival counters
@@ -919,6 +900,21 @@ __device__ __forceinline__ void quad_p3_add(uint32_t* lds, int i, int o, int q) 
     store_fe(lds + P3_WORDS * i + 10 * q, fe_mul(u, v));
 }
 
+// Bucket sum of key `key`: its first piece from bsum plus the continuation pieces of the chunks it
+// spans (T entries per bucket lane), or the identity when the bucket is empty (bsum never
+// written).  The join the round-1 pipeline ran as a separate launch (k_msm_fixup), done by the
+// tail lane that loads the bucket.
+__device__ __forceinline__ ge_p3 msm_bucket_join(const MsmTailArgs& a, uint32_t key) {
+    const uint32_t s = a.kstart[key];
+    const uint32_t e = key + 1 < a.nkeys ? a.kstart[key + 1] : *a.total;
+    if (s == e) return ge_p3_identity();
+    ge_p3 acc = load_p3(a.bsum + (size_t)P3_WORDS * key);
+    const uint32_t i1 = (e - 1) / a.seg;
+#pragma unroll 1
+    for (uint32_t i = s / a.seg + 1; i <= i1; i++) acc = p3_add(acc, load_p3(a.hpart + (size_t)P3_WORDS * i));
+    return acc;
+}
+
 #define NWV_TAIL_STAMP(slot)                                                                       \
     do {                                                                                           \
         if (a.stamps && t == 0) a.stamps[8 * w + (slot)] = __builtin_amdgcn_s_memrealtime();       \
@@ -943,7 +939,7 @@ __device__ __forceinline__ bool msm_tail_window(const MsmLayout& lay, const MsmT
     // ---- chunk butterfly: lane 0 -> R_s, lane 2^k -> T_{s,k}
     uint32_t* mine = lds + P3_WORDS * t;
     ge_p3 p = ge_p3_identity();
-    if (t < C) p = load_p3(a.bsum + (size_t)P3_WORDS * ((size_t)lay.kbase[w] + (size_t)s * C + t));
+    if (t < C) p = msm_bucket_join(a, lay.kbase[w] + (uint32_t)(s * C + t));
     if ((uint32_t)C <= a.quad_max_c) {
         // on quads (latency-bound small batches): every level's C / 2 additions (lanes i with bit
         // o clear add lane i + o, in place) as 64 quads per pass

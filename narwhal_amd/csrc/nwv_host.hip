@@ -505,10 +505,10 @@ static const char* const ED_KERNEL_NAMES[] = {"k_ed_hash", "k_ed_points", "k_ed_
 // the decompression as one grid unless NWV_FLAG_MSM_SPLIT_PREP)
 static const char* const MSM_KERNEL_NAMES[] = {
     "k_msm_prep", nullptr, nullptr, "k_msm_hist", "k_msm_wscan",
-    "k_msm_scatter", "k_msm_bucket+fixup", "k_msm_tail", nullptr};
+    "k_msm_scatter", "k_msm_bucket", "k_msm_tail", nullptr};
 static const char* const MSM_KERNEL_NAMES_SPLIT[] = {
     "k_msm_scalars", nullptr, "k_msm_points", "k_msm_hist", "k_msm_wscan",
-    "k_msm_scatter", "k_msm_bucket+fixup", "k_msm_tail", nullptr};
+    "k_msm_scatter", "k_msm_bucket", "k_msm_tail", nullptr};
 constexpr int MSM_NKERNELS = 9;
 constexpr int MSM_NEVENTS = MSM_NKERNELS + 1;  // one event before each kernel, one after the last
 
@@ -604,8 +604,6 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
         hipLaunchKernelGGL(k_msm_bucket, dim3((unsigned)((p.nseg + 255) / 256)), dim3(256), 0, stream, p.seg,
                            p.nkeys, E, ent, kst, b.m_pts.as<uint32_t>(), b.m_bsum.as<uint32_t>(),
                            b.m_hpart.as<uint32_t>());
-    hipLaunchKernelGGL(k_msm_fixup, dim3((p.nkeys + 255) / 256), dim3(256), 0, stream, p.nkeys,
-                       p.seg, kst, E, b.m_hpart.as<uint32_t>(), b.m_bsum.as<uint32_t>());
     if ((rc = mark(7))) return rc;
     // window sums, their scaling, the basepoint term and the verdict: one launch (its arrival
     // counters were zeroed by k_msm_prep's first workgroup, graph replays included)
@@ -623,7 +621,8 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
         return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)16384;
     }();
     const uint32_t quad_max_c = n <= quad_max_n ? 256u : 0u;
-    const MsmTailArgs ta{b.m_bsum.as<uint32_t>(), b.m_tpart.as<uint32_t>(), b.m_wsum.as<uint32_t>(),
+    const MsmTailArgs ta{b.m_bsum.as<uint32_t>(), b.m_hpart.as<uint32_t>(), kst, E, p.nkeys, p.seg,
+                         b.m_tpart.as<uint32_t>(), b.m_wsum.as<uint32_t>(),
                          b.m_ctr.as<uint32_t>(), state, b.m_bpt.as<uint32_t>(), b.m_partial.as<uint32_t>(),
                          d.gpu->comb.as<uint32_t>(), nblk, quad_max_c, state + 1, state + 2, p.tail_S, st_buf};
     // combine items per thread: (lg C + 1) x S_w over the windows (C = nb / S_w buckets per chunk)

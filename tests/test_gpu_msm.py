@@ -167,7 +167,7 @@ def test_staged_msm_runs_and_times(eng, split):
     st.free()
     assert allv and bits.all()
     want = (["k_msm_scalars", "k_msm_points"] if split else ["k_msm_prep"]) + [
-        "k_msm_hist", "k_msm_wscan", "k_msm_scatter", "k_msm_bucket+fixup", "k_msm_tail"]
+        "k_msm_hist", "k_msm_wscan", "k_msm_scatter", "k_msm_bucket", "k_msm_tail"]
     assert list(t) == want and all(v > 0 for v in t.values())
     bad = [5, 4000, 8191]
     for i in bad:
