@@ -54,6 +54,10 @@ typedef struct nwv_ctx nwv_ctx;
  * workgroup) whenever the sort has more than one chunk; by default it is used for windows of
  * NWV_MSM_SORT2_MIN_PTS points or more (env, default 2^20) */
 #define NWV_FLAG_MSM_SORT2 16u
+/* diagnostic / tests: when a batch MSM over per-signature keys rejects and the verdict bits are
+ * wanted, the per-signature pass builds its point tables from the MSM's decompressed records by
+ * default (k_ed_points_msm); this flag makes it decompress again (k_ed_points) */
+#define NWV_FLAG_NO_MSM_REUSE 32u
 
 /* ------------------------------------------------------------------ lifecycle ----- */
 /* Process-wide context creation (created once, in Primary::spawn).

@@ -27,6 +27,7 @@ NWV_FLAG_MSM_NEVER = 2
 NWV_FLAG_MSM_SPLIT_PREP = 4
 NWV_FLAG_NO_KEYCACHE = 8
 NWV_FLAG_MSM_SORT2 = 16
+NWV_FLAG_NO_MSM_REUSE = 32
 NWV_RUN_TIMED = 0x100
 
 

@@ -268,8 +268,41 @@ __device__ __forceinline__ void msm_points_block(uint32_t blk, const MsmPointArg
     msm_load8(is_r ? g.sig + 64 * i : g.apk + 32 * i, w);
     ge_p3 P;
     const bool ok = ge_decompress(w, P);
-    msm_store_point(g.pts + (size_t)MSM_PT_WORDS * (is_r ? na + 1 + i : i), P);
+    uint32_t* e = g.pts + (size_t)MSM_PT_WORDS * (is_r ? na + 1 + i : i);
+    msm_store_point(e, P);
+    e[MSM_PT_WORDS - 1] = ok ? 0u : 1u;  // decode flag (k_ed_points_msm); ignored by the MSM
     if (!ok) atomicOr(g.fail, 2u);
+}
+
+// C4 fallback after a rejected batch MSM over per-signature keys: the per-signature tables
+// (k_ed_points' R entry and 0..8 A table) built from the MSM's decompressed point records instead
+// of a second decompression.  Record (y+x | y-x | 2dxy, Z = 1) -> x = ((y+x) - (y-x)) / 2,
+// y = ((y+x) + (y-x)) / 2, T = xy; word 31 is the record's decode flag.  Same two lanes per
+// signature, in different waves, as k_ed_points.
+extern "C" __global__ void __launch_bounds__(256) k_ed_points_msm(uint64_t n, uint64_t na,
+                                                                  const uint32_t* __restrict__ pts,
+                                                                  uint32_t* __restrict__ tables,
+                                                                  uint32_t* __restrict__ flags) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t wv = t >> 6;
+    const uint64_t i = (wv >> 1) * 64 + (t & 63);
+    if (i >= n) return;
+    const bool is_r = (wv & 1) == 0;
+    const uint32_t* e = pts + (size_t)MSM_PT_WORDS * (is_r ? na + 1 + i : i);
+    const uint32_t half_w[8] = {0xFFFFFFF7u, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu,
+                                0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0x3FFFFFFFu};  // (p + 1) / 2
+    const fe half = fe_from_words(half_w);
+    const fe ypx = load_fe(e), ymx = load_fe(e + 10);
+    ge_p3 P;
+    P.X = fe_mul(fe_sub(ypx, ymx), half);
+    P.Y = fe_mul(fe_add(ypx, ymx), half);
+    P.Z = fe_one();
+    P.T = fe_mul(P.X, P.Y);
+    uint32_t* tbl = tables + i * LANE_SCRATCH_WORDS;
+    if (is_r) store_cached_entry(tbl + R_ENTRY * CACHED_ENTRY_WORDS, ge_p3_to_cached(P));
+    else build_a_table(P, tbl);
+    const uint32_t f = e[MSM_PT_WORDS - 1] == 0 ? (is_r ? FLAG_R_OK : FLAG_A_OK) : 0u;
+    atomicOr(flags + i, f);
 }
 
 extern "C" __global__ void __launch_bounds__(256) k_msm_scalars(MsmScalarArgs g, MsmLayout lay) {

@@ -354,7 +354,10 @@ int ed_scratch(EdBuffers& b, size_t n) {
     return NWV_OK;
 }
 
-int ed_launch(Lane& d, EdBuffers& b, size_t n, hipStream_t stream, hipEvent_t* ev) {
+// msm_pts: the point records of a batch MSM that just ran on these buffers over per-signature
+// keys (na = n A points): k_ed_points_msm reuses its decompressions.
+int ed_launch(Lane& d, EdBuffers& b, size_t n, hipStream_t stream, hipEvent_t* ev,
+              const uint32_t* msm_pts = nullptr) {
     if (n == 0) return NWV_OK;
     int rc = ed_scratch(b, n);
     if (rc) return rc;
@@ -365,8 +368,12 @@ int ed_launch(Lane& d, EdBuffers& b, size_t n, hipStream_t stream, hipEvent_t* e
                        b.sig.as<uint8_t>(), b.msg.as<uint8_t>(), b.off.as<uint64_t>(),
                        b.len.as<uint32_t>(), b.kbuf.as<uint8_t>(), b.flags.as<uint32_t>());
     if (ev) NWV_HIP(hipEventRecord(ev[1], stream));
-    hipLaunchKernelGGL(k_ed_points, grid2, blk, 0, stream, (uint64_t)n, b.pk.as<uint8_t>(),
-                       b.sig.as<uint8_t>(), b.tables.as<uint32_t>(), b.flags.as<uint32_t>());
+    if (msm_pts)
+        hipLaunchKernelGGL(k_ed_points_msm, grid2, blk, 0, stream, (uint64_t)n, (uint64_t)n, msm_pts,
+                           b.tables.as<uint32_t>(), b.flags.as<uint32_t>());
+    else
+        hipLaunchKernelGGL(k_ed_points, grid2, blk, 0, stream, (uint64_t)n, b.pk.as<uint8_t>(),
+                           b.sig.as<uint8_t>(), b.tables.as<uint32_t>(), b.flags.as<uint32_t>());
     if (ev) NWV_HIP(hipEventRecord(ev[2], stream));
     hipLaunchKernelGGL(k_ed_straus, grid, blk, 0, stream, (uint64_t)n, b.sig.as<uint8_t>(),
                        b.kbuf.as<uint8_t>(), b.tables.as<uint32_t>(), b.flags.as<uint32_t>(),
@@ -1182,6 +1189,13 @@ static void fill_seed(const uint8_t* seed32, uint8_t out[32]) {
     std::memcpy(out, blk, 32);
 }
 
+// point records of the batch MSM that ran last on b, when the per-signature fallback can reuse
+// them: per-signature keys (every A_i decompressed at point i, R_i at n + 1 + i)
+static const uint32_t* msm_reusable(const Lane& d, const EdBuffers& b, bool msm_ran) {
+    if (!msm_ran || b.nkeys_distinct || (d.flags & NWV_FLAG_NO_MSM_REUSE)) return nullptr;
+    return b.m_pts.as<uint32_t>();
+}
+
 static void set_ones(uint64_t* bits, size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; i++) bits[i >> 6] |= 1ULL << (i & 63);
 }
@@ -1218,7 +1232,7 @@ static int batch_on_device(Lane& d, EdBuffers& b, size_t n, const uint8_t seed[3
         }
     }
     htrace("batch:fallback");
-    if ((rc = ed_launch(d, b, n, stream, nullptr))) return rc;
+    if ((rc = ed_launch(d, b, n, stream, nullptr, msm_reusable(d, b, use_msm)))) return rc;
     std::vector<uint64_t> tmp;
     uint64_t* out = bits;
     if (!out) {
@@ -1583,7 +1597,8 @@ int nwv_staged_fetch(nwv_staged* st, uint64_t* verdict_bits, int* all_valid) {
             if (all_valid) *all_valid = 1;
             return NWV_OK;
         }
-        if ((rc = ed_launch(st->own, st->buf, st->n, st->stream, nullptr))) return rc;
+        if ((rc = ed_launch(st->own, st->buf, st->n, st->stream, nullptr, msm_reusable(st->own, st->buf, true))))
+            return rc;
     }
     if (words && !st->buf.verdict.p) return set_err(NWV_ERR_ARG, "staged batch has not run");
     if (words) NWV_HIP(hipMemcpyAsync(bits, st->buf.verdict.p, 8 * words, hipMemcpyDeviceToHost, st->stream));

@@ -37,6 +37,7 @@ pub const NWV_FLAG_MSM_NEVER: u32 = 2;
 pub const NWV_FLAG_MSM_SPLIT_PREP: u32 = 4;
 pub const NWV_FLAG_NO_KEYCACHE: u32 = 8;
 pub const NWV_FLAG_MSM_SORT2: u32 = 16;
+pub const NWV_FLAG_NO_MSM_REUSE: u32 = 32;
 
 pub const NWV_DAG_OK: i32 = 0;
 pub const NWV_DAG_INVALID_EPOCH: i32 = 10;

@@ -121,6 +121,37 @@ def test_golden_and_zip215_vectors_in_batches(eng):
         assert bits == want
 
 
+@pytest.fixture(scope="module")
+def eng_noreuse():
+    """the per-signature pass after a rejected MSM decompresses again (k_ed_points) instead of
+    building its tables from the MSM's point records (k_ed_points_msm, the default)"""
+    import narwhal_amd
+    from narwhal_amd import _lib
+    e = narwhal_amd.Engine(device=0, flags=_lib.NWV_FLAG_MSM_ALWAYS | _lib.NWV_FLAG_NO_MSM_REUSE)
+    yield e
+    e.close()
+
+
+def test_fallback_reuses_msm_points_exactly(eng, eng_noreuse):
+    """a rejected batch holding every golden / ZIP-215 vector (undecodable R and A, non-canonical
+    encodings, small-order points, negative zero) plus forged signatures: the fallback built from
+    the MSM's decompressed records and the one that decompresses again both give the oracle's
+    bits"""
+    g = of.load_golden("ed25519_vectors.json")["vectors"]
+    z = of.load_golden("zip215_small_order.json")["vectors"]
+    items = _synthetic(eng, 300, 32, seed=11)
+    for i in (5, 77, 299):
+        p, s_, m = items[i]
+        items[i] = (p, s_[:3] + bytes([s_[3] ^ 1]) + s_[4:], m)
+    vecs = [_v(v) for v in g + z]
+    batch = items[:150] + vecs + items[150:]
+    want = [of.verify(*it) for it in batch]
+    assert not all(want)
+    for e in (eng, eng_noreuse):
+        ok, bits = e.verify_batch(batch, seed=b"\x21" * 32)
+        assert not ok and bits == want
+
+
 def test_all_small_order_vectors_one_batch(eng):
     z = [_v(v) for v in of.load_golden("zip215_small_order.json")["vectors"]]
     ok, bits = eng.verify_batch(z)

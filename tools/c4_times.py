@@ -1,0 +1,28 @@
+#!/usr/bin/env python3
+"""C4 (65,536 x 512 B, 1 % adversarial) host-to-host call time with the per-signature fallback
+building its tables from the MSM's point records (default) and with a second decompression
+(NWV_FLAG_NO_MSM_REUSE); both bad sets must equal the injected one."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+def main():
+    import narwhal_amd
+    from narwhal_amd import _lib
+    import config_legs as CL
+    out = {}
+    for name, flags in (("reuse", 0), ("no_reuse", _lib.NWV_FLAG_NO_MSM_REUSE)):
+        eng = narwhal_amd.Engine(device=0, flags=flags)
+        r, _ = CL.leg_c4(eng, reps=9)
+        out[name] = r
+        eng.close()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
