@@ -48,13 +48,13 @@ SUBSHARD = 2097152
 # v_mad_u64_u32; a squaring 55), counted on the host-emulation build
 # (tests/test_hostemu.py::test_phase_op_counts, tests/test_msm_hostemu.py)
 MADS_PER_MUL, MADS_PER_SQ = 100, 55
-OPS_POINTS = (111, 514)      # k_ed_points, per signature: decompress R and A + 0..8 A table
+OPS_POINTS = (174, 514)      # k_ed_points, per signature: decompress R and A + the 0..8 A and R tables
 OPS_MSM_POINTS = (48, 514)   # MSM decompression, per signature: R_i and A_i
 MADS_DECOMPRESS = (OPS_MSM_POINTS[0] * MADS_PER_MUL + OPS_MSM_POINTS[1] * MADS_PER_SQ) // 2  # per point
 MADS_MIXED_ADD = 7 * MADS_PER_MUL                          # per bucket entry (affine Niels)
 MADS_ADD = 9 * MADS_PER_MUL                                # extended + extended
 MADS_DBL = 4 * MADS_PER_MUL + 4 * MADS_PER_SQ              # projective doubling
-OPS_STRAUS = (1505, 1020)
+OPS_STRAUS = (1155, 524)     # k_ed_straus: half-size scalars, 132 doublings (ed25519_lane.h)
 # guide-derived VALU peaks (MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32 x 2.4 GHz, a wave64 VALU
 # instruction issues over 2 cycles): 78.6 T lane-ops/s for full-rate 32-bit forms; the 64-bit
 # result VOP3 forms (v_mad_u64_u32) issue at half that

@@ -4,15 +4,16 @@
 // occupancy its own register footprint allows (one fused kernel needed ~250 VGPRs = 1 wave
 // per SIMD; the phases need 70-145):
 //   k_ed_hash     K1+K3  k = SHA-512(R || A || M) mod l, s < l         (one message per lane)
-//   k_ed_points   K2     decompress R and A, build the lane's 0..8 A table in HBM
-//   k_ed_straus   K4     [8]([s]B - [k]A - R) == identity, wave ballot -> verdict words
+//   k_ed_points   K2     decompress R and A, build the lane's 0..8 A and 0..8 R tables in HBM
+//   k_ed_straus   K4     [8]([s]B - [k]A - R) == identity on half-size scalars (ed25519_lane.h),
+//                        wave ballot -> verdict words
 // plus
 //   k_base_table  one-time: j B for j = 0..128 (affine Niels, +-2dxy) + an identity entry
 //   k_sign        RFC 8032 keygen + signing per lane (synthetic data / tests only)
 //
 // Inputs are SoA: pk[n][32], sig[n][64] (coalesced 16-byte loads), a padded message arena
 // addressed by msg_off[n] / msg_len[n].  Intermediate state per signature: k[n][8] words,
-// flags[n], and a 2 KiB point table (LANE_SCRATCH_WORDS words).  The verdict of signature i
+// flags[n], and a 3.5 KiB point table (LANE_SCRATCH_WORDS words).  The verdict of signature i
 // is bit i % 64 of word i / 64, written by lane 0 of the wave that owns those 64 signatures.
 #include "ed25519_lane.h"
 
@@ -34,10 +35,14 @@ __device__ __forceinline__ void store_words8(uint8_t* p, const uint32_t w[8]) {
 
 }  // namespace
 
-// btab: BASE_TABLE_WORDS words of precomp entries followed by one identity cached entry
+// btab (BTAB_WORDS): j B precomp entries (j = 0..128), one identity cached entry, then the
+// j 2^128 B precomp entries (the per-signature check's half-size scalars, ed25519_lane.h)
 extern "C" __global__ void __launch_bounds__(64) k_base_table(uint32_t* btab) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < BASE_TABLE_ENTRIES) store_precomp_entry(btab + j * PRECOMP_ENTRY_WORDS, base_multiple(j));
+    if (j < BASE_TABLE_ENTRIES) {
+        store_precomp_entry(btab + j * PRECOMP_ENTRY_WORDS, base_multiple(j));
+        store_precomp_entry(btab + BASE128_TABLE_OFFSET + j * PRECOMP_ENTRY_WORDS, base128_multiple(j));
+    }
     if (j == 0) store_cached_entry(btab + BASE_TABLE_WORDS, ge_cached_identity());
 }
 

@@ -275,7 +275,7 @@ __device__ __forceinline__ void msm_points_block(uint32_t blk, const MsmPointArg
 }
 
 // C4 fallback after a rejected batch MSM over per-signature keys: the per-signature tables
-// (k_ed_points' R entry and 0..8 A table) built from the MSM's decompressed point records instead
+// (k_ed_points' 0..8 R and 0..8 A tables) built from the MSM's decompressed point records instead
 // of a second decompression.  Record (y+x | y-x | 2dxy, Z = 1) -> x = ((y+x) - (y-x)) / 2,
 // y = ((y+x) + (y-x)) / 2, T = xy; word 31 is the record's decode flag.  Same two lanes per
 // signature, in different waves, as k_ed_points.
@@ -299,8 +299,7 @@ extern "C" __global__ void __launch_bounds__(256) k_ed_points_msm(uint64_t n, ui
     P.Z = fe_one();
     P.T = fe_mul(P.X, P.Y);
     uint32_t* tbl = tables + i * LANE_SCRATCH_WORDS;
-    if (is_r) store_cached_entry(tbl + R_ENTRY * CACHED_ENTRY_WORDS, ge_p3_to_cached(P));
-    else build_a_table(P, tbl);
+    build_a_table(P, is_r ? tbl + R_ENTRY * CACHED_ENTRY_WORDS : tbl);  // j R or j A, j = 0..8
     const uint32_t f = e[MSM_PT_WORDS - 1] == 0 ? (is_r ? FLAG_R_OK : FLAG_A_OK) : 0u;
     atomicOr(flags + i, f);
 }

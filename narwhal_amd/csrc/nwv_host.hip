@@ -305,7 +305,7 @@ int gpu_open(Gpu& g, int ordinal, uint32_t flags) {
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return set_err(NWV_ERR_NODEV, std::string("device is ") + prop.gcnArchName + ", need gfx950");
     NWV_HIP(hipSetDevice(ordinal));
-    int rc = g.btab.ensure((BASE_TABLE_WORDS + CACHED_ENTRY_WORDS) * sizeof(uint32_t));
+    int rc = g.btab.ensure(BTAB_WORDS * sizeof(uint32_t));
     if (rc) return rc;
     Lane* l = nullptr;
     if ((rc = lane_open(g, &l))) return rc;

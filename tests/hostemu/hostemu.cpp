@@ -19,9 +19,11 @@ static std::vector<uint32_t> g_btab;
 
 static void ensure_btab() {
     if (!g_btab.empty()) return;
-    g_btab.resize(BASE_TABLE_WORDS + CACHED_ENTRY_WORDS);
-    for (int j = 0; j < BASE_TABLE_ENTRIES; j++)
+    g_btab.resize(BTAB_WORDS);
+    for (int j = 0; j < BASE_TABLE_ENTRIES; j++) {
         store_precomp_entry(g_btab.data() + j * PRECOMP_ENTRY_WORDS, base_multiple(j));
+        store_precomp_entry(g_btab.data() + BASE128_TABLE_OFFSET + j * PRECOMP_ENTRY_WORDS, base128_multiple(j));
+    }
     store_cached_entry(g_btab.data() + BASE_TABLE_WORDS, ge_cached_identity());
 }
 
@@ -136,6 +138,15 @@ int he_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_
     f |= lane_points(Aw, Rw, tbl.data());
     const bool eq = lane_straus_check(k, Sw, tbl.data(), g_btab.data());
     return (eq && f == FLAGS_ALL) ? 1 : 0;
+}
+
+// the per-signature check's half-size split of k (< l): u (4 words), m = |v| (4 words), vneg
+void he_half_split(const uint8_t* k32, uint32_t* u4, uint32_t* m4, int* vneg) {
+    uint32_t k[8];
+    words(k32, k);
+    bool neg;
+    sc_half_split(k, u4, m4, neg);
+    *vneg = neg ? 1 : 0;
 }
 
 // field multiplies / squarings executed by each kernel phase of one verification:

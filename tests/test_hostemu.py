@@ -117,3 +117,28 @@ def test_phase_op_counts_match_bench_constants(he):
         assert (c[0], c[1]) == (0, 0)
         assert (c[2], c[3]) == bench.OPS_POINTS
         assert (c[4], c[5]) == bench.OPS_STRAUS
+
+
+L = 2**252 + 27742317777372353535851937790883648493
+
+
+def test_half_size_split(he):
+    """ed25519_lane.h sc_half_split (per-signature check on half-size scalars): u = v k (mod l)
+    with 0 <= u < 2^127 and 0 < |v| < 2^126, for random k and the edge values"""
+    import random
+    he.he_half_split.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    rnd = random.Random(5)
+    ks = [0, 1, 2, 3, 2**126, 2**127 - 1, 2**127, 2**127 + 1, 2**128, L // 2, L // 3, L - 1, L - 2,
+          2**252, (L - 1) // 2 + 1]
+    ks += [rnd.randrange(L) for _ in range(3000)]
+    ks += [rnd.randrange(2**k) for k in range(1, 253, 3)]
+    u4 = (ctypes.c_uint32 * 4)()
+    m4 = (ctypes.c_uint32 * 4)()
+    neg = ctypes.c_int(0)
+    for k in ks:
+        he.he_half_split(k.to_bytes(32, "little"), u4, m4, ctypes.byref(neg))
+        u = sum(int(x) << (32 * i) for i, x in enumerate(u4))
+        m = sum(int(x) << (32 * i) for i, x in enumerate(m4))
+        v = -m if neg.value else m
+        assert 0 <= u < 2**127 and 0 < m < 2**126 + 1, k
+        assert (v * k - u) % L == 0, k
