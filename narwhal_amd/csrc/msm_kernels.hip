@@ -972,6 +972,7 @@ __device__ __forceinline__ bool msm_tail_window(const MsmLayout& lay, const MsmT
     uint32_t* mine = lds + P3_WORDS * t;
     ge_p3 p = ge_p3_identity();
     if (t < C) p = msm_bucket_join(a, lay.kbase[w] + (uint32_t)(s * C + t));
+    if (s == 0) NWV_TAIL_STAMP(7);
     if ((uint32_t)C <= a.quad_max_c) {
         // on quads (latency-bound small batches): every level's C / 2 additions (lanes i with bit
         // o clear add lane i + o, in place) as 64 quads per pass

@@ -1483,7 +1483,7 @@ static int staged_collect_times(nwv_staged* st) {
             for (int w = 0; w < MSM_MAX_WINDOWS; w++) {
                 if (!h[8 * w]) continue;
                 std::fprintf(stderr, " | w%d", w);
-                for (int k = 0; k < 7; k++)
+                for (int k = 0; k < 8; k++)
                     std::fprintf(stderr, " %.1f", h[8 * w + k] ? (double)(h[8 * w + k] - t0) / 100.0 : -1.0);
             }
             std::fprintf(stderr, "\n");
