@@ -23,33 +23,45 @@ void htrace(const char* what) {
     std::fprintf(stderr, "nwv-trace %.1f %s\n", us, what);
 }
 
-void put_le64(std::vector<uint8_t>& b, uint64_t v) {
-    for (int i = 0; i < 8; i++) b.push_back((uint8_t)(v >> (8 * i)));
-}
-void put_le32(std::vector<uint8_t>& b, uint32_t v) {
-    for (int i = 0; i < 4; i++) b.push_back((uint8_t)(v >> (8 * i)));
-}
 void put(std::vector<uint8_t>& b, const uint8_t* p, size_t n) { b.insert(b.end(), p, p + n); }
+// little-endian integers at a write cursor (the host is little-endian: x86-64 / aarch64)
+uint8_t* at_le64(uint8_t* w, uint64_t v) {
+    std::memcpy(w, &v, 8);
+    return w + 8;
+}
+uint8_t* at_le32(uint8_t* w, uint32_t v) {
+    std::memcpy(w, &v, 4);
+    return w + 4;
+}
+uint8_t* at_bytes(uint8_t* w, const uint8_t* p, size_t n) {
+    if (n) std::memcpy(w, p, n);
+    return w + n;
+}
 
 // Header::digest preimage (types/src/primary.rs:209-227): author || round_le || epoch_le ||
-// (batch digest || worker id_le)* in payload order || parent digests in BTreeSet order
+// (batch digest || worker id_le)* in payload order || parent digests in BTreeSet order.  The
+// arena grows once per preimage and the fields are copied in.
 void header_preimage(const nwv_header& h, std::vector<uint8_t>& b) {
-    put(b, h.author, 32);
-    put_le64(b, h.round);
-    put_le64(b, h.epoch);
+    const size_t at = b.size();
+    b.resize(at + 48 + 36 * h.n_payload + 32 * h.n_parents);
+    uint8_t* w = at_bytes(b.data() + at, h.author, 32);
+    w = at_le64(w, h.round);
+    w = at_le64(w, h.epoch);
     for (size_t i = 0; i < h.n_payload; i++) {
-        put(b, h.payload_digests + 32 * i, 32);
-        put_le32(b, h.payload_workers[i]);
+        w = at_bytes(w, h.payload_digests + 32 * i, 32);
+        w = at_le32(w, h.payload_workers[i]);
     }
-    if (h.n_parents) put(b, h.parents, 32 * h.n_parents);  // contiguous, already in BTreeSet order
+    at_bytes(w, h.parents, 32 * h.n_parents);  // contiguous, already in BTreeSet order
 }
 // Vote::digest (:351-364) and Certificate::digest (:594-607): id || round_le || epoch_le || origin
 void id_round_epoch_origin(const uint8_t* id, uint64_t round, uint64_t epoch, const uint8_t* origin,
                            std::vector<uint8_t>& b) {
-    put(b, id, 32);
-    put_le64(b, round);
-    put_le64(b, epoch);
-    put(b, origin, 32);
+    const size_t at = b.size();
+    b.resize(at + 80);
+    uint8_t* w = at_bytes(b.data() + at, id, 32);
+    w = at_le64(w, round);
+    w = at_le64(w, epoch);
+    at_bytes(w, origin, 32);
 }
 
 // Preimages appended to one arena, hashed in one nwv_blake2b256_many launch.  The batches of a
@@ -293,6 +305,7 @@ int verify_mixed(nwv_ctx* ctx, const nwv_committee& c, size_t nh, const nwv_head
         plan_header(c, h[i], db, hplan[i]);
         if (!hplan[i].pre && !hplan[i].post) hplan[i].sig = (long)sb.add(h[i].author, h[i].signature, hplan[i].digest);
     }
+    htrace("mixed:headers");
     std::vector<long> vsig(nv, -1);
     for (size_t i = 0; i < nv; i++) {
         const size_t dg = db.add_begin();
@@ -305,6 +318,7 @@ int verify_mixed(nwv_ctx* ctx, const nwv_committee& c, size_t nh, const nwv_head
             vsig[i] = (long)sb.add(v[i].author, v[i].signature, dg);
         }
     }
+    htrace("mixed:votes");
     std::vector<uint8_t> done(nc, 0);
     std::vector<long> agg_first(nc, -1), agg_count(nc, 0);
     std::vector<int32_t> after_header(nc, NWV_DAG_OK);
