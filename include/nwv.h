@@ -55,8 +55,9 @@ typedef struct nwv_ctx nwv_ctx;
  * NWV_MSM_SORT2_MIN_PTS points or more (env, default 2^20) */
 #define NWV_FLAG_MSM_SORT2 16u
 /* diagnostic / tests: when a batch MSM over per-signature keys rejects and the verdict bits are
- * wanted, the per-signature pass builds its point tables from the MSM's decompressed records by
- * default (k_ed_points_msm); this flag makes it decompress again (k_ed_points) */
+ * wanted, the per-signature pass reuses the MSM's work by default: point tables from its
+ * decompressed records (k_ed_points_msm) and k_i / the s < l flag its hash role stored (no
+ * k_ed_hash); this flag makes the pass hash and decompress again */
 #define NWV_FLAG_NO_MSM_REUSE 32u
 
 /* ------------------------------------------------------------------ lifecycle ----- */

@@ -88,6 +88,10 @@ struct MsmScalarArgs {
     // zeroes its digit column (point na, and na - 1 = 2^128 B's column of the key-cache form)
     uint32_t split;
     uint32_t* tail_ctr;  // k_msm_tail's arrival counters (64 words), zeroed by workgroup 0
+    // batches over per-signature keys: k_i and the s < l flag for the per-signature fallback
+    // (k_ed_hash's outputs, so a rejected batch's exact-bad-set pass skips the hashing), or null
+    uint32_t* kout;
+    uint32_t* fout;
 };
 struct MsmPointArgs {
     uint64_t n, na;
@@ -117,6 +121,10 @@ __device__ __forceinline__ void msm_scalars_block(uint32_t blk, const MsmScalarA
         msm_load8(sig + 64 * i + 32, Sw);
         const uint32_t f = lane_hash(Aw, Rw, Sw, msg + g.msg_off[i], g.msg_len[i], k);
         if (f != FLAG_S_OK) atomicOr(fail, 1u);
+        if (g.kout) {
+            msm_store8(g.kout + 8 * i, k);
+            g.fout[i] = f;
+        }
         uint32_t sd[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) sd[k] = seedp[k];

@@ -364,9 +364,10 @@ int ed_launch(Lane& d, EdBuffers& b, size_t n, hipStream_t stream, hipEvent_t* e
     const size_t waves = (n + 63) / 64;
     const dim3 blk(256), grid((unsigned)((n + 255) / 256)), grid2((unsigned)((2 * 64 * waves + 255) / 256));
     if (ev) NWV_HIP(hipEventRecord(ev[0], stream));
-    hipLaunchKernelGGL(k_ed_hash, grid, blk, 0, stream, (uint64_t)n, b.pk.as<uint8_t>(),
-                       b.sig.as<uint8_t>(), b.msg.as<uint8_t>(), b.off.as<uint64_t>(),
-                       b.len.as<uint32_t>(), b.kbuf.as<uint8_t>(), b.flags.as<uint32_t>());
+    if (!msm_pts)  // (after a batch MSM over per-signature keys, k_msm_prep left k and the flags)
+        hipLaunchKernelGGL(k_ed_hash, grid, blk, 0, stream, (uint64_t)n, b.pk.as<uint8_t>(),
+                           b.sig.as<uint8_t>(), b.msg.as<uint8_t>(), b.off.as<uint64_t>(),
+                           b.len.as<uint32_t>(), b.kbuf.as<uint8_t>(), b.flags.as<uint32_t>());
     if (ev) NWV_HIP(hipEventRecord(ev[1], stream));
     if (msm_pts)
         hipLaunchKernelGGL(k_ed_points_msm, grid2, blk, 0, stream, (uint64_t)n, (uint64_t)n, msm_pts,
@@ -540,10 +541,14 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     if ((rc = mark(0))) return rc;
     int16_t* digits = b.m_digits.as<int16_t>();
     const int keyed = b.nkeys_distinct ? 1 : 0;
+    // per-signature keys: the hash role also leaves k_i and the s < l flag for the fallback
+    const bool reuse = !keyed && !(d.flags & NWV_FLAG_NO_MSM_REUSE);
+    if (reuse && ((rc = b.kbuf.ensure(32 * n + 16)) || (rc = b.flags.ensure(4 * n + 4)))) return rc;
     const MsmScalarArgs gs{(uint64_t)n, (uint64_t)na, keyed, b.pk.as<uint8_t>(), b.sig.as<uint8_t>(),
                            b.msg.as<uint8_t>(), b.off.as<uint64_t>(), b.len.as<uint32_t>(), state + 8,
                            b.m_ascal.as<uint32_t>(), digits, b.m_partial.as<uint32_t>(), state,
-                           b.kc_split ? 1u : 0u, b.m_ctr.as<uint32_t>()};
+                           b.kc_split ? 1u : 0u, b.m_ctr.as<uint32_t>(), reuse ? b.kbuf.as<uint32_t>() : nullptr,
+                           reuse ? b.flags.as<uint32_t>() : nullptr};
     const MsmPointArgs gp{(uint64_t)n, (uint64_t)na, b.kc_split ? 0 : (uint64_t)na,
                           keyed ? b.keys.as<uint8_t>() : b.pk.as<uint8_t>(),
                           b.sig.as<uint8_t>(), b.m_pts.as<uint32_t>(), state};
