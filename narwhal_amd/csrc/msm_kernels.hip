@@ -468,7 +468,7 @@ extern "C" __global__ void __launch_bounds__(1024) k_msm_wscan(
 // (replaces hist + scan + scatter)
 extern "C" __global__ void __launch_bounds__(1024) k_msm_sort1(
     uint64_t n, uint64_t na, MsmLayout lay, const int16_t* __restrict__ digits, uint32_t* __restrict__ kstart,
-    uint32_t* __restrict__ tot_out, uint32_t* __restrict__ entries) {
+    uint32_t* __restrict__ tot_out, uint32_t* __restrict__ entries, uint32_t seg, uint32_t* __restrict__ seg_key) {
     extern __shared__ uint32_t cur[];
     __shared__ uint32_t wsum[16];
     const int w = blockIdx.x, nb = 1 << (lay.width[w] - 1);
@@ -516,6 +516,13 @@ extern "C" __global__ void __launch_bounds__(1024) k_msm_sort1(
             kstart[lay.kbase[w] + b] = o;
         }
         carry += step;
+    }
+    __syncthreads();
+    // the bucket each bucket lane of k_msm_bucket[_q] starts in (segment g = entries [g seg, ...)):
+    // written here from the bucket offsets instead of a binary search of kstart per lane
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+        const uint32_t s0 = cur[b], e0 = b + 1 < nb ? cur[b + 1] : ebase + carry;
+        for (uint32_t g = (s0 + seg - 1) / seg; g * seg < e0; g++) seg_key[g] = lay.kbase[w] + (uint32_t)b;
     }
     __syncthreads();
     for (uint64_t j = threadIdx.x; j < cap; j += blockDim.x) {
@@ -635,18 +642,21 @@ __device__ __forceinline__ ge_precomp msm_point_of(const uint32_t w[32], uint32_
 extern "C" __global__ void __launch_bounds__(256) k_msm_bucket(
     uint32_t T, uint32_t nkeys, const uint32_t* __restrict__ total, const uint32_t* __restrict__ entries,
     const uint32_t* __restrict__ kstart, const uint32_t* __restrict__ pts, uint32_t* __restrict__ bsum,
-    uint32_t* __restrict__ hpart) {
+    uint32_t* __restrict__ hpart, const uint32_t* __restrict__ seg_key) {
     const uint32_t E = *total;
     const uint64_t k0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * T;
     if (k0 >= E) return;
     const uint32_t k1 = (uint32_t)(k0 + T < E ? k0 + T : E);
-    // key = the largest key with kstart[key] <= k0 (non-empty, contains entry k0)
+    // key = the largest key with kstart[key] <= k0 (non-empty, contains entry k0): from the sort's
+    // segment map when it wrote one (one-chunk batches), else a binary search
     uint32_t lo = 0, hi = nkeys;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (kstart[mid] <= k0) lo = mid;
-        else hi = mid;
-    }
+    if (seg_key) lo = seg_key[k0 / T];
+    else
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (kstart[mid] <= k0) lo = mid;
+            else hi = mid;
+        }
     uint32_t key = lo;
     uint32_t kend = key + 1 < nkeys ? kstart[key + 1] : E;
     bool head = kstart[key] < k0;
@@ -716,18 +726,20 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_bucket(
 extern "C" __global__ void __launch_bounds__(256) k_msm_bucket_q(
     uint32_t T, uint32_t nkeys, const uint32_t* __restrict__ total, const uint32_t* __restrict__ entries,
     const uint32_t* __restrict__ kstart, const uint32_t* __restrict__ pts, uint32_t* __restrict__ bsum,
-    uint32_t* __restrict__ hpart) {
+    uint32_t* __restrict__ hpart, const uint32_t* __restrict__ seg_key) {
     const uint32_t E = *total;
     const int q = threadIdx.x & 3;
     const uint64_t k0 = ((uint64_t)blockIdx.x * (blockDim.x >> 2) + (threadIdx.x >> 2)) * T;
     if (k0 >= E) return;  // whole quad
     const uint32_t k1 = (uint32_t)(k0 + T < E ? k0 + T : E);
     uint32_t lo = 0, hi = nkeys;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (kstart[mid] <= k0) lo = mid;
-        else hi = mid;
-    }
+    if (seg_key) lo = seg_key[k0 / T];  // (k_msm_sort1's segment map), else a binary search
+    else
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (kstart[mid] <= k0) lo = mid;
+            else hi = mid;
+        }
     uint32_t key = lo;
     uint32_t kend = key + 1 < nkeys ? kstart[key + 1] : E;
     bool head = kstart[key] < k0;

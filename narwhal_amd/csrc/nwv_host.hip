@@ -120,7 +120,7 @@ struct PinnedBuf {
 struct EdBuffers {
     DevBuf pk, sig, msg, off, len, kbuf, flags, tables, verdict;
     DevBuf m_scal, m_partial, m_state, m_pts, m_digits, m_cnt, m_tiles, m_entries, m_kstart, m_hpart,
-        m_bsum, m_wsum, m_tpart, m_ctr, m_stamps, m_bpt, m_mid, m_kst2;
+        m_bsum, m_wsum, m_tpart, m_ctr, m_stamps, m_bpt, m_mid, m_kst2, m_segkey;
     // keyed batches: distinct keys (m x 32), CSR of signatures by key, per-signature z_i k_i
     DevBuf keys, koff, ksig, m_ascal;
     DevBuf kslot;  // keyed batches over the key cache: each distinct key's cache slot
@@ -130,7 +130,7 @@ struct EdBuffers {
     void release() {
         for (DevBuf* b : {&pk, &sig, &msg, &off, &len, &kbuf, &flags, &tables, &verdict, &m_scal,
                           &m_partial, &m_state, &m_pts, &m_digits, &m_cnt, &m_tiles, &m_entries,
-                          &m_kstart, &m_hpart, &m_bsum, &m_wsum, &m_tpart, &m_ctr, &m_stamps, &m_bpt, &m_mid, &m_kst2, &keys, &koff, &ksig, &m_ascal,
+                          &m_kstart, &m_hpart, &m_bsum, &m_wsum, &m_tpart, &m_ctr, &m_stamps, &m_bpt, &m_mid, &m_kst2, &m_segkey, &keys, &koff, &ksig, &m_ascal,
                           &kslot, &in})
             b->release();
         nkeys_distinct = 0;
@@ -500,6 +500,7 @@ int msm_alloc(EdBuffers& b, const MsmPlan& p, size_t n) {
         (p.shift && (rc = b.m_kst2.ensure((size_t)4 * p.lay2.kbase[p.lay2.nw] + 64))) ||
         (rc = b.m_kstart.ensure((size_t)4 * p.nkeys + 64)) ||
         (rc = b.m_hpart.ensure((size_t)4 * P3_WORDS * p.nseg + 64)) ||
+        (p.chunks == 1 && (rc = b.m_segkey.ensure((size_t)4 * p.nseg + 64))) ||
         (rc = b.m_bsum.ensure((size_t)4 * P3_WORDS * p.nkeys + 64)) ||
         (rc = b.m_wsum.ensure((size_t)4 * P3_WORDS * p.lay.nw + 64)) ||
         (rc = b.m_tpart.ensure((size_t)4 * P3_WORDS * TAIL_PART_SLOTS * p.lay.nw * p.tail_S + 64)) ||
@@ -577,7 +578,7 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
         // one chunk per window: the whole counting sort of a window in one workgroup (timed in
         // the k_msm_hist slot)
         hipLaunchKernelGGL(k_msm_sort1, dim3((unsigned)p.lay.nw), dim3(1024), lds_nb, stream, (uint64_t)n,
-                           (uint64_t)na, p.lay, digits, kst, tot, ent);
+                           (uint64_t)na, p.lay, digits, kst, tot, ent, p.seg, b.m_segkey.as<uint32_t>());
         if ((rc = mark(4))) return rc;
         if ((rc = mark(5))) return rc;
     } else {
@@ -603,6 +604,7 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     }
     if ((rc = mark(6))) return rc;
     const uint32_t* E = tot + MSM_MAX_WINDOWS;
+    const uint32_t* seg_key = p.chunks == 1 ? b.m_segkey.as<uint32_t>() : nullptr;
     // bucket sums on quads where they are latency-bound (small batches), else one lane per chunk
     static const uint64_t bucket_quad_max_n = [] {
         const char* e = std::getenv("NWV_BUCKET_QUAD_MAX_N");
@@ -611,11 +613,11 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     if (n <= bucket_quad_max_n)
         hipLaunchKernelGGL(k_msm_bucket_q, dim3((unsigned)((p.nseg + 63) / 64)), dim3(256), 0, stream, p.seg,
                            p.nkeys, E, ent, kst, b.m_pts.as<uint32_t>(), b.m_bsum.as<uint32_t>(),
-                           b.m_hpart.as<uint32_t>());
+                           b.m_hpart.as<uint32_t>(), seg_key);
     else
         hipLaunchKernelGGL(k_msm_bucket, dim3((unsigned)((p.nseg + 255) / 256)), dim3(256), 0, stream, p.seg,
                            p.nkeys, E, ent, kst, b.m_pts.as<uint32_t>(), b.m_bsum.as<uint32_t>(),
-                           b.m_hpart.as<uint32_t>());
+                           b.m_hpart.as<uint32_t>(), seg_key);
     if ((rc = mark(7))) return rc;
     // window sums, their scaling, the basepoint term and the verdict: one launch (its arrival
     // counters were zeroed by k_msm_prep's first workgroup, graph replays included)
