@@ -7,14 +7,14 @@ messages, RFC 8032 signatures made on the GPU), through the batch MSM (K5, ed255
 batch::Verifier semantics).  --inflight K keeps K resident batches on K streams and issues the
 steps round-robin; the single-stream step time is reported beside it.
 
-N > 1 (--gpus N): BASELINE.json configs[2], the firehose.  16,777,216 signatures (32-byte messages)
-are sharded by contiguous 64-aligned index ranges over the N ranks, one process per GPU; a step is
-one pass over all 16M (every rank verifies its resident shard, as sub-shards of <= 2,097,152 on
-their own streams).  Strong scaling: the total is fixed.  There is no data-path collective: after
-the timed region the ranks exchange only the max of their times and, once, their verdict bitmaps
-(one all_gather over gloo) for the exact-bad-set check.  Without WORLD_SIZE in the environment,
---gpus N spawns the N rank processes itself (before anything touches the GPU);
-torch.distributed.run launches them the same way.
+N > 1 (--gpus N): the same configs[1] workload on every rank, one process per GPU, no collective
+in the data path; value = all ranks' signatures / the max-over-ranks time (weak scaling, so the
+1/2/4/8 values form a same-workload series).  Without WORLD_SIZE in the environment, --gpus N
+spawns the N rank processes itself (before anything touches the GPU); torch.distributed.run
+launches them the same way.  The configs[2] firehose then runs as the `firehose` field: 16,777,216
+signatures (32-byte messages) sharded by contiguous 64-aligned index ranges over the ranks (strong
+scaling), verified as resident sub-shards, the verdict bitmaps merged once over gloo for the
+exact-bad-set check.
 
 Extra fields: roofline (dominant kernel) and roofline_per_kernel, cpu_baseline (the oracle's
 batch verifier on the host's usable cores, rank 0, N = 1), host_to_host (pipelined verification of
@@ -234,28 +234,47 @@ def cpu_baseline_configs(legs, data, threads):
 
 
 # ------------------------------------------------------------------------------ roofline --
-def pmc_kernel(kernel, n):
-    """(counters, source) of `kernel` in the newest committed rocprofv3 --pmc summary at batch
-    size n, or (None, None)"""
+MSM_KERNELS = ("k_msm_prep", "k_msm_hash", "k_msm_decomp", "k_msm_hist", "k_msm_wscan", "k_msm_scatter",
+               "k_msm_lsort", "k_msm_sort1", "k_msm_bucket", "k_msm_bucket_q", "k_msm_tail", "k_msm_keysum",
+               "k_msm_fixup", "k_msm_bscalar")
+
+
+def pmc_file(n, launch):
+    """(summary, path) of the newest committed rocprofv3 --pmc summary (tools/pmc_summary.py) that
+    describes TODAY's pipeline at batch size n: its kernel_source_hash equals the hash of the
+    device sources at HEAD, and its MSM kernels are exactly `launch` (the kernels this run
+    launched); else (None, None), and the counter-derived fields are reported as null"""
     import glob
+    from narwhal_amd._lib import kernel_source_hash
+    want = kernel_source_hash()
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
         try:
             with open(f) as fh:
                 d = json.load(fh)
         except (OSError, ValueError):
             continue
-        k = d.get("kernels", {}).get(kernel)
-        if d.get("n") == n and k:
-            return k, os.path.relpath(f, ROOT)
+        if d.get("n") != n or d.get("kernel_source_hash") != want:
+            continue
+        have = {k for k in d.get("kernels", {}) if k in MSM_KERNELS}
+        if have != set(k for k in launch if k in MSM_KERNELS):
+            continue
+        return d, os.path.relpath(f, ROOT)
     return None, None
 
 
-def pmc_traffic(kernels, n):
+def pmc_kernel(kernel, n, launch):
+    """(counters, source) of `kernel` from pmc_file(n, launch), or (None, None)"""
+    d, src = pmc_file(n, launch)
+    k = (d or {}).get("kernels", {}).get(kernel)
+    return (k, src) if k else (None, None)
+
+
+def pmc_traffic(kernels, n, launch):
     """HBM bytes per launch from the committed rocprofv3 --pmc passes (FETCH_SIZE doubled for
     gfx950's half-counted wide reads + WRITE_SIZE, MI355X_MICROARCH.md HBM section)"""
     total, srcs = 0.0, set()
     for k in kernels:
-        c, src = pmc_kernel(k, n)
+        c, src = pmc_kernel(k, n, launch)
         if not c or "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
             return None
         total += 2 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024
@@ -263,7 +282,7 @@ def pmc_traffic(kernels, n):
     return {"bytes": total, "source": sorted(srcs)}
 
 
-def issue_floor(kernels, n, kms, peak):
+def issue_floor(kernels, n, kms, peak, launch):
     """mix-weighted VALU issue floor: the committed PMC pass's wave-level VALU instructions of the
     kernel, the 64-bit integer forms (SQ_INSTS_VALU_INT64) priced at the measured v_mad_u64_u32
     rate and the rest at the measured v_add_u32 rate, against the live kernel time"""
@@ -272,7 +291,7 @@ def issue_floor(kernels, n, kms, peak):
     v = i64 = 0.0
     srcs = set()
     for k in kernels:
-        c, src = pmc_kernel(k, n)
+        c, src = pmc_kernel(k, n, launch)
         if not c or "SQ_INSTS_VALU" not in c or "SQ_INSTS_VALU_INT64" not in c:
             return None
         v += c["SQ_INSTS_VALU"]
@@ -289,6 +308,7 @@ def kernel_rooflines(kt, stats, n, na, peak):
     nw, nwz, buckets, E = stats["windows"], stats["windows_z"], stats["buckets"], stats["entries"]
     digit_slots = (na + 1) * nw + n * nwz
     cnt_len = buckets * stats["chunks"]
+    launch = list(kt)
     out = {}
 
     def valu(name, pmc, mads, what):
@@ -298,13 +318,13 @@ def kernel_rooflines(kt, stats, n, na, peak):
                      "frac": (a / mad_peak) if (a and mad_peak) else None,
                      "peak_guide": GUIDE_MAD64 / 1e12, "frac_guide": (a / (GUIDE_MAD64 / 1e12)) if a else None,
                      "algorithmic": what, "mads_per_launch": mads, "kernel_ms": kms,
-                     "traffic": (pmc_traffic(pmc, n) or {}).get("bytes"),
-                     "issue_floor": issue_floor(pmc, n, kms, peak)}
+                     "traffic": (pmc_traffic(pmc, n, launch) or {}).get("bytes"),
+                     "issue_floor": issue_floor(pmc, n, kms, peak, launch)}
 
     def mem(name, pmc, nbytes, what):
         kms = kt.get(name, 0.0)
         a = nbytes / (kms * 1e-3) / 1e9 if kms > 0 else None
-        tr = pmc_traffic(pmc, n)
+        tr = pmc_traffic(pmc, n, launch)
         out[name] = {"bound": "hbm", "achieved": a, "unit": "GB/s", "peak": HBM_PEAK_GBS,
                      "frac": (a / HBM_PEAK_GBS) if a else None, "algorithmic": what,
                      "bytes_per_launch": nbytes, "kernel_ms": kms,
@@ -331,6 +351,54 @@ def kernel_rooflines(kt, stats, n, na, peak):
 
 
 # ------------------------------------------------------------------------------- N = 1 ----
+def timed_region(stages, args, dist, run):
+    """The bench contract's timed region: W untimed warmup steps, then (every stage synchronised,
+    barrier) exactly K steps, step s on stage s % len(stages), then every stage synchronised and a
+    barrier.  Returns (this rank's seconds, the max over ranks)."""
+    for w in range(args.warmup):
+        run(stages[w % len(stages)])
+    for s_ in stages:
+        s_.sync()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        run(stages[s % len(stages)])
+    for s_ in stages:
+        s_.sync()
+    dt = time.perf_counter() - t0
+    dt_max = dt
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt_max = float(t.item())
+        dist.barrier()
+    return dt, dt_max
+
+
+class DryStage:
+    """NWV_BENCH_DRYRUN stand-in for a resident batch (CPU tests of the multi-rank timing path):
+    a step is a fixed amount of host work, every verdict valid"""
+
+    def __init__(self, n):
+        self.n = n
+        self.runs = 0
+
+    def run(self, mode=1, timed=False):
+        self.runs += 1
+        np.sort(np.random.default_rng(self.runs).integers(0, 1 << 30, 20000))
+
+    def sync(self):
+        pass
+
+
+def run_headline_dry(args, rank, world, dist):
+    stages = [DryStage(args.n) for _ in range(max(1, args.inflight))]
+    dt, dt_max = timed_region(stages, args, dist, lambda st: st.run())
+    return {"dt": dt, "dt_max": dt_max}
+
+
 def run_headline(args, eng, rank, world, dist):
     from narwhal_amd import _lib
     pk, sg, msgs, offs, lens = synth(eng, args.n, args.msg_len, seed=1000 + rank, keys=args.keys)
@@ -352,22 +420,7 @@ def run_headline(args, eng, rank, world, dist):
     for s_ in stages:
         s_.run(mode=args.mode)
     check_all("setup")
-    for w in range(args.warmup):
-        stages[w % len(stages)].run(mode=args.mode)  # seed None: OS entropy, as OsRng
-    # the warmup runs straight into the timed region (no host round trip that would let the GPU
-    # idle and clock down); verdicts are checked after it
-    for s_ in stages:
-        s_.sync()
-    if dist is not None:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        stages[s % len(stages)].run(mode=args.mode)
-    for s_ in stages:
-        s_.sync()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        dist.barrier()
+    dt, dt_max = timed_region(stages, args, dist, lambda st: st.run(mode=args.mode))  # seed None: OS entropy
     check_all("timed region: last run of every stage")
     if args.mode == 1:
         # every run's batch verdict, graph replays included, as tallied on the device by the runs
@@ -392,7 +445,8 @@ def run_headline(args, eng, rank, world, dist):
     assert st.fetch()[0]
     for s_ in stages:
         s_.free()
-    return {"dt": dt, "single": single, "kt": kt, "stats": stats, "data": (pk, sg, msgs, offs, lens)}
+    return {"dt": dt, "dt_max": dt_max, "single": single, "kt": kt, "stats": stats,
+            "data": (pk, sg, msgs, offs, lens)}
 
 
 def kernels_1k(eng, data, reps=20):
@@ -569,23 +623,11 @@ def run_firehose(args, eng, rank, world, dist):
     roof = dict(per["k_msm_prep"], kernel="k_msm_prep", selected_by="largest VALU kernel of the bulk phase",
                 kernel_share=per["k_msm_prep"]["kernel_ms"] / sum(kt.values()), subshard_sigs=sub_n)
     return {
-        "metric": "Ed25519 sigs verified/sec",
-        "value": FIREHOSE_N * args.steps / dt,
-        "unit": "sigs/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": dt / args.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "strong",
-        "vs_baseline": None,
-        "dtype": "u32",
-        "data": "synthetic (key seeds and 32 B messages derived from the global index, RFC 8032 "
-                "signatures made on each rank's GPU)",
-        "config": {"workload": "firehose of 16,777,216 sigs sharded by index over the GPUs, host "
-                               "verdict-bitmap merge (BASELINE.json configs[2])",
-                   "sigs_total": FIREHOSE_N, "sigs_per_gpu": hi - lo, "subshards_per_gpu": nsub,
-                   "msg_len": 32, "parallelism": f"signature-index shards x{world}, no collective"},
+        "workload": "configs[2]: firehose of 16,777,216 sigs (32 B messages) sharded by index over the "
+                    "GPUs, host verdict-bitmap merge; strong scaling (the total is fixed)",
+        "sigs_per_s": FIREHOSE_N * args.steps / dt, "passes": args.steps, "ms_per_pass": dt / args.steps * 1e3,
+        "sigs_total": FIREHOSE_N, "sigs_per_gpu": hi - lo, "subshards_per_gpu": nsub,
+        "parallelism": f"signature-index shards x{world}, no collective",
         "kernel_ms_rank0_subshard": kt,
         "roofline": roof,
         "roofline_per_kernel": per,
@@ -623,12 +665,36 @@ def run_firehose_dry(args, rank, world, dist):
     bits = np.unpackbits(words.view(np.uint8), bitorder="little")[:n_total]
     exact = np.flatnonzero(bits == 0).tolist() == bad and not ok
     if rank == 0:
-        return {"metric": "Ed25519 sigs verified/sec", "value": n_total / float(t.item()), "unit": "sigs/s",
-                "n_gpus": world, "steps": 1, "warmup": 0, "dry_run": True, "scaling": "strong",
-                "config": {"workload": "firehose plumbing dry run (no GPU)", "sigs_total": n_total,
-                           "sigs_per_rank": hi - lo},
+        return {"workload": "firehose plumbing dry run (no GPU)", "sigs_per_s": n_total / float(t.item()),
+                "sigs_total": n_total, "sigs_per_rank": hi - lo, "dry_run": True,
                 "exact_bad_set": {"injected": len(bad), "exact": exact}}
     return None
+
+
+def base_line(args, world, dt):
+    """the contract's fields of the headline line: configs[1] on every rank, dt = max over ranks"""
+    return {
+        "metric": "Ed25519 sigs verified/sec",
+        "value": world * args.n * args.steps / dt,
+        "unit": "sigs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded keys/messages, RFC 8032 signatures made on the GPU)",
+        "config": {"workload": "verify_batch of 65,536 valid sigs, 512 B messages, distinct keys "
+                               "(BASELINE.json configs[1]) on every GPU",
+                   "sigs_per_batch": args.n, "msg_len": args.msg_len,
+                   "path": "batch MSM (K5)" if args.mode == 1 else "per-signature (K1-K4)",
+                   "distinct_keys": args.keys or args.n,
+                   "parallelism": "one GPU" if world == 1 else f"x{world} GPUs, one resident batch "
+                                  "stream per rank, no collective",
+                   "inflight_batches": args.inflight},
+    }
 
 
 def main():
@@ -694,9 +760,13 @@ def main():
     if os.environ.get("NWV_BENCH_DRYRUN") == "1":
         if dist is None:
             raise SystemExit("NWV_BENCH_DRYRUN needs --gpus N > 1")
-        result = run_firehose_dry(args, rank, world, dist)
-        if result is not None:
-            print(json.dumps(result), flush=True)
+        h = run_headline_dry(args, rank, world, dist)
+        fire = run_firehose_dry(args, rank, world, dist)
+        if rank == 0:
+            line = base_line(args, world, h["dt_max"])
+            line.update(dry_run=True, firehose=fire)
+            line["config"]["workload"] += " -- DRY RUN: host stand-in steps, no GPU"
+            print(json.dumps(line), flush=True)
         dist.destroy_process_group()
         return
 
@@ -704,9 +774,15 @@ def main():
 
     eng = narwhal_amd.Engine(device=local)
     if world > 1:
-        result = run_firehose(args, eng, rank, world, dist)
-        if result is not None:
-            print(json.dumps(result), flush=True)
+        # the same configs[1] workload as N = 1 on every rank (weak scaling: value = all ranks'
+        # signatures / the max-over-ranks time), then the configs[2] firehose as an extra field
+        h = run_headline(args, eng, rank, world, dist)
+        fire = run_firehose(args, eng, rank, world, dist)
+        if rank == 0:
+            line = base_line(args, world, h["dt_max"])
+            line.update(rank0_ms_per_step=h["dt"] / args.steps * 1e3, kernel_ms_rank0=h["kt"],
+                        single_stream_rank0={"ms_per_step": float(np.median(h["single"]))}, firehose=fire)
+            print(json.dumps(line), flush=True)
         eng.close()
         dist.destroy_process_group()
         return
@@ -724,25 +800,27 @@ def main():
         per = kernel_rooflines(kt, stats, args.n, na, peak)
         # the dominant kernel of the THROUGHPUT regime: the most VALU work (issue floor) -- with
         # batches in flight the latency-bound tail overlaps other batches' work; by single-stream
-        # time when no PMC pass is committed for this size
+        # time when no PMC pass of today's kernels is committed for this size
         floors = {k: (v.get("issue_floor") or {}).get("floor_ms") for k, v in per.items() if v["bound"] == "valu"}
         if all(f is not None for f in floors.values()):
-            dom, how = max(floors, key=floors.get), "largest VALU issue floor (committed PMC pass)"
+            dom, how = max(floors, key=floors.get), "largest VALU issue floor (committed PMC pass of HEAD's kernels)"
         else:
-            dom, how = max(per, key=lambda k: per[k]["kernel_ms"]), "longest single-stream kernel time"
+            dom, how = "k_msm_prep", "the bulk VALU kernel (no PMC pass of HEAD's kernels is committed)"
         roof = dict(per[dom], kernel=dom, selected_by=how,
                     kernel_share=per[dom]["kernel_ms"] / sum(kt.values()))
-        # the whole step against the chip's VALU issue rate: every MSM kernel's committed PMC
-        # instruction counts (64-bit forms at the v_mad_u64_u32 rate, the rest at v_add_u32's)
-        # over the measured time per batch with batches in flight
-        msm_k = ["k_msm_prep", "k_msm_hist", "k_msm_wscan", "k_msm_scatter", "k_msm_lsort", "k_msm_sort1",
-                 "k_msm_bucket", "k_msm_bucket_q", "k_msm_tail", "k_msm_tail_wide", "k_msm_keysum"]
-        present = [k for k in msm_k if pmc_kernel(k, args.n)[0]]
-        fl = issue_floor(present, args.n, dt / args.steps * 1e3, peak) if present else None
+        # the kernel that takes the most single-stream device time (the MSM tail: one dependent
+        # doubling chain per window, latency-bound) -- reported beside the throughput kernel
+        tdom = max(per, key=lambda k: per[k]["kernel_ms"])
+        roof["dominant_by_time"] = dict(per[tdom], kernel=tdom, kernel_share=per[tdom]["kernel_ms"] / sum(kt.values()))
+        # the whole step against the chip's VALU issue rate: every kernel of the launch list, its
+        # committed PMC instruction counts (64-bit forms at the v_mad_u64_u32 rate, the rest at
+        # v_add_u32's) over the measured time per batch with batches in flight
+        launch = list(kt)
+        fl = issue_floor(launch, args.n, dt / args.steps * 1e3, peak, launch)
         if fl:
-            fl["kernels"] = present
-            fl["note"] = ("VALU issue floor of one whole batch (all MSM kernels) against the step time "
-                          "with batches in flight")
+            fl["kernels"] = launch
+            fl["note"] = ("VALU issue floor of one whole batch (every kernel of the launch list) against the "
+                          "step time with batches in flight")
         roof["batch_issue_floor"] = fl
     else:
         kms = kt.get("k_ed_straus", 0.0)
@@ -776,25 +854,8 @@ def main():
             c5["worker_batch_digests_gpu_over_cpu"] = (c5["worker_batch_digests_ms_per_round"] /
                                                        c5["cpu_baseline"]["worker_batch_digests_ms_per_round"])
         del cdata
-    result = {
-        "metric": "Ed25519 sigs verified/sec",
-        "value": value,
-        "unit": "sigs/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": dt / args.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u32",
-        "data": "synthetic (seeded keys/messages, RFC 8032 signatures made on the GPU)",
-        "config": {"workload": "verify_batch of 65,536 valid sigs, 512 B messages, distinct keys "
-                               "(BASELINE.json configs[1])",
-                   "sigs_per_batch": args.n, "msg_len": args.msg_len,
-                   "path": "batch MSM (K5)" if args.mode == 1 else "per-signature (K1-K4)",
-                   "distinct_keys": args.keys or args.n,
-                   "parallelism": "one GPU", "inflight_batches": args.inflight},
+    result = base_line(args, 1, dt)
+    result.update({
         "single_stream": {"ms_per_step": float(np.median(h["single"])),
                           "sigs_per_s": args.n / (float(np.median(h["single"])) * 1e-3)},
         "latency_1k_batch_ms": lat,
@@ -806,7 +867,7 @@ def main():
         "cpu_baseline": cpu,
         "configs": configs,
         "valu_ubench": peak,
-    }
+    })
     print(json.dumps(result), flush=True)
     eng.close()
 

@@ -31,6 +31,7 @@ extern "C" {
 #define NWV_ERR_NODEV (-4)       /* no usable gfx950 device / code object not loadable      */
 #define NWV_ERR_EMPTY (-5)       /* verify_batch_empty_fail on an empty batch               */
 #define NWV_ERR_LENGTH (-6)      /* |pks| != |sigs| (or messages) in a batch API            */
+#define NWV_ERR_REENTRANT (-7)   /* blocking service call made from a completion callback   */
 
 #define NWV_ABI_VERSION 1
 
@@ -118,6 +119,13 @@ int nwv_ed25519_verify_batch_keyed_digests(nwv_ctx* ctx, size_t n_pre, const uin
                                            size_t n, const uint32_t* key_idx, const uint8_t* sig,
                                            const uint32_t* digest_idx, const uint8_t seed32[32],
                                            int* all_valid, uint64_t* verdict_bits_or_null);
+
+/* Fill every device's committee key cache with n_keys keys (n_keys x 32), e.g. at epoch start
+ * (Core::change_epoch, primary/src/core.rs:592-611).  Batch calls fill the cache themselves;
+ * nwv_ed25519_pubkey_verify only looks its key up (an unseen key runs uncached and takes no
+ * slot), so registering the committee gives its members' single verifies the cached form.  A
+ * full cache leaves further keys uncached; verdicts never depend on the cache. */
+int nwv_keycache_register(nwv_ctx* ctx, size_t n_keys, const uint8_t* keys);
 
 /* ---- fastcrypto 0.1.2 trait surface (Ed25519 scheme module; contract of
  *      crypto/src/bls12377/mod.rs:264-291 and :485-577) ---- */

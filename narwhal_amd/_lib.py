@@ -22,6 +22,7 @@ NWV_ERR_OOM = -3
 NWV_ERR_NODEV = -4
 NWV_ERR_EMPTY = -5
 NWV_ERR_LENGTH = -6
+NWV_ERR_REENTRANT = -7
 NWV_FLAG_MSM_ALWAYS = 1
 NWV_FLAG_MSM_NEVER = 2
 NWV_FLAG_MSM_SPLIT_PREP = 4
@@ -61,6 +62,7 @@ def load():
         "nwv_ed25519_verify_each": ([_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp], _i32),
         "nwv_ed25519_verify_batch": ([_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i32),
         "nwv_ed25519_pubkey_verify": ([_vp, _vp, _vp, _sz, _vp], _i32),
+        "nwv_keycache_register": ([_vp, _sz, _vp], _i32),
         "nwv_ed25519_verify_batch_empty_fail": ([_vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp], _i32),
         "nwv_ed25519_aggregate_verify": ([_vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp], _i32),
         "nwv_ed25519_aggregate_batch_verify": ([_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp], _i32),
@@ -87,6 +89,20 @@ def load():
         f.restype = res
     _lib = lib
     return lib
+
+
+def kernel_source_hash():
+    """sha256 (16 hex digits) over the device-code sources (narwhal_amd/csrc/*.hip, *.h): committed
+    rocprofv3 --pmc summaries carry it, and bench.py uses a summary only while it matches, so
+    counters of kernels that have since changed are never priced against today's timings"""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(_HERE, "csrc", "*.hip")) + glob.glob(os.path.join(_HERE, "csrc", "*.h"))):
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def exported_symbols_from_header():

@@ -172,11 +172,22 @@ struct Key32 {
     uint8_t b[32];
     bool operator==(const Key32& o) const { return std::memcmp(b, o.b, 32) == 0; }
 };
+// All 32 key bytes, mixed with a per-process random seed: keys chosen to collide in the map
+// would otherwise make every lookup under the cache lock linear.
 struct Key32Hash {
     size_t operator()(const Key32& k) const {
-        uint64_t h;
-        std::memcpy(&h, k.b, 8);
-        return (size_t)(h ^ (h >> 29));
+        static const uint64_t seed = [] {
+            std::random_device rd;
+            return ((uint64_t)rd() << 32) ^ rd() ^ 0x9E3779B97F4A7C15ull;
+        }();
+        uint64_t h = seed;
+        for (int i = 0; i < 4; i++) {
+            uint64_t w;
+            std::memcpy(&w, k.b + 8 * i, 8);
+            h = (h ^ w) * 0xFF51AFD7ED558CCDull;
+            h ^= h >> 32;
+        }
+        return (size_t)h;
     }
 };
 struct KeyCache {
@@ -343,8 +354,11 @@ struct KernelTimes {
 
 // Launch the three-phase per-signature pipeline on buffers already resident on `d`.
 // Events bracket each kernel on d.stream when `ev` is non-null (ev[0..5]).
-// Per-signature scratch (k, flags, 2 KiB tables, verdict words): allocated on the first
-// per-signature run of a buffer set, so batches that the MSM accepts never hold it.
+// Per-signature scratch (k 32 B, flags 4 B, the 0..8 A and 0..8 R tables = LANE_SCRATCH_WORDS
+// = 2 x 9 x 50 words = 3,600 B, verdict bits): about 3.6 KiB per signature, allocated on the
+// first per-signature run of a buffer set, so batches that the MSM accepts never hold it.  The
+// largest shard the engine stages (a 2,097,152-signature firehose sub-shard, exercised by the
+// exact-bad-set GPU tests) takes 7.6 GB of it; the 288 GB HBM holds that many times over.
 int ed_scratch(EdBuffers& b, size_t n) {
     int rc;
     if ((rc = b.kbuf.ensure(32 * n + 16)) || (rc = b.flags.ensure(4 * n + 4)) ||
@@ -857,8 +871,10 @@ int ed_stage(Lane& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, con
 // Cache slots of m distinct keys on d's device (misses are filled first, on d.stream, under the
 // cache lock); out is left empty when the call should go uncached (cache disabled or full, or
 // more keys than NWV_KEYCACHE_MAX_KEYS: a batch of mostly fresh keys would pay 128 doublings
-// per key for nothing).
-int keycache_slots(Lane& d, const uint8_t* keys, size_t m, std::vector<uint32_t>& out) {
+// per key for nothing).  lookup_only: use the cache only if every key is already in it (single
+// verifies: a one-off or undecodable key must neither take a slot for good nor make the call
+// wait for a fill under the device-wide lock).
+int keycache_slots(Lane& d, const uint8_t* keys, size_t m, std::vector<uint32_t>& out, bool lookup_only = false) {
     out.clear();
     static const long max_keys = [] {
         const char* e = std::getenv("NWV_KEYCACHE_MAX_KEYS");
@@ -868,6 +884,21 @@ int keycache_slots(Lane& d, const uint8_t* keys, size_t m, std::vector<uint32_t>
     KeyCache& kc = d.gpu->kc;
     std::lock_guard<std::mutex> g(kc.mu);
     if (kc.broken) return NWV_OK;
+    if (lookup_only) {
+        if (!kc.cap || !kc.b_ready) return NWV_OK;
+        out.resize(m);
+        for (size_t j = 0; j < m; j++) {
+            Key32 k;
+            std::memcpy(k.b, keys + 32 * j, 32);
+            auto it = kc.slot.find(k);
+            if (it == kc.slot.end()) {
+                out.clear();
+                return NWV_OK;
+            }
+            out[j] = it->second;
+        }
+        return NWV_OK;
+    }
     constexpr uint32_t kCap = 1u << 16;  // 16 MiB of records
     if (!kc.cap) {
         // allocated once at full size: captured graphs and in-flight batches hold its address
@@ -949,7 +980,7 @@ int keycache_slots(Lane& d, const uint8_t* keys, size_t m, std::vector<uint32_t>
 int ed_stage_keyed(Lane& d, EdBuffers& b, size_t lo, size_t hi, size_t n_keys, const uint8_t* keys,
                    const uint32_t* key_idx, const uint8_t* sig, const uint8_t* msg_base,
                    const uint64_t* msg_off, const uint32_t* msg_len, const uint8_t* seed32,
-                   const DevBuf* dev_msg = nullptr) {
+                   const DevBuf* dev_msg = nullptr, bool kc_lookup_only = false) {
     const size_t n = hi - lo;
     // per-thread scratch reused across calls (fresh large vectors are page-faulted in every call)
     thread_local std::vector<uint32_t> local, cnt, kid, koff, ksig, cur;
@@ -978,7 +1009,7 @@ int ed_stage_keyed(Lane& d, EdBuffers& b, size_t lo, size_t hi, size_t n_keys, c
     cur.assign(koff.begin(), koff.end() - 1);
     for (size_t i = 0; i < n; i++) ksig[cur[kid[i]]++] = (uint32_t)i;
     thread_local std::vector<uint32_t> kslot;
-    int rc = keycache_slots(d, klist.data(), m, kslot);
+    int rc = keycache_slots(d, klist.data(), m, kslot, kc_lookup_only);
     if (rc) return rc;
     const KeyedTail kt{klist.data(), m, koff.data(), ksig.data(), kslot.empty() ? nullptr : kslot.data()};
     return ed_stage(d, b, 0, n, pk.data(), sig + 64 * lo, msg_base, msg_off + lo, msg_len + lo, seed32, &kt,
@@ -1284,10 +1315,11 @@ int nwv_ed25519_verify_batch(nwv_ctx* ctx, size_t n, const uint8_t* pk, const ui
     return rc;
 }
 
-int nwv_ed25519_verify_batch_keyed(nwv_ctx* ctx, size_t n_keys, const uint8_t* keys, size_t n,
+static int verify_batch_keyed_impl(nwv_ctx* ctx, size_t n_keys, const uint8_t* keys, size_t n,
                                    const uint32_t* key_idx, const uint8_t* sig, const uint8_t* msg_base,
                                    const uint64_t* msg_off, const uint32_t* msg_len,
-                                   const uint8_t seed32[32], int* all_valid, uint64_t* verdict_bits_or_null) {
+                                   const uint8_t seed32[32], int* all_valid, uint64_t* verdict_bits_or_null,
+                                   bool kc_lookup_only) {
     if (!ctx || !all_valid || (n && (!keys || !key_idx || !sig || !msg_off || !msg_len)))
         return set_err(NWV_ERR_ARG, "null argument");
     *all_valid = 1;
@@ -1301,7 +1333,8 @@ int nwv_ed25519_verify_batch_keyed(nwv_ctx* ctx, size_t n_keys, const uint8_t* k
         uint8_t s2[32];
         std::memcpy(s2, seed, 32);
         for (int k = 0; k < 8; k++) s2[24 + k] ^= (uint8_t)((uint64_t)lo >> (8 * k));
-        int r = ed_stage_keyed(d, d.ed, lo, hi, n_keys, keys, key_idx, sig, msg_base, msg_off, msg_len, s2);
+        int r = ed_stage_keyed(d, d.ed, lo, hi, n_keys, keys, key_idx, sig, msg_base, msg_off, msg_len, s2,
+                               nullptr, kc_lookup_only);
         if (r) return r;
         int ok = 1;
         r = batch_on_device(d, d.ed, hi - lo, s2, d.stream, &ok,
@@ -1311,6 +1344,30 @@ int nwv_ed25519_verify_batch_keyed(nwv_ctx* ctx, size_t n_keys, const uint8_t* k
         if (!ok) *all_valid = 0;
         return NWV_OK;
     });
+}
+
+int nwv_ed25519_verify_batch_keyed(nwv_ctx* ctx, size_t n_keys, const uint8_t* keys, size_t n,
+                                   const uint32_t* key_idx, const uint8_t* sig, const uint8_t* msg_base,
+                                   const uint64_t* msg_off, const uint32_t* msg_len,
+                                   const uint8_t seed32[32], int* all_valid, uint64_t* verdict_bits_or_null) {
+    return verify_batch_keyed_impl(ctx, n_keys, keys, n, key_idx, sig, msg_base, msg_off, msg_len, seed32, all_valid,
+                                   verdict_bits_or_null, false);
+}
+
+// Committee registration (epoch start, Core::change_epoch primary/src/core.rs:592-611): fill the
+// key cache of every device with the committee's keys, so single verifies by them
+// (nwv_ed25519_pubkey_verify, which only looks keys up) take the 128-bit-scalar form.
+int nwv_keycache_register(nwv_ctx* ctx, size_t n_keys, const uint8_t* keys) {
+    if (!ctx || (n_keys && !keys)) return set_err(NWV_ERR_ARG, "null argument");
+    for (Gpu* g : ctx->devs) {
+        LaneRef lane(*g);
+        int rc = lane.rc();
+        std::vector<uint32_t> slots;
+        for (size_t a = 0; a < n_keys && !rc; a += 4096)
+            rc = keycache_slots(*lane, keys + 32 * a, std::min<size_t>(4096, n_keys - a), slots);
+        if (rc) return rc;
+    }
+    return NWV_OK;
 }
 
 // ---- fastcrypto trait surface ---------------------------------------------------------
@@ -1333,8 +1390,8 @@ int nwv_ed25519_pubkey_verify(nwv_ctx* ctx, const uint8_t pk[32], const uint8_t*
     }
     const uint32_t kidx = 0;
     int all = 0;
-    int rc = nwv_ed25519_verify_batch_keyed(ctx, 1, pk, 1, &kidx, sig, msg_len ? msg : empty, &off, &len, nullptr,
-                                            &all, nullptr);
+    int rc = verify_batch_keyed_impl(ctx, 1, pk, 1, &kidx, sig, msg_len ? msg : empty, &off, &len, nullptr, &all,
+                                     nullptr, true);
     if (rc) return rc;
     return all ? NWV_OK : NWV_ERR_SIGNATURE;
 }

@@ -109,9 +109,16 @@ void waiter_done(void* user, int32_t r) {
     w->cv.notify_one();
 }
 
+// Set while a flusher runs completion callbacks.  A callback may submit asynchronously, but a
+// blocking call from it (nwv_service_verify_*, nwv_service_flush) would wait for batches that
+// this very thread -- or, with both flushers inside callbacks, no thread -- would ever verify:
+// such calls return NWV_ERR_REENTRANT instead of deadlocking.
+thread_local bool tl_in_callback = false;
+
 template <class Submit>
 int verify_blocking(Submit submit, int32_t* result) {
     if (!result) return NWV_ERR_ARG;
+    if (tl_in_callback) return NWV_ERR_REENTRANT;
     Waiter w;
     const int rc = submit(&w);
     if (rc) return rc;
@@ -181,11 +188,13 @@ void nwv_service::run() {
         const int rc_call = nwv_verify_mixed_many(ctx, &com_b->view, H.size(), H.data(), rh.data(), V.size(),
                                                   V.data(), rv.data(), C.size(), C.data(), rc.data());
         size_t ih = 0, iv = 0, ic = 0;
+        tl_in_callback = true;
         for (auto& it : batch) {
             int32_t r = rc_call;
             if (rc_call == 0) r = it->kind == HEADER ? rh[ih++] : it->kind == VOTE ? rv[iv++] : rc[ic++];
             if (it->done) it->done(it->user, r);
         }
+        tl_in_callback = false;
         lk.lock();
         for (auto& it : batch) open.erase(it->seq);
         stats[0]++;
@@ -323,6 +332,7 @@ int nwv_service_verify_certificate(nwv_service* svc, const nwv_certificate* c, i
 
 int nwv_service_flush(nwv_service* svc) {
     if (!svc) return NWV_ERR_ARG;
+    if (tl_in_callback) return NWV_ERR_REENTRANT;
     std::unique_lock<std::mutex> lk(svc->mu);
     const uint64_t upto = svc->next_seq;
     svc->flush_upto = std::max(svc->flush_upto, upto);

@@ -30,6 +30,7 @@ pub const NWV_ERR_OOM: c_int = -3;
 pub const NWV_ERR_NODEV: c_int = -4;
 pub const NWV_ERR_EMPTY: c_int = -5;
 pub const NWV_ERR_LENGTH: c_int = -6;
+pub const NWV_ERR_REENTRANT: c_int = -7;
 pub const NWV_ABI_VERSION: c_int = 1;
 // nwv_init flags
 pub const NWV_FLAG_MSM_ALWAYS: u32 = 1;
@@ -165,6 +166,8 @@ extern "C" {
         all_valid: *mut c_int,
         verdict_bits_or_null: *mut u64,
     ) -> c_int;
+    // committee key cache (include/nwv.h): fill it with the committee's keys at epoch start
+    pub fn nwv_keycache_register(ctx: *mut NwvCtx, n_keys: usize, keys: *const u8) -> c_int;
     // ---- fastcrypto trait surface: Verifier::verify, VerifyingKey::verify_batch_empty_fail, AggregateAuthenticator::{verify, batch_verify} (include/nwv.h)
     pub fn nwv_ed25519_pubkey_verify(
         ctx: *mut NwvCtx,

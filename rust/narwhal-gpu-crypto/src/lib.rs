@@ -94,6 +94,7 @@ fn flat<'a, T: AsRef<[u8]> + 'a>(items: impl IntoIterator<Item = &'a T>) -> Vec<
 // -------------------------------------------------------------------------- signature --
 #[derive(Debug, Clone, PartialEq, Eq, Serialize, Deserialize)]
 #[serde(transparent)]
+#[repr(transparent)]
 pub struct GpuEd25519Signature(pub Ed25519Signature);
 
 impl signature::Signature for GpuEd25519Signature {
@@ -130,6 +131,7 @@ impl Authenticator for GpuEd25519Signature {
 // ------------------------------------------------------------------------- public key --
 #[derive(Debug, Clone, PartialEq, Eq, Hash, Serialize, Deserialize)]
 #[serde(transparent)]
+#[repr(transparent)]
 pub struct GpuEd25519PublicKey(pub Ed25519PublicKey);
 
 impl AsRef<[u8]> for GpuEd25519PublicKey {
@@ -214,6 +216,7 @@ impl VerifyingKey for GpuEd25519PublicKey {
 // ------------------------------------------------------------------------ private key --
 #[derive(Debug, Serialize, Deserialize)]
 #[serde(transparent)]
+#[repr(transparent)]
 pub struct GpuEd25519PrivateKey(pub Ed25519PrivateKey);
 
 impl AsRef<[u8]> for GpuEd25519PrivateKey {
@@ -247,6 +250,7 @@ impl Signer<GpuEd25519Signature> for GpuEd25519PrivateKey {
 // --------------------------------------------------------------------------- key pair --
 #[derive(Debug, Serialize, Deserialize)]
 #[serde(transparent)]
+#[repr(transparent)]
 pub struct GpuEd25519KeyPair(pub Ed25519KeyPair);
 
 impl From<GpuEd25519PrivateKey> for GpuEd25519KeyPair {
@@ -279,7 +283,8 @@ impl KeyPair for GpuEd25519KeyPair {
     type Sig = GpuEd25519Signature;
 
     fn public(&'_ self) -> &'_ Self::PubKey {
-        // GpuEd25519PublicKey is a transparent newtype over fastcrypto's key
+        // GpuEd25519PublicKey is #[repr(transparent)] over fastcrypto's key: same layout, so the
+        // reference cast is sound
         let pk: &Ed25519PublicKey = self.0.public();
         unsafe { &*(pk as *const Ed25519PublicKey as *const GpuEd25519PublicKey) }
     }

@@ -153,6 +153,34 @@ def test_trait_contract(eng):
     assert rc == _lib.NWV_ERR_LENGTH
 
 
+@pytest.mark.parametrize("golden", ["ed25519_vectors.json", "zip215_small_order.json"])
+def test_single_verify_each_vector_alone(golden):
+    """Verifier::verify (nwv_ed25519_pubkey_verify, a one-signature keyed MSM) on every golden and
+    ZIP-215 small-order vector on its own, so no batch AND can hide a wrong individual verdict:
+    first with the key unseen (uncached form: single verifies only look the key cache up), then
+    after nwv_keycache_register (cache hit, 128-bit scalars), then on a context without the key
+    cache -- each verdict equal to the oracle's."""
+    import narwhal_amd
+    from narwhal_amd import _lib
+    vecs = [_v(v) for v in of.load_golden(golden)["vectors"]]
+    want = [of.verify(*it) for it in vecs]
+    e = narwhal_amd.Engine(device=0)
+    e2 = narwhal_amd.Engine(device=0, flags=_lib.NWV_FLAG_NO_KEYCACHE)
+    try:
+        def run(engine):
+            return [engine.lib.nwv_ed25519_pubkey_verify(engine._h, pk, m, len(m), sg) == _lib.NWV_OK
+                    for pk, sg, m in vecs]
+        assert run(e) == want                       # keys not in the cache
+        keys = b"".join(sorted({pk for pk, _, _ in vecs}))
+        _check = e.lib.nwv_keycache_register(e._h, len(keys) // 32, keys)
+        assert _check == _lib.NWV_OK
+        assert run(e) == want                       # every key cached (undecodable ones flagged)
+        assert run(e2) == want                      # key cache disabled
+    finally:
+        e.close()
+        e2.close()
+
+
 def test_staged_resident_batch(eng):
     seeds, msgs, pk, sg = _synthetic(eng, 4096, 512, seed=9)
     from narwhal_amd import _lib

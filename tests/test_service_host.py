@@ -180,3 +180,31 @@ def test_engine_error_reaches_every_submitter_and_free_drains(lib):
     svc.submit_vote(_vote(rnd, 0, False), codes.append)
     svc.close()  # drains the pending item first
     assert codes[:3] == [-2] * 3 and codes[3] == 0
+
+
+def test_callbacks_may_submit_but_blocking_calls_from_them_fail_fast(lib):
+    """a completion callback that calls nwv_service_flush or a blocking verify would wait
+    on the flusher running it; the service returns NWV_ERR_REENTRANT instead, and an asynchronous
+    submit from a callback still completes"""
+    from narwhal_amd import _lib
+    lib.stub_reset(0, 0)
+    rnd = random.Random(6)
+    svc = S.Service(None, _committee(0), max_batch=1, max_wait_us=0, lib=lib, ctx=ctypes.c_void_p(1))
+    try:
+        seen, chained = [], threading.Event()
+
+        def cb(code):
+            for call in (svc.flush, lambda: svc.verify_vote(_vote(rnd, 0, False))):
+                try:
+                    call()
+                    seen.append("returned")
+                except _lib.NwvError as e:
+                    seen.append(e.code)
+            svc.submit_vote(_vote(rnd, 0, True), lambda c: (seen.append(("chained", c)), chained.set()))
+
+        svc.submit_header(_header(rnd, 0, False), cb)
+        assert chained.wait(5)
+        svc.flush()
+        assert seen == [_lib.NWV_ERR_REENTRANT, _lib.NWV_ERR_REENTRANT, ("chained", T.InvalidSignature.code)]
+    finally:
+        svc.close()

@@ -78,7 +78,7 @@ def dag_round(eng, seeds, keys, committee, payload_digests=None, parents=None):
     return headers, votes, certs
 
 
-def leg_c1(eng, reps=300):
+def leg_c1(eng, reps=1000):
     seeds, keys, com = committee_fixture(eng, 4, b"nwv-bench-c1")
     headers, votes, certs = dag_round(eng, seeds, keys, com)
     cert = certs[-1]

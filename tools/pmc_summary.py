@@ -7,6 +7,7 @@ import csv
 import glob
 import json
 import os
+import sys
 
 
 def main():
@@ -15,6 +16,7 @@ def main():
     ap.add_argument("--n", type=int, default=0)
     ap.add_argument("--out", required=True)
     ap.add_argument("--note", default="")
+    ap.add_argument("--launch-list", default="", help="comma-separated kernels of the profiled pipeline")
     a = ap.parse_args()
     sums = collections.defaultdict(lambda: collections.defaultdict(float))
     cnt = collections.defaultdict(lambda: collections.defaultdict(set))
@@ -28,7 +30,10 @@ def main():
                     did = row.get("Dispatch_Id") or row.get("Correlation_Id")
                     sums[k][c] += v
                     cnt[k][c].add(did)
-    out = {"n": a.n, "note": a.note, "kernels": {}}
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from narwhal_amd._lib import kernel_source_hash
+    out = {"n": a.n, "note": a.note, "kernels": {}, "kernel_source_hash": kernel_source_hash(),
+           "launch_list": a.launch_list.split(",") if a.launch_list else None}
     for k, cs in sums.items():
         out["kernels"][k] = {c: v / max(1, len(cnt[k][c])) for c, v in cs.items()}
     with open(a.out, "w") as fh:
