@@ -361,12 +361,19 @@ def timed_region(stages, args, dist, run):
         s_.sync()
     if dist is not None:
         dist.barrier()
+    marks = hasattr(stages[0], "mark") and args.steps < 65535
     t0 = time.perf_counter()
+    if marks:
+        stages[0].mark(0)  # device-side start of the region (the streams are idle here)
     for s in range(args.steps):
         run(stages[s % len(stages)])
+        if marks:
+            stages[s % len(stages)].mark(s + 1)  # fires when step s has completed
     for s_ in stages:
         s_.sync()
     dt = time.perf_counter() - t0
+    timed_region.completions_ms = ([stages[0].mark_elapsed(0, stages[s % len(stages)], s + 1)
+                                    for s in range(args.steps)] if marks else None)
     dt_max = dt
     if dist is not None:
         import torch
@@ -375,6 +382,23 @@ def timed_region(stages, args, dist, run):
         dt_max = float(t.item())
         dist.barrier()
     return dt, dt_max
+
+
+def steady_state(comp, args):
+    """Step-completion view of the timed region (HIP events recorded after every step on its own
+    stream): the interval between completions once the pipeline is full -- the slope of the
+    sorted completion times from the K/4-th on -- next to the first completion (the ramp).  The
+    headline `value` stays the contract's K steps over the host-timed region, ramp and drain
+    included; this field says how much of it the ramp and drain are."""
+    if not comp or len(comp) < 8:
+        return None
+    c = sorted(comp)
+    q = len(c) // 4
+    slope = (c[-1] - c[q]) / (len(c) - 1 - q)
+    return {"ms_per_step": slope, "sigs_per_s": args.n / (slope * 1e-3), "first_completion_ms": c[0],
+            "last_completion_ms": c[-1], "device_span_ms_per_step": c[-1] / len(c),
+            "note": "device-side (HIP events per step): interval between step completions from the "
+                    f"{q}-th of {len(c)} on; `value` is the host-timed K steps including ramp and drain"}
 
 
 class DryStage:
@@ -446,7 +470,7 @@ def run_headline(args, eng, rank, world, dist):
     for s_ in stages:
         s_.free()
     return {"dt": dt, "dt_max": dt_max, "single": single, "kt": kt, "stats": stats,
-            "data": (pk, sg, msgs, offs, lens)}
+            "data": (pk, sg, msgs, offs, lens), "steady": steady_state(timed_region.completions_ms, args)}
 
 
 def kernels_1k(eng, data, reps=20):
@@ -856,6 +880,7 @@ def main():
         del cdata
     result = base_line(args, 1, dt)
     result.update({
+        "steady_state": h["steady"],
         "single_stream": {"ms_per_step": float(np.median(h["single"])),
                           "sigs_per_s": args.n / (float(np.median(h["single"])) * 1e-3)},
         "latency_1k_batch_ms": lat,

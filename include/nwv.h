@@ -69,6 +69,8 @@ int nwv_init(nwv_ctx** out, int n_devices, uint32_t flags);
 int nwv_init_device(nwv_ctx** out, int device_ordinal, uint32_t flags);
 void nwv_free(nwv_ctx* ctx);
 int nwv_device_count(const nwv_ctx* ctx);
+/* HIP ordinal of the context's i-th device (-1 if out of range) */
+int nwv_device_ordinal(const nwv_ctx* ctx, int i);
 int nwv_abi_version(void);
 /* last error text for this thread (static storage, never NULL) */
 const char* nwv_last_error(void);
@@ -208,6 +210,10 @@ int nwv_staged_msm_stats(nwv_staged* st, uint64_t out[8]);
 /* batch verdicts of every mode-1 run since staging, counted on the device by the run itself
  * (graph replays included): out[0] accepted runs, out[1] rejected runs.  Waits for the stream. */
 int nwv_staged_run_tally(nwv_staged* st, uint64_t out[2]);
+/* step-completion timestamps: record HIP event `slot` (< 65536) on the batch's stream (it fires
+ * when the work queued before it on that stream is done); *ms = time from a's mark to b's */
+int nwv_staged_mark(nwv_staged* st, int slot);
+int nwv_staged_mark_elapsed(nwv_staged* a, int slot_a, nwv_staged* b, int slot_b, float* ms);
 void nwv_staged_free(nwv_staged* st);
 
 /* ------------------------------------------------------------------ synthetic data ----- */

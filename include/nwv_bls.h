@@ -1,0 +1,96 @@
+/*
+ * nwv_bls.h -- BLS12-381 (min_sig) verification on MI355X: SURVEY.md §8 row f4, the reference's
+ * default signature scheme.
+ *
+ * Reference boundary replaced: crypto/src/lib.rs:29-33 aliases PublicKey / Signature /
+ * AggregateSignature / PrivateKey / KeyPair to fastcrypto 0.1.2 bls12381::* (Cargo.lock:1534-1561),
+ * backed by blst 0.3.10 (Cargo.lock:609-617) in its min_sig flavour: 96-byte compressed G2 public
+ * keys, 48-byte compressed G1 signatures, hash to G1 by RFC 9380 under fastcrypto's DST
+ * "BLS_SIG_BLS12381G1_XMD:SHA-256_SSWU_RO_NUL_" (NWV_BLS_DST).  The trait contract mirrored is the
+ * in-tree template crypto/src/bls12377/mod.rs:264-291 (VerifyingKey) and :485-577
+ * (AggregateAuthenticator); the call sites are Header::verify types/src/primary.rs:179-182,
+ * Vote::verify :325-327, Certificate::verify :531-534, Certificate::new_unsafe :476-477 and
+ * CertificatesResponse::validate_certificates primary/src/block_synchronizer/responses.rs:95-141.
+ *
+ * Every verification runs on the GPU, one item (one fast_aggregate_verify) per lane: signature
+ * decode + G1 membership, public-key decode + G2 membership (once per distinct key of a call),
+ * aggregate public key, hash to G1, a two-pair Miller loop and a final exponentiation.  Per-item
+ * status codes are exact, so a batch never needs a fallback pass to name its bad items.
+ * Buffers are the caller's; the library never retains them.  Thread-safe.
+ */
+#ifndef NWV_BLS_H
+#define NWV_BLS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "nwv.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NWV_BLS_DST "BLS_SIG_BLS12381G1_XMD:SHA-256_SSWU_RO_NUL_"
+
+/* per-item status (the BLST_ERROR subset blst returns on these paths) */
+#define NWV_BLS_OK 0
+#define NWV_BLS_BAD_ENCODING 1   /* flags / coordinate >= p / stray bits after the infinity flag */
+#define NWV_BLS_NOT_ON_CURVE 2   /* x has no y on the curve */
+#define NWV_BLS_NOT_IN_GROUP 3   /* signature outside G1 / public key outside G2 */
+#define NWV_BLS_AGGR_MISMATCH 4  /* empty key list (or empty aggregation) */
+#define NWV_BLS_VERIFY_FAIL 5    /* the pairing equation does not hold */
+#define NWV_BLS_PK_INFINITY 6    /* identity public key (or a key sum that is the identity) */
+
+/* The batch entry point (validate_certificates, a DAG round's certificates, the bench): item i is
+ * AggregateAuthenticator::verify of the aggregate signature sigs[i] (48 bytes) over the message
+ * msg_base[msg_off[i] .. + msg_len[i]) by the keys keys[pk_idx[pk_off[i] + j]], j < pk_cnt[i]
+ * (keys: n_keys x 96 bytes, e.g. the committee; each distinct key is decoded and subgroup-checked
+ * once per call).  status[i] = NWV_BLS_* for item i.  dst = NULL selects NWV_BLS_DST.
+ * Returns NWV_OK (statuses valid) or a negative error. */
+int nwv_bls_verify_many(nwv_ctx* ctx, size_t n_keys, const uint8_t* keys, size_t n, const uint8_t* sigs,
+                        const uint32_t* pk_off, const uint32_t* pk_cnt, const uint32_t* pk_idx,
+                        const uint8_t* msg_base, const uint64_t* msg_off, const uint32_t* msg_len,
+                        const uint8_t* dst, size_t dst_len, int32_t* status);
+
+/* device time of the last nwv_bls_verify_many call on this context, per kernel (HIP events):
+ * [0] k_bls_keys, [1] k_bls_sigs, [2] k_bls_h2c, [3] k_bls_apk, [4] k_bls_pair */
+int nwv_bls_last_kernel_ms(nwv_ctx* ctx, double out_ms[5]);
+
+/* ---- fastcrypto 0.1.2 trait surface (bls12381 module) ---- */
+/* Verifier::verify(&self = pk, msg, sig): NWV_OK or NWV_ERR_SIGNATURE */
+int nwv_bls_verify(nwv_ctx* ctx, const uint8_t pk[96], const uint8_t* msg, size_t msg_len, const uint8_t sig[48]);
+/* AggregateAuthenticator::verify(&self, pks, msg); sig NULL = an aggregate holding no signature
+ * (sig: None) -> NWV_ERR_SIGNATURE */
+int nwv_bls_aggregate_verify(nwv_ctx* ctx, const uint8_t* sig48_or_null, const uint8_t* pks, size_t n_pks,
+                             const uint8_t* msg, size_t msg_len);
+/* VerifyingKey::verify_batch_empty_fail(msg, pks, sigs): NWV_ERR_EMPTY, NWV_ERR_LENGTH, then the
+ * signatures are aggregated (each must decode and lie in G1) and verified against the key sum */
+int nwv_bls_verify_batch_empty_fail(nwv_ctx* ctx, const uint8_t* msg, size_t msg_len, const uint8_t* pks,
+                                    size_t n_pks, const uint8_t* sigs, size_t n_sigs);
+/* AggregateAuthenticator::batch_verify(sigs, pks_per_sig, msgs): NWV_ERR_LENGTH on any count
+ * mismatch, else NWV_OK iff every aggregate verifies over its message and keys */
+int nwv_bls_aggregate_batch_verify(nwv_ctx* ctx, size_t n_aggs, const uint8_t* const* sigs48,
+                                   const uint8_t* const* pks, const size_t* n_pks, const uint8_t* const* msgs,
+                                   const size_t* msg_lens, size_t n_msgs);
+/* AggregateAuthenticator::aggregate(sigs): out48 = the sum; NWV_ERR_SIGNATURE if n == 0 or any
+ * signature fails to decode / lies outside G1 (*status_or_null = its NWV_BLS_* code) */
+int nwv_bls_aggregate(nwv_ctx* ctx, size_t n, const uint8_t* sigs48, uint8_t out48[48], int32_t* status_or_null);
+
+/* ---- key generation, signing and the primitives (synthetic workloads, tests) ---- */
+/* pk = sk * g2 compressed (sk: 32 bytes big-endian, < r): the BLS12381KeyPair derivation */
+int nwv_bls_keygen_many(nwv_ctx* ctx, size_t n, const uint8_t* sks, uint8_t* pks);
+/* sig = sk * H(msg), compressed */
+int nwv_bls_sign_many(nwv_ctx* ctx, size_t n, const uint8_t* sks, const uint8_t* msg_base, const uint64_t* msg_off,
+                      const uint32_t* msg_len, const uint8_t* dst, size_t dst_len, uint8_t* sigs);
+/* H(msg) = hash_to_curve G1 (RFC 9380), uncompressed affine (x || y, 96 bytes big-endian) */
+int nwv_bls_hash_to_g1_many(nwv_ctx* ctx, size_t n, const uint8_t* msg_base, const uint64_t* msg_off,
+                            const uint32_t* msg_len, const uint8_t* dst, size_t dst_len, uint8_t* out96);
+/* e(P_i, Q_i) (P: 96-byte uncompressed G1, Q: 192-byte uncompressed G2 x.c1||x.c0||y.c1||y.c0,
+ * all-zero = identity) as 12 big-endian Fp in tower order (576 bytes), = the optimal ate pairing
+ * raised to 3 (the final exponentiation's x-chain computes f^(3(p^12-1)/r)) */
+int nwv_bls_pairing_many(nwv_ctx* ctx, size_t n, const uint8_t* P96, const uint8_t* Q192, uint8_t* out576);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

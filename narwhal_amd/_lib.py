@@ -81,6 +81,8 @@ def load():
         "nwv_staged_free": ([_vp], None),
         "nwv_staged_msm_stats": ([_vp, _vp], _i32),
         "nwv_staged_run_tally": ([_vp, _vp], _i32),
+        "nwv_staged_mark": ([_vp, _i32], _i32),
+        "nwv_staged_mark_elapsed": ([_vp, _i32, _vp, _i32, ctypes.POINTER(ctypes.c_float)], _i32),
         "nwv_ed25519_sign_many": ([_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp], _i32),
     }
     for name, (args, res) in sig.items():
@@ -343,6 +345,16 @@ class Staged:
         out = np.zeros(2, dtype=np.uint64)
         _check(self.eng.lib.nwv_staged_run_tally(self._h, _ptr(out)))
         return int(out[0]), int(out[1])
+
+    def mark(self, slot):
+        """record step-completion event `slot` on this batch's stream"""
+        _check(self.eng.lib.nwv_staged_mark(self._h, slot))
+
+    def mark_elapsed(self, slot, other, other_slot):
+        """device ms from this batch's mark `slot` to `other`'s mark `other_slot`"""
+        ms = ctypes.c_float(0)
+        _check(self.eng.lib.nwv_staged_mark_elapsed(self._h, slot, other._h, other_slot, ctypes.byref(ms)))
+        return ms.value
 
     def free(self):
         if self._h:

@@ -41,6 +41,14 @@ void htrace(const char* what) {
     std::fprintf(stderr, "nwv-trace %.1f %s\n", us, what);
 }
 
+}  // namespace
+// shared with the BLS12-381 translation unit (nwv_bls.hip); not part of the public ABI
+__attribute__((visibility("hidden"))) void nwv_bls_ctx_release(nwv_ctx* ctx);
+__attribute__((visibility("hidden"))) int nwv_internal_set_err(int code, const char* msg) {
+    g_last_error = msg;
+    return code;
+}
+namespace {
 int set_err(int code, const std::string& msg) {
     g_last_error = msg;
     return code;
@@ -1071,6 +1079,7 @@ struct nwv_staged {
     PinnedBuf seeds;
     hipEvent_t seed_ev[SEED_SLOTS] = {};
     uint64_t seed_runs = 0;
+    std::vector<hipEvent_t> marks;  // nwv_staged_mark: step-completion timestamps on this stream
 };
 
 // Shard [0, n) into contiguous, 64-aligned ranges over the context's devices and run fn(dev,
@@ -1152,6 +1161,7 @@ int nwv_init_device(nwv_ctx** out, int device_ordinal, uint32_t flags) {
 
 void nwv_free(nwv_ctx* ctx) {
     if (!ctx) return;
+    nwv_bls_ctx_release(ctx);  // the BLS12-381 engine's per-context state (nwv_bls.hip)
     for (Gpu* d : ctx->devs) {
         gpu_close(*d);
         delete d;
@@ -1160,6 +1170,9 @@ void nwv_free(nwv_ctx* ctx) {
 }
 
 int nwv_device_count(const nwv_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+int nwv_device_ordinal(const nwv_ctx* ctx, int i) {
+    return (ctx && i >= 0 && i < (int)ctx->devs.size()) ? ctx->devs[i]->ordinal : -1;
+}
 
 int nwv_ed25519_verify_each(nwv_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* sig,
                             const uint8_t* msg_base, const uint64_t* msg_off,
@@ -1740,6 +1753,27 @@ int nwv_staged_msm_stats(nwv_staged* st, uint64_t out[8]) {
     return NWV_OK;
 }
 
+int nwv_staged_mark(nwv_staged* st, int slot) {
+    if (!st || slot < 0 || slot >= 65536) return set_err(NWV_ERR_ARG, "bad staged/slot");
+    std::lock_guard<std::mutex> g(st->mu);
+    int rc = with_device(st->own);
+    if (rc) return rc;
+    if ((size_t)slot >= st->marks.size()) st->marks.resize((size_t)slot + 1, nullptr);
+    if (!st->marks[slot]) NWV_HIP(hipEventCreate(&st->marks[slot]));
+    NWV_HIP(hipEventRecord(st->marks[slot], st->stream));
+    return NWV_OK;
+}
+
+int nwv_staged_mark_elapsed(nwv_staged* a, int slot_a, nwv_staged* b, int slot_b, float* ms) {
+    if (!a || !b || !ms || slot_a < 0 || slot_b < 0 || (size_t)slot_a >= a->marks.size() ||
+        (size_t)slot_b >= b->marks.size() || !a->marks[slot_a] || !b->marks[slot_b])
+        return set_err(NWV_ERR_ARG, "bad marks");
+    NWV_HIP(hipEventSynchronize(b->marks[slot_b]));
+    NWV_HIP(hipEventSynchronize(a->marks[slot_a]));
+    NWV_HIP(hipEventElapsedTime(ms, a->marks[slot_a], b->marks[slot_b]));
+    return NWV_OK;
+}
+
 void nwv_staged_free(nwv_staged* st) {
     if (!st) return;
     {
@@ -1752,6 +1786,8 @@ void nwv_staged_free(nwv_staged* st) {
         st->seeds.release();
         st->buf.release();
         for (auto& e : st->ev)
+            if (e) (void)hipEventDestroy(e);
+        for (auto& e : st->marks)
             if (e) (void)hipEventDestroy(e);
         if (st->stream) (void)hipStreamDestroy(st->stream);
         st->own.stream = nullptr;

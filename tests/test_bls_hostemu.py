@@ -1,0 +1,112 @@
+"""The gfx950 BLS12-381 code (narwhal_amd/csrc/bls381.h, bls_verify.h) compiled for the host
+(tests/hostemu/bls_hostemu.cpp) against the oracle, on the CPU: pairing values bit-exact,
+hash_to_curve on the RFC 9380 known answers, key generation on the reference's Docker fixtures,
+decode / subgroup statuses of adversarial encodings, and fast_aggregate_verify statuses."""
+import ctypes
+import json
+import os
+import random
+import subprocess
+
+import pytest
+
+import bls_cases as C
+import bls_ffi as B
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+r = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
+
+
+@pytest.fixture(scope="module")
+def emu():
+    path = os.path.join(ROOT, "tests", "_build", "libblsemu.so")
+    if not os.path.exists(path):
+        subprocess.run(["make", "-C", ROOT, "tests/_build/libblsemu.so"], check=True)
+    L = ctypes.CDLL(path)
+    c, sz, vp = ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p
+    L.bh_pairing.argtypes = [c, c, vp]
+    L.bh_hash_to_g1.argtypes = [c, sz, c, sz, vp]
+    L.bh_key_decode.argtypes = [c, vp]
+    L.bh_sig_decode.argtypes = [c, vp]
+    L.bh_keygen.argtypes = [c, vp]
+    L.bh_sign.argtypes = [c, c, sz, c, sz, vp]
+    L.bh_fast_aggregate_verify.argtypes = [c, sz, c, c, sz, c, sz]
+    return L
+
+
+@pytest.fixture(scope="module")
+def gold():
+    with open(os.path.join(ROOT, "tests", "golden", "bls12381_kats.json")) as f:
+        return json.load(f)
+
+
+def _buf(n):
+    return ctypes.create_string_buffer(n)
+
+
+def test_pairing_bit_exact(emu):
+    rnd = random.Random(21)
+    for _ in range(3):
+        P = B.g1_mul(B.g1_gen(), rnd.randrange(1, r))
+        Q = B.g2_mul(B.g2_gen(), rnd.randrange(1, r))
+        o = _buf(576)
+        emu.bh_pairing(P, Q, o)
+        assert o.raw == B.pairing(P, Q)
+
+
+def test_hash_to_g1(emu, gold):
+    for v in gold["hash_to_g1"]:
+        m, d = bytes.fromhex(v["msg"]), v["dst"].encode()
+        o = _buf(96)
+        emu.bh_hash_to_g1(m, len(m), d, len(d), o)
+        assert o.raw.hex() == v["x"] + v["y"]
+    rnd = random.Random(22)
+    for n in (0, 17, 64, 150):
+        m = rnd.randbytes(n)
+        o = _buf(96)
+        emu.bh_hash_to_g1(m, len(m), B.DST_NUL, len(B.DST_NUL), o)
+        assert o.raw == B.hash_to_g1(m)
+
+
+def test_keygen_and_sign(emu, gold):
+    for k in gold["keygen"]:
+        o = _buf(96)
+        emu.bh_keygen(bytes.fromhex(k["sk"]), o)
+        assert o.raw.hex() == k["pk"]
+    for s in gold["sign"][:4]:
+        sk, m = bytes.fromhex(gold["keygen"][s["sk_index"]]["sk"]), bytes.fromhex(s["msg"])
+        o = _buf(48)
+        emu.bh_sign(sk, m, len(m), B.DST_NUL, len(B.DST_NUL), o)
+        assert o.raw.hex() == s["sig"]
+
+
+def test_decode_statuses(emu, gold):
+    """decode + subgroup statuses equal the oracle's for valid, identity, off-curve, bad-encoding
+    and outside-the-subgroup inputs (the endomorphism tests against the oracle's [r]P = O)"""
+    pk = bytes.fromhex(gold["keygen"][0]["pk"])
+    sig = bytes.fromhex(gold["sign"][0]["sig"])
+    o2, o1 = _buf(192), _buf(96)
+    assert emu.bh_key_decode(pk, o2) == 0 and o2.raw == B.g2_decompress(pk)[1]
+    assert emu.bh_key_decode(C.IDENTITY_G2, o2) == B.ORB_PK_INFINITY
+    assert emu.bh_key_decode(C.not_in_g2(), o2) == B.ORB_NOT_IN_GROUP
+    assert emu.bh_key_decode(C.not_in_g2(50), o2) == B.ORB_NOT_IN_GROUP
+    for s in [sig, C.IDENTITY_G1, C.not_in_g1(), C.not_in_g1(100)] + C.bad_encodings_g1(sig):
+        want = B.g1_decompress(s)[0]
+        if want == 0 and s != C.IDENTITY_G1 and not B.lib().orb_g1_in_group(s):
+            want = B.ORB_NOT_IN_GROUP
+        assert emu.bh_sig_decode(s, o1) == want, s.hex()
+
+
+def test_fast_aggregate_verify_statuses(emu, gold):
+    sks = [bytes.fromhex(k["sk"]) for k in gold["keygen"]]
+    pks = [bytes.fromhex(k["pk"]) for k in gold["keygen"]]
+    m = bytes(range(32))
+    sigs = [B.sign(sk, m) for sk in sks]
+    _, agg = B.aggregate(sigs[:3])
+    dst = B.DST_NUL
+    cases = [(agg, pks[:3], m), (agg, pks[:3], m + b"x"), (agg, pks[:2], m), (agg, [], m),
+             (agg, [pks[0], C.negate_g2(pks[0])], m), (agg, pks[:2] + [C.not_in_g2()], m),
+             (C.IDENTITY_G1, pks[:3], m), (C.not_in_g1(), pks[:3], m), (sigs[0], pks[:1], m)]
+    for s, ks, msg in cases:
+        got = emu.bh_fast_aggregate_verify(s, len(ks), b"".join(ks), msg, len(msg), dst, len(dst))
+        assert got == B.fast_aggregate_verify(s, ks, msg)
