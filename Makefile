@@ -4,8 +4,10 @@
 #   make hostemu  tests/_build/libhostemu.so    (test infrastructure: device math on the host)
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
-CSRC := $(wildcard narwhal_amd/csrc/*.h narwhal_amd/csrc/*.hip narwhal_amd/csrc/*.cpp) include/nwv.h include/nwv_types.h \
-	include/nwv_service.h include/nwv_bls.h
+BLS_SRC := narwhal_amd/csrc/nwv_bls.hip narwhal_amd/csrc/bls381.h narwhal_amd/csrc/bls_verify.h \
+	narwhal_amd/csrc/bls381_consts.h narwhal_amd/csrc/bls381_iso.h include/nwv_bls.h
+CSRC := $(filter-out $(BLS_SRC),$(wildcard narwhal_amd/csrc/*.h narwhal_amd/csrc/*.hip narwhal_amd/csrc/*.cpp)) \
+	include/nwv.h include/nwv_types.h include/nwv_service.h
 
 all: lib oracle hostemu tools
 
@@ -19,8 +21,7 @@ narwhal_amd/lib/nwv_service.o: narwhal_amd/csrc/nwv_service.cpp include/nwv.h in
 	@mkdir -p narwhal_amd/lib
 	g++ -O2 -std=c++17 -fPIC -Wall -c -o $@ $<
 # the BLS12-381 engine is its own translation unit (compiled in parallel with the Ed25519 one)
-narwhal_amd/lib/nwv_bls.o: narwhal_amd/csrc/nwv_bls.hip narwhal_amd/csrc/bls381.h narwhal_amd/csrc/bls_verify.h \
-		narwhal_amd/csrc/bls381_consts.h include/nwv.h include/nwv_bls.h
+narwhal_amd/lib/nwv_bls.o: $(BLS_SRC) include/nwv.h
 	@mkdir -p narwhal_amd/lib
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -c -o $@ narwhal_amd/csrc/nwv_bls.hip
 narwhal_amd/lib/nwv_host.o: $(CSRC)
@@ -37,7 +38,7 @@ oracle:
 
 hostemu: tests/_build/libhostemu.so tests/_build/libsvcstub.so tests/_build/libblsemu.so
 # the gfx950 BLS12-381 code compiled for the host (tests/test_bls_hostemu.py)
-tests/_build/libblsemu.so: tests/hostemu/bls_hostemu.cpp narwhal_amd/csrc/bls381.h narwhal_amd/csrc/bls_verify.h narwhal_amd/csrc/bls381_consts.h
+tests/_build/libblsemu.so: tests/hostemu/bls_hostemu.cpp $(BLS_SRC)
 	@mkdir -p tests/_build
 	$(HIPCC) -std=c++17 -O2 --offload-host-only -x hip -fPIC -shared -o $@ tests/hostemu/bls_hostemu.cpp
 # the batching service's host logic over a stubbed engine (tests/test_service_host.py)

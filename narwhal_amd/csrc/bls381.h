@@ -29,7 +29,9 @@
 #define NWV_HD __host__ __device__ __forceinline__
 #endif
 #define BLS_HD __host__ __device__ inline
+#ifndef BLS_NOINLINE
 #define BLS_NOINLINE __host__ __device__ __attribute__((noinline))
+#endif
 
 namespace bls {
 
@@ -217,26 +219,56 @@ NWV_HD bool fp_sqrt(fp& r, const fp& a) {
     r = s;
     return fp_eq(fp_sqr(s), a);
 }
-// plain (non-Montgomery) canonical limbs <-> 48 big-endian bytes
-NWV_HD void plain_from_be(fp& r, const uint8_t* b) {
-    // bit k of the integer = bit (k % 8) of byte 47 - k / 8
+// plain (non-Montgomery) canonical limbs <-> 48 big-endian bytes, through twelve 32-bit words
+// (w[0] least significant); every index is a compile-time constant after unrolling, so nothing is
+// staged in private memory.  mask0 is applied to the first (most significant) byte -- the ZCash
+// flag bits of a compressed point.
+NWV_HD void plain_from_be(fp& r, const uint8_t* b, uint32_t mask0 = 0xff) {
+    uint32_t w[13];
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+        const uint8_t* q = b + 44 - 4 * k;
+        w[k] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
+    }
+    w[11] &= (mask0 << 24) | 0xffffffu;
+    w[12] = 0;
+#pragma unroll
     for (int j = 0; j < NL; j++) {
-        uint32_t v = 0;
-        for (int t = 0; t < 28; t++) {
-            const int k = 28 * j + t;
-            if (k < 384) v |= (uint32_t)((b[47 - k / 8] >> (k % 8)) & 1) << t;
-        }
-        r.l[j] = v;
+        const int bit = 28 * j, idx = bit >> 5, sh = bit & 31;
+        uint32_t v = w[idx] >> sh;
+        if (sh > 4) v |= w[idx + 1] << (32 - sh);
+        r.l[j] = v & LM;
+    }
+}
+// 32 big-endian bytes -> limbs (< 2^256)
+NWV_HD void plain_from_be256(fp& r, const uint8_t* b) {
+    uint32_t w[9];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint8_t* q = b + 28 - 4 * k;
+        w[k] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
+    }
+    w[8] = 0;
+#pragma unroll
+    for (int j = 0; j < NL; j++) {
+        const int bit = 28 * j, idx = bit >> 5, sh = bit & 31;
+        uint32_t v = idx < 9 ? w[idx] >> sh : 0;
+        if (sh > 4 && idx + 1 < 9) v |= w[idx + 1] << (32 - sh);
+        r.l[j] = v & LM;
     }
 }
 NWV_HD void plain_to_be(uint8_t* b, const fp& a) {
-    for (int i = 0; i < 48; i++) {
-        uint32_t v = 0;
-        for (int t = 0; t < 8; t++) {
-            const int k = 8 * (47 - i) + t;
-            v |= ((a.l[k / 28] >> (k % 28)) & 1) << t;
-        }
-        b[i] = (uint8_t)v;
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+        const int bit = 32 * k, j = bit / 28, sh = bit % 28;
+        uint32_t v = a.l[j] >> sh;
+        if (j + 1 < NL) v |= a.l[j + 1] << (28 - sh);
+        if (sh > 24 && j + 2 < NL) v |= a.l[j + 2] << (56 - sh);
+        uint8_t* q = b + 44 - 4 * k;
+        q[0] = (uint8_t)(v >> 24);
+        q[1] = (uint8_t)(v >> 16);
+        q[2] = (uint8_t)(v >> 8);
+        q[3] = (uint8_t)v;
     }
 }
 NWV_HD bool plain_lt_p(const fp& a) {
@@ -597,11 +629,8 @@ NWV_HD int32_t g1_decompress(fp& x, fp& y, bool& inf, const uint8_t* in) {
         inf = true;
         return o ? ST_BAD_ENCODING : ST_OK;
     }
-    uint8_t b[48];
-    for (int i = 0; i < 48; i++) b[i] = in[i];
-    b[0] &= 0x1f;
     fp px;
-    plain_from_be(px, b);
+    plain_from_be(px, in, 0x1f);
     if (!plain_lt_p(px)) return ST_BAD_ENCODING;
     x = fp_to_mont(px);
     const fp rhs = fp_add(fp_mul(fp_sqr(x), x), k_b1());
@@ -619,11 +648,8 @@ NWV_HD int32_t g2_decompress(fp2& x, fp2& y, bool& inf, const uint8_t* in) {
         inf = true;
         return o ? ST_BAD_ENCODING : ST_OK;
     }
-    uint8_t b[48];
-    for (int i = 0; i < 48; i++) b[i] = in[i];
-    b[0] &= 0x1f;
     fp p1, p0;
-    plain_from_be(p1, b);
+    plain_from_be(p1, in, 0x1f);
     plain_from_be(p0, in + 48);
     if (!plain_lt_p(p1) || !plain_lt_p(p0)) return ST_BAD_ENCODING;
     x.c0 = fp_to_mont(p0);
@@ -753,15 +779,9 @@ NWV_HD void expand_xmd_128(uint8_t* out, const uint8_t* msg, uint32_t n, const u
 }
 // 64 big-endian bytes mod p, Montgomery form: hi * 2^256 + lo
 NWV_HD fp fp_from_be64(const uint8_t* b) {
-    uint8_t hi[48], lo[48];
-    for (int i = 0; i < 16; i++) hi[i] = lo[i] = 0;
-    for (int i = 0; i < 32; i++) {
-        hi[16 + i] = b[i];
-        lo[16 + i] = b[32 + i];
-    }
     fp h, l;
-    plain_from_be(h, hi);
-    plain_from_be(l, lo);
+    plain_from_be256(h, b);
+    plain_from_be256(l, b + 32);
     return fp_add(fp_mul(fp_to_mont(h), k_two256()), fp_to_mont(l));
 }
 // simplified SWU on y^2 = x^3 + A'x + B' (RFC 9380 §6.6.2, Z = 11)

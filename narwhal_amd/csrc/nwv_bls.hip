@@ -391,7 +391,7 @@ int nwv_bls_aggregate(nwv_ctx* ctx, size_t n, const uint8_t* sigs48, uint8_t out
     std::lock_guard<std::mutex> g(d->mu);
     BLS_HIP(hipSetDevice(d->ordinal));
     const size_t w_rec = 0, w_st = 4 * G1_REC_WORDS * n, w_out = w_st + 4 * n, w_ost = w_out + 64, w_end = w_ost + 8;
-    if ((rc = d->in.ensure(48 * n)) || (rc = d->work.ensure(w_end)) || (rc = d->stage.ensure(64))) return rc;
+    if ((rc = d->in.ensure(48 * n)) || (rc = d->work.ensure(w_end)) || (rc = d->stage.ensure(128))) return rc;
     uint8_t* w = static_cast<uint8_t*>(d->work.p);
     BLS_HIP(hipMemcpyAsync(d->in.p, sigs48, 48 * n, hipMemcpyHostToDevice, d->stream));
     hipLaunchKernelGGL(k_bls_sigs, dim3(kBlocks(n)), dim3(BLS_LANES), 0, d->stream, (uint32_t)n,

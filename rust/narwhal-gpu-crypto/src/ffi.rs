@@ -40,6 +40,15 @@ pub const NWV_FLAG_NO_KEYCACHE: u32 = 8;
 pub const NWV_FLAG_MSM_SORT2: u32 = 16;
 pub const NWV_FLAG_NO_MSM_REUSE: u32 = 32;
 
+// per-item BLS12-381 statuses (include/nwv_bls.h)
+pub const NWV_BLS_OK: i32 = 0;
+pub const NWV_BLS_BAD_ENCODING: i32 = 1;
+pub const NWV_BLS_NOT_ON_CURVE: i32 = 2;
+pub const NWV_BLS_NOT_IN_GROUP: i32 = 3;
+pub const NWV_BLS_AGGR_MISMATCH: i32 = 4;
+pub const NWV_BLS_VERIFY_FAIL: i32 = 5;
+pub const NWV_BLS_PK_INFINITY: i32 = 6;
+
 pub const NWV_DAG_OK: i32 = 0;
 pub const NWV_DAG_INVALID_EPOCH: i32 = 10;
 pub const NWV_DAG_INVALID_HEADER_ID: i32 = 11;
@@ -110,6 +119,7 @@ extern "C" {
     pub fn nwv_init_device(out: *mut *mut NwvCtx, device_ordinal: c_int, flags: u32) -> c_int;
     pub fn nwv_free(ctx: *mut NwvCtx);
     pub fn nwv_device_count(ctx: *const NwvCtx) -> c_int;
+    pub fn nwv_device_ordinal(ctx: *const NwvCtx, i: c_int) -> c_int;
     pub fn nwv_abi_version() -> c_int;
     pub fn nwv_last_error() -> *const c_char;
     // ---- Ed25519 verification (include/nwv.h)
@@ -208,6 +218,94 @@ extern "C" {
         n_msgs: usize,
         seed32: *const u8,
     ) -> c_int;
+    // ---- BLS12-381 min_sig, the reference's default scheme (include/nwv_bls.h)
+    pub fn nwv_bls_verify_many(
+        ctx: *mut NwvCtx,
+        n_keys: usize,
+        keys: *const u8,
+        n: usize,
+        sigs: *const u8,
+        pk_off: *const u32,
+        pk_cnt: *const u32,
+        pk_idx: *const u32,
+        msg_base: *const u8,
+        msg_off: *const u64,
+        msg_len: *const u32,
+        dst: *const u8,
+        dst_len: usize,
+        status: *mut i32,
+    ) -> c_int;
+    pub fn nwv_bls_last_kernel_ms(ctx: *mut NwvCtx, out_ms: *mut f64) -> c_int;
+    pub fn nwv_bls_verify(
+        ctx: *mut NwvCtx,
+        pk: *const u8,
+        msg: *const u8,
+        msg_len: usize,
+        sig: *const u8,
+    ) -> c_int;
+    pub fn nwv_bls_aggregate_verify(
+        ctx: *mut NwvCtx,
+        sig48_or_null: *const u8,
+        pks: *const u8,
+        n_pks: usize,
+        msg: *const u8,
+        msg_len: usize,
+    ) -> c_int;
+    pub fn nwv_bls_verify_batch_empty_fail(
+        ctx: *mut NwvCtx,
+        msg: *const u8,
+        msg_len: usize,
+        pks: *const u8,
+        n_pks: usize,
+        sigs: *const u8,
+        n_sigs: usize,
+    ) -> c_int;
+    pub fn nwv_bls_aggregate_batch_verify(
+        ctx: *mut NwvCtx,
+        n_aggs: usize,
+        sigs48: *const *const u8,
+        pks: *const *const u8,
+        n_pks: *const usize,
+        msgs: *const *const u8,
+        msg_lens: *const usize,
+        n_msgs: usize,
+    ) -> c_int;
+    pub fn nwv_bls_aggregate(
+        ctx: *mut NwvCtx,
+        n: usize,
+        sigs48: *const u8,
+        out48: *mut u8,
+        status_or_null: *mut i32,
+    ) -> c_int;
+    pub fn nwv_bls_keygen_many(ctx: *mut NwvCtx, n: usize, sks: *const u8, pks: *mut u8) -> c_int;
+    pub fn nwv_bls_sign_many(
+        ctx: *mut NwvCtx,
+        n: usize,
+        sks: *const u8,
+        msg_base: *const u8,
+        msg_off: *const u64,
+        msg_len: *const u32,
+        dst: *const u8,
+        dst_len: usize,
+        sigs: *mut u8,
+    ) -> c_int;
+    pub fn nwv_bls_hash_to_g1_many(
+        ctx: *mut NwvCtx,
+        n: usize,
+        msg_base: *const u8,
+        msg_off: *const u64,
+        msg_len: *const u32,
+        dst: *const u8,
+        dst_len: usize,
+        out96: *mut u8,
+    ) -> c_int;
+    pub fn nwv_bls_pairing_many(
+        ctx: *mut NwvCtx,
+        n: usize,
+        P96: *const u8,
+        Q192: *const u8,
+        out576: *mut u8,
+    ) -> c_int;
     // ---- BLAKE2b-256: Batch::digest, serialized_batch_digest (include/nwv.h)
     pub fn nwv_blake2b256_many(
         ctx: *mut NwvCtx,
@@ -265,6 +363,14 @@ extern "C" {
     ) -> c_int;
     pub fn nwv_staged_msm_stats(st: *mut NwvStaged, out: *mut u64) -> c_int;
     pub fn nwv_staged_run_tally(st: *mut NwvStaged, out: *mut u64) -> c_int;
+    pub fn nwv_staged_mark(st: *mut NwvStaged, slot: c_int) -> c_int;
+    pub fn nwv_staged_mark_elapsed(
+        a: *mut NwvStaged,
+        slot_a: c_int,
+        b: *mut NwvStaged,
+        slot_b: c_int,
+        ms: *mut f32,
+    ) -> c_int;
     pub fn nwv_staged_free(st: *mut NwvStaged);
     // ---- synthetic signing, for workloads and tests (include/nwv.h)
     pub fn nwv_ed25519_sign_many(

@@ -16,7 +16,7 @@ STRUCTS = {"nwv_ctx": "NwvCtx", "nwv_staged": "NwvStaged", "nwv_service": "NwvSe
            "nwv_committee": "NwvCommittee", "nwv_header": "NwvHeader", "nwv_vote": "NwvVote",
            "nwv_certificate": "NwvCertificate"}
 SCALARS = {"size_t": "usize", "int": "c_int", "uint32_t": "u32", "uint64_t": "u64", "int64_t": "i64",
-           "int32_t": "i32", "uint8_t": "u8", "char": "c_char", "double": "f64", "void": "c_void",
+           "int32_t": "i32", "uint8_t": "u8", "char": "c_char", "double": "f64", "float": "f32", "void": "c_void",
            "nwv_done_fn": "NwvDoneFn"}
 
 
