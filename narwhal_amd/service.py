@@ -136,3 +136,87 @@ class Service:
         keys = ("calls", "items", "max_batch", "by_count", "by_deadline", "by_flush")
         return {k: int(v) for k, v in zip(keys, out)}
 
+
+
+class CoreDrain:
+    """Single-consumer coalescer for a Core-shaped loop (Core::run, primary/src/core.rs:614-714):
+    the drain pattern of rust/narwhal-gpu-crypto/src/core_drain.rs.  On a message, take whatever
+    else is already queued (up to max_items, waiting at most max_wait_us for more), verify the lot
+    with ONE nwv_verify_mixed_many call (one digest launch, one batch MSM) and hand back each
+    message's DagError code (0 = Ok) in arrival order -- what Header::verify / Vote::verify /
+    Certificate::verify (types/src/primary.rs:150-183, :307-328, :487-537) return for it.  The
+    loop then runs sanitize_*'s state checks and process_* per message as before: verification
+    depends only on the committee, never on Core's state, so verifying ahead changes no outcome.
+
+    A message is (kind, item): kind 'header' | 'vote' | 'certificate', item a types.Header / Vote
+    / Certificate or its prepared C struct (types._Header / _Vote / _Certificate)."""
+
+    KINDS = ("header", "vote", "certificate")
+    _CLS = {"header": T._Header, "vote": T._Vote, "certificate": T._Certificate}
+
+    def __init__(self, engine, committee, max_items=512, max_wait_us=1000):
+        if max_items < 1:
+            raise ValueError("max_items must be >= 1")
+        self.engine = engine
+        self.max_items = max_items
+        self.max_wait_us = max_wait_us
+        self.set_committee(committee)
+        self.calls = self.items = self.largest = 0
+
+    def set_committee(self, committee):
+        """epoch change (Core::change_epoch, primary/src/core.rs:592-611)"""
+        self._ckeep = T._Keep()
+        self._cc = committee._c(self._ckeep)
+
+    def drain(self, q, first=None):
+        """`first` (or a blocking q.get()) plus whatever q holds or receives before the deadline,
+        at most max_items messages (q: a queue.Queue standing in for Core's channels)"""
+        import queue
+        import time
+        out = [q.get() if first is None else first]
+        deadline = time.perf_counter() + self.max_wait_us * 1e-6
+        while len(out) < self.max_items:
+            try:
+                out.append(q.get_nowait())
+                continue
+            except queue.Empty:
+                pass
+            left = deadline - time.perf_counter()
+            if left <= 0:
+                break
+            try:
+                out.append(q.get(timeout=left))
+            except queue.Empty:
+                break
+        return out
+
+    def verify(self, msgs):
+        """one engine call for every message -> DagError codes in input order"""
+        keep = T._Keep()
+        structs = {k: [] for k in self.KINDS}
+        where = {k: [] for k in self.KINDS}
+        for i, (kind, item) in enumerate(msgs):
+            structs[kind].append(item if isinstance(item, ctypes.Structure) else item._c(keep))
+            where[kind].append(i)
+        args, outs = [], []
+        for k in self.KINDS:
+            n = len(structs[k])
+            arr = (self._CLS[k] * max(n, 1))(*structs[k])
+            res = (ctypes.c_int32 * max(n, 1))()
+            keep.objs += [arr, res]
+            args += [n, ctypes.cast(arr, ctypes.c_void_p), ctypes.cast(res, ctypes.c_void_p)]
+            outs.append(res)
+        _lib._check(T.lib().nwv_verify_mixed_many(self.engine._h, ctypes.byref(self._cc), *args))
+        codes = [0] * len(msgs)
+        for k, res in zip(self.KINDS, outs):
+            for j, i in enumerate(where[k]):
+                codes[i] = res[j]
+        self.calls += 1
+        self.items += len(msgs)
+        self.largest = max(self.largest, len(msgs))
+        return codes
+
+    def next_batch(self, q, first=None):
+        """drain + verify: [(message, code)] in arrival order"""
+        msgs = self.drain(q, first)
+        return list(zip(msgs, self.verify(msgs)))
