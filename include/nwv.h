@@ -60,6 +60,11 @@ typedef struct nwv_ctx nwv_ctx;
  * decompressed records (k_ed_points_msm) and k_i / the s < l flag its hash role stored (no
  * k_ed_hash); this flag makes the pass hash and decompress again */
 #define NWV_FLAG_NO_MSM_REUSE 32u
+/* BLS12-381 (nwv_bls.h): verify every item with its own two-pair Miller loop and final
+ * exponentiation instead of the batch check (a random linear combination over the call's items:
+ * one Miller loop per item, one final exponentiation per call, the per-item form only when the
+ * batch check rejects) -- for tests and A/B measurements; statuses are the same either way */
+#define NWV_FLAG_BLS_PER_ITEM 64u
 
 /* ------------------------------------------------------------------ lifecycle ----- */
 /* Process-wide context creation (created once, in Primary::spawn).

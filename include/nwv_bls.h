@@ -14,8 +14,10 @@
  *
  * Every verification runs on the GPU, one item (one fast_aggregate_verify) per lane: signature
  * decode + G1 membership, public-key decode + G2 membership (once per distinct key of a call),
- * aggregate public key, hash to G1, a two-pair Miller loop and a final exponentiation.  Per-item
- * status codes are exact, so a batch never needs a fallback pass to name its bad items.
+ * aggregate public key, hash to G1; then the pairing equations of all the call's items as one
+ * random-linear-combination check (one Miller loop per item, one final exponentiation per call),
+ * and only if that rejects, each item's own two-pair Miller loop and final exponentiation.
+ * Per-item status codes are exact either way.
  * Buffers are the caller's; the library never retains them.  Thread-safe.
  */
 #ifndef NWV_BLS_H
@@ -52,9 +54,13 @@ int nwv_bls_verify_many(nwv_ctx* ctx, size_t n_keys, const uint8_t* keys, size_t
                         const uint8_t* msg_base, const uint64_t* msg_off, const uint32_t* msg_len,
                         const uint8_t* dst, size_t dst_len, int32_t* status);
 
-/* device time of the last nwv_bls_verify_many call on this context, per kernel (HIP events):
- * [0] k_bls_keys, [1] k_bls_sigs, [2] k_bls_h2c, [3] k_bls_apk, [4] k_bls_pair */
+/* device time of the last nwv_bls_verify_many call on this context, per stage (HIP events):
+ * [0] k_bls_keys, [1] k_bls_sigs, [2] k_bls_h2c, [3] k_bls_apk, [4] the pairing check (the batch
+ * check k_bls_rlc + k_bls_fold + k_bls_final, plus k_bls_pair when it ran) */
 int nwv_bls_last_kernel_ms(nwv_ctx* ctx, double out_ms[5]);
+/* how the last nwv_bls_verify_many call checked its pairings: 0 per item (NWV_FLAG_BLS_PER_ITEM),
+ * 1 one batch check that accepted every item, 2 a batch check that rejected, then per item */
+int nwv_bls_last_path(nwv_ctx* ctx);
 
 /* ---- fastcrypto 0.1.2 trait surface (bls12381 module) ---- */
 /* Verifier::verify(&self = pk, msg, sig): NWV_OK or NWV_ERR_SIGNATURE */

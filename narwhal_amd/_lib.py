@@ -29,6 +29,7 @@ NWV_FLAG_MSM_SPLIT_PREP = 4
 NWV_FLAG_NO_KEYCACHE = 8
 NWV_FLAG_MSM_SORT2 = 16
 NWV_FLAG_NO_MSM_REUSE = 32
+NWV_FLAG_BLS_PER_ITEM = 64
 NWV_RUN_TIMED = 0x100
 
 
@@ -94,13 +95,18 @@ def load():
 
 
 def kernel_source_hash():
-    """sha256 (16 hex digits) over the device-code sources (narwhal_amd/csrc/*.hip, *.h): committed
-    rocprofv3 --pmc summaries carry it, and bench.py uses a summary only while it matches, so
-    counters of kernels that have since changed are never priced against today's timings"""
+    """sha256 (16 hex digits) over the Ed25519 / BLAKE2b device-code sources (narwhal_amd/csrc/*.hip,
+    *.h; the BLS12-381 translation unit nwv_bls.hip and its bls*.h headers are not part of those
+    kernels and are left out): committed rocprofv3 --pmc summaries carry it, and bench.py uses a
+    summary only while it matches, so counters of kernels that have since changed are never
+    priced against today's timings"""
     import glob
     import hashlib
     h = hashlib.sha256()
     for f in sorted(glob.glob(os.path.join(_HERE, "csrc", "*.hip")) + glob.glob(os.path.join(_HERE, "csrc", "*.h"))):
+        b = os.path.basename(f)
+        if b.startswith("bls") or b == "nwv_bls.hip":
+            continue
         h.update(os.path.basename(f).encode() + b"\0")
         with open(f, "rb") as fh:
             h.update(fh.read())

@@ -26,8 +26,10 @@ _SIGS = {
     "nwv_bls_hash_to_g1_many": ([_vp, _sz, _vp, _vp, _vp, _vp, _sz, _vp], _i32),
     "nwv_bls_pairing_many": ([_vp, _sz, _vp, _vp, _vp], _i32),
     "nwv_bls_last_kernel_ms": ([_vp, _vp], _i32),
+    "nwv_bls_last_path": ([_vp], _i32),
 }
-KERNELS = ("k_bls_keys", "k_bls_sigs", "k_bls_h2c", "k_bls_apk", "k_bls_pair")
+KERNELS = ("k_bls_keys", "k_bls_sigs", "k_bls_h2c", "k_bls_apk", "pairing_check")
+PATHS = ("per_item", "batch_accepted", "batch_rejected_then_per_item")
 _bound = set()
 
 
@@ -98,6 +100,10 @@ class Bls:
         out = np.zeros(5, dtype=np.float64)
         _lib._check(self.lib.nwv_bls_last_kernel_ms(self._h, out.ctypes.data))
         return dict(zip(KERNELS, (float(x) for x in out)))
+
+    def last_path(self):
+        """how the last verify_many checked its pairings (PATHS)"""
+        return PATHS[_lib._check(self.lib.nwv_bls_last_path(self._h), allow=(0, 1, 2))]
 
     # fastcrypto trait surface: return codes NWV_OK / NWV_ERR_*
     def verify(self, pk, msg, sig):

@@ -112,4 +112,105 @@ NWV_HD bool pairing_check(const uint32_t* sig_rec, const uint32_t* h_rec, const 
     return f12_is_one(final_exp(miller_loop2(n, px, py, qx, qy)));
 }
 
+// ---- the batch check: a random linear combination over a call's items -----------------------
+// Every item i that decoded and passed the group checks carries a 64-bit coefficient r_i (odd, so
+// nonzero: blst's own multi-verification draws 64-bit coefficients too); the call accepts iff
+//   prod_i e([r_i] H_i, apk_i) * e(-sum_i [r_i] sig_i, g2) == 1,
+// computed as one Miller loop per item, a product tree, one more Miller loop and ONE final
+// exponentiation.  H_i, sig_i lie in G1 and apk_i in G2 (prime order r), so an invalid item makes
+// the product differ from 1 except with probability ~2^-63 over the coefficients; when it is not
+// 1 the engine runs the per-item check (pairing_check) to name the failing items exactly.
+constexpr int F12_REC_WORDS = 12 * NL;     // Fp12, tower order c0.c0.c0 .. c1.c2.c1
+constexpr int G1J_REC_WORDS = 3 * NL + 1;  // Jacobian X, Y, Z, flags (bit 0 = identity)
+
+NWV_HD void st_f12(uint32_t* o, const fp12& e) {
+    const fp* c[12] = {&e.c0.c0.c0, &e.c0.c0.c1, &e.c0.c1.c0, &e.c0.c1.c1, &e.c0.c2.c0, &e.c0.c2.c1,
+                       &e.c1.c0.c0, &e.c1.c0.c1, &e.c1.c1.c0, &e.c1.c1.c1, &e.c1.c2.c0, &e.c1.c2.c1};
+    for (int k = 0; k < 12; k++) st_fp(o + NL * k, *c[k]);
+}
+NWV_HD fp12 ld_f12(const uint32_t* o) {
+    fp12 e;
+    fp* c[12] = {&e.c0.c0.c0, &e.c0.c0.c1, &e.c0.c1.c0, &e.c0.c1.c1, &e.c0.c2.c0, &e.c0.c2.c1,
+                 &e.c1.c0.c0, &e.c1.c0.c1, &e.c1.c1.c0, &e.c1.c1.c1, &e.c1.c2.c0, &e.c1.c2.c1};
+    for (int k = 0; k < 12; k++) *c[k] = ld_fp(o + NL * k);
+    return e;
+}
+NWV_HD void st_g1j(uint32_t* o, const jac<fp>& p) {
+    st_fp(o, p.x);
+    st_fp(o + NL, p.y);
+    st_fp(o + 2 * NL, p.z);
+    o[3 * NL] = p.inf ? 1u : 0u;
+}
+NWV_HD jac<fp> ld_g1j(const uint32_t* o) {
+    jac<fp> p;
+    p.x = ld_fp(o);
+    p.y = ld_fp(o + NL);
+    p.z = ld_fp(o + 2 * NL);
+    p.inf = o[3 * NL] != 0;
+    return p;
+}
+
+// r_i = the first 8 bytes of SHA-256(seed || i_be32), forced odd
+NWV_HD uint64_t rlc_scalar(const uint8_t* seed32, uint32_t i) {
+    uint32_t h[8], blk[16];
+    sha256_iv(h);
+    for (int k = 0; k < 8; k++)
+        blk[k] = ((uint32_t)seed32[4 * k] << 24) | ((uint32_t)seed32[4 * k + 1] << 16) |
+                 ((uint32_t)seed32[4 * k + 2] << 8) | (uint32_t)seed32[4 * k + 3];
+    blk[8] = i;
+    blk[9] = 0x80000000u;  // padding after the 36 message bytes
+    for (int k = 10; k < 15; k++) blk[k] = 0;
+    blk[15] = 36 * 8;
+    sha256_block(h, blk);
+    return (((uint64_t)h[0] << 32) | h[1]) | 1u;
+}
+
+// item i's share: f_i = the (conjugated) Miller loop of ([r] H, apk), s_i = [r] sig (Jacobian)
+NWV_HD void rlc_item(const uint32_t* sig_rec, const uint32_t* h_rec, const uint32_t* apk_rec, uint64_t r,
+                     uint32_t* f_out, uint32_t* s_out) {
+    jac<fp> s;
+    s.inf = true;
+    s.x = s.y = s.z = fp_zero();
+    if (!sig_rec[2 * NL]) s = jac_mul64(jac_from_affine(ld_fp(sig_rec), ld_fp(sig_rec + NL)), r);
+    st_g1j(s_out, s);
+    fp12 f = f12_one();
+    if (!h_rec[2 * NL]) {
+        const jac<fp> hr = jac_mul64(jac_from_affine(ld_fp(h_rec), ld_fp(h_rec + NL)), r);
+        if (!hr.inf) {
+            fp px, py;
+            g1_to_affine(px, py, hr);
+            fp2 qx, qy;
+            ld_g2(apk_rec, qx, qy);
+            f = miller_loop2(1, &px, &py, &qx, &qy);
+        }
+    }
+    st_f12(f_out, f);
+}
+// an item outside the batch (failed an earlier check): the neutral share
+NWV_HD void rlc_neutral(uint32_t* f_out, uint32_t* s_out) {
+    st_f12(f_out, f12_one());
+    jac<fp> s;
+    s.inf = true;
+    s.x = s.y = s.z = fp_zero();
+    st_g1j(s_out, s);
+}
+// (f_a, s_a) <- (f_a f_b, s_a + s_b)
+NWV_HD void rlc_fold(uint32_t* fa, uint32_t* sa, const uint32_t* fb, const uint32_t* sb) {
+    st_f12(fa, f12_mul(ld_f12(fa), ld_f12(fb)));
+    st_g1j(sa, jac_add(ld_g1j(sa), ld_g1j(sb)));
+}
+// the batch verdict: FE(f * ML(-S, g2)) == 1
+NWV_HD bool rlc_final(const uint32_t* f_rec, const uint32_t* s_rec) {
+    fp12 f = ld_f12(f_rec);
+    const jac<fp> S = ld_g1j(s_rec);
+    if (!S.inf) {
+        fp px, py;
+        g1_to_affine(px, py, S);
+        py = fp_neg(py);
+        const fp2 qx = k_g2x(), qy = k_g2y();
+        f = f12_mul(f, miller_loop2(1, &px, &py, &qx, &qy));
+    }
+    return f12_is_one(final_exp(f));
+}
+
 }  // namespace bls

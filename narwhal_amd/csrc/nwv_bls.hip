@@ -6,9 +6,14 @@
 //   k_bls_sigs   one lane per item: decode + G1 membership (phi(P) = [-x^2] P)
 //   k_bls_h2c    one lane per item: H(msg) (RFC 9380 hash_to_curve G1)
 //   k_bls_apk    one lane per item: the sum of the item's validated keys, affine
-//   k_bls_pair   one lane per item: e(-sig, g2) e(H, apk) == 1 (two-pair Miller loop + final exp)
-// and copies the per-item statuses back.  The pairing kernel is the hot one: ~29k Fp products per
-// item on VALU v_mad_u64_u32 (bls381.h), no MFMA (no dense contraction).
+//   the pairing check, by default as ONE batch check over the call (bls_verify.h):
+//     k_bls_rlc    one lane per item: [r_i] H_i, [r_i] sig_i, the Miller loop of ([r_i] H_i, apk_i)
+//     k_bls_fold   ceil(log2 n) levels of a product tree (Fp12 products, G1 sums)
+//     k_bls_final  one lane: times the Miller loop of (-sum r_i sig_i, g2), final exponentiation
+//   and only when that rejects (or under NWV_FLAG_BLS_PER_ITEM)
+//     k_bls_pair   one lane per item: e(-sig, g2) e(H, apk) == 1 (two-pair Miller loop + final exp)
+// and copies the per-item statuses back.  The Miller loops are the hot part: Fp products on VALU
+// v_mad_u64_u32 (bls381.h), no MFMA (no dense contraction).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -25,6 +30,10 @@
 using namespace bls;
 
 __attribute__((visibility("hidden"))) int nwv_internal_set_err(int code, const char* msg);
+extern "C" {  // defined in nwv_host.hip's extern "C" section
+__attribute__((visibility("hidden"))) uint32_t nwv_internal_ctx_flags(const nwv_ctx* ctx);
+__attribute__((visibility("hidden"))) void nwv_internal_fill_seed(const uint8_t* seed32, uint8_t out[32]);
+}
 
 // ------------------------------------------------------------------------------ kernels
 #define BLS_LANES 64
@@ -61,6 +70,32 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_pair(uint32_t n, const uint32
                           apk_rec + (size_t)G2_REC_WORDS * i)
                 ? ST_OK
                 : ST_VERIFY_FAIL;
+}
+// the batch check (bls_verify.h): every item's share, then a product tree, then one lane's final
+__global__ __launch_bounds__(BLS_LANES) void k_bls_rlc(uint32_t n, const uint32_t* sig_rec, const uint32_t* h_rec,
+                                                       const uint32_t* apk_rec, const int32_t* st,
+                                                       const uint8_t* seed, uint32_t* frec, uint32_t* srec) {
+    BLS_IDX();
+    uint32_t* f = frec + (size_t)F12_REC_WORDS * i;
+    uint32_t* s = srec + (size_t)G1J_REC_WORDS * i;
+    if (st[i] != ST_OK) {
+        rlc_neutral(f, s);
+        return;
+    }
+    rlc_item(sig_rec + (size_t)G1_REC_WORDS * i, h_rec + (size_t)G1_REC_WORDS * i, apk_rec + (size_t)G2_REC_WORDS * i,
+             rlc_scalar(seed, i), f, s);
+}
+// one level of the tree over m shares: share j <- share j (+) share j + h, h = ceil(m / 2), j < m - h
+__global__ __launch_bounds__(BLS_LANES) void k_bls_fold(uint32_t m, uint32_t* frec, uint32_t* srec) {
+    const uint32_t h = (m + 1) / 2;
+    const uint32_t n = m - h;
+    BLS_IDX();
+    rlc_fold(frec + (size_t)F12_REC_WORDS * i, srec + (size_t)G1J_REC_WORDS * i,
+             frec + (size_t)F12_REC_WORDS * (i + h), srec + (size_t)G1J_REC_WORDS * (i + h));
+}
+__global__ void k_bls_final(const uint32_t* frec, const uint32_t* srec, int32_t* ok) {
+    if (blockIdx.x || threadIdx.x) return;
+    *ok = rlc_final(frec, srec) ? 1 : 0;
 }
 // sum of n decoded signatures (AggregateAuthenticator::aggregate), one lane
 __global__ void k_bls_g1_sum(uint32_t n, const uint32_t* rec, const int32_t* st, uint8_t* out48, int32_t* out_st) {
@@ -188,12 +223,14 @@ struct HBuf {
 // one device of a context: a stream and reusable staging / scratch buffers (one call at a time)
 struct BlsDev {
     int ordinal = -1;
+    uint32_t flags = 0;  // the context's nwv_init flags
     hipStream_t stream = nullptr;
     std::mutex mu;
     HBuf stage;
     DBuf in, work;
-    hipEvent_t ev[6] = {};       // around the five kernels of the last verify_many call
+    hipEvent_t ev[6] = {};       // around the five stages of the last verify_many call
     double last_ms[5] = {0, 0, 0, 0, 0};
+    int last_path = 0;           // nwv_bls_last_path
     ~BlsDev() {
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
@@ -215,6 +252,7 @@ int dev_of(nwv_ctx* ctx, BlsDev** out) {
     if (ord < 0) return nwv_internal_set_err(NWV_ERR_NODEV, "context has no device");
     auto* d = new BlsDev;
     d->ordinal = ord;
+    d->flags = nwv_internal_ctx_flags(ctx);
     if (hipSetDevice(ord) != hipSuccess || hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) {
         delete d;
         return nwv_internal_set_err(NWV_ERR_HIP, "bls stream");
@@ -248,20 +286,28 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     std::lock_guard<std::mutex> g(d.mu);
     BLS_HIP(hipSetDevice(d.ordinal));
     static const uint8_t zero[8] = {0};
+    const bool batch = !(d.flags & NWV_FLAG_BLS_PER_ITEM);
+    uint8_t seed[32];
+    nwv_internal_fill_seed(nullptr, seed);  // the batch coefficients' key: OS entropy per call
     Arena a;
     const size_t o_keys = a.add(keys, 96 * n_keys), o_sigs = a.add(sigs, 48 * n), o_off = a.add(pk_off, 4 * n),
                  o_cnt = a.add(pk_cnt, 4 * n), o_idx = a.add(n_idx ? (const void*)pk_idx : zero, 4 * n_idx + 4),
                  o_msg = a.add(msg_bytes ? (const void*)msg_base : zero, msg_bytes + 1),
-                 o_moff = a.add(msg_off, 8 * n), o_mlen = a.add(msg_len, 4 * n), o_dst = a.add(dst, dl);
+                 o_moff = a.add(msg_off, 8 * n), o_mlen = a.add(msg_len, 4 * n), o_dst = a.add(dst, dl),
+                 o_seed = a.add(seed, 32);
     int rc;
-    if ((rc = d.stage.ensure(a.total)) || (rc = d.in.ensure(a.total))) return rc;
+    if ((rc = d.stage.ensure(((a.total + 255) & ~(size_t)255) + 64)) || (rc = d.in.ensure(a.total))) return rc;
     uint8_t* h = static_cast<uint8_t*>(d.stage.p);
     for (size_t k = 0; k < a.parts.size(); k++)
         if (a.parts[k].second) std::memcpy(h + a.offs[k], a.parts[k].first, a.parts[k].second);
-    // scratch: key records + statuses, item sig / H / apk records, item statuses
-    const size_t w_krec = 0, w_kst = w_krec + 4 * G2_REC_WORDS * n_keys, w_srec = (w_kst + 4 * n_keys + 255) & ~255ull,
+    // scratch: key records + statuses, item sig / H / apk records, item statuses, the batch
+    // check's shares (Fp12 + Jacobian G1 per item) and its verdict word
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t w_krec = 0, w_kst = w_krec + 4 * G2_REC_WORDS * n_keys, w_srec = al(w_kst + 4 * n_keys),
                  w_hrec = w_srec + 4 * G1_REC_WORDS * n, w_arec = w_hrec + 4 * G1_REC_WORDS * n,
-                 w_st = w_arec + 4 * G2_REC_WORDS * n, w_end = w_st + 4 * n + 4;
+                 w_st = w_arec + 4 * G2_REC_WORDS * n, w_ok = al(w_st + 4 * n), w_frec = al(w_ok + 4),
+                 w_jrec = al(w_frec + 4 * F12_REC_WORDS * (batch ? n : 0)),
+                 w_end = w_jrec + 4 * G1J_REC_WORDS * (batch ? n : 0) + 4;
     if ((rc = d.work.ensure(w_end))) return rc;
     uint8_t* in = static_cast<uint8_t*>(d.in.p);
     uint8_t* w = static_cast<uint8_t*>(d.work.p);
@@ -272,6 +318,9 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     auto* hrec = reinterpret_cast<uint32_t*>(w + w_hrec);
     auto* arec = reinterpret_cast<uint32_t*>(w + w_arec);
     auto* st = reinterpret_cast<int32_t*>(w + w_st);
+    auto* okw = reinterpret_cast<int32_t*>(w + w_ok);
+    auto* frec = reinterpret_cast<uint32_t*>(w + w_frec);
+    auto* jrec = reinterpret_cast<uint32_t*>(w + w_jrec);
     if (!d.ev[0])
         for (auto& e : d.ev) BLS_HIP(hipEventCreate(&e));
     BLS_HIP(hipEventRecord(d.ev[0], d.stream));
@@ -290,8 +339,28 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
                        reinterpret_cast<const uint32_t*>(in + o_cnt), reinterpret_cast<const uint32_t*>(in + o_idx),
                        arec, st);
     BLS_HIP(hipEventRecord(d.ev[4], d.stream));
-    hipLaunchKernelGGL(k_bls_pair, dim3(kBlocks(n)), dim3(BLS_LANES), 0, d.stream, (uint32_t)n, (const uint32_t*)srec,
-                       (const uint32_t*)hrec, (const uint32_t*)arec, st);
+    auto per_item = [&]() {
+        hipLaunchKernelGGL(k_bls_pair, dim3(kBlocks(n)), dim3(BLS_LANES), 0, d.stream, (uint32_t)n,
+                           (const uint32_t*)srec, (const uint32_t*)hrec, (const uint32_t*)arec, st);
+    };
+    int32_t* hst = reinterpret_cast<int32_t*>(h + al(a.total));  // pinned: the batch verdict word
+    if (batch) {
+        hipLaunchKernelGGL(k_bls_rlc, dim3(kBlocks(n)), dim3(BLS_LANES), 0, d.stream, (uint32_t)n,
+                           (const uint32_t*)srec, (const uint32_t*)hrec, (const uint32_t*)arec, (const int32_t*)st,
+                           (const uint8_t*)(in + o_seed), frec, jrec);
+        for (uint32_t m = (uint32_t)n; m > 1; m = (m + 1) / 2)
+            hipLaunchKernelGGL(k_bls_fold, dim3(kBlocks(m / 2)), dim3(BLS_LANES), 0, d.stream, m, frec, jrec);
+        hipLaunchKernelGGL(k_bls_final, dim3(1), dim3(BLS_LANES), 0, d.stream, (const uint32_t*)frec,
+                           (const uint32_t*)jrec, okw);
+        BLS_HIP(hipMemcpyAsync(hst, okw, 4, hipMemcpyDeviceToHost, d.stream));
+        BLS_HIP(hipStreamSynchronize(d.stream));
+        BLS_HIP(hipGetLastError());
+        d.last_path = *hst == 1 ? 1 : 2;
+        if (*hst != 1) per_item();  // the batch check rejected: name the failing items exactly
+    } else {
+        per_item();
+        d.last_path = 0;
+    }
     BLS_HIP(hipEventRecord(d.ev[5], d.stream));
     BLS_HIP(hipGetLastError());
     BLS_HIP(hipMemcpyAsync(status, st, 4 * n, hipMemcpyDeviceToHost, d.stream));
@@ -358,6 +427,14 @@ int nwv_bls_last_kernel_ms(nwv_ctx* ctx, double out_ms[5]) {
     std::lock_guard<std::mutex> g(d->mu);
     for (int k = 0; k < 5; k++) out_ms[k] = d->last_ms[k];
     return NWV_OK;
+}
+
+int nwv_bls_last_path(nwv_ctx* ctx) {
+    BlsDev* d;
+    int rc = dev_of(ctx, &d);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(d->mu);
+    return d->last_path;
 }
 
 int nwv_bls_aggregate_verify(nwv_ctx* ctx, const uint8_t* sig48, const uint8_t* pks, size_t n_pks, const uint8_t* msg,

@@ -1239,6 +1239,13 @@ static void fill_seed(const uint8_t* seed32, uint8_t out[32]) {
     ctr++;
     std::memcpy(out, blk, 32);
 }
+// shared with nwv_bls.hip (hidden): the context's nwv_init flags, and a batch-coefficient seed
+__attribute__((visibility("hidden"))) uint32_t nwv_internal_ctx_flags(const nwv_ctx* ctx) {
+    return (ctx && !ctx->devs.empty()) ? ctx->devs[0]->flags : 0u;
+}
+__attribute__((visibility("hidden"))) void nwv_internal_fill_seed(const uint8_t* seed32, uint8_t out[32]) {
+    fill_seed(seed32, out);
+}
 
 // point records of the batch MSM that ran last on b, when the per-signature fallback can reuse
 // them: per-signature keys (every A_i decompressed at point i, R_i at n + 1 + i)

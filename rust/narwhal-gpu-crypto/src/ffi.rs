@@ -39,6 +39,7 @@ pub const NWV_FLAG_MSM_SPLIT_PREP: u32 = 4;
 pub const NWV_FLAG_NO_KEYCACHE: u32 = 8;
 pub const NWV_FLAG_MSM_SORT2: u32 = 16;
 pub const NWV_FLAG_NO_MSM_REUSE: u32 = 32;
+pub const NWV_FLAG_BLS_PER_ITEM: u32 = 64;
 
 // per-item BLS12-381 statuses (include/nwv_bls.h)
 pub const NWV_BLS_OK: i32 = 0;
@@ -236,6 +237,7 @@ extern "C" {
         status: *mut i32,
     ) -> c_int;
     pub fn nwv_bls_last_kernel_ms(ctx: *mut NwvCtx, out_ms: *mut f64) -> c_int;
+    pub fn nwv_bls_last_path(ctx: *mut NwvCtx) -> c_int;
     pub fn nwv_bls_verify(
         ctx: *mut NwvCtx,
         pk: *const u8,

@@ -100,4 +100,37 @@ int bh_fast_aggregate_verify(const uint8_t* sig, size_t n_pks, const uint8_t* pk
     return pairing_check(srec, hrec, arec) ? ST_OK : ST_VERIFY_FAIL;
 }
 
+// the batch check over n items (item i: signature sig + 48 i, one key pk + 96 i, message msg + 32 i)
+// exactly as the kernels run it: shares, the product tree level by level, the final lane.
+// Returns 1 if the batch check accepts, 0 if it rejects, -1 if some item fails to decode.
+int bh_rlc_batch(size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint8_t* seed,
+                 const uint8_t* dst, size_t dl) {
+    uint32_t* f = new uint32_t[F12_REC_WORDS * n];
+    uint32_t* j = new uint32_t[G1J_REC_WORDS * n];
+    int rc = 1;
+    for (size_t i = 0; i < n; i++) {
+        uint32_t srec[G1_REC_WORDS], hrec[G1_REC_WORDS], krec[G2_REC_WORDS], arec[G2_REC_WORDS];
+        const uint32_t idx = 0;
+        int32_t kst = key_decode(pks + 96 * i, krec);
+        if (sig_decode(sigs + 48 * i, srec) != ST_OK || kst != ST_OK || apk_record(krec, &kst, &idx, 1, arec) != ST_OK) {
+            rc = -1;
+            break;
+        }
+        h2c_record(msgs + 32 * i, 32, dst, (uint32_t)dl, hrec);
+        rlc_item(srec, hrec, arec, rlc_scalar(seed, (uint32_t)i), f + F12_REC_WORDS * i, j + G1J_REC_WORDS * i);
+    }
+    if (rc == 1) {
+        for (size_t m = n; m > 1; m = (m + 1) / 2) {
+            const size_t h = (m + 1) / 2;
+            for (size_t i = 0; i < m - h; i++)
+                rlc_fold(f + F12_REC_WORDS * i, j + G1J_REC_WORDS * i, f + F12_REC_WORDS * (i + h),
+                         j + G1J_REC_WORDS * (i + h));
+        }
+        rc = rlc_final(f, j) ? 1 : 0;
+    }
+    delete[] f;
+    delete[] j;
+    return rc;
+}
+
 }  // extern "C"

@@ -31,6 +31,7 @@ def emu():
     L.bh_keygen.argtypes = [c, vp]
     L.bh_sign.argtypes = [c, c, sz, c, sz, vp]
     L.bh_fast_aggregate_verify.argtypes = [c, sz, c, c, sz, c, sz]
+    L.bh_rlc_batch.argtypes = [sz, c, c, c, c, c, sz]
     return L
 
 
@@ -110,3 +111,24 @@ def test_fast_aggregate_verify_statuses(emu, gold):
     for s, ks, msg in cases:
         got = emu.bh_fast_aggregate_verify(s, len(ks), b"".join(ks), msg, len(msg), dst, len(dst))
         assert got == B.fast_aggregate_verify(s, ks, msg)
+
+
+def test_rlc_batch_check(emu, gold):
+    """the random-linear-combination batch check (bls_verify.h rlc_*): accepts valid items at
+    every tree shape, rejects when any one item's pairing equation fails"""
+    import os
+    sks = [bytes.fromhex(k["sk"]) for k in gold["keygen"]]
+    pks = [bytes.fromhex(k["pk"]) for k in gold["keygen"]]
+    dst = B.DST_NUL
+    seed = os.urandom(32)
+    msgs = [bytes([i]) * 32 for i in range(5)]
+    sigs = [B.sign(sks[i % 4], m) for i, m in enumerate(msgs)]
+    keys = [pks[i % 4] for i in range(5)]
+    for n in (1, 2, 3, 5):
+        assert emu.bh_rlc_batch(n, b"".join(sigs[:n]), b"".join(keys[:n]), b"".join(msgs[:n]), seed, dst,
+                                len(dst)) == 1
+        for bad in range(n):
+            m2 = list(msgs[:n])
+            m2[bad] = bytes([0xee]) * 32
+            assert emu.bh_rlc_batch(n, b"".join(sigs[:n]), b"".join(keys[:n]), b"".join(m2), seed, dst,
+                                    len(dst)) == 0

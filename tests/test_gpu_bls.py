@@ -28,6 +28,17 @@ def bls():
 
 
 @pytest.fixture(scope="module")
+def bls_per_item():
+    """a context under NWV_FLAG_BLS_PER_ITEM: every item's own pairing check, no batch check"""
+    import narwhal_amd
+    from narwhal_amd import _lib
+    from narwhal_amd.bls import Bls
+    e = narwhal_amd.Engine(device=0, flags=_lib.NWV_FLAG_BLS_PER_ITEM)
+    yield Bls(e)
+    e.close()
+
+
+@pytest.fixture(scope="module")
 def gold():
     with open(os.path.join(ROOT, "tests", "golden", "bls12381_kats.json")) as f:
         return json.load(f)
@@ -66,9 +77,12 @@ def _committee(bls, n, seed):
     return sks, bls.keygen(sks)
 
 
-def test_verify_many_mixed_batch_matches_oracle(bls):
+@pytest.mark.parametrize("path", ["batch", "per_item"])
+def test_verify_many_mixed_batch_matches_oracle(bls, bls_per_item, path):
     """certificates of a 10-node committee (quorum 7 signers, 32-byte digests) plus every
-    adversarial category; statuses equal the oracle's codes item by item"""
+    adversarial category; statuses equal the oracle's codes item by item, through the batch check
+    (it rejects, then the per-item check names the failures) and under NWV_FLAG_BLS_PER_ITEM"""
+    bls = bls if path == "batch" else bls_per_item
     sks, pks = _committee(bls, 10, 13)
     keys = pks + [C.not_in_g2(), C.IDENTITY_G2, C.negate_g2(pks[0])]
     rnd = random.Random(14)
@@ -95,6 +109,19 @@ def test_verify_many_mixed_batch_matches_oracle(bls):
     want = [B.fast_aggregate_verify(s, [keys[k] for k in ks], m) for s, ks, m in items]
     assert list(got) == want
     assert want[:12] == [0] * 12 and all(w != 0 for w in want[12:])
+    # the wrong-message / wrong-signer items fail only the pairing equation: the batch check rejects
+    assert bls.last_path() == ("batch_rejected_then_per_item" if path == "batch" else "per_item")
+    # the valid certificates alone: the batch check accepts them in one final exponentiation
+    got = bls.verify_many(keys, [i[0] for i in items[:12]], [i[1] for i in items[:12]], [i[2] for i in items[:12]])
+    assert list(got) == [0] * 12
+    assert bls.last_path() == ("batch_accepted" if path == "batch" else "per_item")
+    # valid certificates beside items that fail before the pairing (decode / group / key errors):
+    # those stay out of the batch check, which accepts the rest
+    pre = [it for it, w in zip(items, want) if w not in (0, B.ORB_VERIFY_FAIL)]
+    sub = items[:12] + pre
+    got = bls.verify_many(keys, [i[0] for i in sub], [i[1] for i in sub], [i[2] for i in sub])
+    assert list(got) == [B.fast_aggregate_verify(s, [keys[k] for k in ks], m) for s, ks, m in sub]
+    assert bls.last_path() == ("batch_accepted" if path == "batch" else "per_item")
 
 
 def test_trait_contract(bls, gold):
@@ -124,9 +151,10 @@ def test_trait_contract(bls, gold):
     assert bls.aggregate_batch_verify([agg, agg2], [pks[:3], pks[1:]], [m]) == _lib.NWV_ERR_LENGTH
 
 
-@pytest.mark.parametrize("n", [1, 63, 64, 65, 200])
+@pytest.mark.parametrize("n", [1, 2, 3, 63, 64, 65, 200])
 def test_batch_sizes(bls, n):
-    """batch tails around the 64-lane wave; every other item corrupted (message flipped)"""
+    """batch tails around the 64-lane wave and the product tree's odd levels; every other item
+    corrupted (message flipped), then the same items all valid (one accepted batch check)"""
     sks, pks = _committee(bls, 4, 15)
     rnd = random.Random(n)
     msgs = [rnd.randbytes(32) for _ in range(n)]
@@ -136,3 +164,6 @@ def test_batch_sizes(bls, n):
     msgs2 = [m + b"x" if b else m for m, b in zip(msgs, bad)]
     got = bls.verify_many(pks, sigs, [[0, 1, 2]] * n, msgs2)
     assert list(got) == [B.ORB_VERIFY_FAIL if b else 0 for b in bad]
+    assert bls.last_path() == ("batch_accepted" if n == 1 else "batch_rejected_then_per_item")
+    got = bls.verify_many(pks, sigs, [[0, 1, 2]] * n, msgs)
+    assert list(got) == [0] * n and bls.last_path() == "batch_accepted"

@@ -99,3 +99,52 @@ def test_async_callbacks_and_flush(eng):
         svc.flush()  # one engine call for everything, long before the deadline
         assert [codes[i] for i in range(len(items))] == want
         assert svc.stats()["calls"] == 1
+
+
+def _kind(item):
+    from narwhal_amd import types as T
+    return {T.Header: "header", T.Vote: "vote", T.Certificate: "certificate"}[type(item)]
+
+
+@pytest.mark.parametrize("max_items,max_wait_us", [(512, 1000), (7, 0), (1, 0)])
+def test_core_drain_single_consumer_matches_oracle(eng, max_items, max_wait_us):
+    """the Core-side drain (service.CoreDrain, rust core_drain.rs): one consumer thread takes the
+    messages a producer thread queues, flushes <= max_items per engine call, and every message's
+    code equals the oracle's, in arrival order"""
+    import queue
+    fx, items, want = _cases(33)
+    order = list(range(len(items)))
+    random.Random(34).shuffle(order)
+    q = queue.Queue()
+
+    def producer():
+        for i in order:
+            q.put((i, (_kind(items[i]), items[i])))
+
+    d = S.CoreDrain(eng, tu.committee(fx.committee), max_items=max_items, max_wait_us=max_wait_us)
+    th = threading.Thread(target=producer)
+    th.start()
+    got, seen = {}, []
+    while len(got) < len(items):
+        batch = d.drain(q)
+        assert 1 <= len(batch) <= max_items
+        codes = d.verify([m for _, m in batch])
+        for (i, _), c in zip(batch, codes):
+            got[i] = c
+            seen.append(i)
+    th.join()
+    assert seen == order  # arrival order kept
+    assert [got[i] for i in range(len(items))] == want
+    assert d.items == len(items) and d.largest <= max_items
+    if max_items == 1:
+        assert d.calls == len(items)
+
+
+def test_core_drain_prepared_structs(eng):
+    """CoreDrain.verify on prepared C structs (the bench's form) gives the same codes"""
+    from narwhal_amd import types as T
+    fx, items, want = _cases(35)
+    keep = T._Keep()
+    d = S.CoreDrain(eng, tu.committee(fx.committee))
+    assert d.verify([(_kind(it), it._c(keep)) for it in items]) == want
+    assert d.calls == 1

@@ -208,3 +208,27 @@ def test_callbacks_may_submit_but_blocking_calls_from_them_fail_fast(lib):
         assert seen == [_lib.NWV_ERR_REENTRANT, _lib.NWV_ERR_REENTRANT, ("chained", T.InvalidSignature.code)]
     finally:
         svc.close()
+
+
+def test_core_drain_policy():
+    """CoreDrain.drain (no engine call): takes what is queued up to max_items, waits at most
+    max_wait_us for more, keeps arrival order"""
+    import queue
+    import threading
+    import time
+    from narwhal_amd import service as S
+    from narwhal_amd import types as T
+    com = T.Committee([bytes([i]) * 32 for i in range(4)], [1] * 4)
+    d = S.CoreDrain(None, com, max_items=5, max_wait_us=0)
+    q = queue.Queue()
+    for i in range(12):
+        q.put(i)
+    assert d.drain(q) == [0, 1, 2, 3, 4]
+    assert d.drain(q, first="x") == ["x", 5, 6, 7, 8]
+    assert d.drain(q) == [9, 10, 11]  # nothing more queued, no wait
+    d2 = S.CoreDrain(None, com, max_items=100, max_wait_us=200_000)
+    q.put(0)
+    threading.Timer(0.02, lambda: q.put(1)).start()
+    t0 = time.perf_counter()
+    assert d2.drain(q) == [0, 1]  # a late message within the deadline joins the flush
+    assert 0.15 < time.perf_counter() - t0 < 2.0  # then the deadline ends the drain

@@ -405,3 +405,72 @@ def leg_c5(eng, rounds=50):
                     "nwv_verify_mixed_many call) and BLAKE2b-256 of 100 x 500,224 B "
                     "worker batches (one GPU call)"}, \
         {"committee": com, "certs": certs, "headers": headers, "votes": vsample, "batches": batches}
+
+
+def leg_bls(eng, certs=100, quorum=67, committee=100, reps=20, throughput_n=16384):
+    """SURVEY §8 row f4, the reference's default scheme (crypto/src/lib.rs:29-33 -> BLS12-381
+    min_sig): (a) a C5-shaped round of `certs` certificates, each an aggregate of `quorum`
+    committee signatures over its 32-byte digest, verified as ONE nwv_bls_verify_many call
+    (CertificatesResponse::validate_certificates, each item = AggregateAuthenticator::verify:
+    key-sum, hash to G1, two-pair Miller loop, final exponentiation), host -> host; (b) one
+    Verifier::verify (Header::verify's single signature); (c) `throughput_n` single-key items in
+    one call.  Synthetic keys / messages; signatures and aggregates made on the GPU."""
+    from narwhal_amd.bls import Bls
+    b = Bls(eng)
+    rnd = np.random.default_rng(77)
+    r = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
+    sks = [int.from_bytes(rnd.bytes(32), "big") % r or 1 for _ in range(committee)]
+    sks = [s.to_bytes(32, "big") for s in sks]
+    pks = b.keygen(sks)
+    digests = [rnd.bytes(32) for _ in range(certs)]
+    signers = [sorted(rnd.choice(committee, quorum, replace=False).tolist()) for _ in range(certs)]
+    flat = b.sign([sks[k] for s in signers for k in s], [d for d, s in zip(digests, signers) for _ in s])
+    aggs = []
+    for c in range(certs):
+        rc, agg, _ = b.aggregate(flat[quorum * c:quorum * (c + 1)])
+        assert rc == 0
+        aggs.append(agg)
+    ts, kms = [], []
+    for i in range(reps + 2):
+        t0 = time.perf_counter()
+        st = b.verify_many(pks, aggs, signers, digests)
+        dt = time.perf_counter() - t0
+        assert not st.any(), st[:8]
+        if i >= 2:
+            ts.append(dt)
+            kms.append(b.last_kernel_ms())
+    out = {"round": {"certificates": certs, "quorum": quorum, "committee": committee,
+                     "ms_host_to_host_p50": float(np.median(ts)) * 1e3,
+                     "certs_per_s": certs / float(np.median(ts)),
+                     "kernel_ms": {k: float(np.median([x[k] for x in kms])) for k in kms[0]}}}
+    m = rnd.bytes(32)
+    s1 = b.sign([sks[0]], [m])[0]
+    t1 = []
+    for i in range(reps + 2):
+        t0 = time.perf_counter()
+        rc = b.verify(pks[0], m, s1)
+        if i >= 2:
+            t1.append(time.perf_counter() - t0)
+        assert rc == 0
+    out["single_verify_ms_p50"] = float(np.median(t1)) * 1e3
+    # throughput: throughput_n items, one key each (a header's / vote's single signature)
+    n = throughput_n
+    msgs = [rnd.bytes(32) for _ in range(n)]
+    kidx = (np.arange(n) % committee).tolist()
+    sigs = b.sign([sks[k] for k in kidx], msgs)
+    t2, km2 = [], []
+    for i in range(3):
+        t0 = time.perf_counter()
+        st = b.verify_many(pks, sigs, [[k] for k in kidx], msgs)
+        dt = time.perf_counter() - t0
+        assert not st.any()
+        if i:
+            t2.append(dt)
+            km2.append(b.last_kernel_ms())
+    out["throughput"] = {"items": n, "ms_host_to_host": float(np.median(t2)) * 1e3,
+                         "verifies_per_s": n / float(np.median(t2)),
+                         "kernel_ms": {k: float(np.median([x[k] for x in km2])) for k in km2[0]}}
+    out["note"] = ("BLS12-381 min_sig (48 B G1 signatures, 96 B G2 keys), fastcrypto's DST; each item "
+                   "= key decode + G2 check (once per distinct key), sig decode + G1 check, hash to G1, "
+                   "key sum, e(-sig, g2) e(H, apk) == 1, one lane per item")
+    return out
