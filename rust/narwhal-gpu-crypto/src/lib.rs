@@ -23,6 +23,7 @@
 //! `crypto/src/bls12377/mod.rs:274-281`.  A runtime failure of the engine (no device, HIP error)
 //! is never reported as valid.
 
+pub mod bls;
 pub mod core_drain;
 pub mod ffi;
 

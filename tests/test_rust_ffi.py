@@ -127,5 +127,16 @@ def test_crate_links_the_engine_and_covers_the_trait_surface():
                    "nwv_validate_certificates", "nwv_service_verify_certificate",
                    "Critical Error! This behavious can signal something dangerous"):
         assert needle in lib, needle
+    bls = open(os.path.join(CRATE, "src", "bls.rs")).read()  # the reference's default scheme
+    for needle in ("impl Verifier<GpuBls12381Signature> for GpuBls12381PublicKey",
+                   "impl VerifyingKey for GpuBls12381PublicKey",
+                   "impl AggregateAuthenticator for GpuBls12381AggregateSignature", "fn batch_verify",
+                   "nwv_bls_verify(", "nwv_bls_verify_batch_empty_fail(", "nwv_bls_aggregate_verify(",
+                   "nwv_bls_aggregate_batch_verify(", "nwv_bls_verify_many(",
+                   "Critical Error! This behavious can signal something dangerous"):
+        assert needle in bls, needle
+    drain = open(os.path.join(CRATE, "src", "core_drain.rs")).read()
+    for needle in ("pub async fn drain", "try_recv", "timeout_at", "nwv_verify_mixed_many", "pub fn verify_items"):
+        assert needle in drain, needle
     cargo = open(os.path.join(CRATE, "Cargo.toml")).read()
     assert 'fastcrypto = { version = "0.1.2"' in cargo  # the reference's pin (Cargo.lock:1534)
