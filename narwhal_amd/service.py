@@ -154,12 +154,13 @@ class CoreDrain:
     KINDS = ("header", "vote", "certificate")
     _CLS = {"header": T._Header, "vote": T._Vote, "certificate": T._Certificate}
 
-    def __init__(self, engine, committee, max_items=512, max_wait_us=1000):
+    def __init__(self, engine, committee, max_items=512, max_wait_us=1000, min_items=64):
         if max_items < 1:
             raise ValueError("max_items must be >= 1")
         self.engine = engine
         self.max_items = max_items
         self.max_wait_us = max_wait_us
+        self.min_items = min_items
         self.set_committee(committee)
         self.calls = self.items = self.largest = 0
 
@@ -169,8 +170,10 @@ class CoreDrain:
         self._cc = committee._c(self._ckeep)
 
     def drain(self, q, first=None):
-        """`first` (or a blocking q.get()) plus whatever q holds or receives before the deadline,
-        at most max_items messages (q: a queue.Queue standing in for Core's channels)"""
+        """`first` (or a blocking q.get()) plus whatever q holds, at most max_items messages; when
+        q runs dry it waits for more until the deadline only while fewer than min_items are taken
+        (a big enough batch goes at once: waiting would only add latency; q: a queue.Queue
+        standing in for Core's channels)"""
         import queue
         import time
         out = [q.get() if first is None else first]
@@ -182,7 +185,7 @@ class CoreDrain:
             except queue.Empty:
                 pass
             left = deadline - time.perf_counter()
-            if left <= 0:
+            if left <= 0 or len(out) >= self.min_items:
                 break
             try:
                 out.append(q.get(timeout=left))

@@ -226,6 +226,11 @@ def test_core_drain_policy():
     assert d.drain(q) == [0, 1, 2, 3, 4]
     assert d.drain(q, first="x") == ["x", 5, 6, 7, 8]
     assert d.drain(q) == [9, 10, 11]  # nothing more queued, no wait
+    d3 = S.CoreDrain(None, com, max_items=100, max_wait_us=200_000, min_items=3)
+    for i in range(4):
+        q.put(i)
+    t0 = time.perf_counter()
+    assert d3.drain(q) == [0, 1, 2, 3] and time.perf_counter() - t0 < 0.1  # >= min_items: no wait
     d2 = S.CoreDrain(None, com, max_items=100, max_wait_us=200_000)
     q.put(0)
     threading.Timer(0.02, lambda: q.put(1)).start()

@@ -233,7 +233,7 @@ def leg_c5_service(eng, com, cc, harr, varr, carr, nsig, rounds=20):
     msgs = [("header", harr[i]) for i in range(len(harr))] + [("vote", varr[i]) for i in range(len(varr))] + \
            [("certificate", carr[i]) for i in range(len(carr))]
     out = {"messages_per_round": len(msgs), "rounds": rounds}
-    drain = S.CoreDrain(eng, com, max_items=512, max_wait_us=1000)
+    drain = S.CoreDrain(eng, com, max_items=512, max_wait_us=1000, min_items=64)
     q = queue.Queue()
     lat, rtimes, sizes = [], [], []
 
@@ -273,7 +273,7 @@ def leg_c5_service(eng, com, cc, harr, varr, carr, nsig, rounds=20):
         go.set()
         th.join()
     a = np.array(lat) * 1e3
-    out.update({"consumer": "one thread, CoreDrain(max_items=512, max_wait_us=1000)",
+    out.update({"consumer": "one thread, CoreDrain(max_items=512, max_wait_us=1000, min_items=64)",
                 "ms_per_round": float(np.median(rtimes)) * 1e3, "sigs_per_s": nsig / float(np.median(rtimes)),
                 "latency_ms_p50": float(np.percentile(a, 50)), "latency_ms_p99": float(np.percentile(a, 99)),
                 "engine_calls": len(sizes), "largest_flush": int(max(sizes)),
