@@ -361,19 +361,12 @@ def timed_region(stages, args, dist, run):
         s_.sync()
     if dist is not None:
         dist.barrier()
-    marks = hasattr(stages[0], "mark") and args.steps < 65535
     t0 = time.perf_counter()
-    if marks:
-        stages[0].mark(0)  # device-side start of the region (the streams are idle here)
     for s in range(args.steps):
         run(stages[s % len(stages)])
-        if marks:
-            stages[s % len(stages)].mark(s + 1)  # fires when step s has completed
     for s_ in stages:
         s_.sync()
     dt = time.perf_counter() - t0
-    timed_region.completions_ms = ([stages[0].mark_elapsed(0, stages[s % len(stages)], s + 1)
-                                    for s in range(args.steps)] if marks else None)
     dt_max = dt
     if dist is not None:
         import torch
@@ -384,21 +377,32 @@ def timed_region(stages, args, dist, run):
     return dt, dt_max
 
 
-def steady_state(comp, args):
-    """Step-completion view of the timed region (HIP events recorded after every step on its own
-    stream): the interval between completions once the pipeline is full -- the slope of the
-    sorted completion times from the K/4-th on -- next to the first completion (the ramp).  The
-    headline `value` stays the contract's K steps over the host-timed region, ramp and drain
-    included; this field says how much of it the ramp and drain are."""
-    if not comp or len(comp) < 8:
+def steady_state(stages, args, run):
+    """After the contract's timed region (never part of `value`): `args.steady_steps` more steps
+    through the same stages, a HIP event recorded on each step's stream when it completes, and
+    the interval between completions from the quarter mark on -- the pipeline's steady-state rate,
+    which a short timed region (the driver's --steps 20) cannot show because it starts from an
+    idle GPU (every stage synchronised) and ends with a drain.  `ramp_and_drain_cost` = how much
+    longer the contract's K steps took than K steady steps."""
+    K = args.steady_steps
+    if K < 16 or K >= 65535 or not hasattr(stages[0], "mark"):
         return None
-    c = sorted(comp)
-    q = len(c) // 4
-    slope = (c[-1] - c[q]) / (len(c) - 1 - q)
-    return {"ms_per_step": slope, "sigs_per_s": args.n / (slope * 1e-3), "first_completion_ms": c[0],
-            "last_completion_ms": c[-1], "device_span_ms_per_step": c[-1] / len(c),
-            "note": "device-side (HIP events per step): interval between step completions from the "
-                    f"{q}-th of {len(c)} on; `value` is the host-timed K steps including ramp and drain"}
+    for s_ in stages:
+        s_.sync()
+    stages[0].mark(0)
+    for s in range(K):
+        run(stages[s % len(stages)])
+        stages[s % len(stages)].mark(s + 1)
+    for s_ in stages:
+        s_.sync()
+    c = sorted(stages[0].mark_elapsed(0, stages[s % len(stages)], s + 1) for s in range(K))
+    q = K // 4
+    slope = (c[-1] - c[q]) / (K - 1 - q)
+    return {"ms_per_step": slope, "sigs_per_s": args.n / (slope * 1e-3), "steps": K,
+            "first_completion_ms": c[0], "last_completion_ms": c[-1],
+            "note": f"{K} extra steps after the timed region, HIP events on step completion: interval "
+                    f"between completions from the {q}-th on (not `value`, which is the contract's host-timed "
+                    "K steps from an idle GPU, ramp and drain included)"}
 
 
 class DryStage:
@@ -446,9 +450,13 @@ def run_headline(args, eng, rank, world, dist):
     check_all("setup")
     dt, dt_max = timed_region(stages, args, dist, lambda st: st.run(mode=args.mode))  # seed None: OS entropy
     check_all("timed region: last run of every stage")
+    steady = steady_state(stages, args, lambda st: st.run(mode=args.mode))
+    if steady is not None:
+        steady["ramp_and_drain_cost"] = dt_max / (args.steps * steady["ms_per_step"] * 1e-3) - 1.0
+        check_all("steady-state steps")
     if args.mode == 1:
         # every run's batch verdict, graph replays included, as tallied on the device by the runs
-        runs = len(stages) + args.warmup + args.steps
+        runs = len(stages) + args.warmup + args.steps + (steady["steps"] if steady else 0)
         acc = rej = 0
         for s_ in stages:
             a_, r_ = s_.run_tally()
@@ -470,7 +478,7 @@ def run_headline(args, eng, rank, world, dist):
     for s_ in stages:
         s_.free()
     return {"dt": dt, "dt_max": dt_max, "single": single, "kt": kt, "stats": stats,
-            "data": (pk, sg, msgs, offs, lens), "steady": steady_state(timed_region.completions_ms, args)}
+            "data": (pk, sg, msgs, offs, lens), "steady": steady}
 
 
 def kernels_1k(eng, data, reps=20):
@@ -739,6 +747,8 @@ def main():
                          "100: its committee variant, keyed batch MSM)")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the C1 / C3 / C4 / C5 legs (other BASELINE.json configs, GPU and CPU)")
+    ap.add_argument("--steady-steps", type=int, default=96,
+                    help="extra steps after the timed region that measure the steady-state rate (not `value`)")
     ap.add_argument("--single-steps", type=int, default=8,
                     help="single-stream steps timed after the run (step latency, per-kernel times)")
     ap.add_argument("--h2h-seconds", type=float, default=2.0)

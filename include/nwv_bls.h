@@ -13,7 +13,9 @@
  * CertificatesResponse::validate_certificates primary/src/block_synchronizer/responses.rs:95-141.
  *
  * Every verification runs on the GPU, one item (one fast_aggregate_verify) per lane: signature
- * decode + G1 membership, public-key decode + G2 membership (once per distinct key of a call),
+ * decode + G1 membership, public-key decode + G2 membership (once per key per device: a key
+ * cache keeps each validated key, as fastcrypto validates keys once at deserialization;
+ * NWV_FLAG_NO_KEYCACHE decodes every call's keys afresh),
  * aggregate public key, hash to G1; then the pairing equations of all the call's items as one
  * random-linear-combination check (one Miller loop per item, one final exponentiation per call),
  * and only if that rejects, each item's own two-pair Miller loop and final exponentiation.
@@ -54,8 +56,9 @@ int nwv_bls_verify_many(nwv_ctx* ctx, size_t n_keys, const uint8_t* keys, size_t
                         const uint8_t* msg_base, const uint64_t* msg_off, const uint32_t* msg_len,
                         const uint8_t* dst, size_t dst_len, int32_t* status);
 
-/* device time of the last nwv_bls_verify_many call on this context, per stage (HIP events):
- * [0] k_bls_keys, [1] k_bls_sigs, [2] k_bls_h2c, [3] k_bls_apk, [4] the pairing check (the batch
+/* device time of the last nwv_bls_verify_many call on this context, per stage (HIP events; the
+ * first four run on three concurrent streams): [0] keys new to the device's key cache, [1]
+ * signature decode + G1 checks, [2] hash to G1, [3] key sums, [4] the pairing check (the batch
  * check k_bls_rlc + k_bls_fold + k_bls_final, plus k_bls_pair when it ran) */
 int nwv_bls_last_kernel_ms(nwv_ctx* ctx, double out_ms[5]);
 /* how the last nwv_bls_verify_many call checked its pairings: 0 per item (NWV_FLAG_BLS_PER_ITEM),

@@ -28,7 +28,7 @@ _SIGS = {
     "nwv_bls_last_kernel_ms": ([_vp, _vp], _i32),
     "nwv_bls_last_path": ([_vp], _i32),
 }
-KERNELS = ("k_bls_keys", "k_bls_sigs", "k_bls_h2c", "k_bls_apk", "pairing_check")
+KERNELS = ("keys_new_to_cache", "sig_decode", "hash_to_g1", "key_sums", "pairing_check")
 PATHS = ("per_item", "batch_accepted", "batch_rejected_then_per_item")
 _bound = set()
 

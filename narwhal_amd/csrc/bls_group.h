@@ -1,0 +1,335 @@
+// bls_group.h -- BLS12-381 Fp12 arithmetic spread over a GROUP of 8 lanes (gfx950), for the Miller
+// loops and final exponentiations of the pairing check.
+//
+// One lane holding a whole Fp12 (12 x 14 limbs = 168 VGPRs per operand) spills to scratch on every
+// tower product, and the product's 54 Fp multiplications run one after another.  Here an Fp12 is
+// read as Fp2[W] / (W^6 - xi) (W = w, so v = W^2): lane k of a group holds the coefficient of W^k
+// (k = 0..5; lanes 6, 7 shadow lanes 0, 1), so an Fp12 product is a length-6 cyclic convolution
+// with the xi wrap -- every lane computes its own output coefficient from six Fp2 products of
+// operands exchanged through LDS: 18 Fp multiplications deep instead of 54, with everything in
+// registers.  The sparse line product is 3 Fp2 products deep, the Granger-Scott cyclotomic square
+// 3 Fp2 squarings deep (lane k computes one of the six Fp4 half-products), the Frobenius map one
+// Fp2 product.  The Miller loop's G2 point and lines are computed redundantly by every lane.
+//
+// Tower slot <-> W power: k 0 c0.c0, 1 c1.c0, 2 c0.c1, 3 c1.c1, 4 c0.c2, 5 c1.c2 (bls381.h).
+//
+// The same algorithms compile for the host (tests/hostemu): there a G12 holds all six coefficients
+// and each group operation loops over k with the same per-coefficient code, so the host build
+// checks the group arithmetic against bls381.h's single-lane tower bit for bit.
+#pragma once
+#include "bls381.h"
+
+// the lane-group form everywhere except in the CPU test build, which defines BLS_GROUP_HOST_EMU
+// (nwv_bls.hip's host compilation pass only analyses the kernels, it never runs them)
+#if !defined(BLS_GROUP_HOST_EMU)
+#define BLS_GDEV 1
+#endif
+
+namespace bls {
+
+constexpr int GRP = 8;                   // lanes per group
+constexpr int F2W = 2 * NL;              // u32 words of an Fp2
+constexpr int GX_WORDS = 2 * GRP * F2W;  // one group's LDS exchange area: operand A slots, B slots
+
+NWV_HD void st_fp(uint32_t* o, const fp& a) { for (int j = 0; j < NL; j++) o[j] = a.l[j]; }
+NWV_HD fp ld_fp(const uint32_t* o) { fp a; for (int j = 0; j < NL; j++) a.l[j] = o[j]; return a; }
+NWV_HD void st_f2(uint32_t* o, const fp2& a) {
+    st_fp(o, a.c0);
+    st_fp(o + NL, a.c1);
+}
+NWV_HD fp2 ld_f2(const uint32_t* o) {
+    fp2 a;
+    a.c0 = ld_fp(o);
+    a.c1 = ld_fp(o + NL);
+    return a;
+}
+
+#ifdef BLS_GDEV
+__constant__ uint32_t c_gamma[6][2][NL] = BLS_GAMMA;
+#endif
+// Frobenius coefficient of W^k (gamma_k of bls381.h; k = 0: 1)
+NWV_HD fp2 w_gamma(int k) {
+#ifdef BLS_GDEV
+    fp2 r;
+    for (int j = 0; j < NL; j++) {
+        r.c0.l[j] = c_gamma[k][0][j];
+        r.c1.l[j] = c_gamma[k][1][j];
+    }
+    return k == 0 ? f2_one() : r;
+#else
+    return k == 0 ? f2_one() : gamma_k(k);
+#endif
+}
+
+// ---- per-coefficient arithmetic (shared by the device and host forms) ----------------------
+// c_k of a * b: sum_r a_{k-r} b_r, the wrapped terms (k < r) times xi
+template <class A, class B>
+NWV_HD fp2 coef_mul(int k, const A& a, const B& b) {
+    fp2 acc = f2_zero();
+#pragma unroll 1
+    for (int r = 0; r < 6; r++) {
+        const int i = k >= r ? k - r : k - r + 6;
+        fp2 t = f2_mul(a(i), b(r));
+        if (k < r) t = f2_mul_xi(t);
+        acc = f2_add(acc, t);
+    }
+    return acc;
+}
+// c_k of a * (L0 + L2 W^2 + L3 W^3): the Miller loop's sparse line product
+template <class A>
+NWV_HD fp2 coef_line(int k, const A& a, const fp2& L0, const fp2& L2, const fp2& L3) {
+    const int i2 = k >= 2 ? k - 2 : k + 4, i3 = k >= 3 ? k - 3 : k + 3;
+    fp2 t2 = f2_mul(a(i2), L2);
+    if (k < 2) t2 = f2_mul_xi(t2);
+    fp2 t3 = f2_mul(a(i3), L3);
+    if (k < 3) t3 = f2_mul_xi(t3);
+    return f2_add(f2_add(f2_mul(a(k), L0), t2), t3);
+}
+// c_k of the Granger-Scott cyclotomic square (f12_cyc_sqr): the Fp4 pairs are (W^0, W^3),
+// (W^1, W^4), (W^2, W^5); lane k takes one output of one pair's square
+//   fp4_sqr(a, b) = (xi b^2 + a^2, (a + b)^2 - a^2 - b^2)
+// k -> (pair, output): 0 (0,3).0, 1 (2,5).1 * xi, 2 (1,4).0, 3 (0,3).1, 4 (2,5).0, 5 (1,4).1;
+// then z_k' = 2 (o - z_k) + o (even k) or 2 (o + z_k) + o (odd k)
+template <class A>
+NWV_HD fp2 coef_cyc_sqr(int k, const A& a) {
+    const int p = (k == 0 || k == 3) ? 0 : (k == 2 || k == 5) ? 1 : 2;
+    const bool second = (k & 1) != 0;
+    const fp2 x = a(p), y = a(p + 3);
+    const fp2 t0 = f2_sqr(x), t1 = f2_sqr(y), s = f2_sqr(f2_add(x, y));
+    fp2 o = second ? f2_sub(f2_sub(s, t0), t1) : f2_add(f2_mul_xi(t1), t0);
+    if (k == 1) o = f2_mul_xi(o);
+    const fp2 z = a(k);
+    return second ? f2_add(f2_dbl(f2_add(o, z)), o) : f2_add(f2_dbl(f2_sub(o, z)), o);
+}
+// tower slot of W^k in an fp12
+NWV_HD fp2& w_slot(fp12& f, int k) {
+    switch (k) {
+        case 0: return f.c0.c0;
+        case 1: return f.c1.c0;
+        case 2: return f.c0.c1;
+        case 3: return f.c1.c1;
+        case 4: return f.c0.c2;
+        default: return f.c1.c2;
+    }
+}
+
+// ---- the group element and its operations ----------------------------------------------------
+#ifdef BLS_GDEV
+
+struct GCtx {
+    uint32_t* xa;  // this group's LDS exchange area (GX_WORDS): A slots [GRP][F2W], then B slots
+    int slot;      // this lane's slot in the group (0..7)
+    int k;         // its coefficient (slot mod 6)
+};
+struct G12 {
+    fp2 v;  // this lane's coefficient of W^k
+};
+__device__ inline GCtx g_ctx(uint32_t* lds_base) {
+    GCtx g;
+    const int lane = (int)(threadIdx.x & 63);
+    g.slot = lane & (GRP - 1);
+    g.k = g.slot < 6 ? g.slot : g.slot - 6;
+    g.xa = lds_base + (size_t)(threadIdx.x / GRP) * GX_WORDS;
+    return g;
+}
+// LDS writes of the group visible to its reads (one wave: in-order LDS; fence the compiler)
+__device__ inline void g_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+struct GRead {
+    const uint32_t* base;
+    __device__ fp2 operator()(int i) const { return ld_f2(base + i * F2W); }
+};
+__device__ inline void g_put(const GCtx& g, int which, const fp2& x) { st_f2(g.xa + which * GRP * F2W + g.slot * F2W, x); }
+__device__ inline GRead g_reader(const GCtx& g, int which) { return GRead{g.xa + which * GRP * F2W}; }
+
+__device__ inline G12 g_mul(const GCtx& g, const G12& a, const G12& b) {
+    g_sync();
+    g_put(g, 0, a.v);
+    g_put(g, 1, b.v);
+    g_sync();
+    return G12{coef_mul(g.k, g_reader(g, 0), g_reader(g, 1))};
+}
+__device__ inline G12 g_sqr(const GCtx& g, const G12& a) {
+    g_sync();
+    g_put(g, 0, a.v);
+    g_sync();
+    return G12{coef_mul(g.k, g_reader(g, 0), g_reader(g, 0))};
+}
+__device__ inline G12 g_mul_line(const GCtx& g, const G12& a, const fp2& L0, const fp2& L2, const fp2& L3) {
+    g_sync();
+    g_put(g, 0, a.v);
+    g_sync();
+    return G12{coef_line(g.k, g_reader(g, 0), L0, L2, L3)};
+}
+__device__ inline G12 g_cyc_sqr(const GCtx& g, const G12& a) {
+    g_sync();
+    g_put(g, 0, a.v);
+    g_sync();
+    return G12{coef_cyc_sqr(g.k, g_reader(g, 0))};
+}
+__device__ inline G12 g_conj(const GCtx& g, const G12& a) { return G12{(g.k & 1) ? f2_neg(a.v) : a.v}; }
+__device__ inline G12 g_frob(const GCtx& g, const G12& a) { return G12{f2_mul(f2_conj(a.v), w_gamma(g.k))}; }
+__device__ inline G12 g_one(const GCtx& g) { return G12{g.k == 0 ? f2_one() : f2_zero()}; }
+__device__ inline fp12 g_gather(const GCtx& g, const G12& a) {
+    g_sync();
+    g_put(g, 0, a.v);
+    g_sync();
+    const GRead rd = g_reader(g, 0);
+    fp12 f;
+    for (int k = 0; k < 6; k++) w_slot(f, k) = rd(k);
+    return f;
+}
+__device__ inline G12 g_scatter(const GCtx& g, const fp12& f) {
+    fp2 r = f.c0.c0;  // a select chain: no dynamically indexed private array
+    if (g.k == 1) r = f.c1.c0;
+    if (g.k == 2) r = f.c0.c1;
+    if (g.k == 3) r = f.c1.c1;
+    if (g.k == 4) r = f.c0.c2;
+    if (g.k == 5) r = f.c1.c2;
+    return G12{r};
+}
+// every lane of the group: a == 1
+__device__ inline bool g_is_one(const GCtx& g, const G12& a) {
+    const bool ok = g.k == 0 ? f2_eq(a.v, f2_one()) : f2_is_zero(a.v);
+    const uint64_t bad = __ballot(!ok);
+    const int first = (int)(threadIdx.x & 63) & ~(GRP - 1);
+    return ((bad >> first) & 0x3fu) == 0;
+}
+// the group's element to / from memory in W order (6 x F2W words); lanes 6, 7 do not store
+__device__ inline void g_store(const GCtx& g, uint32_t* o, const G12& a) {
+    if (g.slot < 6) st_f2(o + g.k * F2W, a.v);
+}
+__device__ inline G12 g_load(const GCtx& g, const uint32_t* o) { return G12{ld_f2(o + g.k * F2W)}; }
+
+#else  // host form: all six coefficients, the same per-coefficient code
+
+struct GCtx {};
+struct G12 {
+    fp2 v[6];
+};
+struct HRead {
+    const fp2* v;
+    fp2 operator()(int i) const { return v[i]; }
+};
+inline G12 g_mul(const GCtx&, const G12& a, const G12& b) {
+    G12 c;
+    for (int k = 0; k < 6; k++) c.v[k] = coef_mul(k, HRead{a.v}, HRead{b.v});
+    return c;
+}
+inline G12 g_sqr(const GCtx& g, const G12& a) { return g_mul(g, a, a); }
+inline G12 g_mul_line(const GCtx&, const G12& a, const fp2& L0, const fp2& L2, const fp2& L3) {
+    G12 c;
+    for (int k = 0; k < 6; k++) c.v[k] = coef_line(k, HRead{a.v}, L0, L2, L3);
+    return c;
+}
+inline G12 g_cyc_sqr(const GCtx&, const G12& a) {
+    G12 c;
+    for (int k = 0; k < 6; k++) c.v[k] = coef_cyc_sqr(k, HRead{a.v});
+    return c;
+}
+inline G12 g_conj(const GCtx&, const G12& a) {
+    G12 c = a;
+    for (int k = 1; k < 6; k += 2) c.v[k] = f2_neg(a.v[k]);
+    return c;
+}
+inline G12 g_frob(const GCtx&, const G12& a) {
+    G12 c;
+    for (int k = 0; k < 6; k++) c.v[k] = f2_mul(f2_conj(a.v[k]), w_gamma(k));
+    return c;
+}
+inline G12 g_one(const GCtx&) {
+    G12 c;
+    for (int k = 0; k < 6; k++) c.v[k] = k == 0 ? f2_one() : f2_zero();
+    return c;
+}
+inline fp12 g_gather(const GCtx&, const G12& a) {
+    fp12 f;
+    for (int k = 0; k < 6; k++) w_slot(f, k) = a.v[k];
+    return f;
+}
+inline G12 g_scatter(const GCtx&, const fp12& f) {
+    fp12 t = f;
+    G12 c;
+    for (int k = 0; k < 6; k++) c.v[k] = w_slot(t, k);
+    return c;
+}
+inline bool g_is_one(const GCtx&, const G12& a) {
+    bool ok = f2_eq(a.v[0], f2_one());
+    for (int k = 1; k < 6; k++) ok = ok && f2_is_zero(a.v[k]);
+    return ok;
+}
+inline void g_store(const GCtx&, uint32_t* o, const G12& a) {
+    for (int k = 0; k < 6; k++) st_f2(o + k * F2W, a.v[k]);
+}
+inline G12 g_load(const GCtx&, const uint32_t* o) {
+    G12 c;
+    for (int k = 0; k < 6; k++) c.v[k] = ld_f2(o + k * F2W);
+    return c;
+}
+
+#endif
+
+// ---- pairing building blocks over a group ---------------------------------------------------
+// device-only in the lane-group form (they use LDS and the lane id), plain host code in the
+// CPU test build
+#ifdef BLS_GDEV
+#define G_HD __device__ inline
+#define G_NOINLINE __device__ __attribute__((noinline))
+#else
+#define G_HD inline
+#define G_NOINLINE __attribute__((noinline))
+#endif
+G_HD G12 g_inv(const GCtx& g, const G12& a) { return g_scatter(g, f12_inv(g_gather(g, a))); }
+
+// prod_{i < n} f_{|x|, Q_i}(P_i), conjugated (x < 0); n <= 2 (miller_loop2 over a group)
+G_NOINLINE G12 g_miller(const GCtx& g, int n, const fp* px, const fp* py, const fp2* qx, const fp2* qy) {
+    jac<fp2> T[2];
+    for (int i = 0; i < n; i++) T[i] = jac_from_affine(qx[i], qy[i]);
+    G12 f = g_one(g);
+    fp2 l0, l1, l4;
+#pragma unroll 1
+    for (int b = 62; b >= 0; b--) {
+        if (b != 62) f = g_sqr(g, f);
+#pragma unroll 1
+        for (int i = 0; i < n; i++) {
+            ml_dbl(T[i], l0, l1, l4);
+            f = g_mul_line(g, f, l0, f2_mul_fp(l1, px[i]), f2_mul_fp(l4, py[i]));
+        }
+        if ((BLS_X_ABS >> b) & 1) {
+#pragma unroll 1
+            for (int i = 0; i < n; i++) {
+                ml_add(T[i], qx[i], qy[i], l0, l1, l4);
+                f = g_mul_line(g, f, l0, f2_mul_fp(l1, px[i]), f2_mul_fp(l4, py[i]));
+            }
+        }
+    }
+    return g_conj(g, f);
+}
+
+// f^x (x = -BLS_X_ABS) for f in the cyclotomic subgroup
+G_NOINLINE G12 g_cyc_exp_x(const GCtx& g, const G12& f) {
+    G12 acc = f;
+#pragma unroll 1
+    for (int b = 62; b >= 0; b--) {
+        acc = g_cyc_sqr(g, acc);
+        if ((BLS_X_ABS >> b) & 1) acc = g_mul(g, acc, f);
+    }
+    return g_conj(g, acc);
+}
+
+// f^(3 (p^12 - 1) / r): final_exp of bls381.h over a group
+G_NOINLINE G12 g_final_exp(const GCtx& g, const G12& f) {
+    G12 m = g_mul(g, g_conj(g, f), g_inv(g, f));  // f^(p^6 - 1)
+    m = g_mul(g, g_frob(g, g_frob(g, m)), m);      // ^(p^2 + 1)
+    G12 a = g_mul(g, g_cyc_exp_x(g, m), g_conj(g, m));
+    a = g_mul(g, g_cyc_exp_x(g, a), g_conj(g, a));
+    const G12 b = g_mul(g, g_cyc_exp_x(g, a), g_frob(g, a));
+    G12 c = g_cyc_exp_x(g, g_cyc_exp_x(g, b));
+    c = g_mul(g, g_mul(g, c, g_frob(g, g_frob(g, b))), g_conj(g, b));
+    return g_mul(g, c, g_mul(g, g_cyc_sqr(g, m), m));
+}
+
+}  // namespace bls

@@ -8,7 +8,7 @@
 // (Header::verify :179-182, Vote::verify :325-327) is the one-key case.  Status codes are the
 // oracle's (oracle/bls_oracle.h ORB_*), checked in its order.
 #pragma once
-#include "bls381.h"
+#include "bls_group.h"
 
 namespace bls {
 
@@ -16,8 +16,6 @@ namespace bls {
 constexpr int G1_REC_WORDS = 2 * NL + 1;   // x, y, flags (bit 0 = identity)
 constexpr int G2_REC_WORDS = 4 * NL + 1;   // x.c0, x.c1, y.c0, y.c1, flags
 
-NWV_HD void st_fp(uint32_t* o, const fp& a) { for (int j = 0; j < NL; j++) o[j] = a.l[j]; }
-NWV_HD fp ld_fp(const uint32_t* o) { fp a; for (int j = 0; j < NL; j++) a.l[j] = o[j]; return a; }
 NWV_HD void st_g1(uint32_t* o, const fp& x, const fp& y, bool inf) {
     st_fp(o, x);
     st_fp(o + NL, y);
@@ -211,6 +209,109 @@ NWV_HD bool rlc_final(const uint32_t* f_rec, const uint32_t* s_rec) {
         f = f12_mul(f, miller_loop2(1, &px, &py, &qx, &qy));
     }
     return f12_is_one(final_exp(f));
+}
+
+// ---- the same checks over a group of lanes (bls_group.h): what the kernels run --------------
+// e(-sig, g2) e(H, apk) == 1 (pairing_check), every lane of the group gets the verdict
+G_HD bool g_pairing_check(const GCtx& g, const uint32_t* sig_rec, const uint32_t* h_rec, const uint32_t* apk_rec) {
+    fp px[2], py[2];
+    fp2 qx[2], qy[2];
+    int n = 0;
+    if (!sig_rec[2 * NL]) {
+        px[n] = ld_fp(sig_rec);
+        py[n] = fp_neg(ld_fp(sig_rec + NL));
+        qx[n] = k_g2x();
+        qy[n] = k_g2y();
+        n++;
+    }
+    if (!h_rec[2 * NL]) {
+        px[n] = ld_fp(h_rec);
+        py[n] = ld_fp(h_rec + NL);
+        ld_g2(apk_rec, qx[n], qy[n]);
+        n++;
+    }
+    return g_is_one(g, g_final_exp(g, g_miller(g, n, px, py, qx, qy)));
+}
+
+// item i's share of the batch check (rlc_item) with its Fp12 stored in W order (6 x F2W words).
+// On the GPU the two scalar multiplications run side by side: lanes 0-3 of the group take
+// [r] H, lanes 4-7 [r] sig; lane 0 hands [r] H (affine) to the group through its LDS area and
+// lane 4 stores [r] sig.
+G_HD void g_rlc_item(const GCtx& g, const uint32_t* sig_rec, const uint32_t* h_rec, const uint32_t* apk_rec,
+                       uint64_t r, uint32_t* f_out, uint32_t* s_out) {
+    jac<fp> inf;
+    inf.inf = true;
+    inf.x = inf.y = inf.z = fp_zero();
+#ifdef BLS_GDEV
+    const bool sig_lane = (g.slot & 4) != 0;
+    const uint32_t* src = sig_lane ? sig_rec : h_rec;
+    jac<fp> m = inf;
+    if (!src[2 * NL]) m = jac_mul64(jac_from_affine(ld_fp(src), ld_fp(src + NL)), r);
+    if (g.slot == 4) st_g1j(s_out, m);
+    fp hx = fp_zero(), hy = fp_zero();
+    if (!m.inf) g1_to_affine(hx, hy, m);
+    g_sync();
+    if (g.slot == 0) {
+        st_fp(g.xa, hx);
+        st_fp(g.xa + NL, hy);
+        g.xa[2 * NL] = m.inf ? 1u : 0u;
+    }
+    g_sync();
+    const bool h_inf = g.xa[2 * NL] != 0;
+    const fp px = ld_fp(g.xa), py = ld_fp(g.xa + NL);
+#else
+    jac<fp> s = inf, h = inf;
+    if (!sig_rec[2 * NL]) s = jac_mul64(jac_from_affine(ld_fp(sig_rec), ld_fp(sig_rec + NL)), r);
+    if (!h_rec[2 * NL]) h = jac_mul64(jac_from_affine(ld_fp(h_rec), ld_fp(h_rec + NL)), r);
+    st_g1j(s_out, s);
+    fp px = fp_zero(), py = fp_zero();
+    if (!h.inf) g1_to_affine(px, py, h);
+    const bool h_inf = h.inf;
+#endif
+    G12 f = g_one(g);
+    if (!h_inf) {
+        fp2 qx, qy;
+        ld_g2(apk_rec, qx, qy);
+        f = g_miller(g, 1, &px, &py, &qx, &qy);
+    }
+    g_store(g, f_out, f);
+}
+// (f_a, s_a) <- (f_a f_b, s_a + s_b); the G1 sum on every lane, stored by lane 0
+G_HD void g_rlc_fold(const GCtx& g, uint32_t* fa, uint32_t* sa, const uint32_t* fb, const uint32_t* sb) {
+    const G12 f = g_mul(g, g_load(g, fa), g_load(g, fb));
+    const jac<fp> s = jac_add(ld_g1j(sa), ld_g1j(sb));
+#ifdef BLS_GDEV
+    g_sync();  // every lane has read sa before it is overwritten
+    if (g.slot == 0) st_g1j(sa, s);
+#else
+    st_g1j(sa, s);
+#endif
+    g_store(g, fa, f);
+}
+// the batch verdict: FE(f * ML(-S, g2)) == 1
+G_HD bool g_rlc_final(const GCtx& g, const uint32_t* f_rec, const uint32_t* s_rec) {
+    G12 f = g_load(g, f_rec);
+    const jac<fp> S = ld_g1j(s_rec);
+    if (!S.inf) {
+        fp px, py;
+        g1_to_affine(px, py, S);
+        py = fp_neg(py);
+        const fp2 qx = k_g2x(), qy = k_g2y();
+        f = g_mul(g, f, g_miller(g, 1, &px, &py, &qx, &qy));
+    }
+    return g_is_one(g, g_final_exp(g, f));
+}
+// an item outside the batch: the neutral share
+G_HD void g_rlc_neutral(const GCtx& g, uint32_t* f_out, uint32_t* s_out) {
+    g_store(g, f_out, g_one(g));
+    jac<fp> s;
+    s.inf = true;
+    s.x = s.y = s.z = fp_zero();
+#ifdef BLS_GDEV
+    if (g.slot == 0) st_g1j(s_out, s);
+#else
+    st_g1j(s_out, s);
+#endif
 }
 
 }  // namespace bls

@@ -1,11 +1,14 @@
 // nwv_bls.hip -- BLS12-381 min_sig verification engine on gfx950: the
 // kernels over bls_verify.h and the C ABI of include/nwv_bls.h.
 //
-// A call stages its inputs in one pinned arena and one H2D copy, then runs
-//   k_bls_keys   one lane per distinct public key: decode + G2 membership (psi(Q) = [x] Q)
-//   k_bls_sigs   one lane per item: decode + G1 membership (phi(P) = [-x^2] P)
-//   k_bls_h2c    one lane per item: H(msg) (RFC 9380 hash_to_curve G1)
-//   k_bls_apk    one lane per item: the sum of the item's validated keys, affine
+// A call stages its inputs in one pinned arena and one H2D copy, then runs on three streams
+//   k_bls_keys_fill  one lane per key the device's key cache has not seen: decode + G2 membership
+//                    (psi(Q) = [x] Q), into the cache (fastcrypto validates a key once, at
+//                    deserialization); then k_bls_apk_g, one 8-lane group per item: the sum of the
+//                    item's keys (eight partial sums and a tree), its first bad key's status
+//   k_bls_sigs       one lane per item: decode + G1 membership (phi(P) = [-x^2] P)
+//   k_bls_h2c        one lane per item: H(msg) (RFC 9380 hash_to_curve G1)
+// joined by k_bls_status (the statuses in the oracle's order), then
 //   the pairing check, by default as ONE batch check over the call (bls_verify.h):
 //     k_bls_rlc    one lane per item: [r_i] H_i, [r_i] sig_i, the Miller loop of ([r_i] H_i, apk_i)
 //     k_bls_fold   ceil(log2 n) levels of a product tree (Fp12 products, G1 sums)
@@ -20,6 +23,7 @@
 #include <cstring>
 #include <functional>
 #include <mutex>
+#include <string>
 #include <unordered_map>
 #include <vector>
 
@@ -40,9 +44,12 @@ __attribute__((visibility("hidden"))) void nwv_internal_fill_seed(const uint8_t*
 #define BLS_IDX() const uint32_t i = blockIdx.x * BLS_LANES + threadIdx.x; \
     if (i >= n) return
 
-__global__ __launch_bounds__(BLS_LANES) void k_bls_keys(uint32_t n, const uint8_t* pk, uint32_t* rec, int32_t* st) {
+// decode + check the keys a call adds to the key cache: key j of the list goes to cache slot slot[j]
+__global__ __launch_bounds__(BLS_LANES) void k_bls_keys_fill(uint32_t n, const uint8_t* pk, const uint32_t* slot,
+                                                             uint32_t* rec, int32_t* st) {
     BLS_IDX();
-    st[i] = key_decode(pk + 96 * (size_t)i, rec + (size_t)G2_REC_WORDS * i);
+    const uint32_t k = slot[i];
+    st[k] = key_decode(pk + 96 * (size_t)i, rec + (size_t)G2_REC_WORDS * k);
 }
 __global__ __launch_bounds__(BLS_LANES) void k_bls_sigs(uint32_t n, const uint8_t* sig, uint32_t* rec, int32_t* st) {
     BLS_IDX();
@@ -55,47 +62,131 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_h2c(uint32_t n, const uint8_t
     if (st && st[i] != ST_OK) return;
     h2c_record(msg + off[i], len[i], dst, dl, rec + (size_t)G1_REC_WORDS * i);
 }
-__global__ __launch_bounds__(BLS_LANES) void k_bls_apk(uint32_t n, const uint32_t* key_rec, const int32_t* key_st,
-                                                       const uint32_t* pk_off, const uint32_t* pk_cnt,
-                                                       const uint32_t* pk_idx, uint32_t* rec, int32_t* st) {
+// the pairing kernels run one item per GROUP of 8 lanes (bls_group.h): 8 items per 64-lane block
+#define BLS_GIDX()                                                                  \
+    __shared__ uint32_t g_lds[(BLS_LANES / GRP) * GX_WORDS];                       \
+    const GCtx g = g_ctx(g_lds);                                                    \
+    const uint32_t i = blockIdx.x * (BLS_LANES / GRP) + threadIdx.x / GRP;          \
+    if (i >= n) return
+
+// the key sum of item i over a group: lane s adds the item's keys s, s + 8, ... (apk_record's
+// formulas), the eight partial sums meet in a three-level tree through the group's LDS area, and
+// the status is that of the item's FIRST bad key in list order (apk_record's), else identity ->
+// PK_INFINITY.  st_apk[i] = the item's key status (the signature's status is combined later).
+constexpr int G2J_WORDS = 6 * NL + 1;  // Jacobian X, Y, Z (Fp2 each), identity flag
+__device__ void st_g2j(uint32_t* o, const jac<fp2>& p) {
+    st_f2(o, p.x);
+    st_f2(o + F2W, p.y);
+    st_f2(o + 2 * F2W, p.z);
+    o[3 * F2W] = p.inf ? 1u : 0u;
+}
+__device__ jac<fp2> ld_g2j(const uint32_t* o) {
+    jac<fp2> p;
+    p.x = ld_f2(o);
+    p.y = ld_f2(o + F2W);
+    p.z = ld_f2(o + 2 * F2W);
+    p.inf = o[3 * F2W] != 0;
+    return p;
+}
+static_assert(4 * G2J_WORDS + 8 <= GX_WORDS, "the tree's first level fits a group's LDS area");
+__global__ __launch_bounds__(BLS_LANES) void k_bls_apk_g(uint32_t n, const uint32_t* key_rec, const int32_t* key_st,
+                                                         const uint32_t* pk_off, const uint32_t* pk_cnt,
+                                                         const uint32_t* pk_idx, uint32_t* rec, int32_t* st_apk) {
+    BLS_GIDX();
+    const uint32_t cnt = pk_cnt[i];
+    const uint32_t* idx = pk_idx + pk_off[i];
+    uint32_t* out = rec + (size_t)G2_REC_WORDS * i;
+    jac<fp2> acc;
+    acc.inf = true;
+    acc.x = acc.y = acc.z = f2_zero();
+    uint32_t first_bad = 0xffffffffu;
+    for (uint32_t j = (uint32_t)g.slot; j < cnt; j += GRP) {
+        const uint32_t k = idx[j];
+        if (key_st[k] != ST_OK) {
+            first_bad = j;
+            break;
+        }
+        fp2 x, y;
+        ld_g2(key_rec + (size_t)k * G2_REC_WORDS, x, y);
+        acc = jac_add(acc, jac_from_affine(x, y));
+    }
+    // the group's first bad position, and the tree over the partial sums
+    uint32_t* xa = g.xa;
+    g_sync();
+    xa[4 * G2J_WORDS + g.slot] = first_bad;
+#pragma unroll 1
+    for (int h = GRP / 2; h >= 1; h /= 2) {
+        g_sync();
+        if (g.slot >= h && g.slot < 2 * h) st_g2j(xa + (g.slot - h) * G2J_WORDS, acc);
+        g_sync();
+        if (g.slot < h) acc = jac_add(acc, ld_g2j(xa + g.slot * G2J_WORDS));
+    }
+    g_sync();
+    uint32_t fb = 0xffffffffu;
+    for (int s2 = 0; s2 < GRP; s2++) fb = min(fb, xa[4 * G2J_WORDS + s2]);
+    if (g.slot != 0) return;
+    int32_t status;
+    fp2 x = f2_zero(), y = f2_zero();
+    bool inf = true;
+    if (cnt == 0) {
+        status = ST_AGGR_MISMATCH;
+    } else if (fb != 0xffffffffu) {
+        status = key_st[idx[fb]];
+    } else {
+        if (!acc.inf) g2_to_affine(x, y, acc);
+        inf = acc.inf;
+        status = acc.inf ? ST_PK_INFINITY : ST_OK;
+    }
+    if (status != ST_OK) {
+        x = y = f2_zero();
+        inf = true;
+    }
+    st_g2(out, x, y, inf);
+    st_apk[i] = status;
+}
+// the item's status in the oracle's order: the signature's, then the keys'
+__global__ __launch_bounds__(BLS_LANES) void k_bls_status(uint32_t n, const int32_t* st_sig, const int32_t* st_apk,
+                                                          int32_t* st) {
     BLS_IDX();
-    if (st[i] != ST_OK) return;
-    st[i] = apk_record(key_rec, key_st, pk_idx + pk_off[i], pk_cnt[i], rec + (size_t)G2_REC_WORDS * i);
+    st[i] = st_sig[i] != ST_OK ? st_sig[i] : st_apk[i];
 }
 __global__ __launch_bounds__(BLS_LANES) void k_bls_pair(uint32_t n, const uint32_t* sig_rec, const uint32_t* h_rec,
                                                         const uint32_t* apk_rec, int32_t* st) {
-    BLS_IDX();
-    if (st[i] != ST_OK) return;
-    st[i] = pairing_check(sig_rec + (size_t)G1_REC_WORDS * i, h_rec + (size_t)G1_REC_WORDS * i,
-                          apk_rec + (size_t)G2_REC_WORDS * i)
-                ? ST_OK
-                : ST_VERIFY_FAIL;
+    BLS_GIDX();
+    if (st[i] != ST_OK) return;  // uniform over the group
+    const bool ok = g_pairing_check(g, sig_rec + (size_t)G1_REC_WORDS * i, h_rec + (size_t)G1_REC_WORDS * i,
+                                    apk_rec + (size_t)G2_REC_WORDS * i);
+    g_sync();
+    if (g.slot == 0) st[i] = ok ? ST_OK : ST_VERIFY_FAIL;
 }
-// the batch check (bls_verify.h): every item's share, then a product tree, then one lane's final
+// the batch check (bls_verify.h): every item's share, then a product tree, then one group's final
 __global__ __launch_bounds__(BLS_LANES) void k_bls_rlc(uint32_t n, const uint32_t* sig_rec, const uint32_t* h_rec,
                                                        const uint32_t* apk_rec, const int32_t* st,
                                                        const uint8_t* seed, uint32_t* frec, uint32_t* srec) {
-    BLS_IDX();
+    BLS_GIDX();
     uint32_t* f = frec + (size_t)F12_REC_WORDS * i;
     uint32_t* s = srec + (size_t)G1J_REC_WORDS * i;
     if (st[i] != ST_OK) {
-        rlc_neutral(f, s);
+        g_rlc_neutral(g, f, s);
         return;
     }
-    rlc_item(sig_rec + (size_t)G1_REC_WORDS * i, h_rec + (size_t)G1_REC_WORDS * i, apk_rec + (size_t)G2_REC_WORDS * i,
-             rlc_scalar(seed, i), f, s);
+    g_rlc_item(g, sig_rec + (size_t)G1_REC_WORDS * i, h_rec + (size_t)G1_REC_WORDS * i, apk_rec + (size_t)G2_REC_WORDS * i,
+               rlc_scalar(seed, i), f, s);
 }
 // one level of the tree over m shares: share j <- share j (+) share j + h, h = ceil(m / 2), j < m - h
 __global__ __launch_bounds__(BLS_LANES) void k_bls_fold(uint32_t m, uint32_t* frec, uint32_t* srec) {
     const uint32_t h = (m + 1) / 2;
     const uint32_t n = m - h;
-    BLS_IDX();
-    rlc_fold(frec + (size_t)F12_REC_WORDS * i, srec + (size_t)G1J_REC_WORDS * i,
-             frec + (size_t)F12_REC_WORDS * (i + h), srec + (size_t)G1J_REC_WORDS * (i + h));
+    BLS_GIDX();
+    g_rlc_fold(g, frec + (size_t)F12_REC_WORDS * i, srec + (size_t)G1J_REC_WORDS * i,
+               frec + (size_t)F12_REC_WORDS * (i + h), srec + (size_t)G1J_REC_WORDS * (i + h));
 }
-__global__ void k_bls_final(const uint32_t* frec, const uint32_t* srec, int32_t* ok) {
-    if (blockIdx.x || threadIdx.x) return;
-    *ok = rlc_final(frec, srec) ? 1 : 0;
+__global__ __launch_bounds__(BLS_LANES) void k_bls_final(const uint32_t* frec, const uint32_t* srec, int32_t* ok) {
+    const uint32_t n = 1;
+    BLS_GIDX();
+    const bool r = g_rlc_final(g, frec, srec);
+    g_sync();
+    if (g.slot == 0) *ok = r ? 1 : 0;
 }
 // sum of n decoded signatures (AggregateAuthenticator::aggregate), one lane
 __global__ void k_bls_g1_sum(uint32_t n, const uint32_t* rec, const int32_t* st, uint8_t* out48, int32_t* out_st) {
@@ -220,20 +311,40 @@ struct HBuf {
     }
 };
 
-// one device of a context: a stream and reusable staging / scratch buffers (one call at a time)
+// the committee key cache of a device: fastcrypto validates a BLS public key once, when it is
+// deserialized; here a key is decoded and subgroup-checked the first time a call names it, and its
+// record (or its failure status) is kept for every later call.  Full -> calls decode uncached.
+struct BlsKeyCache {
+    static constexpr uint32_t CAP = 65536;
+    DBuf rec, st;  // CAP x G2_REC_WORDS u32 records, CAP int32 statuses
+    std::unordered_map<std::string, uint32_t> slot;
+    uint32_t used = 0;
+    void clear() {
+        slot.clear();
+        used = 0;
+    }
+};
+
+// one device of a context: streams and reusable staging / scratch buffers (one call at a time)
 struct BlsDev {
     int ordinal = -1;
     uint32_t flags = 0;  // the context's nwv_init flags
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;        // H2D, signatures, pairing check, D2H
+    hipStream_t side[2] = {nullptr, nullptr};  // keys + key sums; hash to G1
     std::mutex mu;
     HBuf stage;
     DBuf in, work;
-    hipEvent_t ev[6] = {};       // around the five stages of the last verify_many call
+    BlsKeyCache kc;
+    // [0,1] keys, [1,2] key sums (side 0); [3,4] signatures (main); [5,6] hash to G1 (side 1);
+    // [7,8] pairing check (main); [9] inputs resident, [10] side 0 done, [11] side 1 done
+    hipEvent_t ev[12] = {};
     double last_ms[5] = {0, 0, 0, 0, 0};
-    int last_path = 0;           // nwv_bls_last_path
+    int last_path = 0;  // nwv_bls_last_path
     ~BlsDev() {
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
+        for (auto& t : side)
+            if (t) (void)hipStreamDestroy(t);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -253,7 +364,9 @@ int dev_of(nwv_ctx* ctx, BlsDev** out) {
     auto* d = new BlsDev;
     d->ordinal = ord;
     d->flags = nwv_internal_ctx_flags(ctx);
-    if (hipSetDevice(ord) != hipSuccess || hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(ord) != hipSuccess || hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&d->side[0], hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&d->side[1], hipStreamNonBlocking) != hipSuccess) {
         delete d;
         return nwv_internal_set_err(NWV_ERR_HIP, "bls stream");
     }
@@ -277,8 +390,14 @@ struct Arena {
 };
 
 constexpr int kBlocks(size_t n) { return (int)((n + BLS_LANES - 1) / BLS_LANES); }
+// blocks of the group kernels: 8 items per 64-lane block
+constexpr int gBlocks(size_t n) { return (int)((n + BLS_LANES / GRP - 1) / (BLS_LANES / GRP)); }
 
-// the whole verify_many pipeline on one device
+// the whole verify_many pipeline on one device: after one H2D copy, three streams --
+//   side 0: the call's new keys into the key cache (k_bls_keys_fill), then the key sums (k_bls_apk_g)
+//   main  : signature decode + G1 checks (k_bls_sigs)
+//   side 1: hash to G1 (k_bls_h2c)
+// -- then, joined on the main stream, the statuses in the oracle's order and the pairing check
 int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uint8_t* sigs, const uint32_t* pk_off,
               const uint32_t* pk_cnt, const uint32_t* pk_idx, size_t n_idx, const uint8_t* msg_base,
               const uint64_t* msg_off, const uint32_t* msg_len, size_t msg_bytes, const uint8_t* dst, size_t dl,
@@ -287,73 +406,150 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     BLS_HIP(hipSetDevice(d.ordinal));
     static const uint8_t zero[8] = {0};
     const bool batch = !(d.flags & NWV_FLAG_BLS_PER_ITEM);
+    int rc;
+    // key slots: the cache's, or (cache off / full) a per-call table in the scratch
+    bool cached = !(d.flags & NWV_FLAG_NO_KEYCACHE);
+    std::vector<uint32_t> kslot(n_keys), fill_slot;
+    std::vector<uint8_t> fill_keys;
+    if (cached) {
+        if ((rc = d.kc.rec.ensure((size_t)4 * G2_REC_WORDS * BlsKeyCache::CAP)) ||
+            (rc = d.kc.st.ensure((size_t)4 * BlsKeyCache::CAP)))
+            return rc;
+        std::unordered_map<std::string, uint32_t> fresh;
+        for (size_t j = 0; j < n_keys && cached; j++) {
+            std::string kb(reinterpret_cast<const char*>(keys + 96 * j), 96);
+            auto it = d.kc.slot.find(kb);
+            if (it != d.kc.slot.end()) {
+                kslot[j] = it->second;
+                continue;
+            }
+            auto f = fresh.find(kb);
+            if (f != fresh.end()) {
+                kslot[j] = f->second;
+                continue;
+            }
+            if (d.kc.used + fresh.size() >= BlsKeyCache::CAP) {
+                cached = false;
+                break;
+            }
+            const uint32_t sl = d.kc.used + (uint32_t)fresh.size();
+            fresh.emplace(std::move(kb), sl);
+            kslot[j] = sl;
+            fill_slot.push_back(sl);
+            fill_keys.insert(fill_keys.end(), keys + 96 * j, keys + 96 * (j + 1));
+        }
+        if (cached) {
+            for (auto& kv : fresh) d.kc.slot.emplace(kv.first, kv.second);
+            d.kc.used += (uint32_t)fresh.size();
+        } else {
+            fill_slot.clear();
+            fill_keys.clear();
+        }
+    }
+    std::vector<uint32_t> remap;
+    const uint32_t* idx_src = pk_idx;
+    if (cached && n_idx) {
+        remap.resize(n_idx);
+        for (size_t t = 0; t < n_idx; t++) remap[t] = kslot[pk_idx[t]];
+        idx_src = remap.data();
+    }
+    const size_t n_dec = cached ? fill_slot.size() : n_keys;  // keys decoded by this call
+    if (!cached) {
+        fill_slot.resize(n_keys);
+        for (size_t j = 0; j < n_keys; j++) fill_slot[j] = (uint32_t)j;
+    }
     uint8_t seed[32];
     nwv_internal_fill_seed(nullptr, seed);  // the batch coefficients' key: OS entropy per call
     Arena a;
-    const size_t o_keys = a.add(keys, 96 * n_keys), o_sigs = a.add(sigs, 48 * n), o_off = a.add(pk_off, 4 * n),
-                 o_cnt = a.add(pk_cnt, 4 * n), o_idx = a.add(n_idx ? (const void*)pk_idx : zero, 4 * n_idx + 4),
+    const size_t o_keys = a.add(cached ? (n_dec ? (const void*)fill_keys.data() : zero) : (const void*)keys,
+                                cached ? 96 * n_dec + 8 : 96 * n_keys),
+                 o_kslot = a.add(n_dec ? (const void*)fill_slot.data() : zero, 4 * n_dec + 4),
+                 o_sigs = a.add(sigs, 48 * n), o_off = a.add(pk_off, 4 * n), o_cnt = a.add(pk_cnt, 4 * n),
+                 o_idx = a.add(n_idx ? (const void*)idx_src : zero, 4 * n_idx + 4),
                  o_msg = a.add(msg_bytes ? (const void*)msg_base : zero, msg_bytes + 1),
                  o_moff = a.add(msg_off, 8 * n), o_mlen = a.add(msg_len, 4 * n), o_dst = a.add(dst, dl),
                  o_seed = a.add(seed, 32);
-    int rc;
-    if ((rc = d.stage.ensure(((a.total + 255) & ~(size_t)255) + 64)) || (rc = d.in.ensure(a.total))) return rc;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    if ((rc = d.stage.ensure(al(a.total) + 64)) || (rc = d.in.ensure(a.total))) return rc;
     uint8_t* h = static_cast<uint8_t*>(d.stage.p);
     for (size_t k = 0; k < a.parts.size(); k++)
         if (a.parts[k].second) std::memcpy(h + a.offs[k], a.parts[k].first, a.parts[k].second);
-    // scratch: key records + statuses, item sig / H / apk records, item statuses, the batch
-    // check's shares (Fp12 + Jacobian G1 per item) and its verdict word
-    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t w_krec = 0, w_kst = w_krec + 4 * G2_REC_WORDS * n_keys, w_srec = al(w_kst + 4 * n_keys),
-                 w_hrec = w_srec + 4 * G1_REC_WORDS * n, w_arec = w_hrec + 4 * G1_REC_WORDS * n,
-                 w_st = w_arec + 4 * G2_REC_WORDS * n, w_ok = al(w_st + 4 * n), w_frec = al(w_ok + 4),
-                 w_jrec = al(w_frec + 4 * F12_REC_WORDS * (batch ? n : 0)),
+    // scratch: (uncached) key records + statuses, item sig / H / apk records, three status arrays,
+    // the batch check's shares (W-order Fp12 + Jacobian G1 per item) and its verdict word
+    const size_t w_krec = 0, w_kst = w_krec + (cached ? 0 : 4 * G2_REC_WORDS * n_keys),
+                 w_srec = al(w_kst + (cached ? 0 : 4 * n_keys)), w_hrec = w_srec + 4 * G1_REC_WORDS * n,
+                 w_arec = w_hrec + 4 * G1_REC_WORDS * n, w_st = w_arec + 4 * G2_REC_WORDS * n,
+                 w_ssig = al(w_st + 4 * n), w_sapk = al(w_ssig + 4 * n), w_ok = al(w_sapk + 4 * n),
+                 w_frec = al(w_ok + 4), w_jrec = al(w_frec + 4 * F12_REC_WORDS * (batch ? n : 0)),
                  w_end = w_jrec + 4 * G1J_REC_WORDS * (batch ? n : 0) + 4;
     if ((rc = d.work.ensure(w_end))) return rc;
     uint8_t* in = static_cast<uint8_t*>(d.in.p);
     uint8_t* w = static_cast<uint8_t*>(d.work.p);
-    BLS_HIP(hipMemcpyAsync(in, h, a.total, hipMemcpyHostToDevice, d.stream));
-    auto* krec = reinterpret_cast<uint32_t*>(w + w_krec);
-    auto* kst = reinterpret_cast<int32_t*>(w + w_kst);
+    auto* krec = cached ? static_cast<uint32_t*>(d.kc.rec.p) : reinterpret_cast<uint32_t*>(w + w_krec);
+    auto* kst = cached ? static_cast<int32_t*>(d.kc.st.p) : reinterpret_cast<int32_t*>(w + w_kst);
     auto* srec = reinterpret_cast<uint32_t*>(w + w_srec);
     auto* hrec = reinterpret_cast<uint32_t*>(w + w_hrec);
     auto* arec = reinterpret_cast<uint32_t*>(w + w_arec);
     auto* st = reinterpret_cast<int32_t*>(w + w_st);
+    auto* ssig = reinterpret_cast<int32_t*>(w + w_ssig);
+    auto* sapk = reinterpret_cast<int32_t*>(w + w_sapk);
     auto* okw = reinterpret_cast<int32_t*>(w + w_ok);
     auto* frec = reinterpret_cast<uint32_t*>(w + w_frec);
     auto* jrec = reinterpret_cast<uint32_t*>(w + w_jrec);
     if (!d.ev[0])
         for (auto& e : d.ev) BLS_HIP(hipEventCreate(&e));
-    BLS_HIP(hipEventRecord(d.ev[0], d.stream));
-    if (n_keys)
-        hipLaunchKernelGGL(k_bls_keys, dim3(kBlocks(n_keys)), dim3(BLS_LANES), 0, d.stream, (uint32_t)n_keys,
-                           in + o_keys, krec, kst);
-    BLS_HIP(hipEventRecord(d.ev[1], d.stream));
-    hipLaunchKernelGGL(k_bls_sigs, dim3(kBlocks(n)), dim3(BLS_LANES), 0, d.stream, (uint32_t)n, in + o_sigs, srec, st);
-    BLS_HIP(hipEventRecord(d.ev[2], d.stream));
-    hipLaunchKernelGGL(k_bls_h2c, dim3(kBlocks(n)), dim3(BLS_LANES), 0, d.stream, (uint32_t)n, in + o_msg,
-                       reinterpret_cast<const uint64_t*>(in + o_moff), reinterpret_cast<const uint32_t*>(in + o_mlen),
-                       in + o_dst, (uint32_t)dl, (const int32_t*)st, hrec);
-    BLS_HIP(hipEventRecord(d.ev[3], d.stream));
-    hipLaunchKernelGGL(k_bls_apk, dim3(kBlocks(n)), dim3(BLS_LANES), 0, d.stream, (uint32_t)n, (const uint32_t*)krec,
+    hipStream_t s0 = d.stream, s1 = d.side[0], s2 = d.side[1];
+    BLS_HIP(hipMemcpyAsync(in, h, a.total, hipMemcpyHostToDevice, s0));
+    BLS_HIP(hipEventRecord(d.ev[9], s0));
+    BLS_HIP(hipStreamWaitEvent(s1, d.ev[9], 0));
+    BLS_HIP(hipStreamWaitEvent(s2, d.ev[9], 0));
+    // side 0: keys, key sums
+    BLS_HIP(hipEventRecord(d.ev[0], s1));
+    if (n_dec)
+        hipLaunchKernelGGL(k_bls_keys_fill, dim3(kBlocks(n_dec)), dim3(BLS_LANES), 0, s1, (uint32_t)n_dec, in + o_keys,
+                           reinterpret_cast<const uint32_t*>(in + o_kslot), krec, kst);
+    BLS_HIP(hipEventRecord(d.ev[1], s1));
+    hipLaunchKernelGGL(k_bls_apk_g, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s1, (uint32_t)n, (const uint32_t*)krec,
                        (const int32_t*)kst, reinterpret_cast<const uint32_t*>(in + o_off),
                        reinterpret_cast<const uint32_t*>(in + o_cnt), reinterpret_cast<const uint32_t*>(in + o_idx),
-                       arec, st);
-    BLS_HIP(hipEventRecord(d.ev[4], d.stream));
+                       arec, sapk);
+    BLS_HIP(hipEventRecord(d.ev[2], s1));
+    BLS_HIP(hipEventRecord(d.ev[10], s1));
+    // side 1: hash to G1 (every item: the statuses are not known yet)
+    BLS_HIP(hipEventRecord(d.ev[5], s2));
+    hipLaunchKernelGGL(k_bls_h2c, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s2, (uint32_t)n, in + o_msg,
+                       reinterpret_cast<const uint64_t*>(in + o_moff), reinterpret_cast<const uint32_t*>(in + o_mlen),
+                       in + o_dst, (uint32_t)dl, (const int32_t*)nullptr, hrec);
+    BLS_HIP(hipEventRecord(d.ev[6], s2));
+    BLS_HIP(hipEventRecord(d.ev[11], s2));
+    // main: signatures, then the join
+    BLS_HIP(hipEventRecord(d.ev[3], s0));
+    hipLaunchKernelGGL(k_bls_sigs, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, in + o_sigs, srec, ssig);
+    BLS_HIP(hipEventRecord(d.ev[4], s0));
+    BLS_HIP(hipStreamWaitEvent(s0, d.ev[10], 0));
+    BLS_HIP(hipStreamWaitEvent(s0, d.ev[11], 0));
+    hipLaunchKernelGGL(k_bls_status, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, (const int32_t*)ssig,
+                       (const int32_t*)sapk, st);
+    BLS_HIP(hipEventRecord(d.ev[7], s0));
     auto per_item = [&]() {
-        hipLaunchKernelGGL(k_bls_pair, dim3(kBlocks(n)), dim3(BLS_LANES), 0, d.stream, (uint32_t)n,
-                           (const uint32_t*)srec, (const uint32_t*)hrec, (const uint32_t*)arec, st);
+        hipLaunchKernelGGL(k_bls_pair, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, (const uint32_t*)srec,
+                           (const uint32_t*)hrec, (const uint32_t*)arec, st);
     };
     int32_t* hst = reinterpret_cast<int32_t*>(h + al(a.total));  // pinned: the batch verdict word
     if (batch) {
-        hipLaunchKernelGGL(k_bls_rlc, dim3(kBlocks(n)), dim3(BLS_LANES), 0, d.stream, (uint32_t)n,
-                           (const uint32_t*)srec, (const uint32_t*)hrec, (const uint32_t*)arec, (const int32_t*)st,
+        hipLaunchKernelGGL(k_bls_rlc, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, (const uint32_t*)srec,
+                           (const uint32_t*)hrec, (const uint32_t*)arec, (const int32_t*)st,
                            (const uint8_t*)(in + o_seed), frec, jrec);
         for (uint32_t m = (uint32_t)n; m > 1; m = (m + 1) / 2)
-            hipLaunchKernelGGL(k_bls_fold, dim3(kBlocks(m / 2)), dim3(BLS_LANES), 0, d.stream, m, frec, jrec);
-        hipLaunchKernelGGL(k_bls_final, dim3(1), dim3(BLS_LANES), 0, d.stream, (const uint32_t*)frec,
-                           (const uint32_t*)jrec, okw);
-        BLS_HIP(hipMemcpyAsync(hst, okw, 4, hipMemcpyDeviceToHost, d.stream));
-        BLS_HIP(hipStreamSynchronize(d.stream));
+            hipLaunchKernelGGL(k_bls_fold, dim3(gBlocks(m / 2)), dim3(BLS_LANES), 0, s0, m, frec, jrec);
+        hipLaunchKernelGGL(k_bls_final, dim3(1), dim3(BLS_LANES), 0, s0, (const uint32_t*)frec, (const uint32_t*)jrec,
+                           okw);
+        BLS_HIP(hipMemcpyAsync(hst, okw, 4, hipMemcpyDeviceToHost, s0));
+        const hipError_t e = hipStreamSynchronize(s0);
+        if (e != hipSuccess) {
+            d.kc.clear();  // the fill may not have landed
+            return nwv_internal_set_err(NWV_ERR_HIP, hipGetErrorString(e));
+        }
         BLS_HIP(hipGetLastError());
         d.last_path = *hst == 1 ? 1 : 2;
         if (*hst != 1) per_item();  // the batch check rejected: name the failing items exactly
@@ -361,13 +557,18 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
         per_item();
         d.last_path = 0;
     }
-    BLS_HIP(hipEventRecord(d.ev[5], d.stream));
+    BLS_HIP(hipEventRecord(d.ev[8], s0));
     BLS_HIP(hipGetLastError());
-    BLS_HIP(hipMemcpyAsync(status, st, 4 * n, hipMemcpyDeviceToHost, d.stream));
-    BLS_HIP(hipStreamSynchronize(d.stream));
+    BLS_HIP(hipMemcpyAsync(status, st, 4 * n, hipMemcpyDeviceToHost, s0));
+    const hipError_t e = hipStreamSynchronize(s0);
+    if (e != hipSuccess) {
+        d.kc.clear();
+        return nwv_internal_set_err(NWV_ERR_HIP, hipGetErrorString(e));
+    }
+    const int pairs[5][2] = {{0, 1}, {3, 4}, {5, 6}, {1, 2}, {7, 8}};  // keys, sigs, h2c, apk, pairing
     for (int k = 0; k < 5; k++) {
         float ms = 0;
-        BLS_HIP(hipEventElapsedTime(&ms, d.ev[k], d.ev[k + 1]));
+        BLS_HIP(hipEventElapsedTime(&ms, d.ev[pairs[k][0]], d.ev[pairs[k][1]]));
         d.last_ms[k] = ms;
     }
     return NWV_OK;

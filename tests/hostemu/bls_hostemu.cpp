@@ -3,6 +3,7 @@
 // oracle (oracle/bls_oracle.c), so the device arithmetic is checked before it meets a GPU.
 // Encodings as the oracle's: uncompressed affine big-endian (G1 x||y, G2 x.c1||x.c0||y.c1||y.c0),
 // all-zero = identity; GT as 12 big-endian Fp in tower order.
+#define BLS_GROUP_HOST_EMU 1  // bls_group.h: the host form of the lane-group arithmetic
 #include "../../narwhal_amd/csrc/bls_verify.h"
 
 using namespace bls;
@@ -100,11 +101,51 @@ int bh_fast_aggregate_verify(const uint8_t* sig, size_t n_pks, const uint8_t* pk
     return pairing_check(srec, hrec, arec) ? ST_OK : ST_VERIFY_FAIL;
 }
 
+// e(P, Q) through the group arithmetic (bls_group.h, host form): g_final_exp(g_miller(..)) in the
+// tower order of bh_pairing, so the two must agree bit for bit
+void bh_g_pairing(const uint8_t* P, const uint8_t* Q, uint8_t* out) {
+    fp px, py;
+    fp2 qx, qy;
+    be_to_mont(px, P);
+    be_to_mont(py, P + 48);
+    be_to_mont(qx.c1, Q);
+    be_to_mont(qx.c0, Q + 48);
+    be_to_mont(qy.c1, Q + 96);
+    be_to_mont(qy.c0, Q + 144);
+    const GCtx g{};
+    const fp12 e = g_gather(g, g_final_exp(g, g_miller(g, 1, &px, &py, &qx, &qy)));
+    const fp* c[12] = {&e.c0.c0.c0, &e.c0.c0.c1, &e.c0.c1.c0, &e.c0.c1.c1, &e.c0.c2.c0, &e.c0.c2.c1,
+                       &e.c1.c0.c0, &e.c1.c0.c1, &e.c1.c1.c0, &e.c1.c1.c1, &e.c1.c2.c0, &e.c1.c2.c1};
+    for (int i = 0; i < 12; i++) mont_to_be(out + 48 * i, *c[i]);
+}
+// the group form of fast_aggregate_verify's pairing equation for one item (as k_bls_pair runs it)
+int bh_g_fast_aggregate_verify(const uint8_t* sig, size_t n_pks, const uint8_t* pks, const uint8_t* msg, size_t n,
+                               const uint8_t* dst, size_t dl) {
+    uint32_t srec[G1_REC_WORDS], hrec[G1_REC_WORDS], arec[G2_REC_WORDS];
+    int32_t st = sig_decode(sig, srec);
+    if (st != ST_OK) return st;
+    if (n_pks == 0) return ST_AGGR_MISMATCH;
+    uint32_t* krec = new uint32_t[G2_REC_WORDS * n_pks];
+    int32_t* kst = new int32_t[n_pks];
+    uint32_t* idx = new uint32_t[n_pks];
+    for (size_t i = 0; i < n_pks; i++) {
+        kst[i] = key_decode(pks + 96 * i, krec + G2_REC_WORDS * i);
+        idx[i] = (uint32_t)i;
+    }
+    st = apk_record(krec, kst, idx, (uint32_t)n_pks, arec);
+    delete[] krec;
+    delete[] kst;
+    delete[] idx;
+    if (st != ST_OK) return st;
+    h2c_record(msg, (uint32_t)n, dst, (uint32_t)dl, hrec);
+    return g_pairing_check(GCtx{}, srec, hrec, arec) ? ST_OK : ST_VERIFY_FAIL;
+}
+
 // the batch check over n items (item i: signature sig + 48 i, one key pk + 96 i, message msg + 32 i)
 // exactly as the kernels run it: shares, the product tree level by level, the final lane.
 // Returns 1 if the batch check accepts, 0 if it rejects, -1 if some item fails to decode.
 int bh_rlc_batch(size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint8_t* seed,
-                 const uint8_t* dst, size_t dl) {
+                 const uint8_t* dst, size_t dl, int group) {
     uint32_t* f = new uint32_t[F12_REC_WORDS * n];
     uint32_t* j = new uint32_t[G1J_REC_WORDS * n];
     int rc = 1;
@@ -117,16 +158,25 @@ int bh_rlc_batch(size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_
             break;
         }
         h2c_record(msgs + 32 * i, 32, dst, (uint32_t)dl, hrec);
-        rlc_item(srec, hrec, arec, rlc_scalar(seed, (uint32_t)i), f + F12_REC_WORDS * i, j + G1J_REC_WORDS * i);
+        if (group)
+            g_rlc_item(GCtx{}, srec, hrec, arec, rlc_scalar(seed, (uint32_t)i), f + F12_REC_WORDS * i,
+                       j + G1J_REC_WORDS * i);
+        else
+            rlc_item(srec, hrec, arec, rlc_scalar(seed, (uint32_t)i), f + F12_REC_WORDS * i, j + G1J_REC_WORDS * i);
     }
     if (rc == 1) {
         for (size_t m = n; m > 1; m = (m + 1) / 2) {
             const size_t h = (m + 1) / 2;
-            for (size_t i = 0; i < m - h; i++)
-                rlc_fold(f + F12_REC_WORDS * i, j + G1J_REC_WORDS * i, f + F12_REC_WORDS * (i + h),
-                         j + G1J_REC_WORDS * (i + h));
+            for (size_t i = 0; i < m - h; i++) {
+                if (group)
+                    g_rlc_fold(GCtx{}, f + F12_REC_WORDS * i, j + G1J_REC_WORDS * i, f + F12_REC_WORDS * (i + h),
+                               j + G1J_REC_WORDS * (i + h));
+                else
+                    rlc_fold(f + F12_REC_WORDS * i, j + G1J_REC_WORDS * i, f + F12_REC_WORDS * (i + h),
+                             j + G1J_REC_WORDS * (i + h));
+            }
         }
-        rc = rlc_final(f, j) ? 1 : 0;
+        rc = (group ? g_rlc_final(GCtx{}, f, j) : rlc_final(f, j)) ? 1 : 0;
     }
     delete[] f;
     delete[] j;

@@ -31,7 +31,9 @@ def emu():
     L.bh_keygen.argtypes = [c, vp]
     L.bh_sign.argtypes = [c, c, sz, c, sz, vp]
     L.bh_fast_aggregate_verify.argtypes = [c, sz, c, c, sz, c, sz]
-    L.bh_rlc_batch.argtypes = [sz, c, c, c, c, c, sz]
+    L.bh_rlc_batch.argtypes = [sz, c, c, c, c, c, sz, ctypes.c_int]
+    L.bh_g_pairing.argtypes = [c, c, vp]
+    L.bh_g_fast_aggregate_verify.argtypes = [c, sz, c, c, sz, c, sz]
     return L
 
 
@@ -124,11 +126,39 @@ def test_rlc_batch_check(emu, gold):
     msgs = [bytes([i]) * 32 for i in range(5)]
     sigs = [B.sign(sks[i % 4], m) for i, m in enumerate(msgs)]
     keys = [pks[i % 4] for i in range(5)]
-    for n in (1, 2, 3, 5):
-        assert emu.bh_rlc_batch(n, b"".join(sigs[:n]), b"".join(keys[:n]), b"".join(msgs[:n]), seed, dst,
-                                len(dst)) == 1
-        for bad in range(n):
-            m2 = list(msgs[:n])
-            m2[bad] = bytes([0xee]) * 32
-            assert emu.bh_rlc_batch(n, b"".join(sigs[:n]), b"".join(keys[:n]), b"".join(m2), seed, dst,
-                                    len(dst)) == 0
+    for group in (0, 1):  # bls381.h's single-lane tower, then bls_group.h (what the kernels run)
+        for n in (1, 2, 3, 5):
+            assert emu.bh_rlc_batch(n, b"".join(sigs[:n]), b"".join(keys[:n]), b"".join(msgs[:n]), seed, dst,
+                                    len(dst), group) == 1
+            for bad in range(n):
+                m2 = list(msgs[:n])
+                m2[bad] = bytes([0xee]) * 32
+                assert emu.bh_rlc_batch(n, b"".join(sigs[:n]), b"".join(keys[:n]), b"".join(m2), seed, dst,
+                                        len(dst), group) == 0
+
+
+def test_group_pairing_matches_single_lane(emu):
+    """bls_group.h's Miller loop + final exponentiation (the group arithmetic the kernels run) equal
+    bls381.h's single-lane pairing bit for bit, and both equal the oracle"""
+    import random
+    rnd = random.Random(21)
+    for _ in range(3):
+        P = B.g1_mul(B.g1_gen(), rnd.randrange(1, r))
+        Q = B.g2_mul(B.g2_gen(), rnd.randrange(1, r))
+        o1 = ctypes.create_string_buffer(576)
+        o2 = ctypes.create_string_buffer(576)
+        emu.bh_pairing(P, Q, o1)
+        emu.bh_g_pairing(P, Q, o2)
+        assert o1.raw == o2.raw == B.pairing(P, Q)
+
+
+def test_group_fast_aggregate_verify_statuses(emu, gold):
+    sks = [bytes.fromhex(k["sk"]) for k in gold["keygen"]]
+    pks = [bytes.fromhex(k["pk"]) for k in gold["keygen"]]
+    m = bytes(range(32))
+    sigs = [B.sign(sk, m) for sk in sks]
+    _, agg = B.aggregate(sigs[:3])
+    dst = B.DST_NUL
+    for s, ks, msg in [(agg, pks[:3], m), (agg, pks[:3], m + b"x"), (sigs[0], pks[:1], m), (C.IDENTITY_G1, pks[:3], m)]:
+        got = emu.bh_g_fast_aggregate_verify(s, len(ks), b"".join(ks), msg, len(msg), dst, len(dst))
+        assert got == B.fast_aggregate_verify(s, ks, msg)

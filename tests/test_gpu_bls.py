@@ -77,12 +77,23 @@ def _committee(bls, n, seed):
     return sks, bls.keygen(sks)
 
 
-@pytest.mark.parametrize("path", ["batch", "per_item"])
-def test_verify_many_mixed_batch_matches_oracle(bls, bls_per_item, path):
+@pytest.fixture(scope="module")
+def bls_nocache():
+    """a context under NWV_FLAG_NO_KEYCACHE: every call decodes its keys afresh"""
+    import narwhal_amd
+    from narwhal_amd import _lib
+    from narwhal_amd.bls import Bls
+    e = narwhal_amd.Engine(device=0, flags=_lib.NWV_FLAG_NO_KEYCACHE)
+    yield Bls(e)
+    e.close()
+
+
+@pytest.mark.parametrize("path", ["batch", "per_item", "nocache"])
+def test_verify_many_mixed_batch_matches_oracle(bls, bls_per_item, bls_nocache, path):
     """certificates of a 10-node committee (quorum 7 signers, 32-byte digests) plus every
     adversarial category; statuses equal the oracle's codes item by item, through the batch check
     (it rejects, then the per-item check names the failures) and under NWV_FLAG_BLS_PER_ITEM"""
-    bls = bls if path == "batch" else bls_per_item
+    bls = {"batch": bls, "per_item": bls_per_item, "nocache": bls_nocache}[path]
     sks, pks = _committee(bls, 10, 13)
     keys = pks + [C.not_in_g2(), C.IDENTITY_G2, C.negate_g2(pks[0])]
     rnd = random.Random(14)
@@ -110,18 +121,25 @@ def test_verify_many_mixed_batch_matches_oracle(bls, bls_per_item, path):
     assert list(got) == want
     assert want[:12] == [0] * 12 and all(w != 0 for w in want[12:])
     # the wrong-message / wrong-signer items fail only the pairing equation: the batch check rejects
-    assert bls.last_path() == ("batch_rejected_then_per_item" if path == "batch" else "per_item")
+    assert bls.last_path() == ("per_item" if path == "per_item" else "batch_rejected_then_per_item")
     # the valid certificates alone: the batch check accepts them in one final exponentiation
     got = bls.verify_many(keys, [i[0] for i in items[:12]], [i[1] for i in items[:12]], [i[2] for i in items[:12]])
     assert list(got) == [0] * 12
-    assert bls.last_path() == ("batch_accepted" if path == "batch" else "per_item")
+    assert bls.last_path() == ("per_item" if path == "per_item" else "batch_accepted")
     # valid certificates beside items that fail before the pairing (decode / group / key errors):
     # those stay out of the batch check, which accepts the rest
     pre = [it for it, w in zip(items, want) if w not in (0, B.ORB_VERIFY_FAIL)]
     sub = items[:12] + pre
     got = bls.verify_many(keys, [i[0] for i in sub], [i[1] for i in sub], [i[2] for i in sub])
     assert list(got) == [B.fast_aggregate_verify(s, [keys[k] for k in ks], m) for s, ks, m in sub]
-    assert bls.last_path() == ("batch_accepted" if path == "batch" else "per_item")
+    assert bls.last_path() == ("per_item" if path == "per_item" else "batch_accepted")
+    # the same keys in another order and with duplicates (cache hits, repeated slots)
+    perm = list(range(len(keys)))[::-1]
+    keys2 = [keys[p] for p in perm] + [keys[0]]
+    inv = {p: j for j, p in enumerate(perm)}
+    items2 = [(s_, [inv[k] for k in ks] + ([len(keys)] if ks and ks[0] == 0 else []), m) for s_, ks, m in items]
+    got = bls.verify_many(keys2, [i[0] for i in items2], [i[1] for i in items2], [i[2] for i in items2])
+    assert list(got) == [B.fast_aggregate_verify(s_, [keys2[k] for k in ks], m) for s_, ks, m in items2]
 
 
 def test_trait_contract(bls, gold):
@@ -149,6 +167,29 @@ def test_trait_contract(bls, gold):
     assert bls.aggregate_batch_verify([agg, agg2], [pks[:3], pks[1:]], [m, m2]) == _lib.NWV_OK
     assert bls.aggregate_batch_verify([agg, agg2], [pks[:3], pks[:3]], [m, m2]) == _lib.NWV_ERR_SIGNATURE
     assert bls.aggregate_batch_verify([agg, agg2], [pks[:3], pks[1:]], [m]) == _lib.NWV_ERR_LENGTH
+
+
+def test_key_sums_many_keys(bls):
+    """items naming many keys (the key sum runs on 8 lanes and a tree): 1..20 signers, a bad key at
+    every position of the list (the first bad key's status wins), against the oracle"""
+    sks, pks = _committee(bls, 20, 16)
+    keys = pks + [C.not_in_g2(), C.IDENTITY_G2]
+    rnd = random.Random(17)
+    items = []
+    for q in (1, 2, 7, 8, 9, 15, 16, 17, 20):
+        who = sorted(rnd.sample(range(20), q))
+        d = rnd.randbytes(32)
+        _, agg = B.aggregate(bls.sign([sks[k] for k in who], [d] * q))
+        items.append((agg, who, d))
+        for pos in (0, q // 2, q - 1):
+            bad = list(who)
+            bad.insert(pos, 20)
+            items.append((agg, bad, d))
+            bad2 = list(bad)
+            bad2.insert(0 if pos else 1, 21)  # an identity key before / after the subgroup failure
+            items.append((agg, bad2, d))
+    got = bls.verify_many(keys, [i[0] for i in items], [i[1] for i in items], [i[2] for i in items])
+    assert list(got) == [B.fast_aggregate_verify(s, [keys[k] for k in ks], m) for s, ks, m in items]
 
 
 @pytest.mark.parametrize("n", [1, 2, 3, 63, 64, 65, 200])
