@@ -815,7 +815,8 @@ def main():
         if rank == 0:
             line = base_line(args, world, h["dt_max"])
             line.update(rank0_ms_per_step=h["dt"] / args.steps * 1e3, kernel_ms_rank0=h["kt"],
-                        single_stream_rank0={"ms_per_step": float(np.median(h["single"]))}, firehose=fire)
+                        single_stream_rank0={"ms_per_step": float(np.median(h["single"]))},
+                        steady_state_rank0=h["steady"], firehose=fire)
             print(json.dumps(line), flush=True)
         eng.close()
         dist.destroy_process_group()

@@ -87,6 +87,29 @@ __global__ __launch_bounds__(64) void k_fexp(int reps, uint32_t* out) {
     sink(out, t, a.c0.c0.c0);
 }
 
+// the 8-lane group forms (bls_group.h): one element per group, 8 groups per wave
+#define GK(name, body)                                                                   \
+    __global__ __launch_bounds__(64) void name(int reps, uint32_t* out) {               \
+        __shared__ uint32_t lds[8 * GX_WORDS];                                           \
+        const GCtx g = g_ctx(lds);                                                       \
+        const uint32_t t = blockIdx.x * 64 + threadIdx.x;                                \
+        G12 a = g_scatter(g, seed_f12(t >> 3)), b = g_scatter(g, seed_f12((t >> 3) + 1)); \
+        body;                                                                            \
+        sink(out, t, a.v.c0);                                                            \
+    }
+GK(k_g_mul, for (int i = 0; i < reps; i++) a = g_mul(g, a, b))
+GK(k_g_sqr, for (int i = 0; i < reps; i++) a = g_sqr(g, a))
+GK(k_g_cyc, for (int i = 0; i < reps; i++) a = g_cyc_sqr(g, a))
+GK(k_g_line, for (int i = 0; i < reps; i++) a = g_mul_line(g, a, b.v, a.v, b.v))
+GK(k_g_fexp, for (int i = 0; i < reps; i++) a = g_final_exp(g, a))
+__device__ G12 miller_reps(const GCtx& g, G12 a, int reps) {
+    fp px = k_g1x(), py = k_g1y();
+    fp2 qx = k_g2x(), qy = k_g2y();
+    for (int i = 0; i < reps; i++) a = g_mul(g, a, g_miller(g, 1, &px, &py, &qx, &qy));
+    return a;
+}
+GK(k_g_miller, a = miller_reps(g, a, reps))
+
 typedef void (*kfn)(int, uint32_t*);
 
 int main() {
@@ -99,7 +122,10 @@ int main() {
               {"f2_mul", k_f2_mul, 1000, 3},       {"f6_mul", k_f6_mul, 200, 18},
               {"f12_mul", k_f12_mul, 50, 54},      {"f12_sqr", k_f12_sqr, 50, 36},
               {"f12_cyc_sqr", k_f12_cyc, 100, 18}, {"miller_loop_1pair", k_miller, 1, 6800},
-              {"final_exp", k_fexp, 1, 6000}};
+              {"final_exp", k_fexp, 1, 6000},      {"group8_f12_mul", k_g_mul, 200, 54},
+              {"group8_f12_sqr", k_g_sqr, 200, 36}, {"group8_cyc_sqr", k_g_cyc, 200, 18},
+              {"group8_line_mul", k_g_line, 200, 13}, {"group8_miller_loop_1pair", k_g_miller, 1, 6800},
+              {"group8_final_exp", k_g_fexp, 1, 6000}};
     const int blocks_full = 256 * 4 * 2;  // two waves per SIMD
     uint32_t* out;
     if (hipMalloc(&out, 4 * 64 * blocks_full) != hipSuccess) return 2;
@@ -121,7 +147,8 @@ int main() {
             ms[g] = m;
         }
         const double lat_us = ms[0] * 1e3 / k.reps;
-        const double thr = (double)blocks_full * 64 * k.reps / (ms[1] * 1e-3);
+        const bool grp = std::strncmp(k.name, "group8", 6) == 0;  // one element per 8 lanes
+        const double thr = (double)blocks_full * (grp ? 8 : 64) * k.reps / (ms[1] * 1e-3);
         printf("{\"op\": \"%s\", \"latency_us_one_wave\": %.3f, \"per_fp_mult_us\": %.4f, \"ops_per_s_full_chip\": %.4g, "
                "\"fp_mults_per_op\": %.0f}\n",
                k.name, lat_us, lat_us / k.fp_mults, thr, k.fp_mults);
