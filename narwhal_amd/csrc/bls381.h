@@ -57,6 +57,7 @@ BLS_CONST(k_beta, BLS_BETA)
 BLS_CONST(k_sswu_a, BLS_SSWU_A)
 BLS_CONST(k_sswu_b, BLS_SSWU_B)
 BLS_CONST(k_sswu_z, BLS_SSWU_Z)
+BLS_CONST(k_sswu_c2, BLS_SSWU_C2)
 BLS_CONST(k_g1x, BLS_G1X)
 BLS_CONST(k_g1y, BLS_G1Y)
 BLS_CONST(k_two256, BLS_TWO256)
@@ -784,25 +785,31 @@ NWV_HD fp fp_from_be64(const uint8_t* b) {
     plain_from_be256(l, b + 32);
     return fp_add(fp_mul(fp_to_mont(h), k_two256()), fp_to_mont(l));
 }
-// simplified SWU on y^2 = x^3 + A'x + B' (RFC 9380 §6.6.2, Z = 11)
+// simplified SWU on y^2 = x^3 + A'x + B' (RFC 9380 §6.6.2, Z = 11), the straight-line form of
+// Appendix F.2 with sqrt_ratio for q = 3 mod 4 (F.2.1.2): one exponentiation and one inversion
+// per call (the textbook form's inversions of A and tv1 and its second square root are gone)
 NWV_HD void map_sswu(fp& xo, fp& yo, const fp& u) {
     const fp A = k_sswu_a(), B = k_sswu_b(), Z = k_sswu_z();
-    const fp zu2 = fp_mul(Z, fp_sqr(u));
-    const fp tv1 = fp_add(fp_sqr(zu2), zu2);
-    fp x1;
-    if (fp_is_zero(tv1)) x1 = fp_mul(B, fp_inv(fp_mul(Z, A)));
-    else x1 = fp_mul(fp_mul(fp_neg(B), fp_inv(A)), fp_add(k_one(), fp_inv(tv1)));
-    const fp gx1 = fp_add(fp_mul(fp_add(fp_sqr(x1), A), x1), B);
-    fp y;
-    if (fp_sqrt(y, gx1)) {
-        xo = x1;
-    } else {
-        const fp x2 = fp_mul(zu2, x1);
-        const fp gx2 = fp_add(fp_mul(fp_add(fp_sqr(x2), A), x2), B);
-        fp_sqrt(y, gx2);
-        xo = x2;
-    }
+    const fp tv1 = fp_mul(Z, fp_sqr(u));
+    fp tv2 = fp_add(fp_sqr(tv1), tv1);
+    const fp tv3 = fp_mul(B, fp_add(tv2, k_one()));
+    const fp tv4 = fp_mul(A, fp_is_zero(tv2) ? Z : fp_neg(tv2));
+    fp tv6 = fp_sqr(tv4);
+    tv2 = fp_mul(fp_add(fp_sqr(tv3), fp_mul(A, tv6)), tv3);
+    tv6 = fp_mul(tv6, tv4);
+    tv2 = fp_add(tv2, fp_mul(B, tv6));  // gx1 = tv2 / tv6
+    const fp xn = fp_mul(tv1, tv3);
+    // sqrt_ratio(tv2, tv6)
+    const uint32_t c1[12] = BLS_E_QR;  // (p - 3) / 4
+    const fp s1 = fp_mul(fp_sqr(tv6), fp_mul(tv2, tv6));
+    fp y1 = fp_mul(fp_pow(s1, c1), fp_mul(tv2, tv6));
+    const fp y2 = fp_mul(y1, k_sswu_c2());
+    const bool qr = fp_eq(fp_mul(fp_sqr(y1), tv6), tv2);
+    y1 = qr ? y1 : y2;
+    fp y = qr ? y1 : fp_mul(fp_mul(tv1, u), y1);
+    const fp x = qr ? tv3 : xn;
     if (fp_sgn0(u) != fp_sgn0(y)) y = fp_neg(y);
+    xo = fp_mul(x, fp_inv(tv4));
     yo = y;
 }
 // the 11-isogeny (RFC 9380 Appendix E.2), constants from tools/gen_bls_iso.py
@@ -836,15 +843,18 @@ NWV_HD jac<fp> iso_map(const fp& x, const fp& y) {
     o.y = fp_mul(fp_mul(Yn, o.z), fp_mul(o.z, Xd));      // Yn/Yd * Z^3 = Yn Xd^3 Yd^2
     return o;
 }
-// H(m) in Jacobian form
-BLS_NOINLINE jac<fp> hash_to_g1(const uint8_t* msg, uint32_t n, const uint8_t* dst, uint32_t dl) {
+// one of the two field elements of hash_to_field (j = 0, 1) mapped to E: iso(SSWU(u_j))
+BLS_NOINLINE jac<fp> h2c_map(const uint8_t* msg, uint32_t n, const uint8_t* dst, uint32_t dl, int j) {
     uint8_t ub[128];
     expand_xmd_128(ub, msg, n, dst, dl);
+    const fp u0 = fp_from_be64(ub), u1 = fp_from_be64(ub + 64);  // constant offsets, then a select
     fp x, y;
-    map_sswu(x, y, fp_from_be64(ub));
-    const jac<fp> q0 = iso_map(x, y);
-    map_sswu(x, y, fp_from_be64(ub + 64));
-    const jac<fp> q1 = iso_map(x, y);
+    map_sswu(x, y, fp_sel(j == 0, u0, u1));
+    return iso_map(x, y);
+}
+// H(m) in Jacobian form
+BLS_NOINLINE jac<fp> hash_to_g1(const uint8_t* msg, uint32_t n, const uint8_t* dst, uint32_t dl) {
+    const jac<fp> q0 = h2c_map(msg, n, dst, dl, 0), q1 = h2c_map(msg, n, dst, dl, 1);
     return jac_mul64(jac_add(q0, q1), BLS_H_EFF);
 }
 

@@ -114,8 +114,9 @@ NWV_HD bool pairing_check(const uint32_t* sig_rec, const uint32_t* h_rec, const 
 // Every item i that decoded and passed the group checks carries a 64-bit coefficient r_i (odd, so
 // nonzero: blst's own multi-verification draws 64-bit coefficients too); the call accepts iff
 //   prod_i e([r_i] H_i, apk_i) * e(-sum_i [r_i] sig_i, g2) == 1,
-// computed as one Miller loop per item, a product tree, one more Miller loop and ONE final
-// exponentiation.  H_i, sig_i lie in G1 and apk_i in G2 (prime order r), so an invalid item makes
+// computed in stages: every item's [r_i] H_i and [r_i] sig_i; the G1 sum S of the latter (a
+// tree); the Miller loops of ([r_i] H_i, apk_i) and of (-S, g2), all in one grid; a product tree;
+// ONE final exponentiation.  H_i, sig_i lie in G1 and apk_i in G2 (prime order r), so an invalid item makes
 // the product differ from 1 except with probability ~2^-63 over the coefficients; when it is not
 // 1 the engine runs the per-item check (pairing_check) to name the failing items exactly.
 constexpr int F12_REC_WORDS = 12 * NL;     // Fp12, tower order c0.c0.c0 .. c1.c2.c1
@@ -163,54 +164,6 @@ NWV_HD uint64_t rlc_scalar(const uint8_t* seed32, uint32_t i) {
     return (((uint64_t)h[0] << 32) | h[1]) | 1u;
 }
 
-// item i's share: f_i = the (conjugated) Miller loop of ([r] H, apk), s_i = [r] sig (Jacobian)
-NWV_HD void rlc_item(const uint32_t* sig_rec, const uint32_t* h_rec, const uint32_t* apk_rec, uint64_t r,
-                     uint32_t* f_out, uint32_t* s_out) {
-    jac<fp> s;
-    s.inf = true;
-    s.x = s.y = s.z = fp_zero();
-    if (!sig_rec[2 * NL]) s = jac_mul64(jac_from_affine(ld_fp(sig_rec), ld_fp(sig_rec + NL)), r);
-    st_g1j(s_out, s);
-    fp12 f = f12_one();
-    if (!h_rec[2 * NL]) {
-        const jac<fp> hr = jac_mul64(jac_from_affine(ld_fp(h_rec), ld_fp(h_rec + NL)), r);
-        if (!hr.inf) {
-            fp px, py;
-            g1_to_affine(px, py, hr);
-            fp2 qx, qy;
-            ld_g2(apk_rec, qx, qy);
-            f = miller_loop2(1, &px, &py, &qx, &qy);
-        }
-    }
-    st_f12(f_out, f);
-}
-// an item outside the batch (failed an earlier check): the neutral share
-NWV_HD void rlc_neutral(uint32_t* f_out, uint32_t* s_out) {
-    st_f12(f_out, f12_one());
-    jac<fp> s;
-    s.inf = true;
-    s.x = s.y = s.z = fp_zero();
-    st_g1j(s_out, s);
-}
-// (f_a, s_a) <- (f_a f_b, s_a + s_b)
-NWV_HD void rlc_fold(uint32_t* fa, uint32_t* sa, const uint32_t* fb, const uint32_t* sb) {
-    st_f12(fa, f12_mul(ld_f12(fa), ld_f12(fb)));
-    st_g1j(sa, jac_add(ld_g1j(sa), ld_g1j(sb)));
-}
-// the batch verdict: FE(f * ML(-S, g2)) == 1
-NWV_HD bool rlc_final(const uint32_t* f_rec, const uint32_t* s_rec) {
-    fp12 f = ld_f12(f_rec);
-    const jac<fp> S = ld_g1j(s_rec);
-    if (!S.inf) {
-        fp px, py;
-        g1_to_affine(px, py, S);
-        py = fp_neg(py);
-        const fp2 qx = k_g2x(), qy = k_g2y();
-        f = f12_mul(f, miller_loop2(1, &px, &py, &qx, &qy));
-    }
-    return f12_is_one(final_exp(f));
-}
-
 // ---- the same checks over a group of lanes (bls_group.h): what the kernels run --------------
 // e(-sig, g2) e(H, apk) == 1 (pairing_check), every lane of the group gets the verdict
 G_HD bool g_pairing_check(const GCtx& g, const uint32_t* sig_rec, const uint32_t* h_rec, const uint32_t* apk_rec) {
@@ -233,12 +186,11 @@ G_HD bool g_pairing_check(const GCtx& g, const uint32_t* sig_rec, const uint32_t
     return g_is_one(g, g_final_exp(g, g_miller(g, n, px, py, qx, qy)));
 }
 
-// item i's share of the batch check (rlc_item) with its Fp12 stored in W order (6 x F2W words).
-// On the GPU the two scalar multiplications run side by side: lanes 0-3 of the group take
-// [r] H, lanes 4-7 [r] sig; lane 0 hands [r] H (affine) to the group through its LDS area and
-// lane 4 stores [r] sig.
-G_HD void g_rlc_item(const GCtx& g, const uint32_t* sig_rec, const uint32_t* h_rec, const uint32_t* apk_rec,
-                       uint64_t r, uint32_t* f_out, uint32_t* s_out) {
+// stage 1, item i (one group): P_i = [r] H (affine record, identity flag) and s_i = [r] sig
+// (Jacobian).  On the GPU the two scalar multiplications run side by side: lanes 0-3 take [r] H,
+// lanes 4-7 [r] sig; lane 0 stores P_i, lane 4 s_i.
+G_HD void g_rlc_points(const GCtx& g, const uint32_t* sig_rec, const uint32_t* h_rec, uint64_t r, uint32_t* p_out,
+                       uint32_t* s_out) {
     jac<fp> inf;
     inf.inf = true;
     inf.x = inf.y = inf.z = fp_zero();
@@ -248,70 +200,63 @@ G_HD void g_rlc_item(const GCtx& g, const uint32_t* sig_rec, const uint32_t* h_r
     jac<fp> m = inf;
     if (!src[2 * NL]) m = jac_mul64(jac_from_affine(ld_fp(src), ld_fp(src + NL)), r);
     if (g.slot == 4) st_g1j(s_out, m);
-    fp hx = fp_zero(), hy = fp_zero();
-    if (!m.inf) g1_to_affine(hx, hy, m);
-    g_sync();
-    if (g.slot == 0) {
-        st_fp(g.xa, hx);
-        st_fp(g.xa + NL, hy);
-        g.xa[2 * NL] = m.inf ? 1u : 0u;
+    if (!sig_lane) {
+        fp x = fp_zero(), y = fp_zero();
+        if (!m.inf) g1_to_affine(x, y, m);
+        if (g.slot == 0) st_g1(p_out, x, y, m.inf);
     }
-    g_sync();
-    const bool h_inf = g.xa[2 * NL] != 0;
-    const fp px = ld_fp(g.xa), py = ld_fp(g.xa + NL);
 #else
     jac<fp> s = inf, h = inf;
     if (!sig_rec[2 * NL]) s = jac_mul64(jac_from_affine(ld_fp(sig_rec), ld_fp(sig_rec + NL)), r);
     if (!h_rec[2 * NL]) h = jac_mul64(jac_from_affine(ld_fp(h_rec), ld_fp(h_rec + NL)), r);
     st_g1j(s_out, s);
-    fp px = fp_zero(), py = fp_zero();
-    if (!h.inf) g1_to_affine(px, py, h);
-    const bool h_inf = h.inf;
+    fp x = fp_zero(), y = fp_zero();
+    if (!h.inf) g1_to_affine(x, y, h);
+    st_g1(p_out, x, y, h.inf);
 #endif
+}
+// an item outside the batch (failed an earlier check): identity P_i, s_i
+G_HD void g_rlc_neutral(const GCtx& g, uint32_t* p_out, uint32_t* s_out) {
+    jac<fp> s;
+    s.inf = true;
+    s.x = s.y = s.z = fp_zero();
+#ifdef BLS_GDEV
+    if (g.slot != 0) return;
+#endif
+    st_g1j(s_out, s);
+    st_g1(p_out, fp_zero(), fp_zero(), true);
+}
+// stage 3: f = the Miller loop of (P, Q) in W order, 1 for an identity P; Q = apk (affine record),
+// or (neg) the pair (-S, g2) of the combination's signature side, S Jacobian
+G_HD void g_rlc_ml(const GCtx& g, const uint32_t* p_rec, const uint32_t* apk_rec, uint32_t* f_out) {
     G12 f = g_one(g);
-    if (!h_inf) {
+    if (!p_rec[2 * NL]) {
+        const fp px = ld_fp(p_rec), py = ld_fp(p_rec + NL);
         fp2 qx, qy;
         ld_g2(apk_rec, qx, qy);
         f = g_miller(g, 1, &px, &py, &qx, &qy);
     }
     g_store(g, f_out, f);
 }
-// (f_a, s_a) <- (f_a f_b, s_a + s_b); the G1 sum on every lane, stored by lane 0
-G_HD void g_rlc_fold(const GCtx& g, uint32_t* fa, uint32_t* sa, const uint32_t* fb, const uint32_t* sb) {
-    const G12 f = g_mul(g, g_load(g, fa), g_load(g, fb));
-    const jac<fp> s = jac_add(ld_g1j(sa), ld_g1j(sb));
-#ifdef BLS_GDEV
-    g_sync();  // every lane has read sa before it is overwritten
-    if (g.slot == 0) st_g1j(sa, s);
-#else
-    st_g1j(sa, s);
-#endif
-    g_store(g, fa, f);
-}
-// the batch verdict: FE(f * ML(-S, g2)) == 1
-G_HD bool g_rlc_final(const GCtx& g, const uint32_t* f_rec, const uint32_t* s_rec) {
-    G12 f = g_load(g, f_rec);
+G_HD void g_rlc_ml_sig(const GCtx& g, const uint32_t* s_rec, uint32_t* f_out) {
     const jac<fp> S = ld_g1j(s_rec);
+    G12 f = g_one(g);
     if (!S.inf) {
         fp px, py;
         g1_to_affine(px, py, S);
         py = fp_neg(py);
         const fp2 qx = k_g2x(), qy = k_g2y();
-        f = g_mul(g, f, g_miller(g, 1, &px, &py, &qx, &qy));
+        f = g_miller(g, 1, &px, &py, &qx, &qy);
     }
-    return g_is_one(g, g_final_exp(g, f));
+    g_store(g, f_out, f);
 }
-// an item outside the batch: the neutral share
-G_HD void g_rlc_neutral(const GCtx& g, uint32_t* f_out, uint32_t* s_out) {
-    g_store(g, f_out, g_one(g));
-    jac<fp> s;
-    s.inf = true;
-    s.x = s.y = s.z = fp_zero();
-#ifdef BLS_GDEV
-    if (g.slot == 0) st_g1j(s_out, s);
-#else
-    st_g1j(s_out, s);
-#endif
+// the trees: f_a <- f_a f_b (a group), s_a <- s_a + s_b (a lane)
+G_HD void g_rlc_ffold(const GCtx& g, uint32_t* fa, const uint32_t* fb) {
+    const G12 f = g_mul(g, g_load(g, fa), g_load(g, fb));
+    g_store(g, fa, f);
 }
+NWV_HD void rlc_sfold(uint32_t* sa, const uint32_t* sb) { st_g1j(sa, jac_add(ld_g1j(sa), ld_g1j(sb))); }
+// stage 5: the batch verdict, FE(f) == 1
+G_HD bool g_rlc_final(const GCtx& g, const uint32_t* f_rec) { return g_is_one(g, g_final_exp(g, g_load(g, f_rec))); }
 
 }  // namespace bls

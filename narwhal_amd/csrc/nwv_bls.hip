@@ -7,12 +7,12 @@
 //                    deserialization); then k_bls_apk_g, one 8-lane group per item: the sum of the
 //                    item's keys (eight partial sums and a tree), its first bad key's status
 //   k_bls_sigs       one lane per item: decode + G1 membership (phi(P) = [-x^2] P)
-//   k_bls_h2c        one lane per item: H(msg) (RFC 9380 hash_to_curve G1)
+//   k_bls_h2c_g      one 8-lane group per item: H(msg) (RFC 9380 hash_to_curve G1), the two
+//                    field elements mapped side by side
 // joined by k_bls_status (the statuses in the oracle's order), then
-//   the pairing check, by default as ONE batch check over the call (bls_verify.h):
-//     k_bls_rlc    one lane per item: [r_i] H_i, [r_i] sig_i, the Miller loop of ([r_i] H_i, apk_i)
-//     k_bls_fold   ceil(log2 n) levels of a product tree (Fp12 products, G1 sums)
-//     k_bls_final  one lane: times the Miller loop of (-sum r_i sig_i, g2), final exponentiation
+//   the pairing check, by default as ONE batch check over the call (bls_verify.h, kernels below:
+//     [r_i] H_i and [r_i] sig_i per item, S = sum [r_i] sig_i, every item's Miller loop and that
+//     of (-S, g2) in one grid, a product tree, one final exponentiation)
 //   and only when that rejects (or under NWV_FLAG_BLS_PER_ITEM)
 //     k_bls_pair   one lane per item: e(-sig, g2) e(H, apk) == 1 (two-pair Miller loop + final exp)
 // and copies the per-item statuses back.  The Miller loops are the hot part: Fp products on VALU
@@ -54,13 +54,6 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_keys_fill(uint32_t n, const u
 __global__ __launch_bounds__(BLS_LANES) void k_bls_sigs(uint32_t n, const uint8_t* sig, uint32_t* rec, int32_t* st) {
     BLS_IDX();
     st[i] = sig_decode(sig + 48 * (size_t)i, rec + (size_t)G1_REC_WORDS * i);
-}
-__global__ __launch_bounds__(BLS_LANES) void k_bls_h2c(uint32_t n, const uint8_t* msg, const uint64_t* off,
-                                                       const uint32_t* len, const uint8_t* dst, uint32_t dl,
-                                                       const int32_t* st, uint32_t* rec) {
-    BLS_IDX();
-    if (st && st[i] != ST_OK) return;
-    h2c_record(msg + off[i], len[i], dst, dl, rec + (size_t)G1_REC_WORDS * i);
 }
 // the pairing kernels run one item per GROUP of 8 lanes (bls_group.h): 8 items per 64-lane block
 #define BLS_GIDX()                                                                  \
@@ -144,6 +137,23 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_apk_g(uint32_t n, const uint3
     st_g2(out, x, y, inf);
     st_apk[i] = status;
 }
+// H(msg_i) on a group: lanes 0-3 map hash_to_field's u_0, lanes 4-7 u_1 (side by side), lane 4
+// hands its point to lane 0 through the group's LDS area, lane 0 adds and clears the cofactor
+__global__ __launch_bounds__(BLS_LANES) void k_bls_h2c_g(uint32_t n, const uint8_t* msg, const uint64_t* off,
+                                                         const uint32_t* len, const uint8_t* dst, uint32_t dl,
+                                                         uint32_t* rec) {
+    BLS_GIDX();
+    const jac<fp> q = h2c_map(msg + off[i], len[i], dst, dl, (g.slot & 4) ? 1 : 0);
+    g_sync();
+    if (g.slot == 4) st_g1j(g.xa, q);
+    g_sync();
+    const jac<fp> q1 = ld_g1j(g.xa);
+    if (g.slot != 0) return;
+    const jac<fp> h = jac_mul64(jac_add(q, q1), BLS_H_EFF);
+    fp x = fp_zero(), y = fp_zero();
+    if (!h.inf) g1_to_affine(x, y, h);
+    st_g1(rec + (size_t)G1_REC_WORDS * i, x, y, h.inf);
+}
 // the item's status in the oracle's order: the signature's, then the keys'
 __global__ __launch_bounds__(BLS_LANES) void k_bls_status(uint32_t n, const int32_t* st_sig, const int32_t* st_apk,
                                                           int32_t* st) {
@@ -159,32 +169,51 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_pair(uint32_t n, const uint32
     g_sync();
     if (g.slot == 0) st[i] = ok ? ST_OK : ST_VERIFY_FAIL;
 }
-// the batch check (bls_verify.h): every item's share, then a product tree, then one group's final
-__global__ __launch_bounds__(BLS_LANES) void k_bls_rlc(uint32_t n, const uint32_t* sig_rec, const uint32_t* h_rec,
-                                                       const uint32_t* apk_rec, const int32_t* st,
-                                                       const uint8_t* seed, uint32_t* frec, uint32_t* srec) {
+// the batch check (bls_verify.h), in stages:
+//   k_bls_rlc_pts   one group per item: P_i = [r_i] H_i (affine), s_i = [r_i] sig_i
+//   k_bls_sfold     ceil(log2 n) levels of G1 sums: S = sum s_i
+//   k_bls_rlc_ml    one group per item and one more: the Miller loops of (P_i, apk_i) and (-S, g2)
+//   k_bls_ffold     ceil(log2 (n + 1)) levels of group Fp12 products
+//   k_bls_final     one group: the final exponentiation, == 1
+__global__ __launch_bounds__(BLS_LANES) void k_bls_rlc_pts(uint32_t n, const uint32_t* sig_rec, const uint32_t* h_rec,
+                                                           const int32_t* st, const uint8_t* seed, uint32_t* prec,
+                                                           uint32_t* srec) {
     BLS_GIDX();
-    uint32_t* f = frec + (size_t)F12_REC_WORDS * i;
+    uint32_t* p = prec + (size_t)G1_REC_WORDS * i;
     uint32_t* s = srec + (size_t)G1J_REC_WORDS * i;
     if (st[i] != ST_OK) {
-        g_rlc_neutral(g, f, s);
+        g_rlc_neutral(g, p, s);
         return;
     }
-    g_rlc_item(g, sig_rec + (size_t)G1_REC_WORDS * i, h_rec + (size_t)G1_REC_WORDS * i, apk_rec + (size_t)G2_REC_WORDS * i,
-               rlc_scalar(seed, i), f, s);
+    g_rlc_points(g, sig_rec + (size_t)G1_REC_WORDS * i, h_rec + (size_t)G1_REC_WORDS * i, rlc_scalar(seed, i), p, s);
 }
-// one level of the tree over m shares: share j <- share j (+) share j + h, h = ceil(m / 2), j < m - h
-__global__ __launch_bounds__(BLS_LANES) void k_bls_fold(uint32_t m, uint32_t* frec, uint32_t* srec) {
+// one level of a tree over m entries: entry j <- entry j (+) entry j + h, h = ceil(m / 2), j < m - h
+__global__ __launch_bounds__(BLS_LANES) void k_bls_sfold(uint32_t m, uint32_t* srec) {
+    const uint32_t h = (m + 1) / 2;
+    const uint32_t n = m - h;
+    BLS_IDX();
+    rlc_sfold(srec + (size_t)G1J_REC_WORDS * i, srec + (size_t)G1J_REC_WORDS * (i + h));
+}
+__global__ __launch_bounds__(BLS_LANES) void k_bls_rlc_ml(uint32_t n_items, const uint32_t* prec, const uint32_t* apk_rec,
+                                                          const uint32_t* srec, uint32_t* frec) {
+    const uint32_t n = n_items + 1;
+    BLS_GIDX();
+    uint32_t* f = frec + (size_t)F12_REC_WORDS * i;
+    if (i < n_items)
+        g_rlc_ml(g, prec + (size_t)G1_REC_WORDS * i, apk_rec + (size_t)G2_REC_WORDS * i, f);
+    else
+        g_rlc_ml_sig(g, srec, f);  // srec[0] = S after the G1 tree
+}
+__global__ __launch_bounds__(BLS_LANES) void k_bls_ffold(uint32_t m, uint32_t* frec) {
     const uint32_t h = (m + 1) / 2;
     const uint32_t n = m - h;
     BLS_GIDX();
-    g_rlc_fold(g, frec + (size_t)F12_REC_WORDS * i, srec + (size_t)G1J_REC_WORDS * i,
-               frec + (size_t)F12_REC_WORDS * (i + h), srec + (size_t)G1J_REC_WORDS * (i + h));
+    g_rlc_ffold(g, frec + (size_t)F12_REC_WORDS * i, frec + (size_t)F12_REC_WORDS * (i + h));
 }
-__global__ __launch_bounds__(BLS_LANES) void k_bls_final(const uint32_t* frec, const uint32_t* srec, int32_t* ok) {
+__global__ __launch_bounds__(BLS_LANES) void k_bls_final(const uint32_t* frec, int32_t* ok) {
     const uint32_t n = 1;
     BLS_GIDX();
-    const bool r = g_rlc_final(g, frec, srec);
+    const bool r = g_rlc_final(g, frec);
     g_sync();
     if (g.slot == 0) *ok = r ? 1 : 0;
 }
@@ -396,7 +425,7 @@ constexpr int gBlocks(size_t n) { return (int)((n + BLS_LANES / GRP - 1) / (BLS_
 // the whole verify_many pipeline on one device: after one H2D copy, three streams --
 //   side 0: the call's new keys into the key cache (k_bls_keys_fill), then the key sums (k_bls_apk_g)
 //   main  : signature decode + G1 checks (k_bls_sigs)
-//   side 1: hash to G1 (k_bls_h2c)
+//   side 1: hash to G1 (k_bls_h2c_g)
 // -- then, joined on the main stream, the statuses in the oracle's order and the pairing check
 int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uint8_t* sigs, const uint32_t* pk_off,
               const uint32_t* pk_cnt, const uint32_t* pk_idx, size_t n_idx, const uint8_t* msg_base,
@@ -480,8 +509,9 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
                  w_srec = al(w_kst + (cached ? 0 : 4 * n_keys)), w_hrec = w_srec + 4 * G1_REC_WORDS * n,
                  w_arec = w_hrec + 4 * G1_REC_WORDS * n, w_st = w_arec + 4 * G2_REC_WORDS * n,
                  w_ssig = al(w_st + 4 * n), w_sapk = al(w_ssig + 4 * n), w_ok = al(w_sapk + 4 * n),
-                 w_frec = al(w_ok + 4), w_jrec = al(w_frec + 4 * F12_REC_WORDS * (batch ? n : 0)),
-                 w_end = w_jrec + 4 * G1J_REC_WORDS * (batch ? n : 0) + 4;
+                 w_frec = al(w_ok + 4), w_jrec = al(w_frec + 4 * F12_REC_WORDS * (batch ? n + 1 : 0)),
+                 w_prec = al(w_jrec + 4 * G1J_REC_WORDS * (batch ? n : 0)),
+                 w_end = w_prec + 4 * G1_REC_WORDS * (batch ? n : 0) + 4;
     if ((rc = d.work.ensure(w_end))) return rc;
     uint8_t* in = static_cast<uint8_t*>(d.in.p);
     uint8_t* w = static_cast<uint8_t*>(d.work.p);
@@ -496,6 +526,7 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     auto* okw = reinterpret_cast<int32_t*>(w + w_ok);
     auto* frec = reinterpret_cast<uint32_t*>(w + w_frec);
     auto* jrec = reinterpret_cast<uint32_t*>(w + w_jrec);
+    auto* prec = reinterpret_cast<uint32_t*>(w + w_prec);
     if (!d.ev[0])
         for (auto& e : d.ev) BLS_HIP(hipEventCreate(&e));
     hipStream_t s0 = d.stream, s1 = d.side[0], s2 = d.side[1];
@@ -517,9 +548,9 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     BLS_HIP(hipEventRecord(d.ev[10], s1));
     // side 1: hash to G1 (every item: the statuses are not known yet)
     BLS_HIP(hipEventRecord(d.ev[5], s2));
-    hipLaunchKernelGGL(k_bls_h2c, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s2, (uint32_t)n, in + o_msg,
+    hipLaunchKernelGGL(k_bls_h2c_g, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s2, (uint32_t)n, in + o_msg,
                        reinterpret_cast<const uint64_t*>(in + o_moff), reinterpret_cast<const uint32_t*>(in + o_mlen),
-                       in + o_dst, (uint32_t)dl, (const int32_t*)nullptr, hrec);
+                       in + o_dst, (uint32_t)dl, hrec);
     BLS_HIP(hipEventRecord(d.ev[6], s2));
     BLS_HIP(hipEventRecord(d.ev[11], s2));
     // main: signatures, then the join
@@ -537,13 +568,15 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     };
     int32_t* hst = reinterpret_cast<int32_t*>(h + al(a.total));  // pinned: the batch verdict word
     if (batch) {
-        hipLaunchKernelGGL(k_bls_rlc, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, (const uint32_t*)srec,
-                           (const uint32_t*)hrec, (const uint32_t*)arec, (const int32_t*)st,
-                           (const uint8_t*)(in + o_seed), frec, jrec);
+        hipLaunchKernelGGL(k_bls_rlc_pts, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, (const uint32_t*)srec,
+                           (const uint32_t*)hrec, (const int32_t*)st, (const uint8_t*)(in + o_seed), prec, jrec);
         for (uint32_t m = (uint32_t)n; m > 1; m = (m + 1) / 2)
-            hipLaunchKernelGGL(k_bls_fold, dim3(gBlocks(m / 2)), dim3(BLS_LANES), 0, s0, m, frec, jrec);
-        hipLaunchKernelGGL(k_bls_final, dim3(1), dim3(BLS_LANES), 0, s0, (const uint32_t*)frec, (const uint32_t*)jrec,
-                           okw);
+            hipLaunchKernelGGL(k_bls_sfold, dim3(kBlocks(m / 2)), dim3(BLS_LANES), 0, s0, m, jrec);
+        hipLaunchKernelGGL(k_bls_rlc_ml, dim3(gBlocks(n + 1)), dim3(BLS_LANES), 0, s0, (uint32_t)n,
+                           (const uint32_t*)prec, (const uint32_t*)arec, (const uint32_t*)jrec, frec);
+        for (uint32_t m = (uint32_t)n + 1; m > 1; m = (m + 1) / 2)
+            hipLaunchKernelGGL(k_bls_ffold, dim3(gBlocks(m / 2)), dim3(BLS_LANES), 0, s0, m, frec);
+        hipLaunchKernelGGL(k_bls_final, dim3(1), dim3(BLS_LANES), 0, s0, (const uint32_t*)frec, okw);
         BLS_HIP(hipMemcpyAsync(hst, okw, 4, hipMemcpyDeviceToHost, s0));
         const hipError_t e = hipStreamSynchronize(s0);
         if (e != hipSuccess) {

@@ -3,6 +3,8 @@
 // oracle (oracle/bls_oracle.c), so the device arithmetic is checked before it meets a GPU.
 // Encodings as the oracle's: uncompressed affine big-endian (G1 x||y, G2 x.c1||x.c0||y.c1||y.c0),
 // all-zero = identity; GT as 12 big-endian Fp in tower order.
+#include <vector>
+
 #define BLS_GROUP_HOST_EMU 1  // bls_group.h: the host form of the lane-group arithmetic
 #include "../../narwhal_amd/csrc/bls_verify.h"
 
@@ -142,45 +144,34 @@ int bh_g_fast_aggregate_verify(const uint8_t* sig, size_t n_pks, const uint8_t* 
 }
 
 // the batch check over n items (item i: signature sig + 48 i, one key pk + 96 i, message msg + 32 i)
-// exactly as the kernels run it: shares, the product tree level by level, the final lane.
-// Returns 1 if the batch check accepts, 0 if it rejects, -1 if some item fails to decode.
+// exactly as the kernels stage it: points, the G1 tree, the Miller loops (items and (-S, g2)), the
+// Fp12 tree, the final exponentiation.  1 accept, 0 reject, -1 if some item fails to decode.
 int bh_rlc_batch(size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint8_t* seed,
-                 const uint8_t* dst, size_t dl, int group) {
-    uint32_t* f = new uint32_t[F12_REC_WORDS * n];
-    uint32_t* j = new uint32_t[G1J_REC_WORDS * n];
-    int rc = 1;
+                 const uint8_t* dst, size_t dl) {
+    const GCtx g{};
+    std::vector<uint32_t> f(F12_REC_WORDS * (n + 1)), sj(G1J_REC_WORDS * n), pr(G1_REC_WORDS * n),
+        ar(G2_REC_WORDS * n);
     for (size_t i = 0; i < n; i++) {
-        uint32_t srec[G1_REC_WORDS], hrec[G1_REC_WORDS], krec[G2_REC_WORDS], arec[G2_REC_WORDS];
+        uint32_t srec[G1_REC_WORDS], hrec[G1_REC_WORDS], krec[G2_REC_WORDS];
         const uint32_t idx = 0;
         int32_t kst = key_decode(pks + 96 * i, krec);
-        if (sig_decode(sigs + 48 * i, srec) != ST_OK || kst != ST_OK || apk_record(krec, &kst, &idx, 1, arec) != ST_OK) {
-            rc = -1;
-            break;
-        }
+        if (sig_decode(sigs + 48 * i, srec) != ST_OK || kst != ST_OK ||
+            apk_record(krec, &kst, &idx, 1, ar.data() + G2_REC_WORDS * i) != ST_OK)
+            return -1;
         h2c_record(msgs + 32 * i, 32, dst, (uint32_t)dl, hrec);
-        if (group)
-            g_rlc_item(GCtx{}, srec, hrec, arec, rlc_scalar(seed, (uint32_t)i), f + F12_REC_WORDS * i,
-                       j + G1J_REC_WORDS * i);
-        else
-            rlc_item(srec, hrec, arec, rlc_scalar(seed, (uint32_t)i), f + F12_REC_WORDS * i, j + G1J_REC_WORDS * i);
+        g_rlc_points(g, srec, hrec, rlc_scalar(seed, (uint32_t)i), pr.data() + G1_REC_WORDS * i,
+                     sj.data() + G1J_REC_WORDS * i);
     }
-    if (rc == 1) {
-        for (size_t m = n; m > 1; m = (m + 1) / 2) {
-            const size_t h = (m + 1) / 2;
-            for (size_t i = 0; i < m - h; i++) {
-                if (group)
-                    g_rlc_fold(GCtx{}, f + F12_REC_WORDS * i, j + G1J_REC_WORDS * i, f + F12_REC_WORDS * (i + h),
-                               j + G1J_REC_WORDS * (i + h));
-                else
-                    rlc_fold(f + F12_REC_WORDS * i, j + G1J_REC_WORDS * i, f + F12_REC_WORDS * (i + h),
-                             j + G1J_REC_WORDS * (i + h));
-            }
-        }
-        rc = (group ? g_rlc_final(GCtx{}, f, j) : rlc_final(f, j)) ? 1 : 0;
-    }
-    delete[] f;
-    delete[] j;
-    return rc;
+    for (size_t m = n; m > 1; m = (m + 1) / 2)
+        for (size_t i = 0; i < m - (m + 1) / 2; i++)
+            rlc_sfold(sj.data() + G1J_REC_WORDS * i, sj.data() + G1J_REC_WORDS * (i + (m + 1) / 2));
+    for (size_t i = 0; i < n; i++)
+        g_rlc_ml(g, pr.data() + G1_REC_WORDS * i, ar.data() + G2_REC_WORDS * i, f.data() + F12_REC_WORDS * i);
+    g_rlc_ml_sig(g, sj.data(), f.data() + F12_REC_WORDS * n);
+    for (size_t m = n + 1; m > 1; m = (m + 1) / 2)
+        for (size_t i = 0; i < m - (m + 1) / 2; i++)
+            g_rlc_ffold(g, f.data() + F12_REC_WORDS * i, f.data() + F12_REC_WORDS * (i + (m + 1) / 2));
+    return g_rlc_final(g, f.data()) ? 1 : 0;
 }
 
 }  // extern "C"

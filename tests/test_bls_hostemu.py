@@ -31,7 +31,7 @@ def emu():
     L.bh_keygen.argtypes = [c, vp]
     L.bh_sign.argtypes = [c, c, sz, c, sz, vp]
     L.bh_fast_aggregate_verify.argtypes = [c, sz, c, c, sz, c, sz]
-    L.bh_rlc_batch.argtypes = [sz, c, c, c, c, c, sz, ctypes.c_int]
+    L.bh_rlc_batch.argtypes = [sz, c, c, c, c, c, sz]
     L.bh_g_pairing.argtypes = [c, c, vp]
     L.bh_g_fast_aggregate_verify.argtypes = [c, sz, c, c, sz, c, sz]
     return L
@@ -126,15 +126,20 @@ def test_rlc_batch_check(emu, gold):
     msgs = [bytes([i]) * 32 for i in range(5)]
     sigs = [B.sign(sks[i % 4], m) for i, m in enumerate(msgs)]
     keys = [pks[i % 4] for i in range(5)]
-    for group in (0, 1):  # bls381.h's single-lane tower, then bls_group.h (what the kernels run)
-        for n in (1, 2, 3, 5):
-            assert emu.bh_rlc_batch(n, b"".join(sigs[:n]), b"".join(keys[:n]), b"".join(msgs[:n]), seed, dst,
-                                    len(dst), group) == 1
-            for bad in range(n):
-                m2 = list(msgs[:n])
-                m2[bad] = bytes([0xee]) * 32
-                assert emu.bh_rlc_batch(n, b"".join(sigs[:n]), b"".join(keys[:n]), b"".join(m2), seed, dst,
-                                        len(dst), group) == 0
+    for n in (1, 2, 3, 5):
+        assert emu.bh_rlc_batch(n, b"".join(sigs[:n]), b"".join(keys[:n]), b"".join(msgs[:n]), seed, dst,
+                                len(dst)) == 1
+        for bad in range(n):
+            m2 = list(msgs[:n])
+            m2[bad] = bytes([0xee]) * 32
+            assert emu.bh_rlc_batch(n, b"".join(sigs[:n]), b"".join(keys[:n]), b"".join(m2), seed, dst,
+                                    len(dst)) == 0
+        # a signature swapped between two items: each item's equation fails, the sums still match
+        if n >= 2:
+            s2 = list(sigs[:n])
+            s2[0], s2[1] = s2[1], s2[0]
+            assert emu.bh_rlc_batch(n, b"".join(s2), b"".join(keys[:n]), b"".join(msgs[:n]), seed, dst,
+                                    len(dst)) == 0
 
 
 def test_group_pairing_matches_single_lane(emu):
