@@ -284,23 +284,27 @@ inline G12 g_load(const GCtx&, const uint32_t* o) {
 #endif
 G_HD G12 g_inv(const GCtx& g, const G12& a) { return g_scatter(g, f12_inv(g_gather(g, a))); }
 
-// prod_{i < n} f_{|x|, Q_i}(P_i), conjugated (x < 0); n <= 2 (miller_loop2 over a group)
-G_NOINLINE G12 g_miller(const GCtx& g, int n, const fp* px, const fp* py, const fp2* qx, const fp2* qy) {
-    jac<fp2> T[2];
-    for (int i = 0; i < n; i++) T[i] = jac_from_affine(qx[i], qy[i]);
+// prod_{i < N} f_{|x|, Q_i}(P_i), conjugated (x < 0) (miller_loop2 over a group).  N is a template
+// parameter so the per-pair loops unroll and the G2 points stay in registers (a runtime pair count
+// indexes T[], px[], ... dynamically and puts them in scratch: 2x slower, measured)
+template <int N>
+G_NOINLINE G12 g_miller(const GCtx& g, const fp* px, const fp* py, const fp2* qx, const fp2* qy) {
+    jac<fp2> T[N];
+#pragma unroll
+    for (int i = 0; i < N; i++) T[i] = jac_from_affine(qx[i], qy[i]);
     G12 f = g_one(g);
     fp2 l0, l1, l4;
 #pragma unroll 1
     for (int b = 62; b >= 0; b--) {
         if (b != 62) f = g_sqr(g, f);
-#pragma unroll 1
-        for (int i = 0; i < n; i++) {
+#pragma unroll
+        for (int i = 0; i < N; i++) {
             ml_dbl(T[i], l0, l1, l4);
             f = g_mul_line(g, f, l0, f2_mul_fp(l1, px[i]), f2_mul_fp(l4, py[i]));
         }
         if ((BLS_X_ABS >> b) & 1) {
-#pragma unroll 1
-            for (int i = 0; i < n; i++) {
+#pragma unroll
+            for (int i = 0; i < N; i++) {
                 ml_add(T[i], qx[i], qy[i], l0, l1, l4);
                 f = g_mul_line(g, f, l0, f2_mul_fp(l1, px[i]), f2_mul_fp(l4, py[i]));
             }

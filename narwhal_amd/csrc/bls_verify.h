@@ -183,7 +183,9 @@ G_HD bool g_pairing_check(const GCtx& g, const uint32_t* sig_rec, const uint32_t
         ld_g2(apk_rec, qx[n], qy[n]);
         n++;
     }
-    return g_is_one(g, g_final_exp(g, g_miller(g, n, px, py, qx, qy)));
+    const G12 f = n == 2 ? g_miller<2>(g, px, py, qx, qy)
+                : n == 1 ? g_miller<1>(g, px, py, qx, qy) : g_one(g);
+    return g_is_one(g, g_final_exp(g, f));
 }
 
 // stage 1, item i (one group): P_i = [r] H (affine record, identity flag) and s_i = [r] sig
@@ -234,7 +236,7 @@ G_HD void g_rlc_ml(const GCtx& g, const uint32_t* p_rec, const uint32_t* apk_rec
         const fp px = ld_fp(p_rec), py = ld_fp(p_rec + NL);
         fp2 qx, qy;
         ld_g2(apk_rec, qx, qy);
-        f = g_miller(g, 1, &px, &py, &qx, &qy);
+        f = g_miller<1>(g, &px, &py, &qx, &qy);
     }
     g_store(g, f_out, f);
 }
@@ -246,7 +248,7 @@ G_HD void g_rlc_ml_sig(const GCtx& g, const uint32_t* s_rec, uint32_t* f_out) {
         g1_to_affine(px, py, S);
         py = fp_neg(py);
         const fp2 qx = k_g2x(), qy = k_g2y();
-        f = g_miller(g, 1, &px, &py, &qx, &qy);
+        f = g_miller<1>(g, &px, &py, &qx, &qy);
     }
     g_store(g, f_out, f);
 }

@@ -115,7 +115,7 @@ void bh_g_pairing(const uint8_t* P, const uint8_t* Q, uint8_t* out) {
     be_to_mont(qy.c1, Q + 96);
     be_to_mont(qy.c0, Q + 144);
     const GCtx g{};
-    const fp12 e = g_gather(g, g_final_exp(g, g_miller(g, 1, &px, &py, &qx, &qy)));
+    const fp12 e = g_gather(g, g_final_exp(g, g_miller<1>(g, &px, &py, &qx, &qy)));
     const fp* c[12] = {&e.c0.c0.c0, &e.c0.c0.c1, &e.c0.c1.c0, &e.c0.c1.c1, &e.c0.c2.c0, &e.c0.c2.c1,
                        &e.c1.c0.c0, &e.c1.c0.c1, &e.c1.c1.c0, &e.c1.c1.c1, &e.c1.c2.c0, &e.c1.c2.c1};
     for (int i = 0; i < 12; i++) mont_to_be(out + 48 * i, *c[i]);

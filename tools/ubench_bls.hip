@@ -105,7 +105,7 @@ GK(k_g_fexp, for (int i = 0; i < reps; i++) a = g_final_exp(g, a))
 __device__ G12 miller_reps(const GCtx& g, G12 a, int reps) {
     fp px = k_g1x(), py = k_g1y();
     fp2 qx = k_g2x(), qy = k_g2y();
-    for (int i = 0; i < reps; i++) a = g_mul(g, a, g_miller(g, 1, &px, &py, &qx, &qy));
+    for (int i = 0; i < reps; i++) a = g_mul(g, a, g_miller<1>(g, &px, &py, &qx, &qy));
     return a;
 }
 GK(k_g_miller, a = miller_reps(g, a, reps))
