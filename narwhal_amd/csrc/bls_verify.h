@@ -240,17 +240,18 @@ G_HD void g_rlc_ml(const GCtx& g, const uint32_t* p_rec, const uint32_t* apk_rec
     }
     g_store(g, f_out, f);
 }
-G_HD void g_rlc_ml_sig(const GCtx& g, const uint32_t* s_rec, uint32_t* f_out) {
+// the combination's signature side as one more item: P = -S (affine record) and Q = g2, so the
+// Miller-loop grid runs one code path on every group (a different path on one group of a wave
+// would serialise the wave: measured 2x)
+NWV_HD void rlc_sig_item(const uint32_t* s_rec, uint32_t* p_out, uint32_t* q_out) {
     const jac<fp> S = ld_g1j(s_rec);
-    G12 f = g_one(g);
+    fp x = fp_zero(), y = fp_zero();
     if (!S.inf) {
-        fp px, py;
-        g1_to_affine(px, py, S);
-        py = fp_neg(py);
-        const fp2 qx = k_g2x(), qy = k_g2y();
-        f = g_miller<1>(g, &px, &py, &qx, &qy);
+        g1_to_affine(x, y, S);
+        y = fp_neg(y);
     }
-    g_store(g, f_out, f);
+    st_g1(p_out, x, y, S.inf);
+    st_g2(q_out, k_g2x(), k_g2y(), false);
 }
 // the trees: f_a <- f_a f_b (a group), s_a <- s_a + s_b (a lane)
 G_HD void g_rlc_ffold(const GCtx& g, uint32_t* fa, const uint32_t* fb) {

@@ -172,6 +172,7 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_pair(uint32_t n, const uint32
 // the batch check (bls_verify.h), in stages:
 //   k_bls_rlc_pts   one group per item: P_i = [r_i] H_i (affine), s_i = [r_i] sig_i
 //   k_bls_sfold     ceil(log2 n) levels of G1 sums: S = sum s_i
+//   k_bls_sig_item  one lane: (-S, g2) as item n
 //   k_bls_rlc_ml    one group per item and one more: the Miller loops of (P_i, apk_i) and (-S, g2)
 //   k_bls_ffold     ceil(log2 (n + 1)) levels of group Fp12 products
 //   k_bls_final     one group: the final exponentiation, == 1
@@ -194,15 +195,15 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_sfold(uint32_t m, uint32_t* s
     BLS_IDX();
     rlc_sfold(srec + (size_t)G1J_REC_WORDS * i, srec + (size_t)G1J_REC_WORDS * (i + h));
 }
-__global__ __launch_bounds__(BLS_LANES) void k_bls_rlc_ml(uint32_t n_items, const uint32_t* prec, const uint32_t* apk_rec,
-                                                          const uint32_t* srec, uint32_t* frec) {
-    const uint32_t n = n_items + 1;
+// -S (affine) and g2 as item n of the Miller-loop grid (srec[0] = S after the G1 tree)
+__global__ void k_bls_sig_item(uint32_t n, const uint32_t* srec, uint32_t* prec, uint32_t* apk_rec) {
+    if (blockIdx.x || threadIdx.x) return;
+    rlc_sig_item(srec, prec + (size_t)G1_REC_WORDS * n, apk_rec + (size_t)G2_REC_WORDS * n);
+}
+__global__ __launch_bounds__(BLS_LANES) void k_bls_rlc_ml(uint32_t n, const uint32_t* prec, const uint32_t* apk_rec,
+                                                          uint32_t* frec) {
     BLS_GIDX();
-    uint32_t* f = frec + (size_t)F12_REC_WORDS * i;
-    if (i < n_items)
-        g_rlc_ml(g, prec + (size_t)G1_REC_WORDS * i, apk_rec + (size_t)G2_REC_WORDS * i, f);
-    else
-        g_rlc_ml_sig(g, srec, f);  // srec[0] = S after the G1 tree
+    g_rlc_ml(g, prec + (size_t)G1_REC_WORDS * i, apk_rec + (size_t)G2_REC_WORDS * i, frec + (size_t)F12_REC_WORDS * i);
 }
 __global__ __launch_bounds__(BLS_LANES) void k_bls_ffold(uint32_t m, uint32_t* frec) {
     const uint32_t h = (m + 1) / 2;
@@ -507,11 +508,11 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     // the batch check's shares (W-order Fp12 + Jacobian G1 per item) and its verdict word
     const size_t w_krec = 0, w_kst = w_krec + (cached ? 0 : 4 * G2_REC_WORDS * n_keys),
                  w_srec = al(w_kst + (cached ? 0 : 4 * n_keys)), w_hrec = w_srec + 4 * G1_REC_WORDS * n,
-                 w_arec = w_hrec + 4 * G1_REC_WORDS * n, w_st = w_arec + 4 * G2_REC_WORDS * n,
+                 w_arec = w_hrec + 4 * G1_REC_WORDS * n, w_st = w_arec + 4 * G2_REC_WORDS * (n + 1),
                  w_ssig = al(w_st + 4 * n), w_sapk = al(w_ssig + 4 * n), w_ok = al(w_sapk + 4 * n),
                  w_frec = al(w_ok + 4), w_jrec = al(w_frec + 4 * F12_REC_WORDS * (batch ? n + 1 : 0)),
                  w_prec = al(w_jrec + 4 * G1J_REC_WORDS * (batch ? n : 0)),
-                 w_end = w_prec + 4 * G1_REC_WORDS * (batch ? n : 0) + 4;
+                 w_end = w_prec + 4 * G1_REC_WORDS * (batch ? n + 1 : 0) + 4;
     if ((rc = d.work.ensure(w_end))) return rc;
     uint8_t* in = static_cast<uint8_t*>(d.in.p);
     uint8_t* w = static_cast<uint8_t*>(d.work.p);
@@ -572,8 +573,10 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
                            (const uint32_t*)hrec, (const int32_t*)st, (const uint8_t*)(in + o_seed), prec, jrec);
         for (uint32_t m = (uint32_t)n; m > 1; m = (m + 1) / 2)
             hipLaunchKernelGGL(k_bls_sfold, dim3(kBlocks(m / 2)), dim3(BLS_LANES), 0, s0, m, jrec);
-        hipLaunchKernelGGL(k_bls_rlc_ml, dim3(gBlocks(n + 1)), dim3(BLS_LANES), 0, s0, (uint32_t)n,
-                           (const uint32_t*)prec, (const uint32_t*)arec, (const uint32_t*)jrec, frec);
+        hipLaunchKernelGGL(k_bls_sig_item, dim3(1), dim3(BLS_LANES), 0, s0, (uint32_t)n, (const uint32_t*)jrec, prec,
+                           arec);
+        hipLaunchKernelGGL(k_bls_rlc_ml, dim3(gBlocks(n + 1)), dim3(BLS_LANES), 0, s0, (uint32_t)(n + 1),
+                           (const uint32_t*)prec, (const uint32_t*)arec, frec);
         for (uint32_t m = (uint32_t)n + 1; m > 1; m = (m + 1) / 2)
             hipLaunchKernelGGL(k_bls_ffold, dim3(gBlocks(m / 2)), dim3(BLS_LANES), 0, s0, m, frec);
         hipLaunchKernelGGL(k_bls_final, dim3(1), dim3(BLS_LANES), 0, s0, (const uint32_t*)frec, okw);

@@ -453,6 +453,8 @@ def leg_bls(eng, certs=100, quorum=67, committee=100, reps=20, throughput_n=1638
             t1.append(time.perf_counter() - t0)
         assert rc == 0
     out["single_verify_ms_p50"] = float(np.median(t1)) * 1e3
+    if not throughput_n:
+        return out
     # throughput: throughput_n items, one key each (a header's / vote's single signature)
     n = throughput_n
     msgs = [rnd.bytes(32) for _ in range(n)]

@@ -109,6 +109,22 @@ __device__ G12 miller_reps(const GCtx& g, G12 a, int reps) {
     return a;
 }
 GK(k_g_miller, a = miller_reps(g, a, reps))
+// the same Miller loop with P, Q read from memory (runtime values, as the verification kernels see)
+__device__ uint32_t d_pq[2 * NL + 4 * NL];
+__device__ G12 miller_reps_mem(const GCtx& g, G12 a, int reps) {
+    const fp px = ld_fp(d_pq), py = ld_fp(d_pq + NL);
+    const fp2 qx = ld_f2(d_pq + 2 * NL), qy = ld_f2(d_pq + 4 * NL);
+    for (int i = 0; i < reps; i++) a = g_mul(g, a, g_miller<1>(g, &px, &py, &qx, &qy));
+    return a;
+}
+GK(k_g_miller_mem, a = miller_reps_mem(g, a, reps))
+__global__ void k_init_pq() {
+    if (threadIdx.x || blockIdx.x) return;
+    st_fp(d_pq, k_g1x());
+    st_fp(d_pq + NL, k_g1y());
+    st_f2(d_pq + 2 * NL, k_g2x());
+    st_f2(d_pq + 4 * NL, k_g2y());
+}
 
 typedef void (*kfn)(int, uint32_t*);
 
@@ -125,10 +141,11 @@ int main() {
               {"final_exp", k_fexp, 1, 6000},      {"group8_f12_mul", k_g_mul, 200, 54},
               {"group8_f12_sqr", k_g_sqr, 200, 36}, {"group8_cyc_sqr", k_g_cyc, 200, 18},
               {"group8_line_mul", k_g_line, 200, 13}, {"group8_miller_loop_1pair", k_g_miller, 1, 6800},
-              {"group8_final_exp", k_g_fexp, 1, 6000}};
+              {"group8_final_exp", k_g_fexp, 1, 6000}, {"group8_miller_loop_1pair_mem", k_g_miller_mem, 1, 6800}};
     const int blocks_full = 256 * 4 * 2;  // two waves per SIMD
     uint32_t* out;
     if (hipMalloc(&out, 4 * 64 * blocks_full) != hipSuccess) return 2;
+    hipLaunchKernelGGL(k_init_pq, dim3(1), dim3(64), 0, 0);
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
