@@ -89,6 +89,16 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_apk_g(uint32_t n, const uint3
     const uint32_t cnt = pk_cnt[i];
     const uint32_t* idx = pk_idx + pk_off[i];
     uint32_t* out = rec + (size_t)G2_REC_WORDS * i;
+    if (cnt == 1) {  // one key (Verifier::verify): its validated record is the sum, no inversion
+        if (g.slot < G2_REC_WORDS) {
+            const uint32_t k = idx[0];
+            const bool ok = key_st[k] == ST_OK;
+            for (int w = g.slot; w < G2_REC_WORDS; w += GRP)
+                out[w] = ok ? key_rec[(size_t)k * G2_REC_WORDS + w] : (w == 4 * NL ? 1u : 0u);
+            if (g.slot == 0) st_apk[i] = key_st[k];
+        }
+        return;
+    }
     jac<fp2> acc;
     acc.inf = true;
     acc.x = acc.y = acc.z = f2_zero();
