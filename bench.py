@@ -362,10 +362,7 @@ def timed_region(stages, args, dist, run):
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
-    stagger = getattr(args, "stagger_us", 0)
     for s in range(args.steps):
-        if stagger and s < len(stages):
-            stages[s].delay(s * stagger)  # start offsets inside the timed region (they are timed)
         run(stages[s % len(stages)])
     for s_ in stages:
         s_.sync()
@@ -423,9 +420,6 @@ class DryStage:
     def sync(self):
         pass
 
-    def delay(self, us):
-        pass
-
 
 def run_headline_dry(args, rank, world, dist):
     stages = [DryStage(args.n) for _ in range(max(1, args.inflight))]
@@ -454,14 +448,6 @@ def run_headline(args, eng, rank, world, dist):
     for s_ in stages:
         s_.run(mode=args.mode)
     check_all("setup")
-    if args.chain and len(stages) > 1:
-        # ring of preps: stage k's prep starts after stage k - chain's latest prep (step s runs
-        # stage s % K, so with chain 1 step s's prep follows step s - 1's)
-        for k, s_ in enumerate(stages):
-            s_.follow(stages[(k - args.chain) % len(stages)])
-        for s_ in stages:  # capture the split graphs (untimed), verdicts checked again
-            s_.run(mode=args.mode)
-        check_all("setup, chained")
     dt, dt_max = timed_region(stages, args, dist, lambda st: st.run(mode=args.mode))  # seed None: OS entropy
     check_all("timed region: last run of every stage")
     steady = steady_state(stages, args, lambda st: st.run(mode=args.mode))
@@ -470,8 +456,7 @@ def run_headline(args, eng, rank, world, dist):
         check_all("steady-state steps")
     if args.mode == 1:
         # every run's batch verdict, graph replays included, as tallied on the device by the runs
-        runs = (len(stages) * (2 if args.chain and len(stages) > 1 else 1) + args.warmup + args.steps +
-                (steady["steps"] if steady else 0))
+        runs = len(stages) + args.warmup + args.steps + (steady["steps"] if steady else 0)
         acc = rej = 0
         for s_ in stages:
             a_, r_ = s_.run_tally()
@@ -740,8 +725,7 @@ def base_line(args, world, dt):
                    "distinct_keys": args.keys or args.n,
                    "parallelism": "one GPU" if world == 1 else f"x{world} GPUs, one resident batch "
                                   "stream per rank, no collective",
-                   "inflight_batches": args.inflight, "stagger_us": args.stagger_us,
-                   "prep_chain": args.chain},
+                   "inflight_batches": args.inflight},
     }
 
 
@@ -763,10 +747,6 @@ def main():
                          "100: its committee variant, keyed batch MSM)")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the C1 / C3 / C4 / C5 legs (other BASELINE.json configs, GPU and CPU)")
-    ap.add_argument("--chain", type=int, default=0,
-                    help="in-flight batch k's prep waits for batch k - CHAIN's latest prep (0: no chain)")
-    ap.add_argument("--stagger-us", type=int, default=0,
-                    help="start offset between the in-flight batches' first timed steps, us (timed)")
     ap.add_argument("--steady-steps", type=int, default=96,
                     help="extra steps after the timed region that measure the steady-state rate (not `value`)")
     ap.add_argument("--single-steps", type=int, default=8,

@@ -219,17 +219,6 @@ int nwv_staged_run_tally(nwv_staged* st, uint64_t out[2]);
  * when the work queued before it on that stream is done); *ms = time from a's mark to b's */
 int nwv_staged_mark(nwv_staged* st, int slot);
 int nwv_staged_mark_elapsed(nwv_staged* a, int slot_a, nwv_staged* b, int slot_b, float* ms);
-/* queue a start offset of `us` microseconds (<= 100000) on the batch's stream ahead of its next
- * run: one sleeping wave, no other device resources.  Batches started together on several
- * streams run their phases in lockstep (every prep, then every sort, then every latency-bound
- * tail); offsets of a fraction of one batch's latency put them out of phase from the start. */
-int nwv_staged_delay(nwv_staged* st, uint32_t us);
-/* from now on, each batch-MSM run of `st` starts its prep kernels only once the latest prep
- * queued on `prev` (same device) has finished; prev = NULL ends it.  Batches chained in a ring
- * pass their preps (the VALU-bound phase) along in order instead of sharing the chip evenly, so
- * each one's sorts, buckets and latency-bound tail overlap the next ones' preps.  Issue both
- * batches' runs from one thread, and end the link before freeing `prev`. */
-int nwv_staged_follow(nwv_staged* st, nwv_staged* prev);
 void nwv_staged_free(nwv_staged* st);
 
 /* ------------------------------------------------------------------ synthetic data ----- */

@@ -84,8 +84,6 @@ def load():
         "nwv_staged_run_tally": ([_vp, _vp], _i32),
         "nwv_staged_mark": ([_vp, _i32], _i32),
         "nwv_staged_mark_elapsed": ([_vp, _i32, _vp, _i32, ctypes.POINTER(ctypes.c_float)], _i32),
-        "nwv_staged_delay": ([_vp, ctypes.c_uint32], _i32),
-        "nwv_staged_follow": ([_vp, _vp], _i32),
         "nwv_ed25519_sign_many": ([_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp], _i32),
     }
     for name, (args, res) in sig.items():
@@ -357,14 +355,6 @@ class Staged:
     def mark(self, slot):
         """record step-completion event `slot` on this batch's stream"""
         _check(self.eng.lib.nwv_staged_mark(self._h, slot))
-
-    def delay(self, us):
-        """queue a start offset of `us` microseconds on this batch's stream before its next run"""
-        _check(self.eng.lib.nwv_staged_delay(self._h, int(us)))
-
-    def follow(self, prev):
-        """start this batch's prep only after `prev`'s latest prep has finished (None: unlink)"""
-        _check(self.eng.lib.nwv_staged_follow(self._h, prev._h if prev is not None else None))
 
     def mark_elapsed(self, slot, other, other_slot):
         """device ms from this batch's mark `slot` to `other`'s mark `other_slot`"""

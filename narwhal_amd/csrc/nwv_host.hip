@@ -12,7 +12,6 @@
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
-#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -546,10 +545,8 @@ constexpr int MSM_NEVENTS = MSM_NKERNELS + 1;  // one event before each kernel, 
 
 // Launch the batch MSM on resident buffers; the verdict word (1 = batch accepted) is
 // m_state[1] (m_state[0] = failure flags).  ev: MSM_NEVENTS events or null.
-// prep_end: called on the host once the prep kernels are queued (the staged batches' split
-// capture ends its first graph there).
 int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStream_t stream,
-               hipEvent_t* ev, bool state_ready, const std::function<int()>* prep_end = nullptr) {
+               hipEvent_t* ev, bool state_ready) {
     if (n == 0) return NWV_OK;
     const size_t na = msm_na(b, n);
     const MsmPlan p = msm_plan(n, na, b.kc_split, (d.flags & NWV_FLAG_MSM_SORT2) ? 1 : 0);
@@ -595,7 +592,6 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     if ((rc = mark(2))) return rc;
     if (!fused) hipLaunchKernelGGL(k_msm_points, dim3(pblk), dim3(256), 0, stream, gp);
     if ((rc = mark(3))) return rc;
-    if (prep_end && (rc = (*prep_end)())) return rc;
     const size_t lds_nb = (size_t)4 << (p.lay.cmax - 1);
     uint32_t* kst = b.m_kstart.as<uint32_t>();
     uint32_t* tot = b.m_tiles.as<uint32_t>();  // [nw] entries per window, [MSM_MAX_WINDOWS] all
@@ -1084,13 +1080,6 @@ struct nwv_staged {
     hipEvent_t seed_ev[SEED_SLOTS] = {};
     uint64_t seed_runs = 0;
     std::vector<hipEvent_t> marks;  // nwv_staged_mark: step-completion timestamps on this stream
-    // nwv_staged_follow: this batch's prep starts once `follow`'s latest prep has finished; the
-    // MSM is then replayed as two graphs (prep, the rest) with prep_done recorded between them
-    nwv_staged* follow = nullptr;
-    hipGraphExec_t graph_prep = nullptr, graph_rest = nullptr;
-    bool split_failed = false;
-    hipEvent_t prep_done = nullptr;
-    bool prep_recorded = false;
 };
 
 // Shard [0, n) into contiguous, 64-aligned ranges over the context's devices and run fn(dev,
@@ -1610,45 +1599,6 @@ static int staged_graph(nwv_staged* st) {
     return NWV_OK;
 }
 
-// The same batch MSM captured as two graphs, cut after the prep kernels (nwv_staged_follow).
-static int staged_graph_split(nwv_staged* st) {
-    if (st->graph_prep || st->split_failed) return NWV_OK;
-    hipGraph_t g1 = nullptr, g2 = nullptr;
-    hipGraphExec_t x1 = nullptr, x2 = nullptr;
-    bool ok = hipStreamBeginCapture(st->stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
-    const std::function<int()> cut = [&]() -> int {
-        if (hipStreamEndCapture(st->stream, &g1) != hipSuccess || !g1) return NWV_ERR_HIP;
-        if (hipStreamBeginCapture(st->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) return NWV_ERR_HIP;
-        return NWV_OK;
-    };
-    const int rc = ok ? msm_launch(st->own, st->buf, st->n, nullptr, st->stream, nullptr, false, &cut) : NWV_ERR_HIP;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st->stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
-        ok = hipStreamEndCapture(st->stream, &g2) == hipSuccess && ok;
-    ok = ok && !rc && g1 && g2 && hipGraphInstantiate(&x1, g1, nullptr, nullptr, 0) == hipSuccess &&
-         hipGraphInstantiate(&x2, g2, nullptr, nullptr, 0) == hipSuccess;
-    if (ok) {
-        st->graph_prep = x1;
-        st->graph_rest = x2;
-    } else {
-        if (x1) (void)hipGraphExecDestroy(x1);
-        if (x2) (void)hipGraphExecDestroy(x2);
-        st->split_failed = true;  // runs replay the whole-MSM graph, unchained
-        (void)hipGetLastError();
-    }
-    if (g1) (void)hipGraphDestroy(g1);
-    if (g2) (void)hipGraphDestroy(g2);
-    return NWV_OK;
-}
-
-int nwv_staged_follow(nwv_staged* st, nwv_staged* prev) {
-    if (!st || prev == st) return set_err(NWV_ERR_ARG, "bad staged/follow");
-    std::lock_guard<std::mutex> g(st->mu);
-    if (prev && prev->own.ordinal != st->own.ordinal) return set_err(NWV_ERR_ARG, "follow across devices");
-    st->follow = prev;
-    return NWV_OK;
-}
-
 int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]) {
     const bool timed = (mode & NWV_RUN_TIMED) != 0;
     mode &= ~NWV_RUN_TIMED;
@@ -1678,18 +1628,7 @@ int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]) {
             std::memcpy(hs, seed, 32);
             NWV_HIP(hipMemcpyAsync(st->buf.m_state.as<uint32_t>() + 8, hs, 32, hipMemcpyHostToDevice, st->stream));
             NWV_HIP(hipEventRecord(st->seed_ev[slot], st->stream));
-            if (st->follow && (rc = staged_graph_split(st))) return rc;
-            if (st->follow && st->graph_prep) {
-                nwv_staged* f = st->follow;
-                if (f->prep_recorded) NWV_HIP(hipStreamWaitEvent(st->stream, f->prep_done, 0));
-                NWV_HIP(hipGraphLaunch(st->graph_prep, st->stream));
-                if (!st->prep_done) NWV_HIP(hipEventCreateWithFlags(&st->prep_done, hipEventDisableTiming));
-                NWV_HIP(hipEventRecord(st->prep_done, st->stream));
-                st->prep_recorded = true;
-                NWV_HIP(hipGraphLaunch(st->graph_rest, st->stream));
-            } else {
-                NWV_HIP(hipGraphLaunch(st->graph, st->stream));
-            }
+            NWV_HIP(hipGraphLaunch(st->graph, st->stream));
         } else {
             // first run of the batch (allocates its buffers) or a timed run; an untimed first run
             // also captures the graph the later runs replay
@@ -1832,27 +1771,6 @@ int nwv_staged_mark(nwv_staged* st, int slot) {
     return NWV_OK;
 }
 
-// One wave that sleeps until `ticks` of the constant-rate wall clock have passed: a start offset
-// queued ahead of a batch's run (nwv_staged_delay) holds no CU resources beyond that wave.
-__global__ __launch_bounds__(64) void k_stream_delay(uint64_t ticks) {
-    const uint64_t t0 = wall_clock64();
-    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
-}
-
-int nwv_staged_delay(nwv_staged* st, uint32_t us) {
-    if (!st || us > 100000) return set_err(NWV_ERR_ARG, "bad staged/delay");
-    std::lock_guard<std::mutex> g(st->mu);
-    int rc = with_device(st->own);
-    if (rc) return rc;
-    if (!us) return NWV_OK;
-    int khz = 0;
-    NWV_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, st->own.ordinal));
-    if (khz <= 0) return set_err(NWV_ERR_HIP, "no wall clock rate");
-    hipLaunchKernelGGL(k_stream_delay, dim3(1), dim3(64), 0, st->stream, (uint64_t)khz * us / 1000u);
-    NWV_HIP(hipGetLastError());
-    return NWV_OK;
-}
-
 int nwv_staged_mark_elapsed(nwv_staged* a, int slot_a, nwv_staged* b, int slot_b, float* ms) {
     if (!a || !b || !ms || slot_a < 0 || slot_b < 0 || (size_t)slot_a >= a->marks.size() ||
         (size_t)slot_b >= b->marks.size() || !a->marks[slot_a] || !b->marks[slot_b])
@@ -1870,9 +1788,6 @@ void nwv_staged_free(nwv_staged* st) {
         (void)hipSetDevice(st->own.ordinal);
         if (st->stream) (void)hipStreamSynchronize(st->stream);
         if (st->graph) (void)hipGraphExecDestroy(st->graph);
-        if (st->graph_prep) (void)hipGraphExecDestroy(st->graph_prep);
-        if (st->graph_rest) (void)hipGraphExecDestroy(st->graph_rest);
-        if (st->prep_done) (void)hipEventDestroy(st->prep_done);
         for (auto& e : st->seed_ev)
             if (e) (void)hipEventDestroy(e);
         st->seeds.release();

@@ -373,8 +373,6 @@ extern "C" {
         slot_b: c_int,
         ms: *mut f32,
     ) -> c_int;
-    pub fn nwv_staged_delay(st: *mut NwvStaged, us: u32) -> c_int;
-    pub fn nwv_staged_follow(st: *mut NwvStaged, prev: *mut NwvStaged) -> c_int;
     pub fn nwv_staged_free(st: *mut NwvStaged);
     // ---- synthetic signing, for workloads and tests (include/nwv.h)
     pub fn nwv_ed25519_sign_many(
