@@ -75,6 +75,35 @@ NWV_HD fp2 coef_mul(int k, const A& a, const B& b) {
     }
     return acc;
 }
+// c_k of a^2 in four Fp2 products instead of six: the terms a_r a_s and a_s a_r of coef_mul are
+// equal (and wrap together: r + s = k or k + 6), so c_k is the squares a_h^2 + a_{h+3}^2 plus twice
+// the pairs (h+1, h+5), (h+2, h+4) for k = 2h, and twice the pairs (h, h+1), (h+2, h+5),
+// (h+3, h+4) for k = 2h+1 (indices mod 6).  Every lane runs the same four products (the odd
+// lanes' fourth has weight 0), so the lanes of a group do not diverge.
+template <class A>
+NWV_HD fp2 coef_sqr(int k, const A& a) {
+    const int h = k >> 1;
+    const bool odd = (k & 1) != 0;
+    auto m6 = [](int x) { return x >= 6 ? x - 6 : x; };
+    fp2 acc = f2_zero();
+#pragma unroll 1
+    for (int m = 0; m < 4; m++) {
+        int i, j;
+        if (odd) {
+            i = m6(h + (m == 0 ? 0 : m == 1 ? 2 : 3));
+            j = m6(h + (m == 0 ? 1 : m == 1 ? 5 : 4));
+        } else {
+            i = m6(h + (m == 0 ? 0 : m == 1 ? 3 : m == 2 ? 1 : 2));
+            j = m6(h + (m == 0 ? 0 : m == 1 ? 3 : m == 2 ? 5 : 4));
+        }
+        fp2 t = f2_mul(a(i), a(j));
+        if (i + j >= 6) t = f2_mul_xi(t);
+        const int w = odd ? (m < 3 ? 2 : 0) : (m < 2 ? 1 : 2);
+        if (w != 0) acc = f2_add(acc, t);
+        if (w == 2) acc = f2_add(acc, t);
+    }
+    return acc;
+}
 // c_k of a * (L0 + L2 W^2 + L3 W^3): the Miller loop's sparse line product
 template <class A>
 NWV_HD fp2 coef_line(int k, const A& a, const fp2& L0, const fp2& L2, const fp2& L3) {
@@ -156,7 +185,7 @@ __device__ inline G12 g_sqr(const GCtx& g, const G12& a) {
     g_sync();
     g_put(g, 0, a.v);
     g_sync();
-    return G12{coef_mul(g.k, g_reader(g, 0), g_reader(g, 0))};
+    return G12{coef_sqr(g.k, g_reader(g, 0))};
 }
 __device__ inline G12 g_mul_line(const GCtx& g, const G12& a, const fp2& L0, const fp2& L2, const fp2& L3) {
     g_sync();
@@ -227,7 +256,11 @@ inline G12 g_mul(const GCtx&, const G12& a, const G12& b) {
     for (int k = 0; k < 6; k++) c.v[k] = coef_mul(k, HRead{a.v}, HRead{b.v});
     return c;
 }
-inline G12 g_sqr(const GCtx& g, const G12& a) { return g_mul(g, a, a); }
+inline G12 g_sqr(const GCtx&, const G12& a) {
+    G12 c;
+    for (int k = 0; k < 6; k++) c.v[k] = coef_sqr(k, HRead{a.v});
+    return c;
+}
 inline G12 g_mul_line(const GCtx&, const G12& a, const fp2& L0, const fp2& L2, const fp2& L3) {
     G12 c;
     for (int k = 0; k < 6; k++) c.v[k] = coef_line(k, HRead{a.v}, L0, L2, L3);

@@ -339,9 +339,16 @@ __device__ __forceinline__ uint64_t msm_window_points(uint64_t n, uint64_t na, i
 // Two-level sort (large batches, msm.h MsmSort2): lay is the coarse layout (widths reduced by
 // shift) and every digit counts in bin (|d| - 1) >> shift; k_msm_scatter then writes packed
 // entries (msm_pack2) that k_msm_lsort orders by the remaining low bits.
+// A batch whose prep flagged a failed decoding or an s >= l is rejected by k_msm_tail whatever the
+// sum is, so the kernels in between skip their work: the reference's batch verifier returns its
+// error before the multiscalar multiplication too.  (Plain load: the flag
+// was written by an earlier kernel of the same stream.)
+__device__ __forceinline__ bool msm_failed(const uint32_t* fail) { return *fail != 0u; }
+
 extern "C" __global__ void __launch_bounds__(256) k_msm_hist(
     uint64_t n, uint64_t na, MsmLayout lay, uint32_t chunk_pts, const int16_t* __restrict__ digits,
-    uint32_t* __restrict__ cnt, uint32_t* __restrict__ nzc, int shift) {
+    uint32_t* __restrict__ cnt, uint32_t* __restrict__ nzc, int shift, const uint32_t* __restrict__ fail) {
+    if (msm_failed(fail)) return;
     extern __shared__ uint32_t hist[];
     __shared__ uint32_t nz;
     const int w = blockIdx.y, nw_z = lay.nw_z, nb = 1 << (lay.width[w] - 1);
@@ -408,7 +415,8 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* wsum) {
 // every window its own count (tot[w]).
 extern "C" __global__ void __launch_bounds__(1024) k_msm_wscan(
     MsmLayout lay, uint32_t chunks, uint32_t* __restrict__ cnt, const uint32_t* __restrict__ nzc,
-    uint32_t* __restrict__ kstart, uint32_t* __restrict__ tot_out) {
+    uint32_t* __restrict__ kstart, uint32_t* __restrict__ tot_out, const uint32_t* __restrict__ fail) {
+    if (msm_failed(fail)) return;
     __shared__ uint32_t wsum[16];
     const int w = blockIdx.x, nb = 1 << (lay.width[w] - 1);
     uint32_t before = 0;
@@ -468,7 +476,9 @@ extern "C" __global__ void __launch_bounds__(1024) k_msm_wscan(
 // (replaces hist + scan + scatter)
 extern "C" __global__ void __launch_bounds__(1024) k_msm_sort1(
     uint64_t n, uint64_t na, MsmLayout lay, const int16_t* __restrict__ digits, uint32_t* __restrict__ kstart,
-    uint32_t* __restrict__ tot_out, uint32_t* __restrict__ entries, uint32_t seg, uint32_t* __restrict__ seg_key) {
+    uint32_t* __restrict__ tot_out, uint32_t* __restrict__ entries, uint32_t seg, uint32_t* __restrict__ seg_key,
+    const uint32_t* __restrict__ fail) {
+    if (msm_failed(fail)) return;
     extern __shared__ uint32_t cur[];
     __shared__ uint32_t wsum[16];
     const int w = blockIdx.x, nb = 1 << (lay.width[w] - 1);
@@ -544,7 +554,8 @@ extern "C" __global__ void __launch_bounds__(1024) k_msm_sort1(
 extern "C" __global__ void __launch_bounds__(256) k_msm_scatter(
     uint64_t n, uint64_t na, MsmLayout lay, MsmXcdMap xm, uint32_t chunks, uint32_t chunk_pts,
     const int16_t* __restrict__ digits, const uint32_t* __restrict__ off, uint32_t* __restrict__ entries,
-    int shift) {
+    int shift, const uint32_t* __restrict__ fail) {
+    if (msm_failed(fail)) return;
     extern __shared__ uint32_t cur[];
     const uint32_t g = blockIdx.x % MSM_XCD_GROUPS;
     uint32_t s = blockIdx.x / MSM_XCD_GROUPS;
@@ -585,7 +596,9 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_scatter(
 // cursors), so its lines are written whole.
 extern "C" __global__ void __launch_bounds__(256) k_msm_lsort(
     MsmLayout lay, MsmLayout lay2, int shift, const uint32_t* __restrict__ mid, const uint32_t* __restrict__ kst2,
-    const uint32_t* __restrict__ tot, uint32_t* __restrict__ entries, uint32_t* __restrict__ kstart) {
+    const uint32_t* __restrict__ tot, uint32_t* __restrict__ entries, uint32_t* __restrict__ kstart,
+    const uint32_t* __restrict__ fail) {
+    if (msm_failed(fail)) return;
     __shared__ uint32_t cur[1 << MSM_SORT2_MAX_SHIFT];
     __shared__ uint32_t wsum[4];
     const int w = blockIdx.y, s = blockIdx.x;
@@ -642,7 +655,8 @@ __device__ __forceinline__ ge_precomp msm_point_of(const uint32_t w[32], uint32_
 extern "C" __global__ void __launch_bounds__(256) k_msm_bucket(
     uint32_t T, uint32_t nkeys, const uint32_t* __restrict__ total, const uint32_t* __restrict__ entries,
     const uint32_t* __restrict__ kstart, const uint32_t* __restrict__ pts, uint32_t* __restrict__ bsum,
-    uint32_t* __restrict__ hpart, const uint32_t* __restrict__ seg_key) {
+    uint32_t* __restrict__ hpart, const uint32_t* __restrict__ seg_key, const uint32_t* __restrict__ fail) {
+    if (msm_failed(fail)) return;
     const uint32_t E = *total;
     const uint64_t k0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * T;
     if (k0 >= E) return;
@@ -726,7 +740,8 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_bucket(
 extern "C" __global__ void __launch_bounds__(256) k_msm_bucket_q(
     uint32_t T, uint32_t nkeys, const uint32_t* __restrict__ total, const uint32_t* __restrict__ entries,
     const uint32_t* __restrict__ kstart, const uint32_t* __restrict__ pts, uint32_t* __restrict__ bsum,
-    uint32_t* __restrict__ hpart, const uint32_t* __restrict__ seg_key) {
+    uint32_t* __restrict__ hpart, const uint32_t* __restrict__ seg_key, const uint32_t* __restrict__ fail) {
+    if (msm_failed(fail)) return;
     const uint32_t E = *total;
     const int q = threadIdx.x & 3;
     const uint64_t k0 = ((uint64_t)blockIdx.x * (blockDim.x >> 2) + (threadIdx.x >> 2)) * T;
@@ -1082,6 +1097,13 @@ __device__ __forceinline__ bool msm_tail_window(const MsmLayout& lay, const MsmT
 
 template <int PER>
 __device__ __forceinline__ void msm_tail_body(const MsmLayout& lay, const MsmTailArgs& a) {
+    if (msm_failed(a.fail)) {  // rejected at prep (the sort and bucket kernels skipped their work)
+        if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+            *a.verdict = 0u;
+            if (a.runs) a.runs[1] += 1u;
+        }
+        return;
+    }
     // 256 point slots of P3_WORDS; row-limb planes reuse the front once the slots are done;
     // the flag word sits behind the slots
     extern __shared__ uint32_t lds[];

@@ -600,7 +600,7 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
         // one chunk per window: the whole counting sort of a window in one workgroup (timed in
         // the k_msm_hist slot)
         hipLaunchKernelGGL(k_msm_sort1, dim3((unsigned)p.lay.nw), dim3(1024), lds_nb, stream, (uint64_t)n,
-                           (uint64_t)na, p.lay, digits, kst, tot, ent, p.seg, b.m_segkey.as<uint32_t>());
+                           (uint64_t)na, p.lay, digits, kst, tot, ent, p.seg, b.m_segkey.as<uint32_t>(), state);
         if ((rc = mark(4))) return rc;
         if ((rc = mark(5))) return rc;
     } else {
@@ -612,17 +612,17 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
         uint32_t* kst1 = p.shift ? b.m_kst2.as<uint32_t>() : kst;
         uint32_t* ent1 = p.shift ? b.m_mid.as<uint32_t>() : ent;
         hipLaunchKernelGGL(k_msm_hist, dim3(p.chunks, (unsigned)p.lay.nw), dim3(256), lds1, stream, (uint64_t)n,
-                           (uint64_t)na, l1, p.chunk_pts, digits, cnt, nzc, p.shift);
+                           (uint64_t)na, l1, p.chunk_pts, digits, cnt, nzc, p.shift, state);
         if ((rc = mark(4))) return rc;
         // per window: entry base, bucket totals -> scan -> absolute (bucket, chunk) slice offsets
         hipLaunchKernelGGL(k_msm_wscan, dim3((unsigned)p.lay.nw), dim3(1024), 0, stream, l1, p.chunks, cnt, nzc,
-                           kst1, tot);
+                           kst1, tot, state);
         if ((rc = mark(5))) return rc;
         hipLaunchKernelGGL(k_msm_scatter, dim3(MSM_XCD_GROUPS * p.xm.slots), dim3(256), lds1, stream, (uint64_t)n,
-                           (uint64_t)na, l1, p.xm, p.chunks, p.chunk_pts, digits, cnt, ent1, p.shift);
+                           (uint64_t)na, l1, p.xm, p.chunks, p.chunk_pts, digits, cnt, ent1, p.shift, state);
         if (p.shift)  // timed with k_msm_scatter
             hipLaunchKernelGGL(k_msm_lsort, dim3(1u << (p.lay2.cmax - 1), (unsigned)p.lay.nw), dim3(256), 0, stream,
-                               p.lay, p.lay2, p.shift, ent1, kst1, tot, ent, kst);
+                               p.lay, p.lay2, p.shift, ent1, kst1, tot, ent, kst, state);
     }
     if ((rc = mark(6))) return rc;
     const uint32_t* E = tot + MSM_MAX_WINDOWS;
@@ -635,11 +635,11 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     if (n <= bucket_quad_max_n)
         hipLaunchKernelGGL(k_msm_bucket_q, dim3((unsigned)((p.nseg + 63) / 64)), dim3(256), 0, stream, p.seg,
                            p.nkeys, E, ent, kst, b.m_pts.as<uint32_t>(), b.m_bsum.as<uint32_t>(),
-                           b.m_hpart.as<uint32_t>(), seg_key);
+                           b.m_hpart.as<uint32_t>(), seg_key, state);
     else
         hipLaunchKernelGGL(k_msm_bucket, dim3((unsigned)((p.nseg + 255) / 256)), dim3(256), 0, stream, p.seg,
                            p.nkeys, E, ent, kst, b.m_pts.as<uint32_t>(), b.m_bsum.as<uint32_t>(),
-                           b.m_hpart.as<uint32_t>(), seg_key);
+                           b.m_hpart.as<uint32_t>(), seg_key, state);
     if ((rc = mark(7))) return rc;
     // window sums, their scaling, the basepoint term and the verdict: one launch (its arrival
     // counters were zeroed by k_msm_prep's first workgroup, graph replays included)
