@@ -9,7 +9,8 @@
 // operands exchanged through LDS: 18 Fp multiplications deep instead of 54, with everything in
 // registers.  The sparse line product is 3 Fp2 products deep, the Granger-Scott cyclotomic square
 // 3 Fp2 squarings deep (lane k computes one of the six Fp4 half-products), the Frobenius map one
-// Fp2 product.  The Miller loop's G2 point and lines are computed redundantly by every lane.
+// Fp2 product.  The Miller loop's G2 doubling and its line run as rounds of independent Fp
+// products over the lanes (g_ml_dbl); its G2 additions are computed redundantly by every lane.
 //
 // Tower slot <-> W power: k 0 c0.c0, 1 c1.c0, 2 c0.c1, 3 c1.c1, 4 c0.c2, 5 c1.c2 (bls381.h).
 //
@@ -29,7 +30,10 @@ namespace bls {
 
 constexpr int GRP = 8;                   // lanes per group
 constexpr int F2W = 2 * NL;              // u32 words of an Fp2
-constexpr int GX_WORDS = 2 * GRP * F2W;  // one group's LDS exchange area: operand A slots, B slots
+// one group's LDS exchange area: operand A slots [GRP][F2W], B slots, and room for the 18 Fp
+// products of g_cyc_sqr behind the A slots (GRP F2W + 18 NL = 476 words)
+constexpr int GX_WORDS = 480;
+static_assert(GX_WORDS >= 2 * GRP * F2W && GX_WORDS >= GRP * F2W + 18 * NL, "group LDS area");
 
 NWV_HD void st_fp(uint32_t* o, const fp& a) { for (int j = 0; j < NL; j++) o[j] = a.l[j]; }
 NWV_HD fp ld_fp(const uint32_t* o) { fp a; for (int j = 0; j < NL; j++) a.l[j] = o[j]; return a; }
@@ -193,11 +197,39 @@ __device__ inline G12 g_mul_line(const GCtx& g, const G12& a, const fp2& L0, con
     g_sync();
     return G12{coef_line(g.k, g_reader(g, 0), L0, L2, L3)};
 }
+// The Granger-Scott square's 18 Fp products -- three Fp2 squarings x^2, y^2, (x + y)^2 of each
+// Fp4 pair (W^p, W^(p+3)), two products each -- spread over the group in three rounds instead of
+// six products on every lane; then lane k combines its pair's squares exactly as coef_cyc_sqr.
 __device__ inline G12 g_cyc_sqr(const GCtx& g, const G12& a) {
     g_sync();
     g_put(g, 0, a.v);
     g_sync();
-    return G12{coef_cyc_sqr(g.k, g_reader(g, 0))};
+    const GRead rd = g_reader(g, 0);
+    uint32_t* R = g.xa + GRP * F2W;  // product q at R + q NL (q = 6 pair + 2 square + part)
+#pragma unroll 1
+    for (int r = 0; r < 3; r++) {
+        const int q = r * GRP + g.slot;
+        if (r < 2 || g.slot < 2) {  // 18 products: the last round uses two lanes
+            const int p = q / 6, sq = (q % 6) >> 1;
+            const fp2 x = rd(p), y = rd(p + 3);
+            const fp2 v = sq == 0 ? x : sq == 1 ? y : f2_add(x, y);
+            const bool part = (q & 1) != 0;  // f2_sqr: (c0 + c1)(c0 - c1), then c0 c1
+            const fp pr = fp_mul(part ? v.c0 : fp_add(v.c0, v.c1), part ? v.c1 : fp_sub(v.c0, v.c1));
+            st_fp(R + q * NL, pr);
+        }
+    }
+    g_sync();
+    const int k = g.k;
+    const int p = (k == 0 || k == 3) ? 0 : (k == 2 || k == 5) ? 1 : 2;
+    const uint32_t* Rp = R + 6 * p * NL;
+    const fp2 t0 = fp2{ld_fp(Rp), fp_dbl(ld_fp(Rp + NL))};
+    const fp2 t1 = fp2{ld_fp(Rp + 2 * NL), fp_dbl(ld_fp(Rp + 3 * NL))};
+    const fp2 s = fp2{ld_fp(Rp + 4 * NL), fp_dbl(ld_fp(Rp + 5 * NL))};
+    const bool second = (k & 1) != 0;
+    fp2 o = second ? f2_sub(f2_sub(s, t0), t1) : f2_add(f2_mul_xi(t1), t0);
+    if (k == 1) o = f2_mul_xi(o);
+    const fp2 z = a.v;
+    return G12{second ? f2_add(f2_dbl(f2_add(o, z)), o) : f2_add(f2_dbl(f2_sub(o, z)), o)};
 }
 __device__ inline G12 g_conj(const GCtx& g, const G12& a) { return G12{(g.k & 1) ? f2_neg(a.v) : a.v}; }
 __device__ inline G12 g_frob(const GCtx& g, const G12& a) { return G12{f2_mul(f2_conj(a.v), w_gamma(g.k))}; }
@@ -329,6 +361,112 @@ inline G12 g_load(const GCtx&, const uint32_t* o) {
 #define G_HD inline
 #define G_NOINLINE __attribute__((noinline))
 #endif
+// ---- independent Fp products spread over the group's lanes ------------------------------------
+// r[j] = a[j] * b[j] for j < used (<= GRP).  The operands are the same on every lane of the group:
+// slot 0 publishes them through the group's LDS area, lane j computes product j, and every lane
+// reads all of them back -- one product deep instead of `used`.  Every index into a, b, r is a
+// compile-time constant (a lane-dependent index goes to LDS only).  (Publishing each operand as
+// soon as it is formed, so that no operand array stays live, measured 11 % slower on the Miller
+// loop: the arrays live in registers between the rounds' products anyway.)
+#ifdef BLS_GDEV
+__device__ __forceinline__ void g_fp_round(const GCtx& g, const fp (&a)[GRP], const fp (&b)[GRP], fp (&r)[GRP],
+                                           const int used) {
+    uint32_t* A = g.xa;
+    uint32_t* B = g.xa + GRP * NL;
+    uint32_t* R = g.xa + 2 * GRP * NL;  // 3 GRP NL = 336 words <= GX_WORDS
+    g_sync();
+    if (g.slot == 0) {
+#pragma unroll
+        for (int j = 0; j < GRP; j++)
+            if (j < used) {
+                st_fp(A + j * NL, a[j]);
+                st_fp(B + j * NL, b[j]);
+            }
+    }
+    g_sync();
+    const int s = g.slot < used ? g.slot : 0;
+    const fp p = fp_mul(ld_fp(A + s * NL), ld_fp(B + s * NL));
+    if (g.slot < used) st_fp(R + g.slot * NL, p);
+    g_sync();
+#pragma unroll
+    for (int j = 0; j < GRP; j++)
+        if (j < used) r[j] = ld_fp(R + j * NL);
+}
+#else
+inline void g_fp_round(const GCtx&, const fp (&a)[GRP], const fp (&b)[GRP], fp (&r)[GRP], const int used) {
+    for (int j = 0; j < used; j++) r[j] = fp_mul(a[j], b[j]);
+}
+#endif
+// operand pairs of f2_sqr / f2_mul / f2_mul_fp (bls381.h) at slots o.., and their results, so
+// that a round reproduces those functions' products exactly
+NWV_HD void ops_sqr(const fp2& x, fp (&a)[GRP], fp (&b)[GRP], int o) {
+    a[o] = fp_add(x.c0, x.c1);
+    b[o] = fp_sub(x.c0, x.c1);
+    a[o + 1] = x.c0;
+    b[o + 1] = x.c1;
+}
+NWV_HD fp2 res_sqr(const fp (&r)[GRP], int o) { return fp2{r[o], fp_dbl(r[o + 1])}; }
+NWV_HD void ops_mul(const fp2& x, const fp2& y, fp (&a)[GRP], fp (&b)[GRP], int o) {
+    a[o] = x.c0;
+    b[o] = y.c0;
+    a[o + 1] = x.c1;
+    b[o + 1] = y.c1;
+    a[o + 2] = fp_add(x.c0, x.c1);
+    b[o + 2] = fp_add(y.c0, y.c1);
+}
+NWV_HD fp2 res_mul(const fp (&r)[GRP], int o) {
+    return fp2{fp_sub(r[o], r[o + 1]), fp_sub(fp_sub(r[o + 2], r[o]), r[o + 1])};
+}
+NWV_HD void ops_mul_fp(const fp2& x, const fp& s, fp (&a)[GRP], fp (&b)[GRP], int o) {
+    a[o] = x.c0;
+    b[o] = s;
+    a[o + 1] = x.c1;
+    b[o + 1] = s;
+}
+NWV_HD fp2 res_mul_fp(const fp (&r)[GRP], int o) { return fp2{r[o], r[o + 1]}; }
+
+// ml_dbl of bls381.h followed by the line's scaling by (x_P, y_P), as four rounds of products over
+// the group (8 + 8 + 6 + 7 of its 29 Fp products) instead of 29 on every lane; the same
+// operations in the same order, so T and the line come out bit for bit as ml_dbl's.
+//   A: X^2, Y^2, Z^2, (Z + Y)^2   B: t1^2, (t1 + X)^2, t4^2, t6^2   C: t4 zz, Z' zz
+//   D: (t3 - X') t4, l1 x_P, l4 y_P
+G_HD void g_ml_dbl(const GCtx& g, jac<fp2>& T, const fp& px, const fp& py, fp2& l0, fp2& l1p, fp2& l4p) {
+    fp a[GRP], b[GRP], r[GRP];
+    ops_sqr(T.x, a, b, 0);
+    ops_sqr(T.y, a, b, 2);
+    ops_sqr(T.z, a, b, 4);
+    ops_sqr(f2_add(T.z, T.y), a, b, 6);
+    g_fp_round(g, a, b, r, 8);
+    const fp2 t0 = res_sqr(r, 0), t1 = res_sqr(r, 2), zz = res_sqr(r, 4);
+    const fp2 zn = f2_sub(f2_sub(res_sqr(r, 6), t1), zz);
+    const fp2 t4 = f2_add(f2_dbl(t0), t0);
+    const fp2 t6 = f2_add(T.x, t4);
+    ops_sqr(t1, a, b, 0);
+    ops_sqr(f2_add(t1, T.x), a, b, 2);
+    ops_sqr(t4, a, b, 4);
+    ops_sqr(t6, a, b, 6);
+    g_fp_round(g, a, b, r, 8);
+    const fp2 t2 = res_sqr(r, 0), t5 = res_sqr(r, 4);
+    const fp2 t3 = f2_dbl(f2_sub(f2_sub(res_sqr(r, 2), t0), t2));
+    const fp2 xn = f2_sub(f2_sub(t5, t3), t3);
+    l0 = f2_sub(f2_sub(f2_sub(res_sqr(r, 6), t0), t5), f2_dbl(f2_dbl(t1)));
+    const fp2 t2x8 = f2_dbl(f2_dbl(f2_dbl(t2)));
+    ops_mul(t4, zz, a, b, 0);
+    ops_mul(zn, zz, a, b, 3);
+    g_fp_round(g, a, b, r, 6);
+    const fp2 l1 = f2_neg(f2_dbl(res_mul(r, 0)));
+    const fp2 l4 = f2_dbl(res_mul(r, 3));
+    ops_mul(f2_sub(t3, xn), t4, a, b, 0);
+    ops_mul_fp(l1, px, a, b, 3);
+    ops_mul_fp(l4, py, a, b, 5);
+    g_fp_round(g, a, b, r, 7);
+    T.x = xn;
+    T.y = f2_sub(res_mul(r, 0), t2x8);
+    T.z = zn;
+    l1p = res_mul_fp(r, 3);
+    l4p = res_mul_fp(r, 5);
+}
+
 // a^-1 through norms, in group operations only (the one-lane f12_inv spills and took ~1.9 ms):
 // t = a conj(a) lies in Fp6, N(t) = t t^(p^2) t^(p^4) in Fp2, so a^-1 = conj(a) t^(p^2) t^(p^4) / N(t)
 G_HD G12 g_inv(const GCtx& g, const G12& a) {
@@ -356,8 +494,8 @@ G_NOINLINE G12 g_miller(const GCtx& g, const fp* px, const fp* py, const fp2* qx
         if (b != 62) f = g_sqr(g, f);
 #pragma unroll
         for (int i = 0; i < N; i++) {
-            ml_dbl(T[i], l0, l1, l4);
-            f = g_mul_line(g, f, l0, f2_mul_fp(l1, px[i]), f2_mul_fp(l4, py[i]));
+            g_ml_dbl(g, T[i], px[i], py[i], l0, l1, l4);  // the doubling's products over the lanes
+            f = g_mul_line(g, f, l0, l1, l4);
         }
         if ((BLS_X_ABS >> b) & 1) {
 #pragma unroll

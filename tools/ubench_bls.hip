@@ -109,6 +109,25 @@ __device__ G12 miller_reps(const GCtx& g, G12 a, int reps) {
     return a;
 }
 GK(k_g_miller, a = miller_reps(g, a, reps))
+// one Miller-loop doubling step with its line: every lane on its own (ml_dbl) vs over the group
+__device__ G12 dbl_reps(const GCtx& g, G12 a, int reps, bool grouped) {
+    const fp px = k_g1x(), py = k_g1y();
+    jac<fp2> T = jac_from_affine(k_g2x(), k_g2y());
+    fp2 l0, l1, l4;
+    for (int i = 0; i < reps; i++) {
+        if (grouped) {
+            g_ml_dbl(g, T, px, py, l0, l1, l4);
+        } else {
+            ml_dbl(T, l0, l1, l4);
+            l1 = f2_mul_fp(l1, px);
+            l4 = f2_mul_fp(l4, py);
+        }
+    }
+    a.v = f2_add(f2_add(a.v, l0), f2_add(l1, f2_add(l4, T.x)));
+    return a;
+}
+GK(k_g_dbl_lane, a = dbl_reps(g, a, reps, false))
+GK(k_g_dbl_group, a = dbl_reps(g, a, reps, true))
 // the same Miller loop with P, Q read from memory (runtime values, as the verification kernels see)
 __device__ uint32_t d_pq[2 * NL + 4 * NL];
 __device__ G12 miller_reps_mem(const GCtx& g, G12 a, int reps) {
@@ -141,7 +160,8 @@ int main() {
               {"final_exp", k_fexp, 1, 6000},      {"group8_f12_mul", k_g_mul, 200, 54},
               {"group8_f12_sqr", k_g_sqr, 200, 36}, {"group8_cyc_sqr", k_g_cyc, 200, 18},
               {"group8_line_mul", k_g_line, 200, 13}, {"group8_miller_loop_1pair", k_g_miller, 1, 6800},
-              {"group8_final_exp", k_g_fexp, 1, 6000}, {"group8_miller_loop_1pair_mem", k_g_miller_mem, 1, 6800}};
+              {"group8_final_exp", k_g_fexp, 1, 6000}, {"group8_miller_loop_1pair_mem", k_g_miller_mem, 1, 6800},
+              {"group8_ml_dbl_every_lane", k_g_dbl_lane, 200, 29}, {"group8_ml_dbl_over_lanes", k_g_dbl_group, 200, 29}};
     const int blocks_full = 256 * 4 * 2;  // two waves per SIMD
     uint32_t* out;
     if (hipMalloc(&out, 4 * 64 * blocks_full) != hipSuccess) return 2;
