@@ -430,7 +430,9 @@ NWV_HD fp2 res_mul_fp(const fp (&r)[GRP], int o) { return fp2{r[o], r[o + 1]}; }
 // operations in the same order, so T and the line come out bit for bit as ml_dbl's.
 //   A: X^2, Y^2, Z^2, (Z + Y)^2   B: t1^2, (t1 + X)^2, t4^2, t6^2   C: t4 zz, Z' zz
 //   D: (t3 - X') t4, l1 x_P, l4 y_P
-G_HD void g_ml_dbl(const GCtx& g, jac<fp2>& T, const fp& px, const fp& py, fp2& l0, fp2& l1p, fp2& l4p) {
+// z3 (optional): the line is evaluated times z3 (l0 z3 as well), for a Jacobian P (g_rlc_ml).
+G_HD void g_ml_dbl(const GCtx& g, jac<fp2>& T, const fp& px, const fp& py, fp2& l0, fp2& l1p, fp2& l4p,
+                   const fp* z3 = nullptr) {
     fp a[GRP], b[GRP], r[GRP];
     ops_sqr(T.x, a, b, 0);
     ops_sqr(T.y, a, b, 2);
@@ -453,9 +455,11 @@ G_HD void g_ml_dbl(const GCtx& g, jac<fp2>& T, const fp& px, const fp& py, fp2& 
     const fp2 t2x8 = f2_dbl(f2_dbl(f2_dbl(t2)));
     ops_mul(t4, zz, a, b, 0);
     ops_mul(zn, zz, a, b, 3);
-    g_fp_round(g, a, b, r, 6);
+    if (z3) ops_mul_fp(l0, *z3, a, b, 6);
+    g_fp_round(g, a, b, r, z3 ? 8 : 6);
     const fp2 l1 = f2_neg(f2_dbl(res_mul(r, 0)));
     const fp2 l4 = f2_dbl(res_mul(r, 3));
+    if (z3) l0 = res_mul_fp(r, 6);
     ops_mul(f2_sub(t3, xn), t4, a, b, 0);
     ops_mul_fp(l1, px, a, b, 3);
     ops_mul_fp(l4, py, a, b, 5);
@@ -482,8 +486,11 @@ G_HD G12 g_inv(const GCtx& g, const G12& a) {
 // prod_{i < N} f_{|x|, Q_i}(P_i), conjugated (x < 0) (miller_loop2 over a group).  N is a template
 // parameter so the per-pair loops unroll and the G2 points stay in registers (a runtime pair count
 // indexes T[], px[], ... dynamically and puts them in scratch: 2x slower, measured)
-template <int N>
-G_NOINLINE G12 g_miller(const GCtx& g, const fp* px, const fp* py, const fp2* qx, const fp2* qy) {
+// PROJ: P_i given as (X Z, Y) with pz3[i] = Z^3 of a Jacobian P_i; every line is evaluated times
+// Z^3, a factor in Fp* that the final exponentiation maps to 1 (g_rlc_ml)
+template <int N, bool PROJ = false>
+G_NOINLINE G12 g_miller(const GCtx& g, const fp* px, const fp* py, const fp2* qx, const fp2* qy,
+                        const fp* pz3 = nullptr) {
     jac<fp2> T[N];
 #pragma unroll
     for (int i = 0; i < N; i++) T[i] = jac_from_affine(qx[i], qy[i]);
@@ -494,13 +501,14 @@ G_NOINLINE G12 g_miller(const GCtx& g, const fp* px, const fp* py, const fp2* qx
         if (b != 62) f = g_sqr(g, f);
 #pragma unroll
         for (int i = 0; i < N; i++) {
-            g_ml_dbl(g, T[i], px[i], py[i], l0, l1, l4);  // the doubling's products over the lanes
+            g_ml_dbl(g, T[i], px[i], py[i], l0, l1, l4, PROJ ? &pz3[i] : nullptr);  // products over the lanes
             f = g_mul_line(g, f, l0, l1, l4);
         }
         if ((BLS_X_ABS >> b) & 1) {
 #pragma unroll
             for (int i = 0; i < N; i++) {
                 ml_add(T[i], qx[i], qy[i], l0, l1, l4);
+                if (PROJ) l0 = f2_mul_fp(l0, pz3[i]);
                 f = g_mul_line(g, f, l0, f2_mul_fp(l1, px[i]), f2_mul_fp(l4, py[i]));
             }
         }

@@ -202,19 +202,13 @@ G_HD void g_rlc_points(const GCtx& g, const uint32_t* sig_rec, const uint32_t* h
     jac<fp> m = inf;
     if (!src[2 * NL]) m = jac_mul64(jac_from_affine(ld_fp(src), ld_fp(src + NL)), r);
     if (g.slot == 4) st_g1j(s_out, m);
-    if (!sig_lane) {
-        fp x = fp_zero(), y = fp_zero();
-        if (!m.inf) g1_to_affine(x, y, m);
-        if (g.slot == 0) st_g1(p_out, x, y, m.inf);
-    }
+    if (g.slot == 0) st_g1j(p_out, m);  // Jacobian: no inversion (g_rlc_ml)
 #else
     jac<fp> s = inf, h = inf;
     if (!sig_rec[2 * NL]) s = jac_mul64(jac_from_affine(ld_fp(sig_rec), ld_fp(sig_rec + NL)), r);
     if (!h_rec[2 * NL]) h = jac_mul64(jac_from_affine(ld_fp(h_rec), ld_fp(h_rec + NL)), r);
     st_g1j(s_out, s);
-    fp x = fp_zero(), y = fp_zero();
-    if (!h.inf) g1_to_affine(x, y, h);
-    st_g1(p_out, x, y, h.inf);
+    st_g1j(p_out, h);
 #endif
 }
 // an item outside the batch (failed an earlier check): identity P_i, s_i
@@ -226,17 +220,20 @@ G_HD void g_rlc_neutral(const GCtx& g, uint32_t* p_out, uint32_t* s_out) {
     if (g.slot != 0) return;
 #endif
     st_g1j(s_out, s);
-    st_g1(p_out, fp_zero(), fp_zero(), true);
+    st_g1j(p_out, s);
 }
-// stage 3: f = the Miller loop of (P, Q) in W order, 1 for an identity P; Q = apk (affine record),
-// or (neg) the pair (-S, g2) of the combination's signature side, S Jacobian
+// stage 3: f = the Miller loop of (P, Q) in W order, 1 for an identity P; P a Jacobian record
+// (X, Y, Z), Q = apk (affine record) or g2 for the combination's signature side.  With
+// x_P = X / Z^2, y_P = Y / Z^3 every line is evaluated times Z^3 (l0 Z^3 + l1 X Z v + l4 Y v w):
+// f picks up a factor in Fp*, which the final exponentiation maps to 1, and no P is inverted.
 G_HD void g_rlc_ml(const GCtx& g, const uint32_t* p_rec, const uint32_t* apk_rec, uint32_t* f_out) {
     G12 f = g_one(g);
-    if (!p_rec[2 * NL]) {
-        const fp px = ld_fp(p_rec), py = ld_fp(p_rec + NL);
+    const jac<fp> P = ld_g1j(p_rec);
+    if (!P.inf) {
+        const fp px = fp_mul(P.x, P.z), py = P.y, z3 = fp_mul(fp_sqr(P.z), P.z);
         fp2 qx, qy;
         ld_g2(apk_rec, qx, qy);
-        f = g_miller<1>(g, &px, &py, &qx, &qy);
+        f = g_miller<1, true>(g, &px, &py, &qx, &qy, &z3);
     }
     g_store(g, f_out, f);
 }
@@ -244,13 +241,9 @@ G_HD void g_rlc_ml(const GCtx& g, const uint32_t* p_rec, const uint32_t* apk_rec
 // Miller-loop grid runs one code path on every group (a different path on one group of a wave
 // would serialise the wave: measured 2x)
 NWV_HD void rlc_sig_item(const uint32_t* s_rec, uint32_t* p_out, uint32_t* q_out) {
-    const jac<fp> S = ld_g1j(s_rec);
-    fp x = fp_zero(), y = fp_zero();
-    if (!S.inf) {
-        g1_to_affine(x, y, S);
-        y = fp_neg(y);
-    }
-    st_g1(p_out, x, y, S.inf);
+    jac<fp> S = ld_g1j(s_rec);
+    S.y = fp_neg(S.y);  // -S, still Jacobian (g_rlc_ml)
+    st_g1j(p_out, S);
     st_g2(q_out, k_g2x(), k_g2y(), false);
 }
 // the trees: f_a <- f_a f_b (a group), s_a <- s_a + s_b (a lane)

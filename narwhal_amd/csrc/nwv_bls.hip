@@ -180,7 +180,7 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_pair(uint32_t n, const uint32
     if (g.slot == 0) st[i] = ok ? ST_OK : ST_VERIFY_FAIL;
 }
 // the batch check (bls_verify.h), in stages:
-//   k_bls_rlc_pts   one group per item: P_i = [r_i] H_i (affine), s_i = [r_i] sig_i
+//   k_bls_rlc_pts   one group per item: P_i = [r_i] H_i, s_i = [r_i] sig_i (Jacobian)
 //   k_bls_sfold     ceil(log2 n) levels of G1 sums: S = sum s_i
 //   k_bls_sig_item  one lane: (-S, g2) as item n
 //   k_bls_rlc_ml    one group per item and one more: the Miller loops of (P_i, apk_i) and (-S, g2)
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_rlc_pts(uint32_t n, const uin
                                                            const int32_t* st, const uint8_t* seed, uint32_t* prec,
                                                            uint32_t* srec) {
     BLS_GIDX();
-    uint32_t* p = prec + (size_t)G1_REC_WORDS * i;
+    uint32_t* p = prec + (size_t)G1J_REC_WORDS * i;
     uint32_t* s = srec + (size_t)G1J_REC_WORDS * i;
     if (st[i] != ST_OK) {
         g_rlc_neutral(g, p, s);
@@ -208,12 +208,12 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_sfold(uint32_t m, uint32_t* s
 // -S (affine) and g2 as item n of the Miller-loop grid (srec[0] = S after the G1 tree)
 __global__ void k_bls_sig_item(uint32_t n, const uint32_t* srec, uint32_t* prec, uint32_t* apk_rec) {
     if (blockIdx.x || threadIdx.x) return;
-    rlc_sig_item(srec, prec + (size_t)G1_REC_WORDS * n, apk_rec + (size_t)G2_REC_WORDS * n);
+    rlc_sig_item(srec, prec + (size_t)G1J_REC_WORDS * n, apk_rec + (size_t)G2_REC_WORDS * n);
 }
 __global__ __launch_bounds__(BLS_LANES) void k_bls_rlc_ml(uint32_t n, const uint32_t* prec, const uint32_t* apk_rec,
                                                           uint32_t* frec) {
     BLS_GIDX();
-    g_rlc_ml(g, prec + (size_t)G1_REC_WORDS * i, apk_rec + (size_t)G2_REC_WORDS * i, frec + (size_t)F12_REC_WORDS * i);
+    g_rlc_ml(g, prec + (size_t)G1J_REC_WORDS * i, apk_rec + (size_t)G2_REC_WORDS * i, frec + (size_t)F12_REC_WORDS * i);
 }
 __global__ __launch_bounds__(BLS_LANES) void k_bls_ffold(uint32_t m, uint32_t* frec) {
     const uint32_t h = (m + 1) / 2;
@@ -522,7 +522,7 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
                  w_ssig = al(w_st + 4 * n), w_sapk = al(w_ssig + 4 * n), w_ok = al(w_sapk + 4 * n),
                  w_frec = al(w_ok + 4), w_jrec = al(w_frec + 4 * F12_REC_WORDS * (batch ? n + 1 : 0)),
                  w_prec = al(w_jrec + 4 * G1J_REC_WORDS * (batch ? n : 0)),
-                 w_end = w_prec + 4 * G1_REC_WORDS * (batch ? n + 1 : 0) + 4;
+                 w_end = w_prec + 4 * G1J_REC_WORDS * (batch ? n + 1 : 0) + 4;
     if ((rc = d.work.ensure(w_end))) return rc;
     uint8_t* in = static_cast<uint8_t*>(d.in.p);
     uint8_t* w = static_cast<uint8_t*>(d.work.p);

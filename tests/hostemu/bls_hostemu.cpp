@@ -149,7 +149,7 @@ int bh_g_fast_aggregate_verify(const uint8_t* sig, size_t n_pks, const uint8_t* 
 int bh_rlc_batch(size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_t* msgs, const uint8_t* seed,
                  const uint8_t* dst, size_t dl) {
     const GCtx g{};
-    std::vector<uint32_t> f(F12_REC_WORDS * (n + 1)), sj(G1J_REC_WORDS * n), pr(G1_REC_WORDS * (n + 1)),
+    std::vector<uint32_t> f(F12_REC_WORDS * (n + 1)), sj(G1J_REC_WORDS * n), pr(G1J_REC_WORDS * (n + 1)),
         ar(G2_REC_WORDS * (n + 1));
     for (size_t i = 0; i < n; i++) {
         uint32_t srec[G1_REC_WORDS], hrec[G1_REC_WORDS], krec[G2_REC_WORDS];
@@ -159,15 +159,15 @@ int bh_rlc_batch(size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_
             apk_record(krec, &kst, &idx, 1, ar.data() + G2_REC_WORDS * i) != ST_OK)
             return -1;
         h2c_record(msgs + 32 * i, 32, dst, (uint32_t)dl, hrec);
-        g_rlc_points(g, srec, hrec, rlc_scalar(seed, (uint32_t)i), pr.data() + G1_REC_WORDS * i,
+        g_rlc_points(g, srec, hrec, rlc_scalar(seed, (uint32_t)i), pr.data() + G1J_REC_WORDS * i,
                      sj.data() + G1J_REC_WORDS * i);
     }
     for (size_t m = n; m > 1; m = (m + 1) / 2)
         for (size_t i = 0; i < m - (m + 1) / 2; i++)
             rlc_sfold(sj.data() + G1J_REC_WORDS * i, sj.data() + G1J_REC_WORDS * (i + (m + 1) / 2));
-    rlc_sig_item(sj.data(), pr.data() + G1_REC_WORDS * n, ar.data() + G2_REC_WORDS * n);
+    rlc_sig_item(sj.data(), pr.data() + G1J_REC_WORDS * n, ar.data() + G2_REC_WORDS * n);
     for (size_t i = 0; i <= n; i++)
-        g_rlc_ml(g, pr.data() + G1_REC_WORDS * i, ar.data() + G2_REC_WORDS * i, f.data() + F12_REC_WORDS * i);
+        g_rlc_ml(g, pr.data() + G1J_REC_WORDS * i, ar.data() + G2_REC_WORDS * i, f.data() + F12_REC_WORDS * i);
     for (size_t m = n + 1; m > 1; m = (m + 1) / 2)
         for (size_t i = 0; i < m - (m + 1) / 2; i++)
             g_rlc_ffold(g, f.data() + F12_REC_WORDS * i, f.data() + F12_REC_WORDS * (i + (m + 1) / 2));
