@@ -14,7 +14,7 @@ all: lib oracle hostemu tools
 lib: narwhal_amd/lib/libnwv.so
 # nwv_types.cpp is plain host C++ (no kernels): built by g++ on its own, because mixing `-x c++`
 # into the hipcc line makes hipcc drop --offload-arch (the code object silently falls back to gfx906)
-narwhal_amd/lib/nwv_types.o: narwhal_amd/csrc/nwv_types.cpp include/nwv.h include/nwv_types.h
+narwhal_amd/lib/nwv_types.o: narwhal_amd/csrc/nwv_types.cpp include/nwv.h include/nwv_types.h include/nwv_bls.h
 	@mkdir -p narwhal_amd/lib
 	g++ -O2 -std=c++17 -fPIC -Wall -c -o $@ $<
 narwhal_amd/lib/nwv_service.o: narwhal_amd/csrc/nwv_service.cpp include/nwv.h include/nwv_types.h include/nwv_service.h

@@ -19,7 +19,11 @@ exact-bad-set check.
 Extra fields: roofline (dominant kernel) and roofline_per_kernel, cpu_baseline (the oracle's
 batch verifier on the host's usable cores, rank 0, N = 1), host_to_host (pipelined verification of
 host-resident batches, PCIe included), latency of a 1,024-signature batch host -> host, the C3
-firehose on one GPU, and the C1 / C4 / C5 legs with their CPU counterparts.
+firehose on one GPU, the C1 / C4 / C5 legs with their CPU counterparts, and configs.BLS: the
+reference's default scheme (BLS12-381) -- a 100-certificate round, single Verifier::verify latency,
+concurrent callers, 16,384 single-key items, the C5 DAG round through the BLS types layer -- with
+its oracle checks and CPU baseline.  With N > 1 the firehose also appears at top level
+(firehose_sigs_per_s, firehose_scaling "strong").
 """
 import argparse
 import json
@@ -816,7 +820,12 @@ def main():
             line = base_line(args, world, h["dt_max"])
             line.update(rank0_ms_per_step=h["dt"] / args.steps * 1e3, kernel_ms_rank0=h["kt"],
                         single_stream_rank0={"ms_per_step": float(np.median(h["single"]))},
-                        steady_state_rank0=h["steady"], firehose=fire)
+                        steady_state_rank0=h["steady"], firehose=fire,
+                        # configs[2] at top level, labelled: the fixed 16M-signature total sharded by
+                        # index over the ranks (strong scaling), beside the weak-scaling `value`
+                        firehose_metric="configs[2] firehose: 16,777,216 sigs sharded by index, sigs/s",
+                        firehose_sigs_per_s=fire["sigs_per_s"], firehose_scaling="strong",
+                        firehose_exact_bad_set=fire["exact_bad_set"]["exact"])
             print(json.dumps(line), flush=True)
         eng.close()
         dist.destroy_process_group()
@@ -882,6 +891,8 @@ def main():
                                  "(the per-GPU share at 8 GPUs), 32 B messages; --gpus N shards it over N GPUs"}
         configs["C4"], cdata["C4"] = CL.leg_c4(eng)
         configs["C5"], cdata["C5"] = CL.leg_c5(eng)
+        # the reference's default scheme, BLS12-381 (GPU legs, oracle checks, CPU baseline)
+        configs["BLS"] = CL.leg_bls(eng, threads, cpu=not args.no_cpu_baseline)
         if not args.no_cpu_baseline:
             for k, v in cpu_baseline_configs(configs, cdata, threads).items():
                 configs[k]["cpu_baseline"] = v

@@ -13,14 +13,15 @@
  * CertificatesResponse::validate_certificates primary/src/block_synchronizer/responses.rs:95-141.
  *
  * Every verification runs on the GPU, one item (one fast_aggregate_verify) per lane: signature
- * decode + G1 membership, public-key decode + G2 membership (once per key per device: a key
- * cache keeps each validated key, as fastcrypto validates keys once at deserialization;
- * NWV_FLAG_NO_KEYCACHE decodes every call's keys afresh),
+ * decode + G1 membership, public-key decode + G2 membership (once per device for the keys
+ * registered in the key cache below, as fastcrypto validates keys once at deserialization; any
+ * other key is decoded by the call that names it),
  * aggregate public key, hash to G1; then the pairing equations of all the call's items as one
  * random-linear-combination check (one Miller loop per item, one final exponentiation per call),
  * and only if that rejects, each item's own two-pair Miller loop and final exponentiation.
  * Per-item status codes are exact either way.
- * Buffers are the caller's; the library never retains them.  Thread-safe.
+ * Buffers are the caller's; the library never retains them.  Thread-safe: concurrent calls on one
+ * device run side by side (each takes one of up to eight per-device stream sets).
  */
 #ifndef NWV_BLS_H
 #define NWV_BLS_H
@@ -48,8 +49,8 @@ extern "C" {
 /* The batch entry point (validate_certificates, a DAG round's certificates, the bench): item i is
  * AggregateAuthenticator::verify of the aggregate signature sigs[i] (48 bytes) over the message
  * msg_base[msg_off[i] .. + msg_len[i]) by the keys keys[pk_idx[pk_off[i] + j]], j < pk_cnt[i]
- * (keys: n_keys x 96 bytes, e.g. the committee; each distinct key is decoded and subgroup-checked
- * once per call).  status[i] = NWV_BLS_* for item i.  dst = NULL selects NWV_BLS_DST.
+ * (keys: n_keys x 96 bytes, e.g. the committee; a key the device's key cache does not hold is
+ * decoded and subgroup-checked once by the call).  status[i] = NWV_BLS_* for item i.  dst = NULL selects NWV_BLS_DST.
  * Returns NWV_OK (statuses valid) or a negative error. */
 int nwv_bls_verify_many(nwv_ctx* ctx, size_t n_keys, const uint8_t* keys, size_t n, const uint8_t* sigs,
                         const uint32_t* pk_off, const uint32_t* pk_cnt, const uint32_t* pk_idx,
@@ -64,6 +65,21 @@ int nwv_bls_last_kernel_ms(nwv_ctx* ctx, double out_ms[5]);
 /* how the last nwv_bls_verify_many call checked its pairings: 0 per item (NWV_FLAG_BLS_PER_ITEM),
  * 1 one batch check that accepted every item, 2 a batch check that rejected, then per item */
 int nwv_bls_last_path(nwv_ctx* ctx);
+/* keys of the last nwv_bls_verify_many call: out[0] key-list entries found in the key cache,
+ * out[1] distinct keys the call decoded itself */
+int nwv_bls_last_keys(nwv_ctx* ctx, uint64_t out[2]);
+
+/* The committee key cache (per device).  fastcrypto decodes and validates a public key once, at
+ * deserialization; nwv_bls_keycache_register does that once per device for the committee's keys
+ * (epoch start, Core::change_epoch primary/src/core.rs:592-611) and keeps the records of the keys
+ * that are valid.  Verification calls only look keys up: a key the cache does not hold is decoded
+ * by the call itself and never takes a slot (an invalid or stray key cannot fill the cache).
+ * nwv_bls_keycache_reset (epoch change) drops every slot once the calls in flight finish.  A
+ * device keeps at most 65,536 keys; NWV_FLAG_NO_KEYCACHE contexts keep none. */
+int nwv_bls_keycache_register(nwv_ctx* ctx, size_t n_keys, const uint8_t* keys);
+int nwv_bls_keycache_reset(nwv_ctx* ctx);
+/* number of keys the cache holds (>= 0), or a negative error */
+int nwv_bls_keycache_size(nwv_ctx* ctx);
 
 /* ---- fastcrypto 0.1.2 trait surface (bls12381 module) ---- */
 /* Verifier::verify(&self = pk, msg, sig): NWV_OK or NWV_ERR_SIGNATURE */

@@ -34,8 +34,9 @@ typedef struct nwv_service nwv_service;
 
 /* completion callback: called exactly once per submitted item, from a service thread, without
  * the service lock held.  It may submit further items asynchronously; the blocking calls
- * (nwv_service_verify_*, nwv_service_flush) return NWV_ERR_REENTRANT from inside a callback
- * (they would wait on the thread running it), and it must not call nwv_service_free. */
+ * (nwv_service_verify_*, nwv_service_flush) on the SAME service return NWV_ERR_REENTRANT from
+ * inside its callback (they would wait on the thread running it; blocking calls on another
+ * service are allowed), and it must not call nwv_service_free. */
 typedef void (*nwv_done_fn)(void* user, int32_t result);
 
 /* max_batch: flush as soon as this many items are pending (>= 1); max_wait_us: flush when the

@@ -142,6 +142,75 @@ int nwv_certificate_new(const nwv_committee* committee, size_t n_votes, const ui
 /* Committee::quorum_threshold (config/src/lib.rs:537-542): 2 * total / 3 + 1 */
 uint64_t nwv_committee_quorum_threshold(const nwv_committee* committee);
 
+/* ---- the same layer under BLS12-381, the reference's default scheme (crypto/src/lib.rs:29-33:
+ * PublicKey = BLS12381PublicKey, 96 bytes; Signature = BLS12381Signature, 48 bytes;
+ * AggregateSignature = BLS12381AggregateSignature, one 48-byte G1 point or none).  The digests
+ * hash the 96-byte keys where the Ed25519 layout has 32-byte ones (Header::digest :209-227 hashes
+ * the author, Vote / Certificate::digest the origin).  Verification runs on the GPU through
+ * include/nwv_bls.h; the committee's keys are registered in the device's BLS key cache. ---- */
+typedef struct {
+    size_t n;
+    const uint8_t* keys; /* n x 96 bytes, ascending byte order (BTreeMap order = bitmap order) */
+    const uint64_t* stakes;
+    uint64_t epoch;
+    const uint32_t* n_workers;
+    const uint32_t* const* worker_ids;
+} nwv_bls_committee;
+
+typedef struct {
+    const uint8_t* author;          /* 96 */
+    uint64_t round;
+    uint64_t epoch;
+    size_t n_payload;
+    const uint8_t* payload_digests; /* n_payload x 32 */
+    const uint32_t* payload_workers;
+    size_t n_parents;
+    const uint8_t* parents;         /* n_parents x 32 */
+    const uint8_t* id;              /* 32 */
+    const uint8_t* signature;       /* 48 */
+} nwv_bls_header;
+
+typedef struct {
+    const uint8_t* id;        /* 32 */
+    uint64_t round;
+    uint64_t epoch;
+    const uint8_t* origin;    /* 96 */
+    const uint8_t* author;    /* 96 */
+    const uint8_t* signature; /* 48 */
+} nwv_bls_vote;
+
+/* aggregated_signature: the 48-byte aggregate, or NULL for an aggregate holding no signature
+ * (AggregateSignature::default(), sig: None -> verification fails) */
+typedef struct {
+    nwv_bls_header header;
+    size_t n_signed;
+    const uint32_t* signed_authorities;
+    const uint8_t* aggregated_signature;
+} nwv_bls_certificate;
+
+int nwv_bls_header_digest_many(nwv_ctx* ctx, size_t n, const nwv_bls_header* h, uint8_t* out);
+int nwv_bls_vote_digest_many(nwv_ctx* ctx, size_t n, const nwv_bls_vote* v, uint8_t* out);
+int nwv_bls_certificate_digest_many(nwv_ctx* ctx, size_t n, const nwv_bls_certificate* c, uint8_t* out);
+/* Header::verify / Vote::verify / Certificate::verify of a primary's queued messages in ONE call:
+ * every digest in one BLAKE2b launch, every signature check (header and vote signatures:
+ * Verifier::verify; each certificate's aggregate over its signers: fast_aggregate_verify) in one
+ * nwv_bls_verify_many call; results as nwv_verify_mixed_many's (NWV_DAG_* per item). */
+int nwv_bls_verify_mixed_many(nwv_ctx* ctx, const nwv_bls_committee* committee, size_t n_headers,
+                              const nwv_bls_header* headers, int32_t* header_results, size_t n_votes,
+                              const nwv_bls_vote* votes, int32_t* vote_results, size_t n_certs,
+                              const nwv_bls_certificate* certs, int32_t* cert_results);
+/* CertificatesResponse::validate_certificates under BLS (as nwv_validate_certificates) */
+int nwv_bls_validate_certificates(nwv_ctx* ctx, const nwv_bls_committee* committee, size_t n,
+                                  const nwv_bls_certificate* c, size_t* n_invalid, size_t* invalid_idx);
+/* Certificate::new / new_unsigned (types/src/primary.rs:411-485) under BLS: the votes (pk 96,
+ * sig 48) sorted by key, repeats dropped, matched against the committee; the aggregate is the G1
+ * sum of the kept signatures (AggregateSignature::aggregate on the GPU; a signature that does not
+ * decode or lies outside G1 -> NWV_DAG_INVALID_SIGNATURE).  *has_agg = 0 when no vote was kept
+ * (AggregateSignature::default()).  Returns an NWV_DAG_* code or a negative error. */
+int nwv_bls_certificate_new(nwv_ctx* ctx, const nwv_bls_committee* committee, size_t n_votes,
+                            const uint8_t* vote_pks, const uint8_t* vote_sigs, int check_stake,
+                            uint32_t* signed_out, size_t* n_signed, uint8_t* agg_out, int* has_agg);
+
 #ifdef __cplusplus
 }
 #endif

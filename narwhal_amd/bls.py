@@ -27,6 +27,10 @@ _SIGS = {
     "nwv_bls_pairing_many": ([_vp, _sz, _vp, _vp, _vp], _i32),
     "nwv_bls_last_kernel_ms": ([_vp, _vp], _i32),
     "nwv_bls_last_path": ([_vp], _i32),
+    "nwv_bls_last_keys": ([_vp, _vp], _i32),
+    "nwv_bls_keycache_register": ([_vp, _sz, _vp], _i32),
+    "nwv_bls_keycache_reset": ([_vp], _i32),
+    "nwv_bls_keycache_size": ([_vp], _i32),
 }
 KERNELS = ("keys_new_to_cache", "sig_decode", "hash_to_g1", "key_sums", "pairing_check")
 PATHS = ("per_item", "batch_accepted", "batch_rejected_then_per_item")
@@ -101,9 +105,26 @@ class Bls:
         _lib._check(self.lib.nwv_bls_last_kernel_ms(self._h, out.ctypes.data))
         return dict(zip(KERNELS, (float(x) for x in out)))
 
+    def last_keys(self):
+        """(key-list entries the last verify_many found in the key cache, keys it decoded itself)"""
+        out = np.zeros(2, dtype=np.uint64)
+        _lib._check(self.lib.nwv_bls_last_keys(self._h, out.ctypes.data))
+        return int(out[0]), int(out[1])
+
     def last_path(self):
         """how the last verify_many checked its pairings (PATHS)"""
         return PATHS[_lib._check(self.lib.nwv_bls_last_path(self._h), allow=(0, 1, 2))]
+
+    # the committee key cache: register at epoch start, reset at an epoch change
+    def register_keys(self, keys):
+        kb = _arr(b"".join(keys))
+        _lib._check(self.lib.nwv_bls_keycache_register(self._h, len(keys), kb.ctypes.data))
+
+    def reset_keys(self):
+        _lib._check(self.lib.nwv_bls_keycache_reset(self._h))
+
+    def cached_keys(self):
+        return _lib._check(self.lib.nwv_bls_keycache_size(self._h), allow=range(0, 1 << 20))
 
     # fastcrypto trait surface: return codes NWV_OK / NWV_ERR_*
     def verify(self, pk, msg, sig):

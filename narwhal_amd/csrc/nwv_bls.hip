@@ -22,7 +22,10 @@
 #include <algorithm>
 #include <cstring>
 #include <functional>
+#include <condition_variable>
+#include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -44,13 +47,36 @@ __attribute__((visibility("hidden"))) void nwv_internal_fill_seed(const uint8_t*
 #define BLS_IDX() const uint32_t i = blockIdx.x * BLS_LANES + threadIdx.x; \
     if (i >= n) return
 
-// decode + check the keys a call adds to the key cache: key j of the list goes to cache slot slot[j]
+// decode + check keys: key j of the list goes to record slot slot[j] (the committee key cache at
+// registration, or a call's scratch table for keys the cache does not hold)
 __global__ __launch_bounds__(BLS_LANES) void k_bls_keys_fill(uint32_t n, const uint8_t* pk, const uint32_t* slot,
                                                              uint32_t* rec, int32_t* st) {
     BLS_IDX();
     const uint32_t k = slot[i];
     st[k] = key_decode(pk + 96 * (size_t)i, rec + (size_t)G2_REC_WORDS * k);
 }
+// copy validated records into the key cache: record src[j] of `from` -> slot dst[j] of `to`
+__global__ __launch_bounds__(BLS_LANES) void k_bls_rec_copy(uint32_t n, const uint32_t* src, const uint32_t* dst,
+                                                            const uint32_t* from, uint32_t* to, int32_t* to_st) {
+    const uint32_t t = blockIdx.x * BLS_LANES + threadIdx.x;
+    const uint32_t i = t / G2_REC_WORDS, w = t % G2_REC_WORDS;
+    if (i >= n) return;
+    to[(size_t)G2_REC_WORDS * dst[i] + w] = from[(size_t)G2_REC_WORDS * src[i] + w];
+    if (w == 0) to_st[dst[i]] = ST_OK;
+}
+// A call's key table: index k < KC_CAP names slot k of the device's key cache, k >= KC_CAP entry
+// k - KC_CAP of the call's scratch table (keys the cache does not hold, decoded by this call)
+constexpr uint32_t KC_CAP = 65536;
+struct KeyTab {
+    const uint32_t* rc;
+    const int32_t* sc;
+    const uint32_t* rs;
+    const int32_t* ss;
+};
+__device__ inline const uint32_t* key_rec(const KeyTab& t, uint32_t k) {
+    return k < KC_CAP ? t.rc + (size_t)G2_REC_WORDS * k : t.rs + (size_t)G2_REC_WORDS * (k - KC_CAP);
+}
+__device__ inline int32_t key_st(const KeyTab& t, uint32_t k) { return k < KC_CAP ? t.sc[k] : t.ss[k - KC_CAP]; }
 __global__ __launch_bounds__(BLS_LANES) void k_bls_sigs(uint32_t n, const uint8_t* sig, uint32_t* rec, int32_t* st) {
     BLS_IDX();
     st[i] = sig_decode(sig + 48 * (size_t)i, rec + (size_t)G1_REC_WORDS * i);
@@ -82,9 +108,9 @@ __device__ jac<fp2> ld_g2j(const uint32_t* o) {
     return p;
 }
 static_assert(4 * G2J_WORDS + 8 <= GX_WORDS, "the tree's first level fits a group's LDS area");
-__global__ __launch_bounds__(BLS_LANES) void k_bls_apk_g(uint32_t n, const uint32_t* key_rec, const int32_t* key_st,
-                                                         const uint32_t* pk_off, const uint32_t* pk_cnt,
-                                                         const uint32_t* pk_idx, uint32_t* rec, int32_t* st_apk) {
+__global__ __launch_bounds__(BLS_LANES) void k_bls_apk_g(uint32_t n, KeyTab kt, const uint32_t* pk_off,
+                                                         const uint32_t* pk_cnt, const uint32_t* pk_idx, uint32_t* rec,
+                                                         int32_t* st_apk) {
     BLS_GIDX();
     const uint32_t cnt = pk_cnt[i];
     const uint32_t* idx = pk_idx + pk_off[i];
@@ -92,10 +118,10 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_apk_g(uint32_t n, const uint3
     if (cnt == 1) {  // one key (Verifier::verify): its validated record is the sum, no inversion
         if (g.slot < G2_REC_WORDS) {
             const uint32_t k = idx[0];
-            const bool ok = key_st[k] == ST_OK;
-            for (int w = g.slot; w < G2_REC_WORDS; w += GRP)
-                out[w] = ok ? key_rec[(size_t)k * G2_REC_WORDS + w] : (w == 4 * NL ? 1u : 0u);
-            if (g.slot == 0) st_apk[i] = key_st[k];
+            const int32_t ks = key_st(kt, k);
+            const uint32_t* kr = key_rec(kt, k);
+            for (int w = g.slot; w < G2_REC_WORDS; w += GRP) out[w] = ks == ST_OK ? kr[w] : (w == 4 * NL ? 1u : 0u);
+            if (g.slot == 0) st_apk[i] = ks;
         }
         return;
     }
@@ -105,12 +131,12 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_apk_g(uint32_t n, const uint3
     uint32_t first_bad = 0xffffffffu;
     for (uint32_t j = (uint32_t)g.slot; j < cnt; j += GRP) {
         const uint32_t k = idx[j];
-        if (key_st[k] != ST_OK) {
+        if (key_st(kt, k) != ST_OK) {
             first_bad = j;
             break;
         }
         fp2 x, y;
-        ld_g2(key_rec + (size_t)k * G2_REC_WORDS, x, y);
+        ld_g2(key_rec(kt, k), x, y);
         acc = jac_add(acc, jac_from_affine(x, y));
     }
     // the group's first bad position, and the tree over the partial sums
@@ -134,7 +160,7 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_apk_g(uint32_t n, const uint3
     if (cnt == 0) {
         status = ST_AGGR_MISMATCH;
     } else if (fb != 0xffffffffu) {
-        status = key_st[idx[fb]];
+        status = key_st(kt, idx[fb]);
     } else {
         if (!acc.inf) g2_to_affine(x, y, acc);
         inf = acc.inf;
@@ -228,20 +254,28 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_final(const uint32_t* frec, i
     g_sync();
     if (g.slot == 0) *ok = r ? 1 : 0;
 }
-// sum of n decoded signatures (AggregateAuthenticator::aggregate), one lane
-__global__ void k_bls_g1_sum(uint32_t n, const uint32_t* rec, const int32_t* st, uint8_t* out48, int32_t* out_st) {
+// AggregateAuthenticator::aggregate (Certificate::new_unsafe, types/src/primary.rs:476-477): the sum
+// of n decoded signatures as a tree over the lanes -- each decoded record becomes a Jacobian entry
+// (k_bls_sig_jac), ceil(log2 n) levels of k_bls_sfold add pairs, and one lane takes the first bad
+// status in list order and compresses the sum (k_bls_g1_sum_out)
+__global__ __launch_bounds__(BLS_LANES) void k_bls_sig_jac(uint32_t n, const uint32_t* rec, uint32_t* srec) {
+    BLS_IDX();
+    const uint32_t* r = rec + (size_t)G1_REC_WORDS * i;
+    jac<fp> p;
+    p.inf = r[2 * NL] != 0;  // a failed decode is stored as the identity (its status decides)
+    p.x = ld_fp(r);
+    p.y = ld_fp(r + NL);
+    p.z = k_one();
+    st_g1j(srec + (size_t)G1J_REC_WORDS * i, p);
+}
+__global__ void k_bls_g1_sum_out(uint32_t n, const int32_t* st, const uint32_t* srec, uint8_t* out48, int32_t* out_st) {
     if (blockIdx.x || threadIdx.x) return;
-    jac<fp> acc;
-    acc.inf = true;
-    acc.x = acc.y = acc.z = fp_zero();
-    for (uint32_t k = 0; k < n; k++) {
+    for (uint32_t k = 0; k < n; k++)
         if (st[k] != ST_OK) {
             *out_st = st[k];
             return;
         }
-        const uint32_t* r = rec + (size_t)G1_REC_WORDS * k;
-        if (!r[2 * NL]) acc = jac_add(acc, jac_from_affine(ld_fp(r), ld_fp(r + NL)));
-    }
+    const jac<fp> acc = ld_g1j(srec);
     fp x = fp_zero(), y = fp_zero();
     if (!acc.inf) g1_to_affine(x, y, acc);
     g1_compress(out48, x, y, acc.inf);
@@ -351,42 +385,53 @@ struct HBuf {
     }
 };
 
-// the committee key cache of a device: fastcrypto validates a BLS public key once, when it is
-// deserialized; here a key is decoded and subgroup-checked the first time a call names it, and its
-// record (or its failure status) is kept for every later call.  Full -> calls decode uncached.
+// The committee key cache of a device.  fastcrypto validates a BLS public key once, when it is
+// deserialized; here nwv_bls_keycache_register (epoch start: the committee's keys) decodes and
+// subgroup-checks keys once and keeps the records of the VALID ones.  Verification calls only look
+// keys up: a key the cache does not hold (a stray key, a single verify by an outsider, an invalid
+// key) is decoded into the call's own scratch table and never takes a slot.  Slots are published
+// only after the fill kernel has completed; reset (epoch change) waits for calls in flight, which
+// hold the lock shared while their kernels read the records.
 struct BlsKeyCache {
-    static constexpr uint32_t CAP = 65536;
-    DBuf rec, st;  // CAP x G2_REC_WORDS u32 records, CAP int32 statuses
+    std::shared_mutex mu;
+    DBuf rec, st;  // KC_CAP x G2_REC_WORDS u32 records, KC_CAP int32 statuses
     std::unordered_map<std::string, uint32_t> slot;
     uint32_t used = 0;
-    void clear() {
-        slot.clear();
-        used = 0;
-    }
 };
 
-// one device of a context: streams and reusable staging / scratch buffers (one call at a time)
-struct BlsDev {
-    int ordinal = -1;
-    uint32_t flags = 0;  // the context's nwv_init flags
-    hipStream_t stream = nullptr;        // H2D, signatures, pairing check, D2H
+// One call in flight: its streams, staging arena and scratch.  A device keeps a pool of these, so
+// concurrent callers run their pipelines side by side instead of queueing on one device lock.
+struct BlsLane {
+    hipStream_t stream = nullptr;              // H2D, signatures, pairing check, D2H
     hipStream_t side[2] = {nullptr, nullptr};  // keys + key sums; hash to G1
-    std::mutex mu;
     HBuf stage;
     DBuf in, work;
-    BlsKeyCache kc;
     // [0,1] keys, [1,2] key sums (side 0); [3,4] signatures (main); [5,6] hash to G1 (side 1);
     // [7,8] pairing check (main); [9] inputs resident, [10] side 0 done, [11] side 1 done
     hipEvent_t ev[12] = {};
-    double last_ms[5] = {0, 0, 0, 0, 0};
-    int last_path = 0;  // nwv_bls_last_path
-    ~BlsDev() {
+    ~BlsLane() {
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
         for (auto& t : side)
             if (t) (void)hipStreamDestroy(t);
         if (stream) (void)hipStreamDestroy(stream);
     }
+};
+
+constexpr size_t kMaxLanes = 8;
+
+struct BlsDev {
+    int ordinal = -1;
+    uint32_t flags = 0;  // the context's nwv_init flags
+    BlsKeyCache kc;
+    std::mutex pool_mu;
+    std::condition_variable pool_cv;
+    std::vector<std::unique_ptr<BlsLane>> lanes;
+    std::vector<BlsLane*> idle;
+    std::mutex stat_mu;  // the last completed verify_many call's stage times and path
+    double last_ms[5] = {0, 0, 0, 0, 0};
+    int last_path = 0;
+    uint64_t last_keys[2] = {0, 0};  // key-list entries found in the cache, distinct keys decoded
 };
 std::mutex g_mu;
 std::unordered_map<nwv_ctx*, BlsDev*> g_devs;
@@ -404,16 +449,59 @@ int dev_of(nwv_ctx* ctx, BlsDev** out) {
     auto* d = new BlsDev;
     d->ordinal = ord;
     d->flags = nwv_internal_ctx_flags(ctx);
-    if (hipSetDevice(ord) != hipSuccess || hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&d->side[0], hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&d->side[1], hipStreamNonBlocking) != hipSuccess) {
-        delete d;
-        return nwv_internal_set_err(NWV_ERR_HIP, "bls stream");
-    }
     g_devs[ctx] = d;
     *out = d;
     return NWV_OK;
 }
+
+// a lane of the device's pool for the duration of one call (created on demand, at most kMaxLanes)
+class LaneLease {
+  public:
+    explicit LaneLease(BlsDev& d) : d_(d) {
+        std::unique_lock<std::mutex> g(d.pool_mu);
+        for (;;) {
+            if (!d.idle.empty()) {
+                lane_ = d.idle.back();
+                d.idle.pop_back();
+                break;
+            }
+            if (d.lanes.size() < kMaxLanes) {
+                auto l = std::make_unique<BlsLane>();
+                if (hipSetDevice(d.ordinal) != hipSuccess ||
+                    hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking) != hipSuccess ||
+                    hipStreamCreateWithFlags(&l->side[0], hipStreamNonBlocking) != hipSuccess ||
+                    hipStreamCreateWithFlags(&l->side[1], hipStreamNonBlocking) != hipSuccess) {
+                    rc_ = nwv_internal_set_err(NWV_ERR_HIP, "bls stream");
+                    return;
+                }
+                for (auto& e : l->ev)
+                    if (hipEventCreate(&e) != hipSuccess) {
+                        rc_ = nwv_internal_set_err(NWV_ERR_HIP, "bls event");
+                        return;
+                    }
+                lane_ = l.get();
+                d.lanes.push_back(std::move(l));
+                break;
+            }
+            d.pool_cv.wait(g);
+        }
+        if (hipSetDevice(d.ordinal) != hipSuccess) rc_ = nwv_internal_set_err(NWV_ERR_HIP, "hipSetDevice (bls)");
+    }
+    ~LaneLease() {
+        if (!lane_) return;
+        std::lock_guard<std::mutex> g(d_.pool_mu);
+        d_.idle.push_back(lane_);
+        d_.pool_cv.notify_one();
+    }
+    int rc() const { return rc_; }
+    BlsLane& operator*() { return *lane_; }
+    BlsLane* operator->() { return lane_; }
+
+  private:
+    BlsDev& d_;
+    BlsLane* lane_ = nullptr;
+    int rc_ = NWV_OK;
+};
 
 // an arena of sections placed 256-byte aligned, filled on the host, copied with one H2D
 struct Arena {
@@ -432,9 +520,81 @@ struct Arena {
 constexpr int kBlocks(size_t n) { return (int)((n + BLS_LANES - 1) / BLS_LANES); }
 // blocks of the group kernels: 8 items per 64-lane block
 constexpr int gBlocks(size_t n) { return (int)((n + BLS_LANES / GRP - 1) / (BLS_LANES / GRP)); }
+size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// the whole verify_many pipeline on one device: after one H2D copy, three streams --
-//   side 0: the call's new keys into the key cache (k_bls_keys_fill), then the key sums (k_bls_apk_g)
+// Key registration: the keys the cache does not hold are decoded and subgroup-checked into a
+// scratch table, then (after the stream has completed) the valid ones are copied into fresh
+// slots and published.  Invalid keys take no slot; a failure publishes nothing.
+int keycache_register(BlsDev& d, size_t n_keys, const uint8_t* keys) {
+    if (d.flags & NWV_FLAG_NO_KEYCACHE) return NWV_OK;
+    {  // fast path: every key already held
+        std::shared_lock<std::shared_mutex> g(d.kc.mu);
+        bool all = d.kc.rec.p != nullptr;
+        for (size_t j = 0; j < n_keys && all; j++)
+            all = d.kc.slot.count(std::string(reinterpret_cast<const char*>(keys + 96 * j), 96)) != 0;
+        if (all) return NWV_OK;
+    }
+    LaneLease lane(d);
+    if (lane.rc()) return lane.rc();
+    std::unique_lock<std::shared_mutex> g(d.kc.mu);
+    int rc;
+    if ((rc = d.kc.rec.ensure((size_t)4 * G2_REC_WORDS * KC_CAP)) || (rc = d.kc.st.ensure((size_t)4 * KC_CAP)))
+        return rc;
+    std::vector<std::string> fresh;
+    std::vector<uint8_t> fk;
+    std::unordered_map<std::string, uint32_t> seen;
+    for (size_t j = 0; j < n_keys; j++) {
+        std::string kb(reinterpret_cast<const char*>(keys + 96 * j), 96);
+        if (d.kc.slot.count(kb) || seen.count(kb)) continue;
+        seen.emplace(kb, (uint32_t)fresh.size());
+        fresh.push_back(kb);
+        fk.insert(fk.end(), keys + 96 * j, keys + 96 * (j + 1));
+    }
+    const size_t m = fresh.size();
+    if (m == 0) return NWV_OK;
+    // scratch: keys, identity slot list, records, statuses; then the copy lists
+    const size_t o_keys = 0, o_slot = al256(96 * m), o_rec = al256(o_slot + 4 * m),
+                 o_st = al256(o_rec + 4 * G2_REC_WORDS * m), o_src = al256(o_st + 4 * m), o_dst = al256(o_src + 4 * m),
+                 o_end = o_dst + 4 * m;
+    if ((rc = lane->work.ensure(o_end)) || (rc = lane->stage.ensure(o_end))) return rc;
+    uint8_t* w = static_cast<uint8_t*>(lane->work.p);
+    uint8_t* h = static_cast<uint8_t*>(lane->stage.p);
+    std::memcpy(h + o_keys, fk.data(), 96 * m);
+    auto* hs = reinterpret_cast<uint32_t*>(h + o_slot);
+    for (size_t j = 0; j < m; j++) hs[j] = (uint32_t)j;
+    BLS_HIP(hipMemcpyAsync(w, h, o_rec, hipMemcpyHostToDevice, lane->stream));
+    hipLaunchKernelGGL(k_bls_keys_fill, dim3(kBlocks(m)), dim3(BLS_LANES), 0, lane->stream, (uint32_t)m, w + o_keys,
+                       reinterpret_cast<const uint32_t*>(w + o_slot), reinterpret_cast<uint32_t*>(w + o_rec),
+                       reinterpret_cast<int32_t*>(w + o_st));
+    BLS_HIP(hipGetLastError());
+    BLS_HIP(hipMemcpyAsync(h + o_st, w + o_st, 4 * m, hipMemcpyDeviceToHost, lane->stream));
+    BLS_HIP(hipStreamSynchronize(lane->stream));
+    const auto* kst = reinterpret_cast<const int32_t*>(h + o_st);
+    auto* src = reinterpret_cast<uint32_t*>(h + o_src);
+    auto* dst = reinterpret_cast<uint32_t*>(h + o_dst);
+    size_t nv = 0;
+    for (size_t j = 0; j < m && d.kc.used + nv < KC_CAP; j++)
+        if (kst[j] == ST_OK) {
+            src[nv] = (uint32_t)j;
+            dst[nv] = d.kc.used + (uint32_t)nv;
+            nv++;
+        }
+    if (nv == 0) return NWV_OK;
+    BLS_HIP(hipMemcpyAsync(w + o_src, h + o_src, o_end - o_src, hipMemcpyHostToDevice, lane->stream));
+    hipLaunchKernelGGL(k_bls_rec_copy, dim3(kBlocks(nv * G2_REC_WORDS)), dim3(BLS_LANES), 0, lane->stream,
+                       (uint32_t)nv, reinterpret_cast<const uint32_t*>(w + o_src),
+                       reinterpret_cast<const uint32_t*>(w + o_dst), reinterpret_cast<const uint32_t*>(w + o_rec),
+                       static_cast<uint32_t*>(d.kc.rec.p), static_cast<int32_t*>(d.kc.st.p));
+    BLS_HIP(hipGetLastError());
+    BLS_HIP(hipStreamSynchronize(lane->stream));
+    for (size_t k = 0; k < nv; k++) d.kc.slot.emplace(fresh[src[k]], dst[k]);  // published after the copy
+    d.kc.used += (uint32_t)nv;
+    return NWV_OK;
+}
+
+// the whole verify_many pipeline on one lane of a device: after one H2D copy, three streams --
+//   side 0: the call's keys the cache does not hold, decoded into the scratch table
+//           (k_bls_keys_fill), then the key sums (k_bls_apk_g)
 //   main  : signature decode + G1 checks (k_bls_sigs)
 //   side 1: hash to G1 (k_bls_h2c_g)
 // -- then, joined on the main stream, the statuses in the oracle's order and the pairing check
@@ -442,92 +602,74 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
               const uint32_t* pk_cnt, const uint32_t* pk_idx, size_t n_idx, const uint8_t* msg_base,
               const uint64_t* msg_off, const uint32_t* msg_len, size_t msg_bytes, const uint8_t* dst, size_t dl,
               int32_t* status) {
-    std::lock_guard<std::mutex> g(d.mu);
-    BLS_HIP(hipSetDevice(d.ordinal));
+    LaneLease lane(d);
+    if (lane.rc()) return lane.rc();
+    BlsLane& L = *lane;
     static const uint8_t zero[8] = {0};
     const bool batch = !(d.flags & NWV_FLAG_BLS_PER_ITEM);
     int rc;
-    // key slots: the cache's, or (cache off / full) a per-call table in the scratch
-    bool cached = !(d.flags & NWV_FLAG_NO_KEYCACHE);
-    std::vector<uint32_t> kslot(n_keys), fill_slot;
+    // the call's key table: cache slots (lookups only) or scratch entries KC_CAP + j
+    std::shared_lock<std::shared_mutex> kc_hold(d.kc.mu);  // records stay put while our kernels read them
+    const bool cached = !(d.flags & NWV_FLAG_NO_KEYCACHE) && d.kc.rec.p != nullptr;
+    std::vector<uint32_t> ktab(n_keys), fill_slot;
     std::vector<uint8_t> fill_keys;
-    if (cached) {
-        if ((rc = d.kc.rec.ensure((size_t)4 * G2_REC_WORDS * BlsKeyCache::CAP)) ||
-            (rc = d.kc.st.ensure((size_t)4 * BlsKeyCache::CAP)))
-            return rc;
+    uint64_t hits = 0;
+    {
         std::unordered_map<std::string, uint32_t> fresh;
-        for (size_t j = 0; j < n_keys && cached; j++) {
+        for (size_t j = 0; j < n_keys; j++) {
             std::string kb(reinterpret_cast<const char*>(keys + 96 * j), 96);
-            auto it = d.kc.slot.find(kb);
-            if (it != d.kc.slot.end()) {
-                kslot[j] = it->second;
-                continue;
+            if (cached) {
+                auto it = d.kc.slot.find(kb);
+                if (it != d.kc.slot.end()) {
+                    ktab[j] = it->second;
+                    hits++;
+                    continue;
+                }
             }
             auto f = fresh.find(kb);
             if (f != fresh.end()) {
-                kslot[j] = f->second;
+                ktab[j] = KC_CAP + f->second;
                 continue;
             }
-            if (d.kc.used + fresh.size() >= BlsKeyCache::CAP) {
-                cached = false;
-                break;
-            }
-            const uint32_t sl = d.kc.used + (uint32_t)fresh.size();
-            fresh.emplace(std::move(kb), sl);
-            kslot[j] = sl;
-            fill_slot.push_back(sl);
+            const uint32_t e = (uint32_t)fresh.size();
+            fresh.emplace(std::move(kb), e);
+            ktab[j] = KC_CAP + e;
+            fill_slot.push_back(e);
             fill_keys.insert(fill_keys.end(), keys + 96 * j, keys + 96 * (j + 1));
         }
-        if (cached) {
-            for (auto& kv : fresh) d.kc.slot.emplace(kv.first, kv.second);
-            d.kc.used += (uint32_t)fresh.size();
-        } else {
-            fill_slot.clear();
-            fill_keys.clear();
-        }
     }
-    std::vector<uint32_t> remap;
-    const uint32_t* idx_src = pk_idx;
-    if (cached && n_idx) {
-        remap.resize(n_idx);
-        for (size_t t = 0; t < n_idx; t++) remap[t] = kslot[pk_idx[t]];
-        idx_src = remap.data();
-    }
-    const size_t n_dec = cached ? fill_slot.size() : n_keys;  // keys decoded by this call
-    if (!cached) {
-        fill_slot.resize(n_keys);
-        for (size_t j = 0; j < n_keys; j++) fill_slot[j] = (uint32_t)j;
-    }
+    std::vector<uint32_t> remap(n_idx);
+    for (size_t t = 0; t < n_idx; t++) remap[t] = ktab[pk_idx[t]];
+    const size_t n_dec = fill_slot.size();  // keys decoded by this call
     uint8_t seed[32];
     nwv_internal_fill_seed(nullptr, seed);  // the batch coefficients' key: OS entropy per call
     Arena a;
-    const size_t o_keys = a.add(cached ? (n_dec ? (const void*)fill_keys.data() : zero) : (const void*)keys,
-                                cached ? 96 * n_dec + 8 : 96 * n_keys),
+    const size_t o_keys = a.add(n_dec ? (const void*)fill_keys.data() : zero, 96 * n_dec + 8),
                  o_kslot = a.add(n_dec ? (const void*)fill_slot.data() : zero, 4 * n_dec + 4),
                  o_sigs = a.add(sigs, 48 * n), o_off = a.add(pk_off, 4 * n), o_cnt = a.add(pk_cnt, 4 * n),
-                 o_idx = a.add(n_idx ? (const void*)idx_src : zero, 4 * n_idx + 4),
+                 o_idx = a.add(n_idx ? (const void*)remap.data() : zero, 4 * n_idx + 4),
                  o_msg = a.add(msg_bytes ? (const void*)msg_base : zero, msg_bytes + 1),
                  o_moff = a.add(msg_off, 8 * n), o_mlen = a.add(msg_len, 4 * n), o_dst = a.add(dst, dl),
                  o_seed = a.add(seed, 32);
-    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    if ((rc = d.stage.ensure(al(a.total) + 64)) || (rc = d.in.ensure(a.total))) return rc;
-    uint8_t* h = static_cast<uint8_t*>(d.stage.p);
+    if ((rc = L.stage.ensure(al256(a.total) + 64)) || (rc = L.in.ensure(a.total))) return rc;
+    uint8_t* h = static_cast<uint8_t*>(L.stage.p);
     for (size_t k = 0; k < a.parts.size(); k++)
         if (a.parts[k].second) std::memcpy(h + a.offs[k], a.parts[k].first, a.parts[k].second);
-    // scratch: (uncached) key records + statuses, item sig / H / apk records, three status arrays,
+    // scratch: the call's key records + statuses, item sig / H / apk records, three status arrays,
     // the batch check's shares (W-order Fp12 + Jacobian G1 per item) and its verdict word
-    const size_t w_krec = 0, w_kst = w_krec + (cached ? 0 : 4 * G2_REC_WORDS * n_keys),
-                 w_srec = al(w_kst + (cached ? 0 : 4 * n_keys)), w_hrec = w_srec + 4 * G1_REC_WORDS * n,
-                 w_arec = w_hrec + 4 * G1_REC_WORDS * n, w_st = w_arec + 4 * G2_REC_WORDS * (n + 1),
-                 w_ssig = al(w_st + 4 * n), w_sapk = al(w_ssig + 4 * n), w_ok = al(w_sapk + 4 * n),
-                 w_frec = al(w_ok + 4), w_jrec = al(w_frec + 4 * F12_REC_WORDS * (batch ? n + 1 : 0)),
-                 w_prec = al(w_jrec + 4 * G1J_REC_WORDS * (batch ? n : 0)),
+    const size_t w_krec = 0, w_kst = w_krec + 4 * G2_REC_WORDS * n_dec, w_srec = al256(w_kst + 4 * n_dec + 4),
+                 w_hrec = w_srec + 4 * G1_REC_WORDS * n, w_arec = w_hrec + 4 * G1_REC_WORDS * n,
+                 w_st = w_arec + 4 * G2_REC_WORDS * (n + 1), w_ssig = al256(w_st + 4 * n), w_sapk = al256(w_ssig + 4 * n),
+                 w_ok = al256(w_sapk + 4 * n), w_frec = al256(w_ok + 4),
+                 w_jrec = al256(w_frec + 4 * F12_REC_WORDS * (batch ? n + 1 : 0)),
+                 w_prec = al256(w_jrec + 4 * G1J_REC_WORDS * (batch ? n : 0)),
                  w_end = w_prec + 4 * G1J_REC_WORDS * (batch ? n + 1 : 0) + 4;
-    if ((rc = d.work.ensure(w_end))) return rc;
-    uint8_t* in = static_cast<uint8_t*>(d.in.p);
-    uint8_t* w = static_cast<uint8_t*>(d.work.p);
-    auto* krec = cached ? static_cast<uint32_t*>(d.kc.rec.p) : reinterpret_cast<uint32_t*>(w + w_krec);
-    auto* kst = cached ? static_cast<int32_t*>(d.kc.st.p) : reinterpret_cast<int32_t*>(w + w_kst);
+    if ((rc = L.work.ensure(w_end))) return rc;
+    uint8_t* in = static_cast<uint8_t*>(L.in.p);
+    uint8_t* w = static_cast<uint8_t*>(L.work.p);
+    KeyTab kt{cached ? static_cast<const uint32_t*>(d.kc.rec.p) : nullptr,
+              cached ? static_cast<const int32_t*>(d.kc.st.p) : nullptr, reinterpret_cast<uint32_t*>(w + w_krec),
+              reinterpret_cast<int32_t*>(w + w_kst)};
     auto* srec = reinterpret_cast<uint32_t*>(w + w_srec);
     auto* hrec = reinterpret_cast<uint32_t*>(w + w_hrec);
     auto* arec = reinterpret_cast<uint32_t*>(w + w_arec);
@@ -538,46 +680,45 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     auto* frec = reinterpret_cast<uint32_t*>(w + w_frec);
     auto* jrec = reinterpret_cast<uint32_t*>(w + w_jrec);
     auto* prec = reinterpret_cast<uint32_t*>(w + w_prec);
-    if (!d.ev[0])
-        for (auto& e : d.ev) BLS_HIP(hipEventCreate(&e));
-    hipStream_t s0 = d.stream, s1 = d.side[0], s2 = d.side[1];
+    hipStream_t s0 = L.stream, s1 = L.side[0], s2 = L.side[1];
     BLS_HIP(hipMemcpyAsync(in, h, a.total, hipMemcpyHostToDevice, s0));
-    BLS_HIP(hipEventRecord(d.ev[9], s0));
-    BLS_HIP(hipStreamWaitEvent(s1, d.ev[9], 0));
-    BLS_HIP(hipStreamWaitEvent(s2, d.ev[9], 0));
+    BLS_HIP(hipEventRecord(L.ev[9], s0));
+    BLS_HIP(hipStreamWaitEvent(s1, L.ev[9], 0));
+    BLS_HIP(hipStreamWaitEvent(s2, L.ev[9], 0));
     // side 0: keys, key sums
-    BLS_HIP(hipEventRecord(d.ev[0], s1));
+    BLS_HIP(hipEventRecord(L.ev[0], s1));
     if (n_dec)
         hipLaunchKernelGGL(k_bls_keys_fill, dim3(kBlocks(n_dec)), dim3(BLS_LANES), 0, s1, (uint32_t)n_dec, in + o_keys,
-                           reinterpret_cast<const uint32_t*>(in + o_kslot), krec, kst);
-    BLS_HIP(hipEventRecord(d.ev[1], s1));
-    hipLaunchKernelGGL(k_bls_apk_g, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s1, (uint32_t)n, (const uint32_t*)krec,
-                       (const int32_t*)kst, reinterpret_cast<const uint32_t*>(in + o_off),
-                       reinterpret_cast<const uint32_t*>(in + o_cnt), reinterpret_cast<const uint32_t*>(in + o_idx),
-                       arec, sapk);
-    BLS_HIP(hipEventRecord(d.ev[2], s1));
-    BLS_HIP(hipEventRecord(d.ev[10], s1));
+                           reinterpret_cast<const uint32_t*>(in + o_kslot), const_cast<uint32_t*>(kt.rs),
+                           const_cast<int32_t*>(kt.ss));
+    BLS_HIP(hipEventRecord(L.ev[1], s1));
+    hipLaunchKernelGGL(k_bls_apk_g, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s1, (uint32_t)n, kt,
+                       reinterpret_cast<const uint32_t*>(in + o_off), reinterpret_cast<const uint32_t*>(in + o_cnt),
+                       reinterpret_cast<const uint32_t*>(in + o_idx), arec, sapk);
+    BLS_HIP(hipEventRecord(L.ev[2], s1));
+    BLS_HIP(hipEventRecord(L.ev[10], s1));
     // side 1: hash to G1 (every item: the statuses are not known yet)
-    BLS_HIP(hipEventRecord(d.ev[5], s2));
+    BLS_HIP(hipEventRecord(L.ev[5], s2));
     hipLaunchKernelGGL(k_bls_h2c_g, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s2, (uint32_t)n, in + o_msg,
                        reinterpret_cast<const uint64_t*>(in + o_moff), reinterpret_cast<const uint32_t*>(in + o_mlen),
                        in + o_dst, (uint32_t)dl, hrec);
-    BLS_HIP(hipEventRecord(d.ev[6], s2));
-    BLS_HIP(hipEventRecord(d.ev[11], s2));
+    BLS_HIP(hipEventRecord(L.ev[6], s2));
+    BLS_HIP(hipEventRecord(L.ev[11], s2));
     // main: signatures, then the join
-    BLS_HIP(hipEventRecord(d.ev[3], s0));
+    BLS_HIP(hipEventRecord(L.ev[3], s0));
     hipLaunchKernelGGL(k_bls_sigs, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, in + o_sigs, srec, ssig);
-    BLS_HIP(hipEventRecord(d.ev[4], s0));
-    BLS_HIP(hipStreamWaitEvent(s0, d.ev[10], 0));
-    BLS_HIP(hipStreamWaitEvent(s0, d.ev[11], 0));
+    BLS_HIP(hipEventRecord(L.ev[4], s0));
+    BLS_HIP(hipStreamWaitEvent(s0, L.ev[10], 0));
+    BLS_HIP(hipStreamWaitEvent(s0, L.ev[11], 0));
     hipLaunchKernelGGL(k_bls_status, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, (const int32_t*)ssig,
                        (const int32_t*)sapk, st);
-    BLS_HIP(hipEventRecord(d.ev[7], s0));
+    BLS_HIP(hipEventRecord(L.ev[7], s0));
     auto per_item = [&]() {
         hipLaunchKernelGGL(k_bls_pair, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, (const uint32_t*)srec,
                            (const uint32_t*)hrec, (const uint32_t*)arec, st);
     };
-    int32_t* hst = reinterpret_cast<int32_t*>(h + al(a.total));  // pinned: the batch verdict word
+    int32_t* hst = reinterpret_cast<int32_t*>(h + al256(a.total));  // pinned: the batch verdict word
+    int path;
     if (batch) {
         hipLaunchKernelGGL(k_bls_rlc_pts, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, (const uint32_t*)srec,
                            (const uint32_t*)hrec, (const int32_t*)st, (const uint8_t*)(in + o_seed), prec, jrec);
@@ -591,32 +732,30 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
             hipLaunchKernelGGL(k_bls_ffold, dim3(gBlocks(m / 2)), dim3(BLS_LANES), 0, s0, m, frec);
         hipLaunchKernelGGL(k_bls_final, dim3(1), dim3(BLS_LANES), 0, s0, (const uint32_t*)frec, okw);
         BLS_HIP(hipMemcpyAsync(hst, okw, 4, hipMemcpyDeviceToHost, s0));
-        const hipError_t e = hipStreamSynchronize(s0);
-        if (e != hipSuccess) {
-            d.kc.clear();  // the fill may not have landed
-            return nwv_internal_set_err(NWV_ERR_HIP, hipGetErrorString(e));
-        }
+        BLS_HIP(hipStreamSynchronize(s0));
         BLS_HIP(hipGetLastError());
-        d.last_path = *hst == 1 ? 1 : 2;
+        path = *hst == 1 ? 1 : 2;
         if (*hst != 1) per_item();  // the batch check rejected: name the failing items exactly
     } else {
         per_item();
-        d.last_path = 0;
+        path = 0;
     }
-    BLS_HIP(hipEventRecord(d.ev[8], s0));
+    BLS_HIP(hipEventRecord(L.ev[8], s0));
     BLS_HIP(hipGetLastError());
     BLS_HIP(hipMemcpyAsync(status, st, 4 * n, hipMemcpyDeviceToHost, s0));
-    const hipError_t e = hipStreamSynchronize(s0);
-    if (e != hipSuccess) {
-        d.kc.clear();
-        return nwv_internal_set_err(NWV_ERR_HIP, hipGetErrorString(e));
-    }
+    BLS_HIP(hipStreamSynchronize(s0));
     const int pairs[5][2] = {{0, 1}, {3, 4}, {5, 6}, {1, 2}, {7, 8}};  // keys, sigs, h2c, apk, pairing
+    double ms5[5];
     for (int k = 0; k < 5; k++) {
         float ms = 0;
-        BLS_HIP(hipEventElapsedTime(&ms, d.ev[pairs[k][0]], d.ev[pairs[k][1]]));
-        d.last_ms[k] = ms;
+        BLS_HIP(hipEventElapsedTime(&ms, L.ev[pairs[k][0]], L.ev[pairs[k][1]]));
+        ms5[k] = ms;
     }
+    std::lock_guard<std::mutex> g(d.stat_mu);
+    std::memcpy(d.last_ms, ms5, sizeof ms5);
+    d.last_path = path;
+    d.last_keys[0] = hits;
+    d.last_keys[1] = n_dec;
     return NWV_OK;
 }
 
@@ -671,7 +810,7 @@ int nwv_bls_last_kernel_ms(nwv_ctx* ctx, double out_ms[5]) {
     BlsDev* d;
     int rc = dev_of(ctx, &d);
     if (rc) return rc;
-    std::lock_guard<std::mutex> g(d->mu);
+    std::lock_guard<std::mutex> g(d->stat_mu);
     for (int k = 0; k < 5; k++) out_ms[k] = d->last_ms[k];
     return NWV_OK;
 }
@@ -680,8 +819,46 @@ int nwv_bls_last_path(nwv_ctx* ctx) {
     BlsDev* d;
     int rc = dev_of(ctx, &d);
     if (rc) return rc;
-    std::lock_guard<std::mutex> g(d->mu);
+    std::lock_guard<std::mutex> g(d->stat_mu);
     return d->last_path;
+}
+
+int nwv_bls_last_keys(nwv_ctx* ctx, uint64_t out[2]) {
+    if (!out) return nwv_internal_set_err(NWV_ERR_ARG, "null argument");
+    BlsDev* d;
+    int rc = dev_of(ctx, &d);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(d->stat_mu);
+    out[0] = d->last_keys[0];
+    out[1] = d->last_keys[1];
+    return NWV_OK;
+}
+
+int nwv_bls_keycache_register(nwv_ctx* ctx, size_t n_keys, const uint8_t* keys) {
+    if (n_keys && !keys) return nwv_internal_set_err(NWV_ERR_ARG, "null argument");
+    if (n_keys > KC_CAP) return nwv_internal_set_err(NWV_ERR_ARG, "more keys than the cache holds");
+    BlsDev* d;
+    int rc = dev_of(ctx, &d);
+    if (rc) return rc;
+    return n_keys ? keycache_register(*d, n_keys, keys) : NWV_OK;
+}
+
+int nwv_bls_keycache_reset(nwv_ctx* ctx) {
+    BlsDev* d;
+    int rc = dev_of(ctx, &d);
+    if (rc) return rc;
+    std::unique_lock<std::shared_mutex> g(d->kc.mu);  // waits for calls that read the records
+    d->kc.slot.clear();
+    d->kc.used = 0;
+    return NWV_OK;
+}
+
+int nwv_bls_keycache_size(nwv_ctx* ctx) {
+    BlsDev* d;
+    int rc = dev_of(ctx, &d);
+    if (rc) return rc;
+    std::shared_lock<std::shared_mutex> g(d->kc.mu);
+    return (int)d->kc.used;
 }
 
 int nwv_bls_aggregate_verify(nwv_ctx* ctx, const uint8_t* sig48, const uint8_t* pks, size_t n_pks, const uint8_t* msg,
@@ -709,24 +886,32 @@ int nwv_bls_aggregate(nwv_ctx* ctx, size_t n, const uint8_t* sigs48, uint8_t out
     if (status_or_null) *status_or_null = NWV_BLS_AGGR_MISMATCH;
     if (n == 0) return NWV_ERR_SIGNATURE;
     if (!sigs48 || !out48) return nwv_internal_set_err(NWV_ERR_ARG, "null argument");
+    if (n > (1u << 26)) return nwv_internal_set_err(NWV_ERR_ARG, "batch too large");
     BlsDev* d;
     int rc = dev_of(ctx, &d);
     if (rc) return rc;
-    std::lock_guard<std::mutex> g(d->mu);
-    BLS_HIP(hipSetDevice(d->ordinal));
-    const size_t w_rec = 0, w_st = 4 * G1_REC_WORDS * n, w_out = w_st + 4 * n, w_ost = w_out + 64, w_end = w_ost + 8;
-    if ((rc = d->in.ensure(48 * n)) || (rc = d->work.ensure(w_end)) || (rc = d->stage.ensure(128))) return rc;
-    uint8_t* w = static_cast<uint8_t*>(d->work.p);
-    BLS_HIP(hipMemcpyAsync(d->in.p, sigs48, 48 * n, hipMemcpyHostToDevice, d->stream));
-    hipLaunchKernelGGL(k_bls_sigs, dim3(kBlocks(n)), dim3(BLS_LANES), 0, d->stream, (uint32_t)n,
-                       (const uint8_t*)d->in.p, reinterpret_cast<uint32_t*>(w + w_rec), reinterpret_cast<int32_t*>(w + w_st));
-    hipLaunchKernelGGL(k_bls_g1_sum, dim3(1), dim3(1), 0, d->stream, (uint32_t)n,
-                       reinterpret_cast<const uint32_t*>(w + w_rec), reinterpret_cast<const int32_t*>(w + w_st),
-                       w + w_out, reinterpret_cast<int32_t*>(w + w_ost));
+    LaneLease lane(*d);
+    if ((rc = lane.rc())) return rc;
+    BlsLane& L = *lane;
+    const size_t w_rec = 0, w_st = al256(4 * G1_REC_WORDS * n), w_j = al256(w_st + 4 * n),
+                 w_out = al256(w_j + 4 * G1J_REC_WORDS * n), w_ost = w_out + 64, w_end = w_ost + 8;
+    if ((rc = L.in.ensure(48 * n)) || (rc = L.work.ensure(w_end)) || (rc = L.stage.ensure(128))) return rc;
+    uint8_t* w = static_cast<uint8_t*>(L.work.p);
+    auto* srec = reinterpret_cast<uint32_t*>(w + w_j);
+    BLS_HIP(hipMemcpyAsync(L.in.p, sigs48, 48 * n, hipMemcpyHostToDevice, L.stream));
+    hipLaunchKernelGGL(k_bls_sigs, dim3(kBlocks(n)), dim3(BLS_LANES), 0, L.stream, (uint32_t)n,
+                       (const uint8_t*)L.in.p, reinterpret_cast<uint32_t*>(w + w_rec), reinterpret_cast<int32_t*>(w + w_st));
+    hipLaunchKernelGGL(k_bls_sig_jac, dim3(kBlocks(n)), dim3(BLS_LANES), 0, L.stream, (uint32_t)n,
+                       reinterpret_cast<const uint32_t*>(w + w_rec), srec);
+    for (uint32_t m = (uint32_t)n; m > 1; m = (m + 1) / 2)
+        hipLaunchKernelGGL(k_bls_sfold, dim3(kBlocks(m / 2)), dim3(BLS_LANES), 0, L.stream, m, srec);
+    hipLaunchKernelGGL(k_bls_g1_sum_out, dim3(1), dim3(1), 0, L.stream, (uint32_t)n,
+                       reinterpret_cast<const int32_t*>(w + w_st), (const uint32_t*)srec, w + w_out,
+                       reinterpret_cast<int32_t*>(w + w_ost));
     BLS_HIP(hipGetLastError());
-    uint8_t* hs = static_cast<uint8_t*>(d->stage.p);
-    BLS_HIP(hipMemcpyAsync(hs, w + w_out, 64 + 8, hipMemcpyDeviceToHost, d->stream));
-    BLS_HIP(hipStreamSynchronize(d->stream));
+    uint8_t* hs = static_cast<uint8_t*>(L.stage.p);
+    BLS_HIP(hipMemcpyAsync(hs, w + w_out, 64 + 8, hipMemcpyDeviceToHost, L.stream));
+    BLS_HIP(hipStreamSynchronize(L.stream));
     int32_t st;
     std::memcpy(&st, hs + 64, 4);
     if (status_or_null) *status_or_null = st;
@@ -788,17 +973,18 @@ static int simple_launch(nwv_ctx* ctx, size_t in_bytes, const void* in_host, siz
     BlsDev* d;
     int rc = dev_of(ctx, &d);
     if (rc) return rc;
-    std::lock_guard<std::mutex> g(d->mu);
-    BLS_HIP(hipSetDevice(d->ordinal));
+    LaneLease lane(*d);
+    if ((rc = lane.rc())) return rc;
+    BlsLane& L = *lane;
     const size_t o2 = (in_bytes + 255) & ~(size_t)255;
-    if ((rc = d->in.ensure(o2 + in2_bytes + 16)) || (rc = d->work.ensure(out_bytes + 16))) return rc;
-    uint8_t* in = static_cast<uint8_t*>(d->in.p);
-    if (in_bytes) BLS_HIP(hipMemcpyAsync(in, in_host, in_bytes, hipMemcpyHostToDevice, d->stream));
-    if (in2_bytes) BLS_HIP(hipMemcpyAsync(in + o2, in2_host, in2_bytes, hipMemcpyHostToDevice, d->stream));
-    launch(d->stream, in, in + o2, static_cast<uint8_t*>(d->work.p));
+    if ((rc = L.in.ensure(o2 + in2_bytes + 16)) || (rc = L.work.ensure(out_bytes + 16))) return rc;
+    uint8_t* in = static_cast<uint8_t*>(L.in.p);
+    if (in_bytes) BLS_HIP(hipMemcpyAsync(in, in_host, in_bytes, hipMemcpyHostToDevice, L.stream));
+    if (in2_bytes) BLS_HIP(hipMemcpyAsync(in + o2, in2_host, in2_bytes, hipMemcpyHostToDevice, L.stream));
+    launch(L.stream, in, in + o2, static_cast<uint8_t*>(L.work.p));
     BLS_HIP(hipGetLastError());
-    BLS_HIP(hipMemcpyAsync(out_host, d->work.p, out_bytes, hipMemcpyDeviceToHost, d->stream));
-    BLS_HIP(hipStreamSynchronize(d->stream));
+    BLS_HIP(hipMemcpyAsync(out_host, L.work.p, out_bytes, hipMemcpyDeviceToHost, L.stream));
+    BLS_HIP(hipStreamSynchronize(L.stream));
     return NWV_OK;
 }
 

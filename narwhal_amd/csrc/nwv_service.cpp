@@ -109,16 +109,23 @@ void waiter_done(void* user, int32_t r) {
     w->cv.notify_one();
 }
 
-// Set while a flusher runs completion callbacks.  A callback may submit asynchronously, but a
-// blocking call from it (nwv_service_verify_*, nwv_service_flush) would wait for batches that
-// this very thread -- or, with both flushers inside callbacks, no thread -- would ever verify:
-// such calls return NWV_ERR_REENTRANT instead of deadlocking.
-thread_local bool tl_in_callback = false;
+// The service whose completion callbacks this thread is running (null outside callbacks).  A
+// callback may submit asynchronously, but a blocking call on THAT service (nwv_service_verify_*,
+// nwv_service_flush) would wait for batches that this very thread -- or, with both flushers inside
+// callbacks, no thread -- would ever verify: such calls return NWV_ERR_REENTRANT instead of
+// deadlocking.  Blocking calls on another service (or the engine) are not refused.  Set and
+// restored by an RAII guard, so a callback that unwinds cannot leave it set.
+thread_local const nwv_service* tl_cb_svc = nullptr;
+struct CallbackScope {
+    const nwv_service* prev;
+    explicit CallbackScope(const nwv_service* s) : prev(tl_cb_svc) { tl_cb_svc = s; }
+    ~CallbackScope() { tl_cb_svc = prev; }
+};
 
 template <class Submit>
-int verify_blocking(Submit submit, int32_t* result) {
+int verify_blocking(const nwv_service* svc, Submit submit, int32_t* result) {
     if (!result) return NWV_ERR_ARG;
-    if (tl_in_callback) return NWV_ERR_REENTRANT;
+    if (svc && tl_cb_svc == svc) return NWV_ERR_REENTRANT;
     Waiter w;
     const int rc = submit(&w);
     if (rc) return rc;
@@ -188,13 +195,14 @@ void nwv_service::run() {
         const int rc_call = nwv_verify_mixed_many(ctx, &com_b->view, H.size(), H.data(), rh.data(), V.size(),
                                                   V.data(), rv.data(), C.size(), C.data(), rc.data());
         size_t ih = 0, iv = 0, ic = 0;
-        tl_in_callback = true;
-        for (auto& it : batch) {
-            int32_t r = rc_call;
-            if (rc_call == 0) r = it->kind == HEADER ? rh[ih++] : it->kind == VOTE ? rv[iv++] : rc[ic++];
-            if (it->done) it->done(it->user, r);
+        {
+            CallbackScope scope(this);
+            for (auto& it : batch) {
+                int32_t r = rc_call;
+                if (rc_call == 0) r = it->kind == HEADER ? rh[ih++] : it->kind == VOTE ? rv[iv++] : rc[ic++];
+                if (it->done) it->done(it->user, r);
+            }
         }
-        tl_in_callback = false;
         lk.lock();
         for (auto& it : batch) open.erase(it->seq);
         stats[0]++;
@@ -320,19 +328,19 @@ int nwv_service_submit_certificate(nwv_service* svc, const nwv_certificate* c, n
 }
 
 int nwv_service_verify_header(nwv_service* svc, const nwv_header* h, int32_t* result) {
-    return verify_blocking([&](Waiter* w) { return nwv_service_submit_header(svc, h, waiter_done, w); }, result);
+    return verify_blocking(svc, [&](Waiter* w) { return nwv_service_submit_header(svc, h, waiter_done, w); }, result);
 }
 int nwv_service_verify_vote(nwv_service* svc, const nwv_vote* v, int32_t* result) {
-    return verify_blocking([&](Waiter* w) { return nwv_service_submit_vote(svc, v, waiter_done, w); }, result);
+    return verify_blocking(svc, [&](Waiter* w) { return nwv_service_submit_vote(svc, v, waiter_done, w); }, result);
 }
 int nwv_service_verify_certificate(nwv_service* svc, const nwv_certificate* c, int32_t* result) {
-    return verify_blocking([&](Waiter* w) { return nwv_service_submit_certificate(svc, c, waiter_done, w); },
+    return verify_blocking(svc, [&](Waiter* w) { return nwv_service_submit_certificate(svc, c, waiter_done, w); },
                            result);
 }
 
 int nwv_service_flush(nwv_service* svc) {
     if (!svc) return NWV_ERR_ARG;
-    if (tl_in_callback) return NWV_ERR_REENTRANT;
+    if (tl_cb_svc == svc) return NWV_ERR_REENTRANT;
     std::unique_lock<std::mutex> lk(svc->mu);
     const uint64_t upto = svc->next_seq;
     svc->flush_upto = std::max(svc->flush_upto, upto);

@@ -501,3 +501,339 @@ int nwv_certificate_new(const nwv_committee* committee, size_t n_votes, const ui
 }
 
 }  // extern "C"
+
+// ====================================================================================== BLS
+// The types layer under the reference's default scheme, BLS12-381 (crypto/src/lib.rs:29-33).  The
+// control flow is the Ed25519 layer's, check by check (types/src/primary.rs); what differs is the
+// key length in the digests (96-byte authors / origins) and the signature checks: a header's or a
+// vote's signature is Verifier::verify (one key), a certificate's aggregate is ONE
+// fast_aggregate_verify over its signers' keys (blst; no |pks| = |sigs| check: the aggregate is
+// a single G1 point), an aggregate holding no signature fails (sig: None).  All of a call's
+// signature checks go to the GPU as one nwv_bls_verify_many call over the committee's keys, which
+// are registered in the device's BLS key cache.
+#include "../../include/nwv_bls.h"
+
+namespace {
+constexpr size_t BK = 96;  // BLS public key bytes
+constexpr size_t BS = 48;  // BLS signature bytes
+
+void bls_header_preimage(const nwv_bls_header& h, std::vector<uint8_t>& b) {
+    const size_t at = b.size();
+    b.resize(at + BK + 16 + 36 * h.n_payload + 32 * h.n_parents);
+    uint8_t* w = at_bytes(b.data() + at, h.author, BK);
+    w = at_le64(w, h.round);
+    w = at_le64(w, h.epoch);
+    for (size_t i = 0; i < h.n_payload; i++) {
+        w = at_bytes(w, h.payload_digests + 32 * i, 32);
+        w = at_le32(w, h.payload_workers[i]);
+    }
+    at_bytes(w, h.parents, 32 * h.n_parents);
+}
+void bls_id_round_epoch_origin(const uint8_t* id, uint64_t round, uint64_t epoch, const uint8_t* origin,
+                               std::vector<uint8_t>& b) {
+    const size_t at = b.size();
+    b.resize(at + 48 + BK);
+    uint8_t* w = at_bytes(b.data() + at, id, 32);
+    w = at_le64(w, round);
+    w = at_le64(w, epoch);
+    at_bytes(w, origin, BK);
+}
+long bls_index(const nwv_bls_committee& c, const uint8_t* pk) {
+    size_t lo = 0, hi = c.n;
+    while (lo < hi) {
+        const size_t mid = (lo + hi) / 2;
+        const int r = std::memcmp(c.keys + BK * mid, pk, BK);
+        if (r == 0) return (long)mid;
+        if (r < 0) lo = mid + 1;
+        else hi = mid;
+    }
+    return -1;
+}
+uint64_t bls_stake(const nwv_bls_committee& c, const uint8_t* pk) {
+    const long i = bls_index(c, pk);
+    return i < 0 ? 0 : c.stakes[i];
+}
+bool bls_worker_known(const nwv_bls_committee& c, const uint8_t* author, uint32_t id) {
+    const long i = bls_index(c, author);
+    if (i < 0 || !c.n_workers) return false;
+    for (uint32_t k = 0; k < c.n_workers[i]; k++)
+        if (c.worker_ids[i][k] == id) return true;
+    return false;
+}
+uint64_t bls_quorum(const nwv_bls_committee& c) {
+    uint64_t total = 0;
+    for (size_t i = 0; i < c.n; i++) total += c.stakes[i];
+    return 2 * total / 3 + 1;
+}
+bool bls_is_genesis(const nwv_bls_committee& c, const nwv_bls_certificate& cert) {
+    return is_zero32(cert.header.id) && cert.header.round == 0 && cert.header.epoch == c.epoch &&
+           bls_index(c, cert.header.author) >= 0;
+}
+void bls_plan_header(const nwv_bls_committee& c, const nwv_bls_header& h, DigestBatch& db, HeaderPlan& p) {
+    if (h.epoch != c.epoch) {
+        p.pre = NWV_DAG_INVALID_EPOCH;
+        return;
+    }
+    p.digest = (long)db.add_begin();
+    bls_header_preimage(h, db.arena);
+    db.add_end();
+    if (bls_stake(c, h.author) == 0) {
+        p.post = NWV_DAG_UNKNOWN_AUTHORITY;
+        return;
+    }
+    for (size_t i = 0; i < h.n_payload; i++)
+        if (!bls_worker_known(c, h.author, h.payload_workers[i])) {
+            p.post = NWV_DAG_MALFORMED_HEADER;
+            return;
+        }
+}
+bool bls_valid_args(const nwv_bls_committee* c) { return c && (c->n == 0 || (c->keys && c->stakes)); }
+
+// The signature checks of one call as nwv_bls_verify_many items over the committee's keys: item =
+// (signature, signer indices, message).  A header's signature is checked over its id (when that
+// verdict is used, id == digest: InvalidHeaderId comes first), a vote's and a certificate's over
+// the digest computed by the call.
+struct BlsItems {
+    std::vector<uint8_t> sig, msg;
+    std::vector<uint32_t> off, cnt, idx, mlen;
+    std::vector<uint64_t> moff;
+    std::vector<int32_t> st;
+    void reset() {
+        sig.clear();
+        msg.clear();
+        off.clear();
+        cnt.clear();
+        idx.clear();
+        mlen.clear();
+        moff.clear();
+    }
+    long add(const uint8_t* s, const uint32_t* keys, size_t nk, const uint8_t* m) {
+        put(sig, s, BS);
+        off.push_back((uint32_t)idx.size());
+        cnt.push_back((uint32_t)nk);
+        idx.insert(idx.end(), keys, keys + nk);
+        moff.push_back(msg.size());
+        mlen.push_back(32);
+        put(msg, m, 32);
+        return (long)off.size() - 1;
+    }
+    int run(nwv_ctx* ctx, const nwv_bls_committee& c) {
+        st.assign(off.size(), 0);
+        if (off.empty()) return NWV_OK;
+        msg.resize(msg.size() + 8);
+        return nwv_bls_verify_many(ctx, c.n, c.keys, off.size(), sig.data(), off.data(), cnt.data(),
+                                   idx.empty() ? nullptr : idx.data(), msg.data(), moff.data(), mlen.data(), nullptr, 0,
+                                   st.data());
+    }
+};
+
+int bls_verify_mixed(nwv_ctx* ctx, const nwv_bls_committee& c, size_t nh, const nwv_bls_header* h, int32_t* hres,
+                     size_t nv, const nwv_bls_vote* v, int32_t* vres, size_t nc, const nwv_bls_certificate* cs,
+                     int32_t* cres) {
+    const uint64_t quorum = bls_quorum(c);
+    thread_local DigestBatch db;
+    thread_local BlsItems items;
+    db.reset();
+    items.reset();
+    // phase 1 (host): every preimage; the signature checks are listed once the digests are known
+    std::vector<HeaderPlan> hplan(nh), cplan(nc);
+    for (size_t i = 0; i < nh; i++) bls_plan_header(c, h[i], db, hplan[i]);
+    std::vector<long> vdig(nv, -1);
+    for (size_t i = 0; i < nv; i++) {
+        vdig[i] = (long)db.add_begin();
+        bls_id_round_epoch_origin(v[i].id, v[i].round, v[i].epoch, v[i].origin, db.arena);
+        db.add_end();
+    }
+    std::vector<uint8_t> done(nc, 0);
+    std::vector<long> cdig(nc, -1);
+    for (size_t i = 0; i < nc; i++) {
+        const nwv_bls_certificate& x = cs[i];
+        if (x.header.epoch != c.epoch || bls_is_genesis(c, x)) {
+            done[i] = 1;
+            continue;
+        }
+        bls_plan_header(c, x.header, db, cplan[i]);
+        cdig[i] = (long)db.add_begin();
+        bls_id_round_epoch_origin(x.header.id, x.header.round, x.header.epoch, x.header.author, db.arena);
+        db.add_end();
+    }
+    // phase 2: the digests (one BLAKE2b launch), then every signature check (one BLS call)
+    std::vector<uint8_t> dig;
+    int rc = db.run(ctx, dig);
+    if (rc) return rc;
+    std::vector<long> hsig(nh, -1), vsig(nv, -1), csig(nc, -1), asig(nc, -1);
+    std::vector<int32_t> after_header(nc, NWV_DAG_OK);
+    for (size_t i = 0; i < nh; i++) {
+        const HeaderPlan& p = hplan[i];
+        if (p.pre || p.post || std::memcmp(dig.data() + 32 * p.digest, h[i].id, 32) != 0) continue;
+        const uint32_t a = (uint32_t)bls_index(c, h[i].author);
+        hsig[i] = items.add(h[i].signature, &a, 1, h[i].id);
+    }
+    for (size_t i = 0; i < nv; i++) {
+        if (v[i].epoch != c.epoch || bls_stake(c, v[i].author) == 0) continue;
+        const uint32_t a = (uint32_t)bls_index(c, v[i].author);
+        vsig[i] = items.add(v[i].signature, &a, 1, dig.data() + 32 * vdig[i]);
+    }
+    std::vector<uint32_t> pks;
+    for (size_t i = 0; i < nc; i++) {
+        if (done[i]) continue;
+        const nwv_bls_certificate& x = cs[i];
+        const HeaderPlan& p = cplan[i];
+        if (p.pre || p.post || std::memcmp(dig.data() + 32 * p.digest, x.header.id, 32) != 0) continue;
+        const uint32_t a = (uint32_t)bls_index(c, x.header.author);
+        csig[i] = items.add(x.header.signature, &a, 1, x.header.id);
+        // bitmap -> pks in committee order (:505-520), quorum, then the aggregate
+        uint64_t weight = 0;
+        size_t it = 0;
+        pks.clear();
+        for (size_t k = 0; k < c.n; k++)
+            if (it < x.n_signed && x.signed_authorities[it] == (uint32_t)k) {
+                weight += c.stakes[k];
+                it++;
+                pks.push_back((uint32_t)k);
+            }
+        if (weight < quorum) {
+            after_header[i] = NWV_DAG_CERTIFICATE_REQUIRES_QUORUM;
+            continue;
+        }
+        if (!x.aggregated_signature) {  // sig: None -> signature::Error
+            after_header[i] = NWV_DAG_INVALID_SIGNATURE;
+            continue;
+        }
+        asig[i] = items.add(x.aggregated_signature, pks.data(), pks.size(), dig.data() + 32 * cdig[i]);
+    }
+    if ((rc = nwv_bls_keycache_register(ctx, c.n, c.keys))) return rc;  // no-op once registered
+    if ((rc = items.run(ctx, c))) return rc;
+    auto bad = [&](long k) { return k >= 0 && items.st[k] != NWV_BLS_OK; };
+    // phase 3: verdicts in the reference's check order
+    for (size_t i = 0; i < nh; i++) {
+        const HeaderPlan& p = hplan[i];
+        if (p.pre) hres[i] = p.pre;
+        else if (std::memcmp(dig.data() + 32 * p.digest, h[i].id, 32) != 0) hres[i] = NWV_DAG_INVALID_HEADER_ID;
+        else if (p.post) hres[i] = p.post;
+        else hres[i] = bad(hsig[i]) ? NWV_DAG_INVALID_SIGNATURE : NWV_DAG_OK;
+    }
+    for (size_t i = 0; i < nv; i++) {
+        if (v[i].epoch != c.epoch) vres[i] = NWV_DAG_INVALID_EPOCH;
+        else if (bls_stake(c, v[i].author) == 0) vres[i] = NWV_DAG_UNKNOWN_AUTHORITY;
+        else vres[i] = bad(vsig[i]) ? NWV_DAG_INVALID_SIGNATURE : NWV_DAG_OK;
+    }
+    for (size_t i = 0; i < nc; i++) {
+        const nwv_bls_certificate& x = cs[i];
+        if (x.header.epoch != c.epoch) {
+            cres[i] = NWV_DAG_INVALID_EPOCH;
+            continue;
+        }
+        if (done[i]) {  // genesis
+            cres[i] = NWV_DAG_OK;
+            continue;
+        }
+        const HeaderPlan& p = cplan[i];
+        if (p.pre) cres[i] = p.pre;
+        else if (std::memcmp(dig.data() + 32 * p.digest, x.header.id, 32) != 0) cres[i] = NWV_DAG_INVALID_HEADER_ID;
+        else if (p.post) cres[i] = p.post;
+        else if (bad(csig[i])) cres[i] = NWV_DAG_INVALID_SIGNATURE;
+        else if (after_header[i]) cres[i] = after_header[i];
+        else cres[i] = bad(asig[i]) ? NWV_DAG_INVALID_SIGNATURE : NWV_DAG_OK;
+    }
+    return NWV_OK;
+}
+template <class T, class F>
+int bls_digest_many(nwv_ctx* ctx, size_t n, const T* x, uint8_t* out, F pre) {
+    if (!ctx || (n && (!x || !out))) return NWV_ERR_ARG;
+    DigestBatch db;
+    for (size_t i = 0; i < n; i++) {
+        db.add_begin();
+        pre(x[i], db.arena);
+        db.add_end();
+    }
+    std::vector<uint8_t> d;
+    int rc = db.run(ctx, d);
+    if (rc) return rc;
+    if (n) std::memcpy(out, d.data(), 32 * n);
+    return NWV_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int nwv_bls_header_digest_many(nwv_ctx* ctx, size_t n, const nwv_bls_header* h, uint8_t* out) {
+    return bls_digest_many(ctx, n, h, out, [](const nwv_bls_header& x, std::vector<uint8_t>& b) { bls_header_preimage(x, b); });
+}
+int nwv_bls_vote_digest_many(nwv_ctx* ctx, size_t n, const nwv_bls_vote* v, uint8_t* out) {
+    return bls_digest_many(ctx, n, v, out, [](const nwv_bls_vote& x, std::vector<uint8_t>& b) {
+        bls_id_round_epoch_origin(x.id, x.round, x.epoch, x.origin, b);
+    });
+}
+int nwv_bls_certificate_digest_many(nwv_ctx* ctx, size_t n, const nwv_bls_certificate* c, uint8_t* out) {
+    return bls_digest_many(ctx, n, c, out, [](const nwv_bls_certificate& x, std::vector<uint8_t>& b) {
+        bls_id_round_epoch_origin(x.header.id, x.header.round, x.header.epoch, x.header.author, b);
+    });
+}
+
+int nwv_bls_verify_mixed_many(nwv_ctx* ctx, const nwv_bls_committee* committee, size_t n_headers,
+                              const nwv_bls_header* headers, int32_t* header_results, size_t n_votes,
+                              const nwv_bls_vote* votes, int32_t* vote_results, size_t n_certs,
+                              const nwv_bls_certificate* certs, int32_t* cert_results) {
+    if (!ctx || !bls_valid_args(committee) || (n_headers && (!headers || !header_results)) ||
+        (n_votes && (!votes || !vote_results)) || (n_certs && (!certs || !cert_results)))
+        return NWV_ERR_ARG;
+    return bls_verify_mixed(ctx, *committee, n_headers, headers, header_results, n_votes, votes, vote_results,
+                            n_certs, certs, cert_results);
+}
+
+int nwv_bls_validate_certificates(nwv_ctx* ctx, const nwv_bls_committee* committee, size_t n,
+                                  const nwv_bls_certificate* c, size_t* n_invalid, size_t* invalid_idx) {
+    if (!n_invalid || (n && !invalid_idx)) return NWV_ERR_ARG;
+    *n_invalid = 0;
+    if (n == 0) return NWV_OK;
+    std::vector<int32_t> r(n);
+    int rc = nwv_bls_verify_mixed_many(ctx, committee, 0, nullptr, nullptr, 0, nullptr, nullptr, n, c, r.data());
+    if (rc) return rc;
+    for (size_t i = 0; i < n; i++)
+        if (r[i] != NWV_DAG_OK) invalid_idx[(*n_invalid)++] = i;
+    return *n_invalid ? NWV_ERR_SIGNATURE : NWV_OK;
+}
+
+int nwv_bls_certificate_new(nwv_ctx* ctx, const nwv_bls_committee* committee, size_t n_votes,
+                            const uint8_t* vote_pks, const uint8_t* vote_sigs, int check_stake,
+                            uint32_t* signed_out, size_t* n_signed, uint8_t* agg_out, int* has_agg) {
+    if (!ctx || !bls_valid_args(committee) || !n_signed || !has_agg || !agg_out ||
+        (n_votes && (!vote_pks || !vote_sigs)))
+        return NWV_ERR_ARG;
+    const nwv_bls_committee& c = *committee;
+    std::vector<size_t> order(n_votes);
+    for (size_t i = 0; i < n_votes; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+        return std::memcmp(vote_pks + BK * a, vote_pks + BK * b, BK) < 0;
+    });
+    auto same_vote = [&](size_t a, size_t b) {
+        return std::memcmp(vote_pks + BK * a, vote_pks + BK * b, BK) == 0 &&
+               std::memcmp(vote_sigs + BS * a, vote_sigs + BS * b, BS) == 0;
+    };
+    size_t front = 0, ns = 0;
+    uint64_t weight = 0;
+    std::vector<uint8_t> kept;
+    for (size_t k = 0; k < c.n; k++) {
+        if (front < n_votes && std::memcmp(c.keys + BK * k, vote_pks + BK * order[front], BK) == 0) {
+            const size_t t = order[front++];
+            put(kept, vote_sigs + BS * t, BS);
+            weight += c.stakes[k];
+            while (front < n_votes && same_vote(order[front], t)) front++;
+            if (signed_out) signed_out[ns] = (uint32_t)k;
+            ns++;
+        }
+    }
+    if (front < n_votes) return NWV_DAG_UNKNOWN_AUTHORITY;
+    if (check_stake && weight < bls_quorum(c)) return NWV_DAG_CERTIFICATE_REQUIRES_QUORUM;
+    *n_signed = ns;
+    *has_agg = 0;
+    if (kept.empty()) return NWV_DAG_OK;  // AggregateSignature::default()
+    const int rc = nwv_bls_aggregate(ctx, kept.size() / BS, kept.data(), agg_out, nullptr);
+    if (rc == NWV_ERR_SIGNATURE) return NWV_DAG_INVALID_SIGNATURE;  // AggregateSignature::aggregate fails
+    if (rc) return rc;
+    *has_agg = 1;
+    return NWV_DAG_OK;
+}
+
+}  // extern "C"

@@ -149,14 +149,23 @@ class CoreDrain:
     depends only on the committee, never on Core's state, so verifying ahead changes no outcome.
 
     A message is (kind, item): kind 'header' | 'vote' | 'certificate', item a types.Header / Vote
-    / Certificate or its prepared C struct (types._Header / _Vote / _Certificate)."""
+    / Certificate or its prepared C struct (types._Header / _Vote / _Certificate).
+
+    scheme='bls': the reference's default scheme (crypto/src/lib.rs:29-33), BLS12-381 -- 96-byte
+    keys, 48-byte signatures, certificates as types.BlsCertificate (or _BlsCertificate); the call
+    is nwv_bls_verify_mixed_many (single-key checks for headers and votes, one
+    fast_aggregate_verify per certificate, all in one BLS verification call)."""
 
     KINDS = ("header", "vote", "certificate")
     _CLS = {"header": T._Header, "vote": T._Vote, "certificate": T._Certificate}
+    _CLS_BLS = {"header": T._Header, "vote": T._Vote, "certificate": T._BlsCertificate}
 
-    def __init__(self, engine, committee, max_items=512, max_wait_us=1000, min_items=64):
+    def __init__(self, engine, committee, max_items=512, max_wait_us=1000, min_items=64, scheme="ed25519"):
         if max_items < 1:
             raise ValueError("max_items must be >= 1")
+        if scheme not in ("ed25519", "bls"):
+            raise ValueError("scheme must be 'ed25519' or 'bls'")
+        self.scheme = scheme
         self.engine = engine
         self.max_items = max_items
         self.max_wait_us = max_wait_us
@@ -202,14 +211,16 @@ class CoreDrain:
             structs[kind].append(item if isinstance(item, ctypes.Structure) else item._c(keep))
             where[kind].append(i)
         args, outs = [], []
+        cls = self._CLS_BLS if self.scheme == "bls" else self._CLS
         for k in self.KINDS:
             n = len(structs[k])
-            arr = (self._CLS[k] * max(n, 1))(*structs[k])
+            arr = (cls[k] * max(n, 1))(*structs[k])
             res = (ctypes.c_int32 * max(n, 1))()
             keep.objs += [arr, res]
             args += [n, ctypes.cast(arr, ctypes.c_void_p), ctypes.cast(res, ctypes.c_void_p)]
             outs.append(res)
-        _lib._check(T.lib().nwv_verify_mixed_many(self.engine._h, ctypes.byref(self._cc), *args))
+        fn = T.lib().nwv_bls_verify_mixed_many if self.scheme == "bls" else T.lib().nwv_verify_mixed_many
+        _lib._check(fn(self.engine._h, ctypes.byref(self._cc), *args))
         codes = [0] * len(msgs)
         for k, res in zip(self.KINDS, outs):
             for j, i in enumerate(where[k]):

@@ -101,6 +101,17 @@ _SIGS = {
     "nwv_certificate_new": ([ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     "nwv_committee_quorum_threshold": ([ctypes.c_void_p], ctypes.c_uint64),
+    "nwv_bls_header_digest_many": ([ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "nwv_bls_vote_digest_many": ([ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "nwv_bls_certificate_digest_many": ([ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p],
+                                        ctypes.c_int),
+    "nwv_bls_verify_mixed_many": ([ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_size_t, ctypes.c_void_p,
+                                                                         ctypes.c_void_p] * 3, ctypes.c_int),
+    "nwv_bls_validate_certificates": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "nwv_bls_certificate_new": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p,
+                                 ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
+                                ctypes.c_int),
 }
 
 
@@ -338,5 +349,89 @@ def validate_certificates(engine, committee, certs) -> Tuple[bool, List[int]]:
     nbad = ctypes.c_size_t(0)
     idx = (ctypes.c_size_t * max(n, 1))()
     rc = lib().nwv_validate_certificates(engine._h, ctypes.byref(c), n, arr, ctypes.byref(nbad), idx)
+    _lib._check(rc, allow=(_lib.NWV_OK, _lib.NWV_ERR_SIGNATURE))
+    return rc == _lib.NWV_OK, list(idx[:nbad.value])
+
+
+# ---- BLS12-381, the reference's default scheme (crypto/src/lib.rs:29-33) ------------------
+# Committee, Header and Vote are shared with the Ed25519 layer (the C structs have the same
+# layout; keys are 96 bytes, signatures 48).  A certificate's aggregate is ONE 48-byte G1 point,
+# or None for AggregateSignature::default().
+class _BlsCertificate(ctypes.Structure):
+    _fields_ = [("header", _Header), ("n_signed", ctypes.c_size_t), ("signed_authorities", ctypes.c_void_p),
+                ("aggregated_signature", ctypes.c_void_p)]
+
+
+@dataclass
+class BlsCertificate:
+    header: Header
+    signed_authorities: List[int] = field(default_factory=list)
+    aggregated_signature: Optional[bytes] = None
+
+    @staticmethod
+    def genesis(committee: Committee) -> List["BlsCertificate"]:
+        return [BlsCertificate(Header(author=k, epoch=committee.epoch, signature=bytes(48))) for k in committee.keys]
+
+    @staticmethod
+    def new(engine, committee, header, votes, check_stake=True):
+        """Certificate::new under BLS: votes [(pk96, sig48)] -> BlsCertificate (the aggregate is
+        summed on the GPU); raises UnknownAuthority / CertificateRequiresQuorum / InvalidSignature"""
+        keep = _Keep()
+        c = committee._c(keep)
+        signed = (ctypes.c_uint32 * max(len(committee.keys), 1))()
+        ns, has = ctypes.c_size_t(0), ctypes.c_int(0)
+        agg = ctypes.create_string_buffer(48)
+        rc = lib().nwv_bls_certificate_new(engine._h, ctypes.byref(c), len(votes), b"".join(p for p, _ in votes) or None,
+                                           b"".join(s_ for _, s_ in votes) or None, 1 if check_stake else 0, signed,
+                                           ctypes.byref(ns), agg, ctypes.byref(has))
+        _raise(rc)
+        return BlsCertificate(header, list(signed[:ns.value]), agg.raw if has.value else None)
+
+    def _c(self, keep):
+        c = _BlsCertificate()
+        c.header = self.header._c(keep)
+        c.n_signed = len(self.signed_authorities)
+        c.signed_authorities = keep.arr(ctypes.c_uint32, self.signed_authorities)
+        c.aggregated_signature = keep.buf(self.aggregated_signature) if self.aggregated_signature is not None else None
+        return c
+
+
+def bls_header_digests(engine, headers):
+    return _many(engine, lib().nwv_bls_header_digest_many, None, list(headers))
+
+
+def bls_vote_digests(engine, votes):
+    return _many(engine, lib().nwv_bls_vote_digest_many, None, list(votes))
+
+
+def bls_certificate_digests(engine, certs):
+    return _many(engine, lib().nwv_bls_certificate_digest_many, None, list(certs))
+
+
+def bls_verify_mixed(engine, committee, headers=(), votes=(), certs=()):
+    """nwv_bls_verify_mixed_many: a Core's queued headers, votes and certificates in one call (one
+    digest launch, one BLS verification call) -> (header codes, vote codes, certificate codes)"""
+    keep = _Keep()
+    c = committee._c(keep)
+    args, outs = [], []
+    for items, cls in ((list(headers), _Header), (list(votes), _Vote), (list(certs), _BlsCertificate)):
+        n = len(items)
+        arr = (cls * max(n, 1))(*[it._c(keep) for it in items])
+        res = (ctypes.c_int32 * max(n, 1))()
+        keep.objs += [arr, res]
+        args += [n, ctypes.cast(arr, ctypes.c_void_p), ctypes.cast(res, ctypes.c_void_p)]
+        outs.append((res, n))
+    _lib._check(lib().nwv_bls_verify_mixed_many(engine._h, ctypes.byref(c), *args))
+    return tuple(list(r[:n]) for r, n in outs)
+
+
+def bls_validate_certificates(engine, committee, certs) -> Tuple[bool, List[int]]:
+    keep = _Keep()
+    n = len(certs)
+    arr = (_BlsCertificate * max(n, 1))(*[x._c(keep) for x in certs])
+    c = committee._c(keep)
+    nbad = ctypes.c_size_t(0)
+    idx = (ctypes.c_size_t * max(n, 1))()
+    rc = lib().nwv_bls_validate_certificates(engine._h, ctypes.byref(c), n, arr, ctypes.byref(nbad), idx)
     _lib._check(rc, allow=(_lib.NWV_OK, _lib.NWV_ERR_SIGNATURE))
     return rc == _lib.NWV_OK, list(idx[:nbad.value])

@@ -1653,3 +1653,74 @@ void orb_fast_aggregate_verify_mt(size_t n_items, const uint8_t* sigs48, const u
     }
     for (int t = 0; t < k; t++) pthread_join(th[t], NULL);
 }
+
+/* The same statuses as orb_fast_aggregate_verify item by item, with each key of the table decoded
+ * and validated ONCE (as fastcrypto deserializes a public key once, crypto/src/lib.rs:29-33 ->
+ * BLS12381PublicKey::from_bytes) instead of once per item: item i names keys[pk_idx[pk_off[i] + j]],
+ * j < pk_cnt[i].  Items are split over `threads` host threads.  The CPU baseline of the BLS leg and
+ * the checker of large GPU batches (100-node committees). */
+typedef struct {
+    size_t lo, hi;
+    const uint8_t *sigs, *msg, *dst;
+    const uint32_t *pk_off, *pk_cnt, *pk_idx, *msg_len;
+    const uint64_t* msg_off;
+    size_t dst_len;
+    const g2j* keys;
+    const int* key_st;
+    int32_t* status;
+} tab_job;
+static void* tab_keys_run(void* arg) {
+    tab_job* j = (tab_job*)arg;
+    for (size_t k = j->lo; k < j->hi; k++) ((int*)j->key_st)[k] = pk_load((g2j*)&j->keys[k], j->sigs + 96 * k);
+    return NULL;
+}
+static void* tab_items_run(void* arg) {
+    tab_job* j = (tab_job*)arg;
+    for (size_t i = j->lo; i < j->hi; i++) {
+        g1j S;
+        int rc = sig_load(&S, j->sigs + 48 * i);
+        if (!rc && j->pk_cnt[i] == 0) rc = ORB_AGGR_MISMATCH;
+        g2j acc;
+        acc.inf = 1;
+        for (uint32_t t = 0; !rc && t < j->pk_cnt[i]; t++) {
+            const uint32_t k = j->pk_idx[j->pk_off[i] + t];
+            if (j->key_st[k]) rc = j->key_st[k];
+            else g2_add(&acc, &acc, &j->keys[k]);
+        }
+        if (!rc) rc = verify_core(&acc, j->msg + j->msg_off[i], j->msg_len[i], &S, j->dst, j->dst_len);
+        j->status[i] = rc;
+    }
+    return NULL;
+}
+static void tab_parallel(void* (*fn)(void*), tab_job base, size_t n, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    tab_job jobs[256];
+    const size_t per = (n + (size_t)threads - 1) / (size_t)threads;
+    int k = 0;
+    for (int t = 0; t < threads; t++) {
+        const size_t lo = (size_t)t * per, hi = lo + per < n ? lo + per : n;
+        if (lo >= hi) break;
+        jobs[k] = base;
+        jobs[k].lo = lo;
+        jobs[k].hi = hi;
+        pthread_create(&th[k], NULL, fn, &jobs[k]);
+        k++;
+    }
+    for (int t = 0; t < k; t++) pthread_join(th[t], NULL);
+}
+void orb_verify_items_keytab_mt(size_t n_keys, const uint8_t* keys96, size_t n_items, const uint8_t* sigs48,
+                                const uint32_t* pk_off, const uint32_t* pk_cnt, const uint32_t* pk_idx,
+                                const uint8_t* msg_base, const uint64_t* msg_off, const uint32_t* msg_len,
+                                const uint8_t* dst, size_t dst_len, int32_t* status, int threads) {
+    INIT();
+    g2j* keys = (g2j*)calloc(n_keys ? n_keys : 1, sizeof(g2j));
+    int* kst = (int*)calloc(n_keys ? n_keys : 1, sizeof(int));
+    tab_job b = {0, 0, keys96, msg_base, dst, pk_off, pk_cnt, pk_idx, msg_len, msg_off, dst_len, keys, kst, status};
+    tab_parallel(tab_keys_run, b, n_keys, threads);  /* .sigs carries the key bytes for this pass */
+    b.sigs = sigs48;
+    tab_parallel(tab_items_run, b, n_items, threads);
+    free(keys);
+    free(kst);
+}

@@ -70,6 +70,14 @@ void orb_fast_aggregate_verify_mt(size_t n_items, const uint8_t* sigs48, const u
                                   const uint64_t* msg_off, const uint32_t* msg_len, const uint8_t* dst,
                                   size_t dst_len, uint8_t* verdict, int threads);
 
+/* orb_fast_aggregate_verify's status for every item, the key table decoded and validated once (as
+ * fastcrypto deserializes each public key once): item i = (sigs48[i], keys96[pk_idx[pk_off[i] + j]]
+ * for j < pk_cnt[i], message i); items split over `threads` host threads */
+void orb_verify_items_keytab_mt(size_t n_keys, const uint8_t* keys96, size_t n_items, const uint8_t* sigs48,
+                                const uint32_t* pk_off, const uint32_t* pk_cnt, const uint32_t* pk_idx,
+                                const uint8_t* msg_base, const uint64_t* msg_off, const uint32_t* msg_len,
+                                const uint8_t* dst, size_t dst_len, int32_t* status, int threads);
+
 /* pairing on uncompressed affine inputs (P: 96 bytes in G1, Q: 192 bytes in G2); out = 12 Fp
  * coefficients (576 bytes big-endian) in the tower order c0.c0.c0, c0.c0.c1, c0.c1.c0, ... */
 void orb_pairing(const uint8_t P[96], const uint8_t Q[192], uint8_t out[576]);      /* fast: f^(3(p^12-1)/r) */

@@ -116,6 +116,33 @@ def certificate_verify(c, cert, verify):
     return OK if all(verify(pk, s, d) for pk, s in zip(pks, sigs)) else INVALID_SIGNATURE
 
 
+def certificate_verify_bls(c, cert, verify, agg_verify):
+    """Certificate::verify under BLS12-381 (crypto/src/lib.rs:29-33): cert["agg"] is ONE aggregate
+    (48 bytes) or None (AggregateSignature::default(): sig None -> signature::Error); the check is
+    agg_verify(pks, agg, digest) = fast_aggregate_verify, with no |pks| = |sigs| test"""
+    h = cert["header"]
+    if h["epoch"] != c.epoch:
+        return INVALID_EPOCH
+    if is_genesis(c, cert):
+        return OK
+    r = header_verify(c, h, verify)
+    if r:
+        return r
+    weight, it, pks = 0, 0, []
+    idx = cert["signed"]
+    for a, pk in enumerate(c.keys):
+        if it < len(idx) and idx[it] == a:
+            weight += c.stakes[a]
+            it += 1
+            pks.append(pk)
+    if weight < c.quorum_threshold():
+        return REQUIRES_QUORUM
+    if cert["agg"] is None:
+        return INVALID_SIGNATURE
+    d = certificate_digest(h["id"], h["round"], h["epoch"], h["author"])
+    return OK if agg_verify(pks, cert["agg"], d) else INVALID_SIGNATURE
+
+
 def certificate_new(c, votes, check_stake=True):
     """-> (code, signed indices, aggregated signature list)"""
     votes = sorted(votes, key=lambda v: v[0])  # stable, by pk

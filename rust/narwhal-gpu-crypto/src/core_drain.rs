@@ -117,6 +117,58 @@ pub fn verify_items(committee: &ffi::NwvCommittee, items: &[Item]) -> Result<Vec
     Ok(codes)
 }
 
+/// One message under BLS12-381, the reference's default scheme (`crypto/src/lib.rs:29-33`): the
+/// C views of `include/nwv_types.h`'s `nwv_bls_*` structs.
+#[derive(Clone, Copy)]
+pub enum BlsItem {
+    Header(ffi::NwvBlsHeader),
+    Vote(ffi::NwvBlsVote),
+    Certificate(ffi::NwvBlsCertificate),
+}
+
+/// `verify_items` under BLS12-381: every item in ONE engine call (`nwv_bls_verify_mixed_many`:
+/// one digest launch, one BLS verification call -- single-key checks for headers and votes, one
+/// fast_aggregate_verify per certificate), codes in the items' order.
+pub fn verify_bls_items(committee: &ffi::NwvBlsCommittee, items: &[BlsItem]) -> Result<Vec<DagCode>, String> {
+    let (mut hs, mut vs, mut cs) = (Vec::new(), Vec::new(), Vec::new());
+    let (mut hi, mut vi, mut ci) = (Vec::new(), Vec::new(), Vec::new());
+    for (i, it) in items.iter().enumerate() {
+        match it {
+            BlsItem::Header(h) => {
+                hs.push(*h);
+                hi.push(i)
+            }
+            BlsItem::Vote(v) => {
+                vs.push(*v);
+                vi.push(i)
+            }
+            BlsItem::Certificate(c) => {
+                cs.push(*c);
+                ci.push(i)
+            }
+        }
+    }
+    let mut rh = vec![0i32; hs.len()];
+    let mut rv = vec![0i32; vs.len()];
+    let mut rc = vec![0i32; cs.len()];
+    let r = unsafe {
+        ffi::nwv_bls_verify_mixed_many(
+            crate::ctx(), committee, hs.len(), hs.as_ptr(), rh.as_mut_ptr(), vs.len(), vs.as_ptr(), rv.as_mut_ptr(),
+            cs.len(), cs.as_ptr(), rc.as_mut_ptr(),
+        )
+    };
+    if r != ffi::NWV_OK {
+        return Err(last_error());
+    }
+    let mut codes = vec![0i32; items.len()];
+    for (pos, res) in [(&hi, &rh), (&vi, &rv), (&ci, &rc)] {
+        for (j, &i) in pos.iter().enumerate() {
+            codes[i] = res[j];
+        }
+    }
+    Ok(codes)
+}
+
 /// Running counters of a Core loop's drains (engine calls, items, largest flush).
 #[derive(Default, Debug, Clone, Copy)]
 pub struct DrainStats {

@@ -110,6 +110,56 @@ pub struct NwvCertificate {
     pub aggregated_signature: *const u8,
 }
 
+/// `nwv_bls_committee`: the committee under BLS12-381 (96-byte keys in BTreeMap order).
+#[repr(C)]
+#[derive(Clone, Copy)]
+pub struct NwvBlsCommittee {
+    pub n: usize,
+    pub keys: *const u8,
+    pub stakes: *const u64,
+    pub epoch: u64,
+    pub n_workers: *const u32,
+    pub worker_ids: *const *const u32,
+}
+
+/// `nwv_bls_header` (types::Header with a 96-byte author and a 48-byte signature).
+#[repr(C)]
+#[derive(Clone, Copy)]
+pub struct NwvBlsHeader {
+    pub author: *const u8,
+    pub round: u64,
+    pub epoch: u64,
+    pub n_payload: usize,
+    pub payload_digests: *const u8,
+    pub payload_workers: *const u32,
+    pub n_parents: usize,
+    pub parents: *const u8,
+    pub id: *const u8,
+    pub signature: *const u8,
+}
+
+/// `nwv_bls_vote` (types::Vote under BLS12-381).
+#[repr(C)]
+#[derive(Clone, Copy)]
+pub struct NwvBlsVote {
+    pub id: *const u8,
+    pub round: u64,
+    pub epoch: u64,
+    pub origin: *const u8,
+    pub author: *const u8,
+    pub signature: *const u8,
+}
+
+/// `nwv_bls_certificate`: the aggregate is one 48-byte G1 point, or null for `sig: None`.
+#[repr(C)]
+#[derive(Clone, Copy)]
+pub struct NwvBlsCertificate {
+    pub header: NwvBlsHeader,
+    pub n_signed: usize,
+    pub signed_authorities: *const u32,
+    pub aggregated_signature: *const u8,
+}
+
 /// `nwv_done_fn`: completion callback of the batching service.
 pub type NwvDoneFn = Option<unsafe extern "C" fn(user: *mut c_void, result: i32)>;
 
@@ -238,6 +288,10 @@ extern "C" {
     ) -> c_int;
     pub fn nwv_bls_last_kernel_ms(ctx: *mut NwvCtx, out_ms: *mut f64) -> c_int;
     pub fn nwv_bls_last_path(ctx: *mut NwvCtx) -> c_int;
+    pub fn nwv_bls_last_keys(ctx: *mut NwvCtx, out: *mut u64) -> c_int;
+    pub fn nwv_bls_keycache_register(ctx: *mut NwvCtx, n_keys: usize, keys: *const u8) -> c_int;
+    pub fn nwv_bls_keycache_reset(ctx: *mut NwvCtx) -> c_int;
+    pub fn nwv_bls_keycache_size(ctx: *mut NwvCtx) -> c_int;
     pub fn nwv_bls_verify(
         ctx: *mut NwvCtx,
         pk: *const u8,
@@ -458,6 +512,48 @@ extern "C" {
         n_sigs: *mut usize,
     ) -> c_int;
     pub fn nwv_committee_quorum_threshold(committee: *const NwvCommittee) -> u64;
+    // ---- the types layer under BLS12-381 (include/nwv_types.h)
+    pub fn nwv_bls_header_digest_many(ctx: *mut NwvCtx, n: usize, h: *const NwvBlsHeader, out: *mut u8) -> c_int;
+    pub fn nwv_bls_vote_digest_many(ctx: *mut NwvCtx, n: usize, v: *const NwvBlsVote, out: *mut u8) -> c_int;
+    pub fn nwv_bls_certificate_digest_many(
+        ctx: *mut NwvCtx,
+        n: usize,
+        c: *const NwvBlsCertificate,
+        out: *mut u8,
+    ) -> c_int;
+    pub fn nwv_bls_verify_mixed_many(
+        ctx: *mut NwvCtx,
+        committee: *const NwvBlsCommittee,
+        n_headers: usize,
+        headers: *const NwvBlsHeader,
+        header_results: *mut i32,
+        n_votes: usize,
+        votes: *const NwvBlsVote,
+        vote_results: *mut i32,
+        n_certs: usize,
+        certs: *const NwvBlsCertificate,
+        cert_results: *mut i32,
+    ) -> c_int;
+    pub fn nwv_bls_validate_certificates(
+        ctx: *mut NwvCtx,
+        committee: *const NwvBlsCommittee,
+        n: usize,
+        c: *const NwvBlsCertificate,
+        n_invalid: *mut usize,
+        invalid_idx: *mut usize,
+    ) -> c_int;
+    pub fn nwv_bls_certificate_new(
+        ctx: *mut NwvCtx,
+        committee: *const NwvBlsCommittee,
+        n_votes: usize,
+        vote_pks: *const u8,
+        vote_sigs: *const u8,
+        check_stake: c_int,
+        signed_out: *mut u32,
+        n_signed: *mut usize,
+        agg_out: *mut u8,
+        has_agg: *mut c_int,
+    ) -> c_int;
     // ---- batching service in front of Core::sanitize_* (include/nwv_service.h)
     pub fn nwv_service_create(
         ctx: *mut NwvCtx,

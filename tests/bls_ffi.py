@@ -36,6 +36,7 @@ def lib():
             ("orb_aggregate_pubkeys", [sz, c, vp], ctypes.c_int),
             ("orb_fast_aggregate_verify", [c, sz, c, c, sz, c, sz], ctypes.c_int),
             ("orb_fast_aggregate_verify_mt", [sz, vp, vp, vp, vp, vp, vp, vp, c, sz, vp, ctypes.c_int], None),
+            ("orb_verify_items_keytab_mt", [sz, vp, sz, vp, vp, vp, vp, vp, vp, vp, c, sz, vp, ctypes.c_int], None),
             ("orb_pairing", [c, c, vp], None),
             ("orb_pairing_ref", [c, c, vp], None),
             ("orb_gt_pow", [c, c, sz, vp], None),
@@ -120,6 +121,31 @@ def aggregate_pubkeys(pks):
 
 def fast_aggregate_verify(sig, pks, msg, dst=DST_NUL):
     return lib().orb_fast_aggregate_verify(sig, len(pks), b"".join(pks), msg, len(msg), dst, len(dst))
+
+
+def verify_items(keys, sigs, key_lists, msgs, threads=None, dst=DST_NUL):
+    """orb_fast_aggregate_verify's status per item with the key table validated once:
+    item i = (sigs[i], [keys[k] for k in key_lists[i]], msgs[i]) -> list of ORB_* codes"""
+    import numpy as np
+    n = len(sigs)
+    kb = np.frombuffer(b"".join(keys) or b"\0", dtype=np.uint8)
+    sg = np.frombuffer(b"".join(sigs) or b"\0", dtype=np.uint8)
+    cnt = np.array([len(k) for k in key_lists] or [0], dtype=np.uint32)
+    off = np.zeros(max(n, 1), dtype=np.uint32)
+    if n > 1:
+        off[1:] = np.cumsum(cnt[:-1], dtype=np.uint32)
+    idx = np.array([k for ks in key_lists for k in ks] or [0], dtype=np.uint32)
+    arena = np.frombuffer(b"".join(msgs) + b"\0" * 8, dtype=np.uint8)
+    lens = np.array([len(m) for m in msgs] or [0], dtype=np.uint32)
+    moff = np.zeros(max(n, 1), dtype=np.uint64)
+    if n > 1:
+        moff[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    st = np.zeros(max(n, 1), dtype=np.int32)
+    threads = threads or min(16, os.cpu_count() or 1)
+    lib().orb_verify_items_keytab_mt(len(keys), kb.ctypes.data, n, sg.ctypes.data, off.ctypes.data, cnt.ctypes.data,
+                                     idx.ctypes.data, arena.ctypes.data, moff.ctypes.data, lens.ctypes.data, dst,
+                                     len(dst), st.ctypes.data, threads)
+    return [int(x) for x in st[:n]]
 
 
 def pairing(P, Q):

@@ -96,6 +96,8 @@ def test_verify_many_mixed_batch_matches_oracle(bls, bls_per_item, bls_nocache, 
     bls = {"batch": bls, "per_item": bls_per_item, "nocache": bls_nocache}[path]
     sks, pks = _committee(bls, 10, 13)
     keys = pks + [C.not_in_g2(), C.IDENTITY_G2, C.negate_g2(pks[0])]
+    if path != "nocache":  # the committee in the key cache; the stray keys decoded per call
+        bls.register_keys(pks)
     rnd = random.Random(14)
     items = []  # (sig, key index list, msg)
     for c in range(12):
@@ -208,3 +210,92 @@ def test_batch_sizes(bls, n):
     assert bls.last_path() == ("batch_accepted" if n == 1 else "batch_rejected_then_per_item")
     got = bls.verify_many(pks, sigs, [[0, 1, 2]] * n, msgs)
     assert list(got) == [0] * n and bls.last_path() == "batch_accepted"
+
+
+def test_keycache_register_only(bls):
+    """the key cache takes only registered (committee) keys that validate: 70,000 stray keys named
+    by verify calls (undecodable, off-curve, outside G2, and valid keys of outsiders) never take a
+    slot, an invalid key passed to register takes none either, and the committee's keys still hit
+    the cache afterwards with statuses equal to the oracle's"""
+    bls.reset_keys()
+    assert bls.cached_keys() == 0
+    sks, pks = _committee(bls, 10, 21)
+    bad_key = C.not_in_g2()
+    bls.register_keys(pks + [bad_key, C.IDENTITY_G2])
+    assert bls.cached_keys() == 10
+    rnd = random.Random(22)
+    d = rnd.randbytes(32)
+    who = sorted(rnd.sample(range(10), 7))
+    _, agg = B.aggregate(bls.sign([sks[k] for k in who], [d] * 7))
+    # 70,000 distinct stray keys in verify calls: mostly undecodable (cheap to make and check), plus
+    # invalid points and valid keys of outsiders signing their own messages
+    osk, opk = _committee(bls, 16, 23)
+    om = [rnd.randbytes(32) for _ in range(16)]
+    osig = bls.sign(osk, om)
+    stray = [bytes([0x80 | (i & 0x1f)]) + i.to_bytes(4, "big") + bytes(91) for i in range(70000 - 20)]
+    stray = [bytes([k[0] & 0x7f]) + k[1:] if i % 3 == 0 else k for i, k in enumerate(stray)]
+    stray += [C.not_in_g2(1000 * (i + 1)) for i in range(4)] + opk
+    n0 = len(stray)
+    items = [(C.IDENTITY_G1, [i], d) for i in range(n0 - 16)] + [(osig[j], [n0 - 16 + j], om[j]) for j in range(16)]
+    for lo in range(0, len(items), 20000):
+        part = items[lo:lo + 20000]
+        got = bls.verify_many(stray, [i[0] for i in part], [i[1] for i in part], [i[2] for i in part])
+        assert bls.last_keys()[0] == 0  # nothing found in the cache: none of them were registered
+        want_tail = [0] * 16 if lo + 20000 >= len(items) else []
+        if want_tail:
+            assert list(got[-16:]) == want_tail  # the outsiders' valid single signatures verify
+        sample = rnd.sample(range(len(part) - len(want_tail)), 40)
+        sub_keys = [stray[part[k][1][0]] for k in sample]  # the oracle validates only these
+        assert [int(got[k]) for k in sample] == B.verify_items(sub_keys, [part[k][0] for k in sample],
+                                                               [[j] for j in range(len(sample))],
+                                                               [part[k][2] for k in sample])
+    assert bls.cached_keys() == 10  # no stray key took a slot
+    # the committee's keys still come from the cache, statuses as the oracle's
+    keys = pks + [bad_key]
+    its = [(agg, who, d), (agg, who, d + b"!"), (agg, who + [10], d), (agg, who[:-1], d)]
+    got = bls.verify_many(keys, [i[0] for i in its], [i[1] for i in its], [i[2] for i in its])
+    assert list(got) == B.verify_items(keys, [i[0] for i in its], [i[1] for i in its], [i[2] for i in its])
+    assert list(got)[0] == 0
+    assert bls.last_keys() == (10, 1)  # the committee from the cache; the bad key decoded by the call
+    bls.reset_keys()
+    assert bls.cached_keys() == 0
+
+
+@pytest.mark.parametrize("path", ["batch", "per_item"])
+def test_committee_shape_100(bls, bls_per_item, path):
+    """the reference's committee shape: a 100-key committee (registered), certificates of 67 and
+    100 signers (the key-sum tree at full depth) mixed with every adversarial category, through the
+    batch check and per item, against the oracle"""
+    bls = {"batch": bls, "per_item": bls_per_item}[path]
+    sks, pks = _committee(bls, 100, 31)
+    bls.register_keys(pks)
+    keys = pks + [C.not_in_g2(), C.IDENTITY_G2, C.negate_g2(pks[5])]
+    rnd = random.Random(32)
+    items = []
+    for q in (67, 100, 67, 68, 99, 100):
+        d = rnd.randbytes(32)
+        who = sorted(rnd.sample(range(100), q))
+        _, agg = B.aggregate(bls.sign([sks[k] for k in who], [d] * q))
+        items.append((agg, who, d))
+    agg, who, d = items[0]
+    agg2, who2, d2 = items[1]
+    items += [
+        (agg, who, d + b"!"),                                  # wrong message
+        (agg, who[:-1], d),                                    # missing signer
+        (agg, who[:-1] + [next(k for k in range(100) if k not in who)], d),  # wrong signer
+        (agg2, who2[1:], d2),                                  # 99 of the 100 signers
+        (agg, [], d),                                          # empty key list
+        (agg, who[:30] + [100] + who[30:], d),                 # a key outside G2 mid-list
+        (agg, who + [101], d),                                 # identity key last
+        (agg, [5, 102], d),                                    # apk = identity (pk + (-pk))
+        (C.not_in_g1(), who, d),                               # signature outside G1
+        (C.IDENTITY_G1, who, d),                               # identity signature
+        (agg2, who, d),                                        # another certificate's aggregate
+    ] + [(b, who, d) for b in C.bad_encodings_g1(agg)]
+    got = bls.verify_many(keys, [i[0] for i in items], [i[1] for i in items], [i[2] for i in items])
+    want = B.verify_items(keys, [i[0] for i in items], [i[1] for i in items], [i[2] for i in items])
+    assert list(got) == want
+    assert want[:6] == [0] * 6 and all(w != 0 for w in want[6:])
+    assert bls.last_path() == ("per_item" if path == "per_item" else "batch_rejected_then_per_item")
+    got = bls.verify_many(keys, [i[0] for i in items[:6]], [i[1] for i in items[:6]], [i[2] for i in items[:6]])
+    assert list(got) == [0] * 6

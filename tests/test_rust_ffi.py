@@ -14,7 +14,9 @@ CRATE = os.path.join(ROOT, "rust", "narwhal-gpu-crypto")
 
 STRUCTS = {"nwv_ctx": "NwvCtx", "nwv_staged": "NwvStaged", "nwv_service": "NwvService",
            "nwv_committee": "NwvCommittee", "nwv_header": "NwvHeader", "nwv_vote": "NwvVote",
-           "nwv_certificate": "NwvCertificate"}
+           "nwv_certificate": "NwvCertificate", "nwv_bls_committee": "NwvBlsCommittee",
+           "nwv_bls_header": "NwvBlsHeader", "nwv_bls_vote": "NwvBlsVote",
+           "nwv_bls_certificate": "NwvBlsCertificate"}
 SCALARS = {"size_t": "usize", "int": "c_int", "uint32_t": "u32", "uint64_t": "u64", "int64_t": "i64",
            "int32_t": "i32", "uint8_t": "u8", "char": "c_char", "double": "f64", "float": "f32", "void": "c_void",
            "nwv_done_fn": "NwvDoneFn"}
@@ -87,7 +89,8 @@ def test_every_c_function_is_bound_with_the_same_signature():
 def test_repr_c_structs_match_the_c_layout():
     hdr = c_headers()
     src = open(os.path.join(CRATE, "src", "ffi.rs")).read()
-    for cname in ("nwv_committee", "nwv_header", "nwv_vote", "nwv_certificate"):
+    for cname in ("nwv_committee", "nwv_header", "nwv_vote", "nwv_certificate", "nwv_bls_committee",
+                  "nwv_bls_header", "nwv_bls_vote", "nwv_bls_certificate"):
         body = re.search(r"typedef struct \{([^}]*)\}\s*" + cname + r"\s*;", hdr).group(1)
         cfields = [c_to_rust(f.strip()) for f in body.split(";") if f.strip()]
         rbody = re.search(r"pub struct " + STRUCTS[cname] + r" \{([^}]*)\}", src).group(1)

@@ -210,6 +210,34 @@ def test_callbacks_may_submit_but_blocking_calls_from_them_fail_fast(lib):
         svc.close()
 
 
+def test_callback_may_block_on_another_service(lib):
+    """the reentrancy refusal is per service -- a callback of service A may make a
+    blocking call on service B (B's flushers are free), and A's own blocking calls still fail fast"""
+    from narwhal_amd import _lib
+    lib.stub_reset(0, 0)
+    rnd = random.Random(7)
+    a = S.Service(None, _committee(0), max_batch=1, max_wait_us=0, lib=lib, ctx=ctypes.c_void_p(1))
+    b = S.Service(None, _committee(0), max_batch=1, max_wait_us=0, lib=lib, ctx=ctypes.c_void_p(1))
+    try:
+        seen, done = [], threading.Event()
+
+        def cb(code):
+            seen.append(b.verify_vote(_vote(rnd, 0, False)))
+            try:
+                a.flush()
+                seen.append("returned")
+            except _lib.NwvError as e:
+                seen.append(e.code)
+            done.set()
+
+        a.submit_header(_header(rnd, 0, True), cb)
+        assert done.wait(5)
+        assert seen == [0, _lib.NWV_ERR_REENTRANT]
+    finally:
+        a.close()
+        b.close()
+
+
 def test_core_drain_policy():
     """CoreDrain.drain (no engine call): takes what is queued up to max_items, waits at most
     max_wait_us for more, keeps arrival order"""

@@ -407,21 +407,16 @@ def leg_c5(eng, rounds=50):
         {"committee": com, "certs": certs, "headers": headers, "votes": vsample, "batches": batches}
 
 
-def leg_bls(eng, certs=100, quorum=67, committee=100, reps=20, throughput_n=16384):
-    """SURVEY §8 row f4, the reference's default scheme (crypto/src/lib.rs:29-33 -> BLS12-381
-    min_sig): (a) a C5-shaped round of `certs` certificates, each an aggregate of `quorum`
-    committee signatures over its 32-byte digest, verified as ONE nwv_bls_verify_many call
-    (CertificatesResponse::validate_certificates, each item = AggregateAuthenticator::verify:
-    key-sum, hash to G1, two-pair Miller loop, final exponentiation), host -> host; (b) one
-    Verifier::verify (Header::verify's single signature); (c) `throughput_n` single-key items in
-    one call.  Synthetic keys / messages; signatures and aggregates made on the GPU."""
-    from narwhal_amd.bls import Bls
-    b = Bls(eng)
-    rnd = np.random.default_rng(77)
+def _bls_committee(b, n, rnd):
     r = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
-    sks = [int.from_bytes(rnd.bytes(32), "big") % r or 1 for _ in range(committee)]
-    sks = [s.to_bytes(32, "big") for s in sks]
-    pks = b.keygen(sks)
+    sks = [(int.from_bytes(rnd.bytes(32), "big") % r or 1).to_bytes(32, "big") for _ in range(n)]
+    return sks, b.keygen(sks)
+
+
+def _bls_round_items(b, sks, rnd, certs, quorum):
+    """`certs` certificates of the committee: each an aggregate of `quorum` signatures over its
+    32-byte digest (made on the GPU) -> (aggregates, signer lists, digests)"""
+    committee = len(sks)
     digests = [rnd.bytes(32) for _ in range(certs)]
     signers = [sorted(rnd.choice(committee, quorum, replace=False).tolist()) for _ in range(certs)]
     flat = b.sign([sks[k] for s in signers for k in s], [d for d, s in zip(digests, signers) for _ in s])
@@ -430,6 +425,35 @@ def leg_bls(eng, certs=100, quorum=67, committee=100, reps=20, throughput_n=1638
         rc, agg, _ = b.aggregate(flat[quorum * c:quorum * (c + 1)])
         assert rc == 0
         aggs.append(agg)
+    return aggs, signers, digests
+
+
+def leg_bls(eng, threads=1, certs=100, quorum=67, committee=100, reps=20, throughput_n=16384, single_reps=200,
+            dag_rounds=20, concurrency=8, cpu=True):
+    """SURVEY §8 row f4, the reference's default scheme (crypto/src/lib.rs:29-33 -> BLS12-381
+    min_sig), host -> host, synthetic keys / messages (signatures and aggregates made on the GPU),
+    the committee registered in the key cache (epoch start):
+      round       `certs` certificates x `quorum` signers of a `committee`-key committee, ONE
+                  nwv_bls_verify_many call (CertificatesResponse::validate_certificates; item =
+                  AggregateAuthenticator::verify = fast_aggregate_verify)
+      single      one Verifier::verify (Header::verify / Vote::verify's check) p50 / p99
+      concurrent  `concurrency` threads issuing single verifies at once vs one thread
+      throughput  `throughput_n` single-key items in one call
+      dag_round   the C5 shape under BLS: 100 headers + 99 votes + 100 certificates through ONE
+                  nwv_bls_verify_mixed_many call (types layer: digests + every signature check)
+    Statuses are checked against the oracle (oracle/bls_oracle.c, keys validated once per call as
+    fastcrypto validates a key at deserialization); the CPU baseline times that oracle on the host
+    cores over the same round (kind: port)."""
+    import sys
+    import threading
+    sys.path.insert(0, __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.dirname(
+        __import__("os").path.abspath(__file__))), "tests"))
+    from narwhal_amd.bls import Bls
+    b = Bls(eng)
+    rnd = np.random.default_rng(77)
+    sks, pks = _bls_committee(b, committee, rnd)
+    b.register_keys(pks)
+    aggs, signers, digests = _bls_round_items(b, sks, rnd, certs, quorum)
     ts, kms = [], []
     for i in range(reps + 2):
         t0 = time.perf_counter()
@@ -439,41 +463,141 @@ def leg_bls(eng, certs=100, quorum=67, committee=100, reps=20, throughput_n=1638
         if i >= 2:
             ts.append(dt)
             kms.append(b.last_kernel_ms())
-    out = {"round": {"certificates": certs, "quorum": quorum, "committee": committee,
-                     "ms_host_to_host_p50": float(np.median(ts)) * 1e3,
-                     "certs_per_s": certs / float(np.median(ts)),
+    out = {"round": {"certificates": certs, "quorum": quorum, "committee": committee, **_pcts(ts),
+                     "certs_per_s": certs / float(np.median(ts)), "path": b.last_path(),
                      "kernel_ms": {k: float(np.median([x[k] for x in kms])) for k in kms[0]}}}
     m = rnd.bytes(32)
     s1 = b.sign([sks[0]], [m])[0]
     t1 = []
-    for i in range(reps + 2):
+    for i in range(single_reps + 3):
         t0 = time.perf_counter()
         rc = b.verify(pks[0], m, s1)
-        if i >= 2:
+        if i >= 3:
             t1.append(time.perf_counter() - t0)
         assert rc == 0
-    out["single_verify_ms_p50"] = float(np.median(t1)) * 1e3
-    if not throughput_n:
-        return out
-    # throughput: throughput_n items, one key each (a header's / vote's single signature)
-    n = throughput_n
-    msgs = [rnd.bytes(32) for _ in range(n)]
-    kidx = (np.arange(n) % committee).tolist()
-    sigs = b.sign([sks[k] for k in kidx], msgs)
-    t2, km2 = [], []
-    for i in range(3):
+    assert b.verify(pks[0], m + b"!", s1) == _lib.NWV_ERR_SIGNATURE
+    out["single_verify"] = dict(_pcts(t1), kernel_ms=b.last_kernel_ms())
+    # concurrent single verifies: one thread, then `concurrency` threads, for the same wall time
+    sig_k = b.sign(sks[:concurrency], [m] * concurrency)
+
+    def rate(nthreads, seconds=1.5):
+        cnt, stop, err = [0] * nthreads, time.perf_counter() + seconds, []
+
+        def work(k):
+            while time.perf_counter() < stop:
+                if b.verify(pks[k], m, sig_k[k]) != 0:
+                    err.append(k)
+                    return
+                cnt[k] += 1
+        th = [threading.Thread(target=work, args=(k,)) for k in range(nthreads)]
         t0 = time.perf_counter()
-        st = b.verify_many(pks, sigs, [[k] for k in kidx], msgs)
-        dt = time.perf_counter() - t0
-        assert not st.any()
-        if i:
-            t2.append(dt)
-            km2.append(b.last_kernel_ms())
-    out["throughput"] = {"items": n, "ms_host_to_host": float(np.median(t2)) * 1e3,
-                         "verifies_per_s": n / float(np.median(t2)),
-                         "kernel_ms": {k: float(np.median([x[k] for x in km2])) for k in km2[0]}}
-    out["note"] = ("BLS12-381 min_sig (48 B G1 signatures, 96 B G2 keys), fastcrypto's DST; each item "
-                   "= key decode + G2 check (once per distinct key), sig decode + G1 check, hash to G1, "
-                   "key sum; the pairing equations of all items checked as one random linear "
-                   "combination on 8-lane groups (per-item check only on a reject)")
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not err
+        return sum(cnt) / (time.perf_counter() - t0)
+    r1, rn = rate(1), rate(concurrency)
+    out["concurrent_single_verify"] = {"threads": concurrency, "verifies_per_s_1_thread": r1,
+                                       f"verifies_per_s_{concurrency}_threads": rn, "speedup": rn / r1}
+    if throughput_n:
+        n = throughput_n
+        msgs = [rnd.bytes(32) for _ in range(n)]
+        kidx = (np.arange(n) % committee).tolist()
+        sigs = b.sign([sks[k] for k in kidx], msgs)
+        t2, km2 = [], []
+        for i in range(3):
+            t0 = time.perf_counter()
+            st = b.verify_many(pks, sigs, [[k] for k in kidx], msgs)
+            dt = time.perf_counter() - t0
+            assert not st.any()
+            if i:
+                t2.append(dt)
+                km2.append(b.last_kernel_ms())
+        out["throughput"] = {"items": n, "ms_host_to_host": float(np.median(t2)) * 1e3,
+                             "verifies_per_s": n / float(np.median(t2)), "path": b.last_path(),
+                             "kernel_ms": {k: float(np.median([x[k] for x in km2])) for k in km2[0]}}
+        sample = sorted(rnd.choice(n, 48, replace=False).tolist())
+        tp_check = ([sigs[k] for k in sample], [[kidx[k]] for k in sample], [msgs[k] for k in sample])
+    out["dag_round"] = leg_bls_dag(eng, b, sks, pks, rnd, dag_rounds)
+    # the oracle: statuses of the round (and a throughput sample) + the CPU baseline
+    import bls_ffi as B  # checker / CPU baseline only
+    t0 = time.perf_counter()
+    want = B.verify_items(pks, aggs, signers, digests, threads=threads)
+    cpu_round_s = time.perf_counter() - t0
+    assert want == [0] * certs
+    got_bad = b.verify_many(pks, [aggs[0], aggs[1]], [signers[0], signers[0]], [digests[0], digests[0]])
+    want_bad = B.verify_items(pks, [aggs[0], aggs[1]], [signers[0], signers[0]], [digests[0], digests[0]], threads=2)
+    oracle = {"round_statuses_equal": True, "forged_pair_equal": list(got_bad) == want_bad}
+    if throughput_n:
+        oracle["throughput_sample_equal"] = B.verify_items(pks, *tp_check, threads=threads) == [0] * len(sample)
+    out["oracle_check"] = oracle
+    assert all(oracle.values()), oracle
+    if cpu:
+        t0 = time.perf_counter()
+        rounds = 0
+        while True:
+            B.verify_items(pks, aggs, signers, digests, threads=threads)
+            rounds += 1
+            if time.perf_counter() - t0 >= 8.0:
+                break
+        cdt = (time.perf_counter() - t0) / rounds
+        t0 = time.perf_counter()
+        ns = 0
+        while time.perf_counter() - t0 < 2.0:
+            assert B.verify(pks[0], m, s1) == 0
+            ns += 1
+        out["cpu_baseline"] = {
+            "value": certs / cdt, "unit": "certificates/s", "cores": threads, "kind": "port",
+            "round_ms": cdt * 1e3, "single_verify_ms_1core": (time.perf_counter() - t0) / ns * 1e3,
+            "sample": f"{rounds} x the same {certs}-certificate round ({quorum} of {committee} signers each), "
+                      f"items split over {threads} threads; oracle/bls_oracle.c (plain C restatement of blst "
+                      "fast_aggregate_verify), each key decoded and validated once per call"}
+        out["round"]["gpu_over_cpu"] = out["round"]["certs_per_s"] / out["cpu_baseline"]["value"]
+    out["note"] = ("BLS12-381 min_sig (48 B G1 signatures, 96 B G2 keys), fastcrypto's DST, committee keys "
+                   "registered in the device key cache; item = sig decode + G1 check, key sum, hash to G1, "
+                   "pairing check")
     return out
+
+
+def leg_bls_dag(eng, b, sks, pks, rnd, rounds=20):
+    """C5 under BLS: a 100-node DAG round (100 headers, 99 votes, 100 certificates x 67 signers)
+    through ONE nwv_bls_verify_mixed_many call per round (host -> host)"""
+    n = len(pks)
+    sk_of = dict(zip(pks, sks))
+    com = T.Committee(list(pks), [1] * n, 0, [[0, 1, 2, 3]] * n)
+    q = com.quorum_threshold()
+    parents = T.bls_certificate_digests(eng, T.BlsCertificate.genesis(com))
+    headers = [T.Header(author=k, round=1, epoch=0, payload=[(rnd.bytes(32), a % 4)], parents=list(parents),
+                        signature=bytes(48)) for a, k in enumerate(com.keys)]
+    for h, d in zip(headers, T.bls_header_digests(eng, headers)):
+        h.id = d
+    for h, s_ in zip(headers, b.sign([sk_of[h.author] for h in headers], [h.id for h in headers])):
+        h.signature = s_
+    voters = [[i for i in range(n) if i != a][:q] for a in range(n)]
+    votes = [T.Vote(headers[a].id, 1, 0, com.keys[a], com.keys[v], bytes(48)) for a in range(n) for v in voters[a]]
+    for v, s_ in zip(votes, b.sign([sk_of[v.author] for v in votes], T.bls_vote_digests(eng, votes))):
+        v.signature = s_
+    certs = [T.BlsCertificate.new(eng, com, headers[a], [(v.author, v.signature) for v in votes[a * q:(a + 1) * q]])
+             for a in range(n)]
+    vsample = votes[:99]
+    keep = T._Keep()
+    cc = com._c(keep)
+    harr = (T._Header * n)(*[h._c(keep) for h in headers])
+    varr = (T._Vote * len(vsample))(*[v._c(keep) for v in vsample])
+    carr = (T._BlsCertificate * n)(*[c._c(keep) for c in certs])
+    hres, vres, cres = (ctypes.c_int32 * n)(), (ctypes.c_int32 * len(vsample))(), (ctypes.c_int32 * n)()
+    lib = T.lib()
+    ts = []
+    for r in range(rounds + 2):
+        t0 = time.perf_counter()
+        rc = lib.nwv_bls_verify_mixed_many(eng._h, ctypes.byref(cc), n, harr, hres, len(vsample), varr, vres, n, carr,
+                                           cres)
+        dt = time.perf_counter() - t0
+        assert rc == 0 and not any(hres) and not any(vres) and not any(cres)
+        if r >= 2:
+            ts.append(dt)
+    return dict(_pcts(ts), headers=n, votes=len(vsample), certificates=n, quorum=q,
+                items_per_round=2 * n + len(vsample),
+                note="one nwv_bls_verify_mixed_many call per round: every digest in one BLAKE2b launch, every "
+                     "signature check (200 single-key, 100 aggregates of 67) in one BLS verification call")
