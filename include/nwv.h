@@ -61,10 +61,13 @@ typedef struct nwv_ctx nwv_ctx;
  * k_ed_hash); this flag makes the pass hash and decompress again */
 #define NWV_FLAG_NO_MSM_REUSE 32u
 /* BLS12-381 (nwv_bls.h): verify every item with its own two-pair Miller loop and final
- * exponentiation instead of the batch check (a random linear combination over the call's items:
- * one Miller loop per item, one final exponentiation per call, the per-item form only when the
- * batch check rejects) -- for tests and A/B measurements; statuses are the same either way */
+ * exponentiation on the 8-lane group kernels (round-3 form) instead of the default wave engine --
+ * for tests and A/B measurements; statuses are the same either way */
 #define NWV_FLAG_BLS_PER_ITEM 64u
+/* BLS12-381 (nwv_bls.h): check a call's pairing equations as ONE random linear combination on the
+ * 8-lane group kernels (per item only after a rejection) instead of the default, every item's
+ * own pairing check on one 64-lane wave (exact per-item statuses either way) */
+#define NWV_FLAG_BLS_BATCH 128u
 
 /* ------------------------------------------------------------------ lifecycle ----- */
 /* Process-wide context creation (created once, in Primary::spawn).

@@ -12,13 +12,14 @@
  * Vote::verify :325-327, Certificate::verify :531-534, Certificate::new_unsafe :476-477 and
  * CertificatesResponse::validate_certificates primary/src/block_synchronizer/responses.rs:95-141.
  *
- * Every verification runs on the GPU, one item (one fast_aggregate_verify) per lane: signature
- * decode + G1 membership, public-key decode + G2 membership (once per device for the keys
- * registered in the key cache below, as fastcrypto validates keys once at deserialization; any
- * other key is decoded by the call that names it),
- * aggregate public key, hash to G1; then the pairing equations of all the call's items as one
- * random-linear-combination check (one Miller loop per item, one final exponentiation per call),
- * and only if that rejects, each item's own two-pair Miller loop and final exponentiation.
+ * Every verification runs on the GPU: signature decode + G1 membership, public-key decode + G2
+ * membership (once per device for the keys registered in the key cache below, as fastcrypto
+ * validates keys once at deserialization; any other key is decoded by the call that names it),
+ * aggregate public key, hash to G1 and the pairing equation e(-sig, g2) e(H(msg), apk) = 1.  By
+ * default each item's hash, G1 check and pairing check run on one 64-lane wave each
+ * (bls_wave.h: the Miller loop and final exponentiation as lane-parallel stage programs);
+ * NWV_FLAG_BLS_BATCH checks all items' equations as one random linear combination instead (one
+ * Miller loop per item, one final exponentiation per call; per item only after a rejection).
  * Per-item status codes are exact either way.
  * Buffers are the caller's; the library never retains them.  Thread-safe: concurrent calls on one
  * device run side by side (each takes one of up to eight per-device stream sets).
@@ -62,8 +63,9 @@ int nwv_bls_verify_many(nwv_ctx* ctx, size_t n_keys, const uint8_t* keys, size_t
  * signature decode + G1 checks, [2] hash to G1, [3] key sums, [4] the pairing check (the batch
  * check k_bls_rlc + k_bls_fold + k_bls_final, plus k_bls_pair when it ran) */
 int nwv_bls_last_kernel_ms(nwv_ctx* ctx, double out_ms[5]);
-/* how the last nwv_bls_verify_many call checked its pairings: 0 per item (NWV_FLAG_BLS_PER_ITEM),
- * 1 one batch check that accepted every item, 2 a batch check that rejected, then per item */
+/* how the last nwv_bls_verify_many call checked its pairings: 0 per item on the 8-lane group
+ * kernels (NWV_FLAG_BLS_PER_ITEM), 1 one batch check that accepted every item and 2 a batch check
+ * that rejected, then per item (NWV_FLAG_BLS_BATCH), 3 every item on its own wave (the default) */
 int nwv_bls_last_path(nwv_ctx* ctx);
 /* keys of the last nwv_bls_verify_many call: out[0] key-list entries found in the key cache,
  * out[1] distinct keys the call decoded itself */

@@ -33,7 +33,7 @@ _SIGS = {
     "nwv_bls_keycache_size": ([_vp], _i32),
 }
 KERNELS = ("keys_new_to_cache", "sig_decode", "hash_to_g1", "key_sums", "pairing_check")
-PATHS = ("per_item", "batch_accepted", "batch_rejected_then_per_item")
+PATHS = ("per_item", "batch_accepted", "batch_rejected_then_per_item", "wave")
 _bound = set()
 
 
@@ -113,7 +113,7 @@ class Bls:
 
     def last_path(self):
         """how the last verify_many checked its pairings (PATHS)"""
-        return PATHS[_lib._check(self.lib.nwv_bls_last_path(self._h), allow=(0, 1, 2))]
+        return PATHS[_lib._check(self.lib.nwv_bls_last_path(self._h), allow=(0, 1, 2, 3))]
 
     # the committee key cache: register at epoch start, reset at an epoch change
     def register_keys(self, keys):

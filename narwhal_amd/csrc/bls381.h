@@ -788,7 +788,15 @@ NWV_HD fp fp_from_be64(const uint8_t* b) {
 // simplified SWU on y^2 = x^3 + A'x + B' (RFC 9380 §6.6.2, Z = 11), the straight-line form of
 // Appendix F.2 with sqrt_ratio for q = 3 mod 4 (F.2.1.2): one exponentiation and one inversion
 // per call (the textbook form's inversions of A and tv1 and its second square root are gone)
+// the same map with x left as the fraction xn / xd (no inversion: the wave engine takes the
+// isogeny map in homogeneous coordinates)
+NWV_HD void map_sswu_frac(fp& xn_o, fp& xd_o, fp& yo, const fp& u);
 NWV_HD void map_sswu(fp& xo, fp& yo, const fp& u) {
+    fp xn, xd;
+    map_sswu_frac(xn, xd, yo, u);
+    xo = fp_mul(xn, fp_inv(xd));
+}
+NWV_HD void map_sswu_frac(fp& xn_o, fp& xd_o, fp& yo, const fp& u) {
     const fp A = k_sswu_a(), B = k_sswu_b(), Z = k_sswu_z();
     const fp tv1 = fp_mul(Z, fp_sqr(u));
     fp tv2 = fp_add(fp_sqr(tv1), tv1);
@@ -809,7 +817,8 @@ NWV_HD void map_sswu(fp& xo, fp& yo, const fp& u) {
     fp y = qr ? y1 : fp_mul(fp_mul(tv1, u), y1);
     const fp x = qr ? tv3 : xn;
     if (fp_sgn0(u) != fp_sgn0(y)) y = fp_neg(y);
-    xo = fp_mul(x, fp_inv(tv4));
+    xn_o = x;
+    xd_o = tv4;
     yo = y;
 }
 // the 11-isogeny (RFC 9380 Appendix E.2), constants from tools/gen_bls_iso.py

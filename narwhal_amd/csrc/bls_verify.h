@@ -9,6 +9,7 @@
 // oracle's (oracle/bls_oracle.h ORB_*), checked in its order.
 #pragma once
 #include "bls_group.h"
+#include "bls_wave.h"
 
 namespace bls {
 
@@ -255,4 +256,125 @@ NWV_HD void rlc_sfold(uint32_t* sa, const uint32_t* sb) { st_g1j(sa, jac_add(ld_
 // stage 5: the batch verdict, FE(f) == 1
 G_HD bool g_rlc_final(const GCtx& g, const uint32_t* f_rec) { return g_is_one(g, g_final_exp(g, g_load(g, f_rec))); }
 
+// ---- the same check on one whole wave (bls_wave.h) -------------------------------------------
+// the line table of an affine Q (a G2 record): (l0, l1, l4) of every Miller-loop step, NSTEPS x 6
+// slots of 14 words -- what the loop computes from T when no table is given
+template <class W>
+NWV_HD void w_key_lines(const W& w, const uint32_t* q_rec, uint32_t* out) {
+    using namespace wave;
+    init_slots(w);
+    w.zero(REG_QB, 6);
+    w.sync();
+    w.put_words(REG_QB, q_rec, 4);
+    w.put_fp(REG_QB + 4, k_one());
+    w.sync();
+    w.put_words(REG_TB, w.wm + SW * REG_QB, 6);
+    w.sync();
+    const char* steps = BLS_WAVE_STEPS_STR;
+#pragma unroll 1
+    for (int k = 0; k < NSTEPS; k++) {
+        w.run(steps[k] == 'a' ? P_LINES_ADD : P_LINES_DBL);
+        w.get_words(REG_LB, out + (size_t)k * 6 * SW, 6);
+        w.sync();
+    }
+}
+
+// e(-sig, g2) e(H, apk) == 1 from the item's records (sig, H affine G1 records, apk an affine G2
+// record); qlines = apk's precomputed line table (a cached key) or null.  The identity signature
+// enters as P = (0, 0): its lines reduce to their l0 in Fp2, which the final exponentiation maps
+// to 1 (e(O, g2) = 1); every l0 of g2's table is nonzero (checked by the generator).
+template <class W>
+NWV_HD bool w_pairing_check(const W& w, const uint32_t* sig_rec, const uint32_t* h_rec, const uint32_t* apk_rec,
+                            const uint32_t* qlines) {
+    using namespace wave;
+    init_slots(w);
+    w.zero(REG_PA, 2);
+    w.zero(REG_PB, 3);
+    w.zero(REG_QB, 6);
+    w.sync();
+    if (!sig_rec[2 * NL]) {
+        w.put_words(REG_PA, sig_rec, 1);
+        w.put_fp(REG_PA + 1, fp_neg(ld_fp(sig_rec + NL)));
+    }
+    if (!h_rec[2 * NL]) w.put_words(REG_PB, h_rec, 2);
+    w.put_fp(REG_PB + 2, k_one());
+    w.put_words(REG_QB, apk_rec, 4);
+    w.put_fp(REG_QB + 4, k_one());
+    w.sync();
+    return wave::pairing_check(w, qlines);
+}
+
+// H(msg) on a wave: lanes 0 and 1 each expand the message and map u_0 / u_1 with SSWU (x as a
+// fraction: no inversion); the two isogeny maps (homogeneous), their sum and [h_eff] run as
+// stage programs.  out: X, Y, Z (x = X / Z, y = Y / Z) and an identity flag (3 NL + 1 words).
+constexpr int G1H_REC_WORDS = 3 * NL + 1;
+template <class W>
+NWV_HD void w_hash_to_g1(const W& w, const uint8_t* msg, uint32_t n, const uint8_t* dst, uint32_t dl, uint32_t* out) {
+    using namespace wave;
+    init_slots(w);
+    w.lanes(2, [&](int j) {
+        uint8_t ub[128];
+        expand_xmd_128(ub, msg, n, dst, dl);
+        const fp u0 = fp_from_be64(ub), u1 = fp_from_be64(ub + 64);  // constant offsets, then a select
+        fp xn, xd, y;
+        map_sswu_frac(xn, xd, y, fp_sel(j == 0, u0, u1));
+        w.set(REG_S + 3 * j, xn);
+        w.set(REG_S + 3 * j + 1, xd);
+        w.set(REG_S + 3 * j + 2, y);
+    });
+    w.sync();
+    w.run(P_ISO2_ADD);
+    g1_chain(w, BLS_H_EFF);
+    w.get_words(REG_U, out, 3);
+    w.sync();
+    const bool inf = fp_is_zero(w.get(REG_U + 2));
+    w.lanes(1, [&](int) { out[3 * NL] = inf ? 1u : 0u; });
+}
+
+// the signature's G1 membership on a wave (sig_decode's g1_in_group): [x^2] P = -phi(P) with
+// complete formulas; P = the affine record (not the identity)
+template <class W>
+NWV_HD bool w_g1_in_group(const W& w, const uint32_t* rec) {
+    using namespace wave;
+    init_slots(w);
+    w.put_words(REG_V, rec, 2);
+    w.put_words(REG_U, rec, 2);
+    w.put_words(REG_S, rec, 2);
+    w.put_fp(REG_V + 2, k_one());
+    w.put_fp(REG_U + 2, k_one());
+    w.sync();
+    g1_chain(w, BLS_X_ABS);
+    w.run(P_COPY_U_TO_V);
+    g1_chain(w, BLS_X_ABS);
+    w.run(P_G1_PHI_CHECK);
+    return fp_is_zero(w.get(REG_S + 2)) && fp_is_zero(w.get(REG_S + 3));
+}
+
+// w_pairing_check with H in homogeneous coordinates (w_hash_to_g1's record)
+template <class W>
+NWV_HD bool w_pairing_check_h(const W& w, const uint32_t* sig_rec, const uint32_t* hh_rec, const uint32_t* apk_rec,
+                              const uint32_t* qlines) {
+    using namespace wave;
+    init_slots(w);
+    w.zero(REG_PA, 2);
+    w.zero(REG_QB, 6);
+    w.sync();
+    if (!sig_rec[2 * NL]) {
+        w.put_words(REG_PA, sig_rec, 1);
+        w.put_fp(REG_PA + 1, fp_neg(ld_fp(sig_rec + NL)));
+    }
+    if (hh_rec[3 * NL]) {  // H = O (never from a hash in practice): only the lines' l0 remain
+        w.zero(REG_PB, 2);
+        w.sync();
+        w.put_fp(REG_PB + 2, k_one());
+    } else {
+        w.put_words(REG_PB, hh_rec, 3);
+    }
+    w.put_words(REG_QB, apk_rec, 4);
+    w.put_fp(REG_QB + 4, k_one());
+    w.sync();
+    return wave::pairing_check(w, qlines);
+}
+
 }  // namespace bls
+

@@ -342,6 +342,56 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_pairing_raw(uint32_t n, const
     for (int k = 0; k < 12; k++) plain_to_be(o + 48 * k, fp_from_mont(*c[k]));
 }
 
+// ---- the wave engine (bls_wave.h): one 64-lane wave per item ------------------------------------
+#define BLSW_IDX()                                        \
+    __shared__ uint32_t wm[wave::SW * wave::NSLOTS];      \
+    const uint32_t i = blockIdx.x;                        \
+    if (i >= n) return;                                   \
+    const wave::Wave w{wm, (int)threadIdx.x}
+// H(msg_i), homogeneous
+__global__ __launch_bounds__(64) void k_blsw_h2c(uint32_t n, const uint8_t* msg, const uint64_t* off,
+                                                 const uint32_t* len, const uint8_t* dst, uint32_t dl, uint32_t* hrec) {
+    BLSW_IDX();
+    w_hash_to_g1(w, msg + off[i], len[i], dst, dl, hrec + (size_t)G1H_REC_WORDS * i);
+}
+// signature decode only (one lane per item); the G1 check runs beside the pairing (k_blsw_sub)
+__global__ __launch_bounds__(BLS_LANES) void k_blsw_sigdec(uint32_t n, const uint8_t* sig, uint32_t* rec, int32_t* st) {
+    BLS_IDX();
+    fp x, y;
+    bool inf;
+    const int32_t s = g1_decompress(x, y, inf, sig + 48 * (size_t)i);
+    if (s != ST_OK || inf) x = y = fp_zero();
+    st_g1(rec + (size_t)G1_REC_WORDS * i, x, y, s == ST_OK && inf);
+    st[i] = s;
+}
+__global__ __launch_bounds__(64) void k_blsw_sub(uint32_t n, const uint32_t* rec, const int32_t* st_dec, int32_t* st_sub) {
+    BLSW_IDX();
+    const uint32_t* r = rec + (size_t)G1_REC_WORDS * i;
+    int32_t s = ST_OK;
+    if (st_dec[i] == ST_OK && !r[2 * NL]) s = w_g1_in_group(w, r) ? ST_OK : ST_NOT_IN_GROUP;
+    if (threadIdx.x == 0) st_sub[i] = s;
+}
+// e(-sig, g2) e(H, apk) == 1 for every item whose signature decoded and whose keys are valid
+// (run beside the signature's G1 check: the status join puts that check first)
+__global__ __launch_bounds__(64) void k_blsw_pair(uint32_t n, const uint32_t* srec, const int32_t* st_dec,
+                                                  const uint32_t* hrec, const uint32_t* arec, const int32_t* st_apk,
+                                                  int32_t* st_pair) {
+    BLSW_IDX();
+    int32_t s = ST_VERIFY_FAIL;
+    if (st_dec[i] == ST_OK && st_apk[i] == ST_OK)
+        s = w_pairing_check_h(w, srec + (size_t)G1_REC_WORDS * i, hrec + (size_t)G1H_REC_WORDS * i,
+                              arec + (size_t)G2_REC_WORDS * i, nullptr)
+                ? ST_OK
+                : ST_VERIFY_FAIL;
+    if (threadIdx.x == 0) st_pair[i] = s;
+}
+// the oracle's order: signature decode, its G1 check, the keys, the pairing equation
+__global__ __launch_bounds__(BLS_LANES) void k_blsw_status(uint32_t n, const int32_t* dec, const int32_t* sub,
+                                                           const int32_t* apk, const int32_t* pair, int32_t* st) {
+    BLS_IDX();
+    st[i] = dec[i] != ST_OK ? dec[i] : sub[i] != ST_OK ? sub[i] : apk[i] != ST_OK ? apk[i] : pair[i];
+}
+
 // ------------------------------------------------------------------------------- host side
 namespace {
 
@@ -402,13 +452,14 @@ struct BlsKeyCache {
 // One call in flight: its streams, staging arena and scratch.  A device keeps a pool of these, so
 // concurrent callers run their pipelines side by side instead of queueing on one device lock.
 struct BlsLane {
-    hipStream_t stream = nullptr;              // H2D, signatures, pairing check, D2H
-    hipStream_t side[2] = {nullptr, nullptr};  // keys + key sums; hash to G1
+    hipStream_t stream = nullptr;                       // H2D, signatures, pairing check, D2H
+    hipStream_t side[3] = {nullptr, nullptr, nullptr};  // keys + key sums; hash to G1; G1 checks
     HBuf stage;
     DBuf in, work;
-    // [0,1] keys, [1,2] key sums (side 0); [3,4] signatures (main); [5,6] hash to G1 (side 1);
-    // [7,8] pairing check (main); [9] inputs resident, [10] side 0 done, [11] side 1 done
-    hipEvent_t ev[12] = {};
+    // [0,1] keys, [1,2] key sums (side 0); [3,4] signatures (main; wave mode: decode on main, the
+    // G1 check on side 2); [5,6] hash to G1 (side 1); [7,8] pairing check (main); [9] inputs
+    // resident, [10] side 0 done, [11] side 1 done, [12] signatures decoded, [13] side 2 done
+    hipEvent_t ev[14] = {};
     ~BlsLane() {
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
@@ -470,7 +521,8 @@ class LaneLease {
                 if (hipSetDevice(d.ordinal) != hipSuccess ||
                     hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking) != hipSuccess ||
                     hipStreamCreateWithFlags(&l->side[0], hipStreamNonBlocking) != hipSuccess ||
-                    hipStreamCreateWithFlags(&l->side[1], hipStreamNonBlocking) != hipSuccess) {
+                    hipStreamCreateWithFlags(&l->side[1], hipStreamNonBlocking) != hipSuccess ||
+                    hipStreamCreateWithFlags(&l->side[2], hipStreamNonBlocking) != hipSuccess) {
                     rc_ = nwv_internal_set_err(NWV_ERR_HIP, "bls stream");
                     return;
                 }
@@ -606,7 +658,11 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     if (lane.rc()) return lane.rc();
     BlsLane& L = *lane;
     static const uint8_t zero[8] = {0};
-    const bool batch = !(d.flags & NWV_FLAG_BLS_PER_ITEM);
+    // pairing-check mode: the wave engine per item (default), or the 8-lane group kernels -- one
+    // random-linear-combination batch check (NWV_FLAG_BLS_BATCH) or per item (NWV_FLAG_BLS_PER_ITEM)
+    const bool group_item = (d.flags & NWV_FLAG_BLS_PER_ITEM) != 0;
+    const bool batch = !group_item && (d.flags & NWV_FLAG_BLS_BATCH) != 0;
+    const bool wavem = !group_item && !batch;
     int rc;
     // the call's key table: cache slots (lookups only) or scratch entries KC_CAP + j
     std::shared_lock<std::shared_mutex> kc_hold(d.kc.mu);  // records stay put while our kernels read them
@@ -663,7 +719,9 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
                  w_ok = al256(w_sapk + 4 * n), w_frec = al256(w_ok + 4),
                  w_jrec = al256(w_frec + 4 * F12_REC_WORDS * (batch ? n + 1 : 0)),
                  w_prec = al256(w_jrec + 4 * G1J_REC_WORDS * (batch ? n : 0)),
-                 w_end = w_prec + 4 * G1J_REC_WORDS * (batch ? n + 1 : 0) + 4;
+                 w_hh = al256(w_prec + 4 * G1J_REC_WORDS * (batch ? n + 1 : 0) + 4),
+                 w_sdec = al256(w_hh + 4 * G1H_REC_WORDS * (wavem ? n : 0)), w_ssub = al256(w_sdec + 4 * n),
+                 w_spair = al256(w_ssub + 4 * n), w_end = w_spair + 4 * n + 4;
     if ((rc = L.work.ensure(w_end))) return rc;
     uint8_t* in = static_cast<uint8_t*>(L.in.p);
     uint8_t* w = static_cast<uint8_t*>(L.work.p);
@@ -680,7 +738,27 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     auto* frec = reinterpret_cast<uint32_t*>(w + w_frec);
     auto* jrec = reinterpret_cast<uint32_t*>(w + w_jrec);
     auto* prec = reinterpret_cast<uint32_t*>(w + w_prec);
-    hipStream_t s0 = L.stream, s1 = L.side[0], s2 = L.side[1];
+    auto* hh = reinterpret_cast<uint32_t*>(w + w_hh);
+    auto* sdec = reinterpret_cast<int32_t*>(w + w_sdec);
+    auto* ssub = reinterpret_cast<int32_t*>(w + w_ssub);
+    auto* spair = reinterpret_cast<int32_t*>(w + w_spair);
+    hipStream_t s0 = L.stream, s1 = L.side[0], s2 = L.side[1], s3 = L.side[2];
+    // stage times of the completed call, its path and key counts -> the device's "last call"
+    auto finish = [&](int path_done) -> int {
+        const int pairs[5][2] = {{0, 1}, {3, 4}, {5, 6}, {1, 2}, {7, 8}};  // keys, sigs, h2c, apk, pairing
+        double ms5[5];
+        for (int k = 0; k < 5; k++) {
+            float ms = 0;
+            BLS_HIP(hipEventElapsedTime(&ms, L.ev[pairs[k][0]], L.ev[pairs[k][1]]));
+            ms5[k] = ms;
+        }
+        std::lock_guard<std::mutex> g(d.stat_mu);
+        std::memcpy(d.last_ms, ms5, sizeof ms5);
+        d.last_path = path_done;
+        d.last_keys[0] = hits;
+        d.last_keys[1] = n_dec;
+        return NWV_OK;
+    };
     BLS_HIP(hipMemcpyAsync(in, h, a.total, hipMemcpyHostToDevice, s0));
     BLS_HIP(hipEventRecord(L.ev[9], s0));
     BLS_HIP(hipStreamWaitEvent(s1, L.ev[9], 0));
@@ -699,11 +777,43 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     BLS_HIP(hipEventRecord(L.ev[10], s1));
     // side 1: hash to G1 (every item: the statuses are not known yet)
     BLS_HIP(hipEventRecord(L.ev[5], s2));
-    hipLaunchKernelGGL(k_bls_h2c_g, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s2, (uint32_t)n, in + o_msg,
-                       reinterpret_cast<const uint64_t*>(in + o_moff), reinterpret_cast<const uint32_t*>(in + o_mlen),
-                       in + o_dst, (uint32_t)dl, hrec);
+    if (wavem)
+        hipLaunchKernelGGL(k_blsw_h2c, dim3((unsigned)n), dim3(64), 0, s2, (uint32_t)n, in + o_msg,
+                           reinterpret_cast<const uint64_t*>(in + o_moff),
+                           reinterpret_cast<const uint32_t*>(in + o_mlen), in + o_dst, (uint32_t)dl, hh);
+    else
+        hipLaunchKernelGGL(k_bls_h2c_g, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s2, (uint32_t)n, in + o_msg,
+                           reinterpret_cast<const uint64_t*>(in + o_moff),
+                           reinterpret_cast<const uint32_t*>(in + o_mlen), in + o_dst, (uint32_t)dl, hrec);
     BLS_HIP(hipEventRecord(L.ev[6], s2));
     BLS_HIP(hipEventRecord(L.ev[11], s2));
+    if (wavem) {
+        // main: signature decode; side 2: its G1 check; main: every item's pairing check beside
+        // it, then the statuses joined in the oracle's order
+        BLS_HIP(hipEventRecord(L.ev[3], s0));
+        hipLaunchKernelGGL(k_blsw_sigdec, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, in + o_sigs, srec,
+                           sdec);
+        BLS_HIP(hipEventRecord(L.ev[12], s0));
+        BLS_HIP(hipStreamWaitEvent(s3, L.ev[12], 0));
+        hipLaunchKernelGGL(k_blsw_sub, dim3((unsigned)n), dim3(64), 0, s3, (uint32_t)n, (const uint32_t*)srec,
+                           (const int32_t*)sdec, ssub);
+        BLS_HIP(hipEventRecord(L.ev[4], s3));
+        BLS_HIP(hipEventRecord(L.ev[13], s3));
+        BLS_HIP(hipStreamWaitEvent(s0, L.ev[10], 0));
+        BLS_HIP(hipStreamWaitEvent(s0, L.ev[11], 0));
+        BLS_HIP(hipEventRecord(L.ev[7], s0));
+        hipLaunchKernelGGL(k_blsw_pair, dim3((unsigned)n), dim3(64), 0, s0, (uint32_t)n, (const uint32_t*)srec,
+                           (const int32_t*)sdec, (const uint32_t*)hh, (const uint32_t*)arec, (const int32_t*)sapk,
+                           spair);
+        BLS_HIP(hipEventRecord(L.ev[8], s0));
+        BLS_HIP(hipStreamWaitEvent(s0, L.ev[13], 0));
+        hipLaunchKernelGGL(k_blsw_status, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n,
+                           (const int32_t*)sdec, (const int32_t*)ssub, (const int32_t*)sapk, (const int32_t*)spair, st);
+        BLS_HIP(hipGetLastError());
+        BLS_HIP(hipMemcpyAsync(status, st, 4 * n, hipMemcpyDeviceToHost, s0));
+        BLS_HIP(hipStreamSynchronize(s0));
+        return finish(3);
+    }
     // main: signatures, then the join
     BLS_HIP(hipEventRecord(L.ev[3], s0));
     hipLaunchKernelGGL(k_bls_sigs, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, in + o_sigs, srec, ssig);
@@ -744,19 +854,7 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     BLS_HIP(hipGetLastError());
     BLS_HIP(hipMemcpyAsync(status, st, 4 * n, hipMemcpyDeviceToHost, s0));
     BLS_HIP(hipStreamSynchronize(s0));
-    const int pairs[5][2] = {{0, 1}, {3, 4}, {5, 6}, {1, 2}, {7, 8}};  // keys, sigs, h2c, apk, pairing
-    double ms5[5];
-    for (int k = 0; k < 5; k++) {
-        float ms = 0;
-        BLS_HIP(hipEventElapsedTime(&ms, L.ev[pairs[k][0]], L.ev[pairs[k][1]]));
-        ms5[k] = ms;
-    }
-    std::lock_guard<std::mutex> g(d.stat_mu);
-    std::memcpy(d.last_ms, ms5, sizeof ms5);
-    d.last_path = path;
-    d.last_keys[0] = hits;
-    d.last_keys[1] = n_dec;
-    return NWV_OK;
+    return finish(path);
 }
 
 const uint8_t* dst_or_default(const uint8_t* dst, size_t* dl) {

@@ -174,4 +174,109 @@ int bh_rlc_batch(size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_
     return g_rlc_final(g, f.data()) ? 1 : 0;
 }
 
+// ---- the wave engine (bls_wave.h) on the host: the same interpreter and stage tables -----------
+static wave::Wave host_wave() {
+    static thread_local std::vector<uint32_t> wm(wave::SW * wave::NSLOTS);
+    wave::Wave w;
+    w.wm = wm.data();
+    return w;
+}
+static void f12_from_be(const uint8_t* in, uint32_t* slots) {
+    for (int k = 0; k < 12; k++) {
+        fp v;
+        be_to_mont(v, in + 48 * k);
+        st_fp(slots + NL * k, v);
+    }
+}
+static void f12_to_be(const uint32_t* slots, uint8_t* out) {
+    for (int k = 0; k < 12; k++) mont_to_be(out + 48 * k, ld_fp(slots + NL * k));
+}
+// op 0: F G (P_MUL_F_G), 1: cyclotomic square (P_CYC_SQR_F), 2: F^2 (P_SQR_F), 3: the final
+// exponentiation; a, b: 12 big-endian Fp in tower order
+void bh_w_f12_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
+    const wave::Wave w = host_wave();
+    wave::init_slots(w);
+    f12_from_be(a, w.wm + NL * wave::REG_F);
+    if (b) f12_from_be(b, w.wm + NL * wave::REG_G);
+    if (op == 0) w.run(wave::P_MUL_F_G);
+    else if (op == 1) w.run(wave::P_CYC_SQR_F);
+    else if (op == 2) w.run(wave::P_SQR_F);
+    else wave::final_exp(w);
+    f12_to_be(w.wm + NL * wave::REG_F, out);
+}
+// fast_aggregate_verify with the pairing check on the (host-emulated) wave; lines: 1 = apk's line
+// table precomputed by the lines programs (the cached-key path), 0 = computed in the loop
+int bh_w_fast_aggregate_verify(const uint8_t* sig, size_t n_pks, const uint8_t* pks, const uint8_t* msg, size_t n,
+                               const uint8_t* dst, size_t dl, int lines) {
+    uint32_t srec[G1_REC_WORDS], hrec[G1_REC_WORDS], arec[G2_REC_WORDS];
+    int32_t st = sig_decode(sig, srec);
+    if (st != ST_OK) return st;
+    if (n_pks == 0) return ST_AGGR_MISMATCH;
+    std::vector<uint32_t> krec(G2_REC_WORDS * n_pks), idx(n_pks);
+    std::vector<int32_t> kst(n_pks);
+    for (size_t i = 0; i < n_pks; i++) {
+        kst[i] = key_decode(pks + 96 * i, krec.data() + G2_REC_WORDS * i);
+        idx[i] = (uint32_t)i;
+    }
+    st = apk_record(krec.data(), kst.data(), idx.data(), (uint32_t)n_pks, arec);
+    if (st != ST_OK) return st;
+    h2c_record(msg, (uint32_t)n, dst, (uint32_t)dl, hrec);
+    const wave::Wave w = host_wave();
+    std::vector<uint32_t> tab;
+    if (lines) {
+        tab.resize((size_t)wave::NSTEPS * 6 * NL);
+        w_key_lines(w, arec, tab.data());
+    }
+    return w_pairing_check(w, srec, hrec, arec, lines ? tab.data() : nullptr) ? ST_OK : ST_VERIFY_FAIL;
+}
+
+// H(msg) by the wave programs (homogeneous), returned affine like bh_hash_to_g1
+void bh_w_hash_to_g1(const uint8_t* msg, size_t n, const uint8_t* dst, size_t dl, uint8_t* out) {
+    const wave::Wave w = host_wave();
+    uint32_t rec[G1H_REC_WORDS];
+    w_hash_to_g1(w, msg, (uint32_t)n, dst, (uint32_t)dl, rec);
+    if (rec[3 * NL]) {
+        for (int i = 0; i < 96; i++) out[i] = 0;
+        return;
+    }
+    const fp zi = fp_inv(ld_fp(rec + 2 * NL));
+    mont_to_be(out, fp_mul(ld_fp(rec), zi));
+    mont_to_be(out + 48, fp_mul(ld_fp(rec + NL), zi));
+}
+// the signature's status with the G1 membership test on the wave (decode, then w_g1_in_group)
+int bh_w_sig_status(const uint8_t* sig) {
+    fp x, y;
+    bool inf;
+    int32_t st = g1_decompress(x, y, inf, sig);
+    if (st != ST_OK || inf) return st;
+    uint32_t rec[G1_REC_WORDS];
+    st_g1(rec, x, y, false);
+    return w_g1_in_group(host_wave(), rec) ? ST_OK : ST_NOT_IN_GROUP;
+}
+// fast_aggregate_verify with every step of the wave pipeline: signature decode + wave G1 check,
+// keys, wave hash to G1 (homogeneous), wave pairing check
+int bh_w2_fast_aggregate_verify(const uint8_t* sig, size_t n_pks, const uint8_t* pks, const uint8_t* msg, size_t n,
+                                const uint8_t* dst, size_t dl) {
+    int32_t st = bh_w_sig_status(sig);
+    if (st != ST_OK) return st;
+    uint32_t srec[G1_REC_WORDS], hrec[G1H_REC_WORDS], arec[G2_REC_WORDS];
+    fp x, y;
+    bool inf;
+    g1_decompress(x, y, inf, sig);
+    st_g1(srec, inf ? fp_zero() : x, inf ? fp_zero() : y, inf);
+    if (n_pks == 0) return ST_AGGR_MISMATCH;
+    std::vector<uint32_t> krec(G2_REC_WORDS * n_pks), idx(n_pks);
+    std::vector<int32_t> kst(n_pks);
+    for (size_t i = 0; i < n_pks; i++) {
+        kst[i] = key_decode(pks + 96 * i, krec.data() + G2_REC_WORDS * i);
+        idx[i] = (uint32_t)i;
+    }
+    st = apk_record(krec.data(), kst.data(), idx.data(), (uint32_t)n_pks, arec);
+    if (st != ST_OK) return st;
+    const wave::Wave w = host_wave();
+    w_hash_to_g1(w, msg, (uint32_t)n, dst, (uint32_t)dl, hrec);
+    return w_pairing_check_h(w, srec, hrec, arec, nullptr) ? ST_OK : ST_VERIFY_FAIL;
+}
+
 }  // extern "C"
+

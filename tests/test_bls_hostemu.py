@@ -34,6 +34,11 @@ def emu():
     L.bh_rlc_batch.argtypes = [sz, c, c, c, c, c, sz]
     L.bh_g_pairing.argtypes = [c, c, vp]
     L.bh_g_fast_aggregate_verify.argtypes = [c, sz, c, c, sz, c, sz]
+    L.bh_w_f12_op.argtypes = [ctypes.c_int, c, c, vp]
+    L.bh_w_fast_aggregate_verify.argtypes = [c, sz, c, c, sz, c, sz, ctypes.c_int]
+    L.bh_w_hash_to_g1.argtypes = [c, sz, c, sz, vp]
+    L.bh_w_sig_status.argtypes = [c]
+    L.bh_w2_fast_aggregate_verify.argtypes = [c, sz, c, c, sz, c, sz]
     return L
 
 
@@ -167,3 +172,86 @@ def test_group_fast_aggregate_verify_statuses(emu, gold):
     for s, ks, msg in [(agg, pks[:3], m), (agg, pks[:3], m + b"x"), (sigs[0], pks[:1], m), (C.IDENTITY_G1, pks[:3], m)]:
         got = emu.bh_g_fast_aggregate_verify(s, len(ks), b"".join(ks), msg, len(msg), dst, len(dst))
         assert got == B.fast_aggregate_verify(s, ks, msg)
+
+
+# ---- the wave engine (bls_wave.h: stage programs of tools/gen_bls_wave.py) on the host --------
+def _rand_f12(rnd):
+    p = C.p
+    return b"".join(rnd.randrange(p).to_bytes(48, "big") for _ in range(12))
+
+
+def test_wave_f12_ops_match_oracle(emu):
+    """the stage programs' Fp12 product and square equal the oracle's Fp12 arithmetic bit for bit
+    (canonical outputs), the cyclotomic square on GT elements as well"""
+    rnd = random.Random(51)
+    for _ in range(3):
+        a, b = _rand_f12(rnd), _rand_f12(rnd)
+        o = _buf(576)
+        emu.bh_w_f12_op(0, a, b, o)
+        assert o.raw == B.gt_mul(a, b)
+        emu.bh_w_f12_op(2, a, None, o)
+        assert o.raw == B.gt_mul(a, a)
+    g = B.pairing(B.g1_mul(B.g1_gen(), 7), B.g2_gen())  # in the cyclotomic subgroup
+    o = _buf(576)
+    emu.bh_w_f12_op(1, g, None, o)
+    assert o.raw == B.gt_mul(g, g)
+
+
+@pytest.mark.parametrize("lines", [0, 1])
+def test_wave_fast_aggregate_verify_matches_oracle(emu, lines):
+    """fast_aggregate_verify with the pairing check on the wave (Miller loop and final
+    exponentiation as stage programs): valid items, wrong message / key set, identity signature,
+    pre-pairing failures; the apk's lines computed in the loop (0) or precomputed (1)"""
+    rnd = random.Random(52 + lines)
+    sks = [rnd.randrange(1, r).to_bytes(32, "big") for _ in range(4)]
+    pks = [B.keygen(k)[1] for k in sks]
+    m = rnd.randbytes(32)
+    sigs = [B.sign(k, m) for k in sks]
+    _, agg = B.aggregate(sigs[:3])
+    cases = [(agg, pks[:3], m), (sigs[0], pks[:1], m), (agg, pks[:3], m + b"!"), (agg, pks[1:], m),
+             (C.IDENTITY_G1, pks[:2], m), (C.not_in_g1(), pks[:2], m), (agg, [], m)]
+    for sig, ks, msg in cases:
+        got = emu.bh_w_fast_aggregate_verify(sig, len(ks), b"".join(ks) or None, msg, len(msg), B.DST_NUL,
+                                             len(B.DST_NUL), lines)
+        assert got == B.fast_aggregate_verify(sig, ks, msg), (ks == pks[:3], msg == m)
+
+
+def test_wave_hash_to_g1_rfc9380(emu, gold):
+    """hash to G1 with the isogeny map, the sum and [h_eff] as wave programs (homogeneous, no
+    inversion): the RFC 9380 J.9.1 known answers and the oracle on other messages"""
+    o = _buf(96)
+    for v in gold["hash_to_g1"]:
+        m, dst = bytes.fromhex(v["msg"]), v["dst"].encode()
+        emu.bh_w_hash_to_g1(m, len(m), dst, len(dst), o)
+        assert o.raw.hex() == v["x"] + v["y"]
+    rnd = random.Random(53)
+    for n in (0, 1, 32, 77, 200):
+        m = rnd.randbytes(n)
+        emu.bh_w_hash_to_g1(m, len(m), B.DST_NUL, len(B.DST_NUL), o)
+        assert o.raw == B.hash_to_g1(m)
+
+
+def test_wave_g1_membership(emu):
+    """the signature's G1 check on the wave: valid signatures, points of E outside G1 (several),
+    the identity, bad encodings -- statuses equal the oracle's decode + group check"""
+    rnd = random.Random(54)
+    sk = rnd.randrange(1, r).to_bytes(32, "big")
+    cases = [B.sign(sk, rnd.randbytes(32)) for _ in range(2)] + [C.not_in_g1(s) for s in (5, 50, 500)] + \
+        [C.IDENTITY_G1, C.off_curve_g1()] + C.bad_encodings_g1(B.sign(sk, b"x"))
+    for sg in cases:
+        want = B.g1_decompress(sg)[0] or (0 if sg == C.IDENTITY_G1 or B.lib().orb_g1_in_group(sg) else B.ORB_NOT_IN_GROUP)
+        assert emu.bh_w_sig_status(sg) == want
+
+
+def test_wave_pipeline_fast_aggregate_verify(emu):
+    """every step on the wave (decode + wave G1 check, wave hash to G1, wave pairing check)
+    against the oracle"""
+    rnd = random.Random(55)
+    sks = [rnd.randrange(1, r).to_bytes(32, "big") for _ in range(3)]
+    pks = [B.keygen(k)[1] for k in sks]
+    m = rnd.randbytes(32)
+    _, agg = B.aggregate([B.sign(k, m) for k in sks])
+    for sig, ks, msg in [(agg, pks, m), (agg, pks, m + b"?"), (agg, pks[:2], m), (C.not_in_g1(), pks, m),
+                         (C.IDENTITY_G1, pks, m)]:
+        got = emu.bh_w2_fast_aggregate_verify(sig, len(ks), b"".join(ks), msg, len(msg), B.DST_NUL, len(B.DST_NUL))
+        assert got == B.fast_aggregate_verify(sig, ks, msg)

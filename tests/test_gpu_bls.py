@@ -28,6 +28,18 @@ def bls():
 
 
 @pytest.fixture(scope="module")
+def bls_batch():
+    """a context under NWV_FLAG_BLS_BATCH: the call's pairing equations as one random linear
+    combination on the 8-lane group kernels (per item only after a rejection)"""
+    import narwhal_amd
+    from narwhal_amd import _lib
+    from narwhal_amd.bls import Bls
+    e = narwhal_amd.Engine(device=0, flags=_lib.NWV_FLAG_BLS_BATCH)
+    yield Bls(e)
+    e.close()
+
+
+@pytest.fixture(scope="module")
 def bls_per_item():
     """a context under NWV_FLAG_BLS_PER_ITEM: every item's own pairing check, no batch check"""
     import narwhal_amd
@@ -88,12 +100,17 @@ def bls_nocache():
     e.close()
 
 
-@pytest.mark.parametrize("path", ["batch", "per_item", "nocache"])
-def test_verify_many_mixed_batch_matches_oracle(bls, bls_per_item, bls_nocache, path):
+EXPECT_PATH = {"wave": ("wave", "wave"), "nocache": ("wave", "wave"), "per_item": ("per_item", "per_item"),
+               "batch": ("batch_rejected_then_per_item", "batch_accepted")}
+
+
+@pytest.mark.parametrize("path", ["wave", "batch", "per_item", "nocache"])
+def test_verify_many_mixed_batch_matches_oracle(bls, bls_batch, bls_per_item, bls_nocache, path):
     """certificates of a 10-node committee (quorum 7 signers, 32-byte digests) plus every
-    adversarial category; statuses equal the oracle's codes item by item, through the batch check
-    (it rejects, then the per-item check names the failures) and under NWV_FLAG_BLS_PER_ITEM"""
-    bls = {"batch": bls, "per_item": bls_per_item, "nocache": bls_nocache}[path]
+    adversarial category; statuses equal the oracle's codes item by item: on the wave engine
+    (default), through the batch check (it rejects, then the per-item check names the failures)
+    and under NWV_FLAG_BLS_PER_ITEM"""
+    bls = {"wave": bls, "batch": bls_batch, "per_item": bls_per_item, "nocache": bls_nocache}[path]
     sks, pks = _committee(bls, 10, 13)
     keys = pks + [C.not_in_g2(), C.IDENTITY_G2, C.negate_g2(pks[0])]
     if path != "nocache":  # the committee in the key cache; the stray keys decoded per call
@@ -123,18 +140,18 @@ def test_verify_many_mixed_batch_matches_oracle(bls, bls_per_item, bls_nocache, 
     assert list(got) == want
     assert want[:12] == [0] * 12 and all(w != 0 for w in want[12:])
     # the wrong-message / wrong-signer items fail only the pairing equation: the batch check rejects
-    assert bls.last_path() == ("per_item" if path == "per_item" else "batch_rejected_then_per_item")
+    assert bls.last_path() == EXPECT_PATH[path][0]
     # the valid certificates alone: the batch check accepts them in one final exponentiation
     got = bls.verify_many(keys, [i[0] for i in items[:12]], [i[1] for i in items[:12]], [i[2] for i in items[:12]])
     assert list(got) == [0] * 12
-    assert bls.last_path() == ("per_item" if path == "per_item" else "batch_accepted")
+    assert bls.last_path() == EXPECT_PATH[path][1]
     # valid certificates beside items that fail before the pairing (decode / group / key errors):
     # those stay out of the batch check, which accepts the rest
     pre = [it for it, w in zip(items, want) if w not in (0, B.ORB_VERIFY_FAIL)]
     sub = items[:12] + pre
     got = bls.verify_many(keys, [i[0] for i in sub], [i[1] for i in sub], [i[2] for i in sub])
     assert list(got) == [B.fast_aggregate_verify(s, [keys[k] for k in ks], m) for s, ks, m in sub]
-    assert bls.last_path() == ("per_item" if path == "per_item" else "batch_accepted")
+    assert bls.last_path() == EXPECT_PATH[path][1]
     # the same keys in another order and with duplicates (cache hits, repeated slots)
     perm = list(range(len(keys)))[::-1]
     keys2 = [keys[p] for p in perm] + [keys[0]]
@@ -194,10 +211,12 @@ def test_key_sums_many_keys(bls):
     assert list(got) == [B.fast_aggregate_verify(s, [keys[k] for k in ks], m) for s, ks, m in items]
 
 
+@pytest.mark.parametrize("engine", ["wave", "batch"])
 @pytest.mark.parametrize("n", [1, 2, 3, 63, 64, 65, 200])
-def test_batch_sizes(bls, n):
+def test_batch_sizes(bls, bls_batch, n, engine):
     """batch tails around the 64-lane wave and the product tree's odd levels; every other item
     corrupted (message flipped), then the same items all valid (one accepted batch check)"""
+    bls = {"wave": bls, "batch": bls_batch}[engine]
     sks, pks = _committee(bls, 4, 15)
     rnd = random.Random(n)
     msgs = [rnd.randbytes(32) for _ in range(n)]
@@ -207,9 +226,12 @@ def test_batch_sizes(bls, n):
     msgs2 = [m + b"x" if b else m for m, b in zip(msgs, bad)]
     got = bls.verify_many(pks, sigs, [[0, 1, 2]] * n, msgs2)
     assert list(got) == [B.ORB_VERIFY_FAIL if b else 0 for b in bad]
-    assert bls.last_path() == ("batch_accepted" if n == 1 else "batch_rejected_then_per_item")
+    if engine == "wave":
+        assert bls.last_path() == "wave"
+    else:
+        assert bls.last_path() == ("batch_accepted" if n == 1 else "batch_rejected_then_per_item")
     got = bls.verify_many(pks, sigs, [[0, 1, 2]] * n, msgs)
-    assert list(got) == [0] * n and bls.last_path() == "batch_accepted"
+    assert list(got) == [0] * n and bls.last_path() == ("wave" if engine == "wave" else "batch_accepted")
 
 
 def test_keycache_register_only(bls):
@@ -261,12 +283,12 @@ def test_keycache_register_only(bls):
     assert bls.cached_keys() == 0
 
 
-@pytest.mark.parametrize("path", ["batch", "per_item"])
-def test_committee_shape_100(bls, bls_per_item, path):
+@pytest.mark.parametrize("path", ["wave", "batch", "per_item"])
+def test_committee_shape_100(bls, bls_batch, bls_per_item, path):
     """the reference's committee shape: a 100-key committee (registered), certificates of 67 and
-    100 signers (the key-sum tree at full depth) mixed with every adversarial category, through the
-    batch check and per item, against the oracle"""
-    bls = {"batch": bls, "per_item": bls_per_item}[path]
+    100 signers (the key-sum tree at full depth) mixed with every adversarial category, on the wave
+    engine, through the batch check and per item, against the oracle"""
+    bls = {"wave": bls, "batch": bls_batch, "per_item": bls_per_item}[path]
     sks, pks = _committee(bls, 100, 31)
     bls.register_keys(pks)
     keys = pks + [C.not_in_g2(), C.IDENTITY_G2, C.negate_g2(pks[5])]
@@ -296,6 +318,6 @@ def test_committee_shape_100(bls, bls_per_item, path):
     want = B.verify_items(keys, [i[0] for i in items], [i[1] for i in items], [i[2] for i in items])
     assert list(got) == want
     assert want[:6] == [0] * 6 and all(w != 0 for w in want[6:])
-    assert bls.last_path() == ("per_item" if path == "per_item" else "batch_rejected_then_per_item")
+    assert bls.last_path() == EXPECT_PATH[path][0]
     got = bls.verify_many(keys, [i[0] for i in items[:6]], [i[1] for i in items[:6]], [i[2] for i in items[:6]])
     assert list(got) == [0] * 6
