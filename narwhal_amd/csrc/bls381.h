@@ -213,6 +213,134 @@ NWV_HD fp fp_inv(const fp& a) {
     const uint32_t e[12] = BLS_E_INV;
     return fp_pow(a, e);
 }
+// ---- variable-time inversion (binary extended Euclid on 32-bit words) -------------------------
+// The inputs of a verification are public, so the inversion need not be constant time: the
+// binary algorithm (u, v) = (a, p) with x1 a^-1-cofactor of u, x2 of v (Hankerson-Menezes-
+// Vanstone Alg. 2.22), with every run of trailing zeros shifted out at once (x <- x 2^-k mod p
+// as (x + m p) / 2^k, m = x (-p^-1) mod 2^k).  x1, x2 stay below 2p.  About 380 rounds of
+// 12-word subtractions and shifts: ~5x faster on one lane than the 381-bit exponentiation.
+constexpr int BW = 12;
+NWV_HD void w_from_fp(uint32_t* o, const fp& a) {  // a canonical, limbs < 2^28
+#pragma unroll
+    for (int k = 0; k < BW; k++) {
+        const int bit = 32 * k, j = bit / 28, sh = bit % 28;
+        uint32_t v = a.l[j] >> sh;
+        if (j + 1 < NL) v |= a.l[j + 1] << (28 - sh);
+        if (sh > 24 && j + 2 < NL) v |= a.l[j + 2] << (56 - sh);
+        o[k] = v;
+    }
+}
+NWV_HD fp fp_from_w(const uint32_t* w) {
+    fp r;
+#pragma unroll
+    for (int j = 0; j < NL; j++) {
+        const int bit = 28 * j, idx = bit >> 5, sh = bit & 31;
+        uint32_t v = idx < BW ? w[idx] >> sh : 0;
+        if (sh > 4 && idx + 1 < BW) v |= w[idx + 1] << (32 - sh);
+        r.l[j] = v & LM;
+    }
+    return r;
+}
+NWV_HD bool w_is_one(const uint32_t* u) {
+    uint32_t o = u[0] ^ 1u;
+#pragma unroll
+    for (int k = 1; k < BW; k++) o |= u[k];
+    return o == 0;
+}
+// u >>= k (0 < k < 32)
+NWV_HD void w_shr(uint32_t* u, int k) {
+#pragma unroll
+    for (int i = 0; i < BW - 1; i++) u[i] = (u[i] >> k) | (u[i + 1] << (32 - k));
+    u[BW - 1] >>= k;
+}
+// x <- x 2^-k mod p (x < 2p on entry and exit, 0 < k < 32)
+NWV_HD void w_half_k(uint32_t* x, int k, const uint32_t* P) {
+    const uint32_t m = (x[0] * BLS_P_NINV32) & ((k == 32 ? 0u : (1u << k)) - 1u);
+    uint64_t c = 0;
+    uint32_t t[BW + 1];
+#pragma unroll
+    for (int i = 0; i < BW; i++) {
+        c += (uint64_t)m * P[i] + x[i];
+        t[i] = (uint32_t)c;
+        c >>= 32;
+    }
+    t[BW] = (uint32_t)c;
+#pragma unroll
+    for (int i = 0; i < BW; i++) x[i] = (t[i] >> k) | (t[i + 1] << (32 - k));
+}
+// a -= b (true when no borrow)
+NWV_HD bool w_sub(uint32_t* a, const uint32_t* b) {
+    uint64_t br = 0;
+#pragma unroll
+    for (int i = 0; i < BW; i++) {
+        const uint64_t d = (uint64_t)a[i] - b[i] - br;
+        a[i] = (uint32_t)d;
+        br = (d >> 32) & 1;
+    }
+    return br == 0;
+}
+NWV_HD void w_add(uint32_t* a, const uint32_t* b) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < BW; i++) {
+        c += (uint64_t)a[i] + b[i];
+        a[i] = (uint32_t)c;
+        c >>= 32;
+    }
+}
+NWV_HD bool w_ge(const uint32_t* a, const uint32_t* b) {
+    for (int i = BW - 1; i >= 0; i--)
+        if (a[i] != b[i]) return a[i] > b[i];
+    return true;
+}
+// x <- x - y mod p for x, y < 2p (result < 2p)
+NWV_HD void w_submod(uint32_t* x, const uint32_t* y, const uint32_t* P2) {
+    if (!w_sub(x, y)) w_add(x, P2);
+}
+NWV_HD int w_ctz(const uint32_t* u) {  // u odd-making shift, capped at 31 per round
+    const uint32_t lo = u[0];
+    return lo ? __builtin_ctz(lo) : 31;
+}
+BLS_NOINLINE fp fp_inv_vt(const fp& a) {
+    const fp ac = fp_canon(a);
+    if (fp_is_zero(ac)) return fp_zero();
+    uint32_t u[BW], v[BW], x1[BW], x2[BW], P[BW], P2[BW];
+    w_from_fp(u, ac);
+    w_from_fp(P, k_p());
+    w_from_fp(v, k_p());
+    fp p2 = k_p2();
+    w_from_fp(P2, p2);
+    for (int i = 0; i < BW; i++) x1[i] = x2[i] = 0;
+    x1[0] = 1;
+    for (;;) {
+        while (!(u[0] & 1)) {
+            const int k = w_ctz(u);
+            w_shr(u, k);
+            w_half_k(x1, k, P);
+        }
+        while (!(v[0] & 1)) {
+            const int k = w_ctz(v);
+            w_shr(v, k);
+            w_half_k(x2, k, P);
+        }
+        if (w_is_one(u) || w_is_one(v)) break;
+        if (w_ge(u, v)) {
+            w_sub(u, v);
+            w_submod(x1, x2, P2);
+        } else {
+            w_sub(v, u);
+            w_submod(x2, x1, P2);
+        }
+    }
+    fp x = fp_from_w(w_is_one(u) ? x1 : x2);  // A^-1 (plain), < 2p
+    fp r3;
+    {
+        const uint32_t c[NL] = BLS_R3;
+        for (int j = 0; j < NL; j++) r3.l[j] = c[j];
+    }
+    return fp_mul(x, r3);  // A^-1 R^3 / R = (a R)^-1 R^2 = a^-1 R: the Montgomery form of a^-1
+}
+
 // sqrt for p = 3 mod 4; false if a is not a square
 NWV_HD bool fp_sqrt(fp& r, const fp& a) {
     const uint32_t e[12] = BLS_E_SQRT;

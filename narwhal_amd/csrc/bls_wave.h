@@ -47,40 +47,68 @@ namespace wave {
 
 constexpr int SW = NL;  // words per slot
 
-// sum of the terms (slot | weight << 12) into 32-bit limb sums
-NWV_HD void acc_terms(const uint32_t* wm, const uint16_t* t, int n, uint32_t* a) {
-    for (int i = 0; i < n; i++) {
-        const uint32_t w = t[i];
-        const uint32_t* x = wm + SW * (w & 0xfffu);
-        const int sh = (int)(w >> 12);
+// A lane's record in registers: REC u16 words (five 16-byte loads).  [0] destination slot, [1]
+// flags (1 product, 2 reduce, 4 A signed, 8 B signed), [2] k+1 of A's 2^k p (0 none), [3] k+1 of
+// B's, then A's positive terms at [4, 4+TMAX), A's negative, B's positive, B's negative, each term
+// slot | weight << 12.  Every term index below is a compile-time constant after unrolling (the
+// per-stage counts only predicate the loop bodies), so the record stays in VGPRs.
+struct Rec {
+    uint32_t w[REC / 2];
+};
+NWV_HD uint32_t rec_u16(const Rec& r, int i) { return (r.w[i >> 1] >> ((i & 1) * 16)) & 0xffffu; }
+NWV_HD Rec load_rec(const uint16_t* p) {
+    Rec r;
+    const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
-        for (int j = 0; j < NL; j++) a[j] += x[j] << sh;
+    for (int k = 0; k < REC / 8; k++) {
+        const uint4 v = q[k];
+        r.w[4 * k] = v.x;
+        r.w[4 * k + 1] = v.y;
+        r.w[4 * k + 2] = v.z;
+        r.w[4 * k + 3] = v.w;
+    }
+    return r;
+}
+
+// the n terms of a section into 32-bit limb sums
+template <int BASE>
+NWV_HD void acc_terms(const uint32_t* wm, const Rec& r, int n, uint32_t* a) {
+#pragma unroll
+    for (int t = 0; t < TMAX; t++) {
+        if (t < n) {
+            const uint32_t w = rec_u16(r, BASE + t);
+            const uint32_t* x = wm + SW * (w & 0xfffu);
+            const int sh = (int)(w >> 12);
+#pragma unroll
+            for (int j = 0; j < NL; j++) a[j] += x[j] << sh;
+        }
     }
 }
 
-// the lane's combination: positive terms + 2^k p - negative terms, one carry pass (signed when
-// the lane has negative terms), normalised limbs
-NWV_HD fp lin_comb(const uint32_t* wm, const uint16_t* tp, int np, const uint16_t* tn, int nn, int k1, bool sgn) {
+// a combination: positive terms + 2^k p - negative terms, one carry pass (signed when the lane
+// has negative terms), normalised limbs
+template <int BASE>
+NWV_HD fp lin_comb(const uint32_t* wm, const Rec& r, int np, int nn, uint32_t k1, bool sgn) {
     uint32_t a[NL], b[NL];
 #pragma unroll
     for (int j = 0; j < NL; j++) a[j] = b[j] = 0;
-    acc_terms(wm, tp, np, a);
-    acc_terms(wm, tn, nn, b);
+    acc_terms<BASE>(wm, r, np, a);
+    acc_terms<BASE + TMAX>(wm, r, nn, b);
     if (k1) {
         const uint32_t* kp = T_KP[k1 - 1];
 #pragma unroll
         for (int j = 0; j < NL; j++) a[j] += kp[j];
     }
-    fp r;
+    fp v;
     uint32_t c = 0;
 #pragma unroll
     for (int j = 0; j < NL - 1; j++) {
         const uint32_t d = a[j] - b[j] + c;
-        r.l[j] = d & LM;
+        v.l[j] = d & LM;
         c = sgn ? (uint32_t)((int32_t)d >> 28) : d >> 28;
     }
-    r.l[NL - 1] = a[NL - 1] - b[NL - 1] + c;
-    return r;
+    v.l[NL - 1] = a[NL - 1] - b[NL - 1] + c;
+    return v;
 }
 
 // x - q p with q = floor(top limb * QM / 2^32) <= x / p: the result is < 1.1 p (< 2p)
@@ -102,20 +130,16 @@ NWV_HD fp quick_reduce(const fp& x) {
     return r;
 }
 
-// lane record: [0] destination slot, [1] flags (1 product, 2 reduce, 4 A signed, 8 B signed),
-// [2] k+1 of A's 2^k p (0 none), [3] k+1 of B's, then A's positive and negative terms, B's
-NWV_HD fp lane_value(const uint32_t* wm, const Stage& h, const uint16_t* rec) {
-    const uint32_t fl = rec[1];
-    const uint16_t* ta = rec + 4;
-    fp r = lin_comb(wm, ta, h.nap, ta + h.nap, h.nan, rec[2], (fl & 4) != 0);
+NWV_HD fp lane_value(const uint32_t* wm, const Stage& h, const Rec& r) {
+    const uint32_t fl = rec_u16(r, 1);
+    fp v = lin_comb<4>(wm, r, h.nap, h.nan, rec_u16(r, 2), (fl & 4) != 0);
     if (fl & 1) {
-        const uint16_t* tb = ta + h.nap + h.nan;
-        const fp b = lin_comb(wm, tb, h.nbp, tb + h.nbp, h.nbn, rec[3], (fl & 8) != 0);
-        r = fp_mul(r, b);
+        const fp b = lin_comb<4 + 2 * TMAX>(wm, r, h.nbp, h.nbn, rec_u16(r, 3), (fl & 8) != 0);
+        v = fp_mul(v, b);
     } else if (fl & 2) {
-        r = quick_reduce(r);
+        v = quick_reduce(v);
     }
-    return r;
+    return v;
 }
 
 #ifdef BLS_WAVE_DEV
@@ -129,19 +153,44 @@ struct Wave {
     uint32_t* wm;
     int lane;
     __device__ void sync() const { wsync(); }
+    // the program's stages; each lane's record for the next stage is loaded while this one runs
     __device__ void run(Prog p) const {
+        const int end = p.first + p.n;
+        Stage h = T_STAGES[p.first];
+        Rec cur = load_rec(T_DATA + h.off + (uint32_t)min(lane, (int)h.nl) * REC);
 #pragma unroll 1
-        for (int s = p.first; s < p.first + p.n; s++) {
-            const Stage h = T_STAGES[s];
+        for (int s = p.first; s < end; s++) {
+            Stage hn = h;
+            Rec nxt = cur;
+            if (s + 1 < end) {
+                hn = T_STAGES[s + 1];
+                nxt = load_rec(T_DATA + hn.off + (uint32_t)min(lane, (int)hn.nl) * REC);
+            }
             if (lane < h.nl) {
-                const uint16_t* rec = T_DATA + h.off + (uint32_t)lane * h.rec_len;
-                const uint32_t dst = rec[0];
-                const fp v = lane_value(wm, h, rec);
+                const uint32_t dst = rec_u16(cur, 0);
+                const fp v = lane_value(wm, h, cur);
 #pragma unroll
                 for (int j = 0; j < NL; j++) wm[SW * dst + j] = v.l[j];
             }
             wsync();
+            h = hn;
+            cur = nxt;
         }
+    }
+    // up to 128 words of global memory fetched into registers ahead of use (a prefetch), and
+    // written into slots later
+    struct Pre {
+        uint32_t a, b;
+    };
+    __device__ Pre fetch(const uint32_t* src, int nw) const {
+        Pre p;
+        p.a = lane < nw ? src[lane] : 0u;
+        p.b = lane + 64 < nw ? src[lane + 64] : 0u;
+        return p;
+    }
+    __device__ void put_pre(int slot, const Pre& p, int nw) const {
+        if (lane < nw) wm[SW * slot + lane] = p.a;
+        if (lane + 64 < nw) wm[SW * slot + lane + 64] = p.b;
     }
     // n consecutive slots from 14 n words (global or LDS), lane-parallel
     __device__ void put_words(int slot, const uint32_t* src, int n) const {
@@ -194,13 +243,20 @@ struct Wave {
         for (int s = p.first; s < p.first + p.n; s++) {
             const Stage h = T_STAGES[s];
             for (int l = 0; l < h.nl; l++) {  // every lane's reads ...
-                const uint16_t* rec = T_DATA + h.off + (uint32_t)l * h.rec_len;
-                dst[l] = rec[0];
-                out[l] = lane_value(wm, h, rec);
+                const Rec r = load_rec(T_DATA + h.off + (uint32_t)l * REC);
+                dst[l] = rec_u16(r, 0);
+                out[l] = lane_value(wm, h, r);
             }
             for (int l = 0; l < h.nl; l++)  // ... then its writes
                 for (int j = 0; j < NL; j++) wm[SW * dst[l] + j] = out[l].l[j];
         }
+    }
+    struct Pre {
+        const uint32_t* src;
+    };
+    Pre fetch(const uint32_t* src, int) const { return Pre{src}; }
+    void put_pre(int slot, const Pre& p, int nw) const {
+        for (int w = 0; w < nw; w++) wm[SW * slot + w] = p.src[w];
     }
     void put_words(int slot, const uint32_t* src, int n) const {
         for (int w = 0; w < SW * n; w++) wm[SW * slot + w] = src[w];
@@ -269,7 +325,7 @@ template <class W>
 NWV_HD void final_exp(const W& w) {
     w.run(P_INV_A);
     const fp n = w.get(REG_N);
-    w.put_fp(REG_N + 1, fp_inv(n));
+    w.put_fp(REG_N + 1, fp_inv_vt(n));
     w.sync();
     w.run(P_INV_B);
     w.run(P_EASY1);
@@ -308,11 +364,18 @@ NWV_HD bool pairing_check(const W& w, const uint32_t* qlines) {
     w.put_words(REG_TB, w.wm + SW * REG_QB, 6);
     w.sync();
     const char* steps = BLS_WAVE_STEPS_STR;
+    constexpr int LW = 6 * SW;  // words of a step's line
+    auto la = w.fetch(&T_G2_LINES[0][0][0], LW);
+    auto lb = w.fetch(qlines ? qlines : &T_G2_LINES[0][0][0], qlines ? LW : 0);
 #pragma unroll 1
     for (int k = 0; k < NSTEPS; k++) {
-        w.put_words(REG_LA, &T_G2_LINES[k][0][0], 6);
-        if (qlines) w.put_words(REG_LB, qlines + (size_t)k * 6 * SW, 6);
+        w.put_pre(REG_LA, la, LW);
+        if (qlines) w.put_pre(REG_LB, lb, LW);
         w.sync();
+        if (k + 1 < NSTEPS) {  // the next step's lines load while this step runs
+            la = w.fetch(&T_G2_LINES[k + 1][0][0], LW);
+            if (qlines) lb = w.fetch(qlines + (size_t)(k + 1) * LW, LW);
+        }
         const bool add = steps[k] == 'a';
         w.run(qlines ? (add ? P_ML_ADD_FIXED : P_ML_DBL_FIXED) : (add ? P_ML_ADD_STEP : P_ML_DBL_STEP));
     }

@@ -278,5 +278,12 @@ int bh_w2_fast_aggregate_verify(const uint8_t* sig, size_t n_pks, const uint8_t*
     return w_pairing_check_h(w, srec, hrec, arec, nullptr) ? ST_OK : ST_VERIFY_FAIL;
 }
 
+// the variable-time inversion of the wave engine's final exponentiation (plain big-endian in / out)
+void bh_fp_inv_vt(const uint8_t* a, uint8_t* out) {
+    fp x;
+    be_to_mont(x, a);
+    mont_to_be(out, fp_inv_vt(x));
+}
+
 }  // extern "C"
 

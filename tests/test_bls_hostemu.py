@@ -39,6 +39,7 @@ def emu():
     L.bh_w_hash_to_g1.argtypes = [c, sz, c, sz, vp]
     L.bh_w_sig_status.argtypes = [c]
     L.bh_w2_fast_aggregate_verify.argtypes = [c, sz, c, c, sz, c, sz]
+    L.bh_fp_inv_vt.argtypes = [c, vp]
     return L
 
 
@@ -255,3 +256,16 @@ def test_wave_pipeline_fast_aggregate_verify(emu):
                          (C.IDENTITY_G1, pks, m)]:
         got = emu.bh_w2_fast_aggregate_verify(sig, len(ks), b"".join(ks), msg, len(msg), B.DST_NUL, len(B.DST_NUL))
         assert got == B.fast_aggregate_verify(sig, ks, msg)
+
+
+def test_fp_inv_variable_time(emu):
+    """the binary extended-Euclid inversion (variable time: public inputs) against a^(p-2)"""
+    rnd = random.Random(56)
+    p = C.p
+    vals = [1, 2, p - 1, p - 2, (p + 1) // 2, 1 << 380, (1 << 381) % p] + [rnd.randrange(1, p) for _ in range(200)]
+    o = _buf(48)
+    for a in vals:
+        emu.bh_fp_inv_vt(a.to_bytes(48, "big"), o)
+        assert int.from_bytes(o.raw, "big") == pow(a, p - 2, p), hex(a)
+    emu.bh_fp_inv_vt(bytes(48), o)
+    assert o.raw == bytes(48)

@@ -41,6 +41,7 @@ X_ABS = 0xd201000000010000
 # pos + (2^k p) - neg lies in (-2^31, 2^31) (signed 32-bit sums); without negative terms the
 # positive weights sum to <= 16 (unsigned sums < 2^32); at most TMAX terms per side
 POS_UNITS, NEG_UNITS, POS_ONLY_UNITS, TMAX = 7, 8, 16, 8
+REC = 4 + 4 * TMAX + 4  # lane record words (u16), padded to a multiple of 8 (16-byte loads)
 LANES = 64
 REDUCED = 2 * P  # bound after the quick reduction (exactly < 1.1 p, see reduce_bound_check)
 
@@ -1400,8 +1401,9 @@ def emit(compiled, path):
             nan = max(len(r["a"][1]) for r in st)
             nbp = max((len(r["b"][0]) for r in st if r["mul"]), default=0)
             nbn = max((len(r["b"][1]) for r in st if r["mul"]), default=0)
-            rec_len = 4 + nap + nan + nbp + nbn
-            rec_len += rec_len & 1  # u32-aligned records
+            # fixed layout, REC words per lane (five 16-byte loads): header, then A+ A- B+ B- at
+            # TMAX-word sections, so every term has a compile-time position in the lane's record
+            rec_len = REC
             off = len(data)
             anymul = any(r["mul"] for r in st)
             anyred = any(r["reduce"] for r in st)
@@ -1410,14 +1412,12 @@ def emit(compiled, path):
                        (4 if r["a"][1] else 0) | (8 if (r["b"] and r["b"][1]) else 0),
                        r["ka"] + 1, r["kb"] + 1]
 
-                def terms(lst, n):
+                def terms(lst):
                     out = [sl | (sh << 12) for sl, sh in lst]
-                    return out + [0] * (n - len(out))
-                rec += terms(r["a"][0], nap) + terms(r["a"][1], nan)
-                if r["mul"]:
-                    rec += terms(r["b"][0], nbp) + terms(r["b"][1], nbn)
-                else:
-                    rec += [0] * (nbp + nbn)
+                    assert len(out) <= TMAX
+                    return out + [0] * (TMAX - len(out))
+                rec += terms(r["a"][0]) + terms(r["a"][1])
+                rec += terms(r["b"][0]) + terms(r["b"][1]) if r["mul"] else [0] * (2 * TMAX)
                 rec += [0] * (rec_len - len(rec))
                 assert all(0 <= x < 65536 for x in rec)
                 data += rec
@@ -1440,6 +1440,8 @@ def emit(compiled, path):
     L.append(f"constexpr int NSTAGES = {len(stages)};")
     L.append(f"constexpr int NSTEPS = {len(la)};  // Miller-loop steps over |x|")
     L.append(f"constexpr uint32_t QM = {QM}u;  // floor(2^32 / (p_13 + 1)), the quick reduction's multiplier")
+    L.append(f"constexpr int REC = {REC};  // u16 words per lane record: header 4, then A+ A- B+ B- x {TMAX}")
+    L.append(f"constexpr int TMAX = {TMAX};")
     for name, first, n in progs:
         L.append(f"constexpr Prog P_{name.upper()} = {{{first}, {n}}};")
     L.append("#define BLS_WAVE_STEPS_STR \"" + "".join(miller_steps()) + "\"")
@@ -1455,7 +1457,8 @@ def emit(compiled, path):
     for st in stages:
         L.append("    {" + ", ".join(str(x) for x in st) + "},")
     L.append("};")
-    L.append(f"BLS_WAVE_TABLE uint16_t T_DATA[{len(data)}] = {{")
+    data += [0] * (2 * REC)  # the last lane's record may be read past its end by a prefetch
+    L.append(f"BLS_WAVE_TABLE uint16_t T_DATA[{len(data)}] __attribute__((aligned(16))) = {{")
     for k in range(0, len(data), 24):
         L.append("    " + ", ".join(str(x) for x in data[k:k + 24]) + ",")
     L.append("};")
