@@ -350,30 +350,34 @@ NWV_HD bool w_g1_in_group(const W& w, const uint32_t* rec) {
     return fp_is_zero(w.get(REG_S + 2)) && fp_is_zero(w.get(REG_S + 3));
 }
 
-// w_pairing_check with H in homogeneous coordinates (w_hash_to_g1's record)
+// the general form: H as an affine record (G1_REC_WORDS) or w_hash_to_g1's homogeneous one
+// (h_hom), apk as an affine G2 record or a Jacobian one (X, Y, Z; q_jac: k_blsw_apk's)
 template <class W>
-NWV_HD bool w_pairing_check_h(const W& w, const uint32_t* sig_rec, const uint32_t* hh_rec, const uint32_t* apk_rec,
-                              const uint32_t* qlines) {
+NWV_HD bool w_pairing_check_g(const W& w, const uint32_t* sig_rec, const uint32_t* h_rec, bool h_hom,
+                              const uint32_t* q_rec, bool q_jac, const uint32_t* qlines) {
     using namespace wave;
     init_slots(w);
     w.zero(REG_PA, 2);
+    w.zero(REG_PB, 3);
     w.zero(REG_QB, 6);
     w.sync();
     if (!sig_rec[2 * NL]) {
         w.put_words(REG_PA, sig_rec, 1);
         w.put_fp(REG_PA + 1, fp_neg(ld_fp(sig_rec + NL)));
     }
-    if (hh_rec[3 * NL]) {  // H = O (never from a hash in practice): only the lines' l0 remain
-        w.zero(REG_PB, 2);
-        w.sync();
-        w.put_fp(REG_PB + 2, k_one());
-    } else {
-        w.put_words(REG_PB, hh_rec, 3);
-    }
-    w.put_words(REG_QB, apk_rec, 4);
-    w.put_fp(REG_QB + 4, k_one());
+    const bool h_inf = h_rec[(h_hom ? 3 : 2) * NL] != 0;
+    if (!h_inf) w.put_words(REG_PB, h_rec, h_hom ? 3 : 2);  // H = O (never from a hash): only l0 remain
+    if (h_inf || !h_hom) w.put_fp(REG_PB + 2, k_one());
+    w.put_words(REG_QB, q_rec, q_jac ? 6 : 4);
+    if (!q_jac) w.put_fp(REG_QB + 4, k_one());
     w.sync();
     return wave::pairing_check(w, qlines);
+}
+// w_pairing_check with H in homogeneous coordinates (w_hash_to_g1's record)
+template <class W>
+NWV_HD bool w_pairing_check_h(const W& w, const uint32_t* sig_rec, const uint32_t* hh_rec, const uint32_t* apk_rec,
+                              const uint32_t* qlines) {
+    return w_pairing_check_g(w, sig_rec, hh_rec, true, apk_rec, false, qlines);
 }
 
 }  // namespace bls

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <condition_variable>
@@ -373,18 +374,85 @@ __global__ __launch_bounds__(64) void k_blsw_sub(uint32_t n, const uint32_t* rec
 }
 // e(-sig, g2) e(H, apk) == 1 for every item whose signature decoded and whose keys are valid
 // (run beside the signature's G1 check: the status join puts that check first)
+// H: homogeneous records (k_blsw_h2c) or affine ones (k_bls_h2c_g, h_hom = 0); apk: Jacobian
+// records (k_blsw_apk)
 __global__ __launch_bounds__(64) void k_blsw_pair(uint32_t n, const uint32_t* srec, const int32_t* st_dec,
-                                                  const uint32_t* hrec, const uint32_t* arec, const int32_t* st_apk,
-                                                  int32_t* st_pair) {
+                                                  const uint32_t* hrec, int h_hom, const uint32_t* arec,
+                                                  const int32_t* st_apk, int32_t* st_pair) {
     BLSW_IDX();
     int32_t s = ST_VERIFY_FAIL;
     if (st_dec[i] == ST_OK && st_apk[i] == ST_OK)
-        s = w_pairing_check_h(w, srec + (size_t)G1_REC_WORDS * i, hrec + (size_t)G1H_REC_WORDS * i,
-                              arec + (size_t)G2_REC_WORDS * i, nullptr)
+        s = w_pairing_check_g(w, srec + (size_t)G1_REC_WORDS * i,
+                              hrec + (size_t)(h_hom ? G1H_REC_WORDS : G1_REC_WORDS) * i, h_hom != 0,
+                              arec + (size_t)G2J_WORDS * i, true, nullptr)
                 ? ST_OK
                 : ST_VERIFY_FAIL;
     if (threadIdx.x == 0) st_pair[i] = s;
 }
+// the key sum of item i on a wave: lane j adds the item's keys j, j + 64, ... (Jacobian, jac_add:
+// exact in every case), then a six-level tree through LDS.  The status is that of the item's first
+// bad key in list order (else AGGR_MISMATCH for an empty list, PK_INFINITY for an identity sum).
+// The sum stays Jacobian (G2J_WORDS record: the Miller-loop programs take a Jacobian Q), so there
+// is no inversion; a one-key item copies its validated record with Z = 1.
+__global__ __launch_bounds__(64) void k_blsw_apk(uint32_t n, KeyTab kt, const uint32_t* pk_off, const uint32_t* pk_cnt,
+                                                 const uint32_t* pk_idx, uint32_t* rec, int32_t* st_apk) {
+    __shared__ uint32_t xa[32 * G2J_WORDS];
+    const uint32_t i = blockIdx.x;
+    if (i >= n) return;
+    const int lane = (int)threadIdx.x;
+    const uint32_t cnt = pk_cnt[i];
+    const uint32_t* idx = pk_idx + pk_off[i];
+    uint32_t* out = rec + (size_t)G2J_WORDS * i;
+    if (cnt == 1) {
+        const uint32_t k = idx[0];
+        const int32_t ks = key_st(kt, k);
+        const uint32_t* kr = key_rec(kt, k);
+        const fp one = k_one();
+        for (int wd = lane; wd < G2J_WORDS; wd += 64) {
+            uint32_t v = 0;
+            if (wd < 4 * NL) v = ks == ST_OK ? kr[wd] : 0u;
+            else if (wd < 5 * NL) v = one.l[wd - 4 * NL];
+            else if (wd == 6 * NL) v = ks == ST_OK ? 0u : 1u;
+            out[wd] = v;
+        }
+        if (lane == 0) st_apk[i] = ks;
+        return;
+    }
+    jac<fp2> acc;
+    acc.inf = true;
+    acc.x = acc.y = acc.z = f2_zero();
+    uint32_t first_bad = 0xffffffffu;
+    for (uint32_t j = (uint32_t)lane; j < cnt; j += 64) {
+        const uint32_t k = idx[j];
+        if (key_st(kt, k) != ST_OK) {
+            first_bad = j;
+            break;
+        }
+        fp2 x, y;
+        ld_g2(key_rec(kt, k), x, y);
+        acc = jac_add(acc, jac_from_affine(x, y));
+    }
+    for (int m = 32; m >= 1; m >>= 1) first_bad = min(first_bad, (uint32_t)__shfl_xor((int)first_bad, m));
+#pragma unroll 1
+    for (int h = 32; h >= 1; h >>= 1) {
+        __syncthreads();
+        if (lane >= h && lane < 2 * h) st_g2j(xa + (lane - h) * G2J_WORDS, acc);
+        __syncthreads();
+        if (lane < h) acc = jac_add(acc, ld_g2j(xa + lane * G2J_WORDS));
+    }
+    if (lane != 0) return;
+    int32_t status = ST_OK;
+    if (cnt == 0) status = ST_AGGR_MISMATCH;
+    else if (first_bad != 0xffffffffu) status = key_st(kt, idx[first_bad]);
+    else if (acc.inf) status = ST_PK_INFINITY;
+    if (status != ST_OK) {
+        acc.inf = true;
+        acc.x = acc.y = acc.z = f2_zero();
+    }
+    st_g2j(out, acc);
+    st_apk[i] = status;
+}
+
 // the oracle's order: signature decode, its G1 check, the keys, the pairing equation
 __global__ __launch_bounds__(BLS_LANES) void k_blsw_status(uint32_t n, const int32_t* dec, const int32_t* sub,
                                                            const int32_t* apk, const int32_t* pair, int32_t* st) {
@@ -663,6 +731,13 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     const bool group_item = (d.flags & NWV_FLAG_BLS_PER_ITEM) != 0;
     const bool batch = !group_item && (d.flags & NWV_FLAG_BLS_BATCH) != 0;
     const bool wavem = !group_item && !batch;
+    // wave-per-item hashing and G1 checks while the call has fewer items than the chip has SIMDs
+    // (latency); above that, one item per lane keeps every lane busy (throughput)
+    static const size_t wave_max = [] {
+        const char* e = std::getenv("NWV_BLS_WAVE_MAX");
+        return e ? (size_t)std::strtoul(e, nullptr, 10) : (size_t)1024;
+    }();
+    const bool wave_small = wavem && n <= wave_max;
     int rc;
     // the call's key table: cache slots (lookups only) or scratch entries KC_CAP + j
     std::shared_lock<std::shared_mutex> kc_hold(d.kc.mu);  // records stay put while our kernels read them
@@ -721,7 +796,8 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
                  w_prec = al256(w_jrec + 4 * G1J_REC_WORDS * (batch ? n : 0)),
                  w_hh = al256(w_prec + 4 * G1J_REC_WORDS * (batch ? n + 1 : 0) + 4),
                  w_sdec = al256(w_hh + 4 * G1H_REC_WORDS * (wavem ? n : 0)), w_ssub = al256(w_sdec + 4 * n),
-                 w_spair = al256(w_ssub + 4 * n), w_end = w_spair + 4 * n + 4;
+                 w_spair = al256(w_ssub + 4 * n), w_aj = al256(w_spair + 4 * n + 4),
+                 w_end = w_aj + 4 * G2J_WORDS * (wavem ? n : 0) + 4;
     if ((rc = L.work.ensure(w_end))) return rc;
     uint8_t* in = static_cast<uint8_t*>(L.in.p);
     uint8_t* w = static_cast<uint8_t*>(L.work.p);
@@ -742,6 +818,7 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     auto* sdec = reinterpret_cast<int32_t*>(w + w_sdec);
     auto* ssub = reinterpret_cast<int32_t*>(w + w_ssub);
     auto* spair = reinterpret_cast<int32_t*>(w + w_spair);
+    auto* ajrec = reinterpret_cast<uint32_t*>(w + w_aj);
     hipStream_t s0 = L.stream, s1 = L.side[0], s2 = L.side[1], s3 = L.side[2];
     // stage times of the completed call, its path and key counts -> the device's "last call"
     auto finish = [&](int path_done) -> int {
@@ -770,14 +847,19 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
                            reinterpret_cast<const uint32_t*>(in + o_kslot), const_cast<uint32_t*>(kt.rs),
                            const_cast<int32_t*>(kt.ss));
     BLS_HIP(hipEventRecord(L.ev[1], s1));
-    hipLaunchKernelGGL(k_bls_apk_g, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s1, (uint32_t)n, kt,
-                       reinterpret_cast<const uint32_t*>(in + o_off), reinterpret_cast<const uint32_t*>(in + o_cnt),
-                       reinterpret_cast<const uint32_t*>(in + o_idx), arec, sapk);
+    if (wavem)
+        hipLaunchKernelGGL(k_blsw_apk, dim3((unsigned)n), dim3(64), 0, s1, (uint32_t)n, kt,
+                           reinterpret_cast<const uint32_t*>(in + o_off), reinterpret_cast<const uint32_t*>(in + o_cnt),
+                           reinterpret_cast<const uint32_t*>(in + o_idx), ajrec, sapk);
+    else
+        hipLaunchKernelGGL(k_bls_apk_g, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s1, (uint32_t)n, kt,
+                           reinterpret_cast<const uint32_t*>(in + o_off), reinterpret_cast<const uint32_t*>(in + o_cnt),
+                           reinterpret_cast<const uint32_t*>(in + o_idx), arec, sapk);
     BLS_HIP(hipEventRecord(L.ev[2], s1));
     BLS_HIP(hipEventRecord(L.ev[10], s1));
     // side 1: hash to G1 (every item: the statuses are not known yet)
     BLS_HIP(hipEventRecord(L.ev[5], s2));
-    if (wavem)
+    if (wave_small)
         hipLaunchKernelGGL(k_blsw_h2c, dim3((unsigned)n), dim3(64), 0, s2, (uint32_t)n, in + o_msg,
                            reinterpret_cast<const uint64_t*>(in + o_moff),
                            reinterpret_cast<const uint32_t*>(in + o_mlen), in + o_dst, (uint32_t)dl, hh);
@@ -790,21 +872,30 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     if (wavem) {
         // main: signature decode; side 2: its G1 check; main: every item's pairing check beside
         // it, then the statuses joined in the oracle's order
+        // (large calls: the one-lane-per-item decode + G1 check of the group path, which keeps
+        // every lane busy, and an all-Ok subgroup column)
         BLS_HIP(hipEventRecord(L.ev[3], s0));
-        hipLaunchKernelGGL(k_blsw_sigdec, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, in + o_sigs, srec,
-                           sdec);
-        BLS_HIP(hipEventRecord(L.ev[12], s0));
-        BLS_HIP(hipStreamWaitEvent(s3, L.ev[12], 0));
-        hipLaunchKernelGGL(k_blsw_sub, dim3((unsigned)n), dim3(64), 0, s3, (uint32_t)n, (const uint32_t*)srec,
-                           (const int32_t*)sdec, ssub);
-        BLS_HIP(hipEventRecord(L.ev[4], s3));
-        BLS_HIP(hipEventRecord(L.ev[13], s3));
+        if (wave_small) {
+            hipLaunchKernelGGL(k_blsw_sigdec, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, in + o_sigs, srec,
+                               sdec);
+            BLS_HIP(hipEventRecord(L.ev[12], s0));
+            BLS_HIP(hipStreamWaitEvent(s3, L.ev[12], 0));
+            hipLaunchKernelGGL(k_blsw_sub, dim3((unsigned)n), dim3(64), 0, s3, (uint32_t)n, (const uint32_t*)srec,
+                               (const int32_t*)sdec, ssub);
+            BLS_HIP(hipEventRecord(L.ev[4], s3));
+        } else {
+            hipLaunchKernelGGL(k_bls_sigs, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, in + o_sigs, srec,
+                               sdec);
+            BLS_HIP(hipMemsetAsync(ssub, 0, 4 * n, s0));
+            BLS_HIP(hipEventRecord(L.ev[4], s0));
+        }
+        BLS_HIP(hipEventRecord(L.ev[13], wave_small ? s3 : s0));
         BLS_HIP(hipStreamWaitEvent(s0, L.ev[10], 0));
         BLS_HIP(hipStreamWaitEvent(s0, L.ev[11], 0));
         BLS_HIP(hipEventRecord(L.ev[7], s0));
         hipLaunchKernelGGL(k_blsw_pair, dim3((unsigned)n), dim3(64), 0, s0, (uint32_t)n, (const uint32_t*)srec,
-                           (const int32_t*)sdec, (const uint32_t*)hh, (const uint32_t*)arec, (const int32_t*)sapk,
-                           spair);
+                           (const int32_t*)sdec, wave_small ? (const uint32_t*)hh : (const uint32_t*)hrec,
+                           wave_small ? 1 : 0, (const uint32_t*)ajrec, (const int32_t*)sapk, spair);
         BLS_HIP(hipEventRecord(L.ev[8], s0));
         BLS_HIP(hipStreamWaitEvent(s0, L.ev[13], 0));
         hipLaunchKernelGGL(k_blsw_status, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n,
