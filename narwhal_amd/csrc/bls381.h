@@ -213,12 +213,17 @@ NWV_HD fp fp_inv(const fp& a) {
     const uint32_t e[12] = BLS_E_INV;
     return fp_pow(a, e);
 }
-// ---- variable-time inversion (binary extended Euclid on 32-bit words) -------------------------
-// The inputs of a verification are public, so the inversion need not be constant time: the
-// binary algorithm (u, v) = (a, p) with x1 a^-1-cofactor of u, x2 of v (Hankerson-Menezes-
-// Vanstone Alg. 2.22), with every run of trailing zeros shifted out at once (x <- x 2^-k mod p
-// as (x + m p) / 2^k, m = x (-p^-1) mod 2^k).  x1, x2 stay below 2p.  About 380 rounds of
-// 12-word subtractions and shifts: ~5x faster on one lane than the 381-bit exponentiation.
+// ---- variable-time inversion: batched binary GCD (Pornin, eprint 2020/972) -------------------
+// The inputs of a verification are public, so the inversion need not be constant time.  Binary
+// extended Euclid with the invariants a = u y, b = v y (mod p), started at (a, b) = (y, p),
+// (u, v) = (1, 0): while a != 0, an odd a below b swaps with b, then a -= b, and a, u halve.
+// Thirty such steps run at a time on 62-bit approximations of a and b (each one's low 30 bits and
+// its top 32 bits at the larger length) collecting a matrix [f0 g0; f1 g1], |entries| <= 2^30; the
+// matrix then updates the 384-bit values once: (a, b) <- M (a, b) / 2^30 (exact; a negative
+// result is negated with its row) and (u, v) <- M (u, v) / 2^30 mod p (Montgomery halving by
+// 2^30).  About 26 batches for a 381-bit y (at most 2 len - 1 = 761 steps); when a reaches 0,
+// b = 1 and v = y^-1.  On the device the values are wave-uniform, so the steps run on the scalar
+// unit.
 constexpr int BW = 12;
 NWV_HD void w_from_fp(uint32_t* o, const fp& a) {  // a canonical, limbs < 2^28
 #pragma unroll
@@ -241,104 +246,153 @@ NWV_HD fp fp_from_w(const uint32_t* w) {
     }
     return r;
 }
-NWV_HD bool w_is_one(const uint32_t* u) {
-    uint32_t o = u[0] ^ 1u;
-#pragma unroll
-    for (int k = 1; k < BW; k++) o |= u[k];
-    return o == 0;
+NWV_HD uint32_t w_uni(uint32_t x) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_amdgcn_readfirstlane(x);
+#else
+    return x;
+#endif
 }
-// u >>= k (0 < k < 32)
-NWV_HD void w_shr(uint32_t* u, int k) {
-#pragma unroll
-    for (int i = 0; i < BW - 1; i++) u[i] = (u[i] >> k) | (u[i + 1] << (32 - k));
-    u[BW - 1] >>= k;
+NWV_HD int w_bitlen(const uint32_t* a) {
+    for (int i = BW - 1; i >= 0; i--)
+        if (a[i]) return 32 * i + 32 - __builtin_clz(a[i]);
+    return 0;
 }
-// x <- x 2^-k mod p (x < 2p on entry and exit, 0 < k < 32)
-NWV_HD void w_half_k(uint32_t* x, int k, const uint32_t* P) {
-    const uint32_t m = (x[0] * BLS_P_NINV32) & ((k == 32 ? 0u : (1u << k)) - 1u);
-    uint64_t c = 0;
-    uint32_t t[BW + 1];
-#pragma unroll
+// bits [lo, lo + 32) of a (lo >= 0)
+NWV_HD uint32_t w_bits32(const uint32_t* a, int lo) {
+    const int i = lo >> 5, sh = lo & 31;
+    const uint32_t x = i < BW ? a[i] : 0u, y = i + 1 < BW ? a[i + 1] : 0u;
+    return sh ? (x >> sh) | (y << (32 - sh)) : x;
+}
+// r = (f a + g b) as a 13-word two's complement number (|f|, |g| <= 2^30, a, b < 2^384)
+NWV_HD void w_lin2(uint32_t* r, int64_t f, const uint32_t* a, int64_t g, const uint32_t* b) {
+    int64_t c = 0;
     for (int i = 0; i < BW; i++) {
-        c += (uint64_t)m * P[i] + x[i];
+        c += f * (int64_t)a[i] + g * (int64_t)b[i];
+        r[i] = (uint32_t)c;
+        c >>= 32;  // arithmetic
+    }
+    r[BW] = (uint32_t)c;
+}
+// x (13 words, two's complement) >> 30 into 12 words; returns true if x was negative (then
+// the result holds |x| >> 30: the caller negates first)
+NWV_HD bool w_neg13(uint32_t* x) {
+    if ((int32_t)x[BW] >= 0) return false;
+    uint64_t c = 1;
+    for (int i = 0; i <= BW; i++) {
+        c += (uint32_t)~x[i];
+        x[i] = (uint32_t)c;
+        c >>= 32;
+    }
+    return true;
+}
+NWV_HD void w_shr30(uint32_t* o, const uint32_t* x) {
+    for (int i = 0; i < BW; i++) o[i] = (x[i] >> 30) | (x[i + 1] << 2);
+}
+// o += s P (s = +1 or -1; 12 words, two's complement wrap)
+NWV_HD void w_addp(uint32_t* o, const uint32_t* P, int64_t s) {
+    int64_t c = 0;
+    for (int i = 0; i < BW; i++) {
+        c += (int64_t)o[i] + s * (int64_t)P[i];
+        o[i] = (uint32_t)c;
+        c >>= 32;
+    }
+}
+NWV_HD bool w_lt(const uint32_t* a, const uint32_t* b) {
+    for (int i = BW - 1; i >= 0; i--)
+        if (a[i] != b[i]) return a[i] < b[i];
+    return false;
+}
+// (f u + g v) / 2^30 mod p for u, v < p: the signed sum plus m p with m = sum (-p^-1) mod 2^30
+// is divisible by 2^30; the quotient V has |V| < 3p (fits 12 words as two's complement) and is
+// brought into [0, p)
+NWV_HD void w_lin2_modp(uint32_t* o, int64_t f, const uint32_t* u, int64_t g, const uint32_t* v, const uint32_t* P) {
+    uint32_t t[BW + 1];
+    w_lin2(t, f, u, g, v);
+    const uint32_t m = (t[0] * BLS_P_NINV32) & ((1u << 30) - 1u);
+    int64_t c = 0;
+    for (int i = 0; i < BW; i++) {
+        c += (int64_t)t[i] + (int64_t)m * P[i];
         t[i] = (uint32_t)c;
         c >>= 32;
     }
-    t[BW] = (uint32_t)c;
-#pragma unroll
-    for (int i = 0; i < BW; i++) x[i] = (t[i] >> k) | (t[i + 1] << (32 - k));
+    t[BW] = (uint32_t)((int64_t)(int32_t)t[BW] + c);
+    w_shr30(o, t);
+    while ((int32_t)o[BW - 1] < 0) w_addp(o, P, 1);
+    while (!w_lt(o, P)) w_addp(o, P, -1);
 }
-// a -= b (true when no borrow)
-NWV_HD bool w_sub(uint32_t* a, const uint32_t* b) {
-    uint64_t br = 0;
-#pragma unroll
-    for (int i = 0; i < BW; i++) {
-        const uint64_t d = (uint64_t)a[i] - b[i] - br;
-        a[i] = (uint32_t)d;
-        br = (d >> 32) & 1;
-    }
-    return br == 0;
+NWV_HD bool w_is_zero(const uint32_t* a) {
+    uint32_t o = 0;
+    for (int i = 0; i < BW; i++) o |= a[i];
+    return o == 0;
 }
-NWV_HD void w_add(uint32_t* a, const uint32_t* b) {
-    uint64_t c = 0;
-#pragma unroll
-    for (int i = 0; i < BW; i++) {
-        c += (uint64_t)a[i] + b[i];
-        a[i] = (uint32_t)c;
-        c >>= 32;
-    }
-}
-NWV_HD bool w_ge(const uint32_t* a, const uint32_t* b) {
-    for (int i = BW - 1; i >= 0; i--)
-        if (a[i] != b[i]) return a[i] > b[i];
-    return true;
-}
-// x <- x - y mod p for x, y < 2p (result < 2p)
-NWV_HD void w_submod(uint32_t* x, const uint32_t* y, const uint32_t* P2) {
-    if (!w_sub(x, y)) w_add(x, P2);
-}
-NWV_HD int w_ctz(const uint32_t* u) {  // u odd-making shift, capped at 31 per round
-    const uint32_t lo = u[0];
-    return lo ? __builtin_ctz(lo) : 31;
-}
-BLS_NOINLINE fp fp_inv_vt(const fp& a) {
-    const fp ac = fp_canon(a);
-    if (fp_is_zero(ac)) return fp_zero();
-    uint32_t u[BW], v[BW], x1[BW], x2[BW], P[BW], P2[BW];
-    w_from_fp(u, ac);
+BLS_NOINLINE fp fp_inv_vt(const fp& x) {
+    const fp xc = fp_canon(x);
+    if (fp_is_zero(xc)) return fp_zero();
+    uint32_t a[BW], b[BW], u[BW], v[BW], P[BW];
+    w_from_fp(a, xc);
     w_from_fp(P, k_p());
-    w_from_fp(v, k_p());
-    fp p2 = k_p2();
-    w_from_fp(P2, p2);
-    for (int i = 0; i < BW; i++) x1[i] = x2[i] = 0;
-    x1[0] = 1;
-    for (;;) {
-        while (!(u[0] & 1)) {
-            const int k = w_ctz(u);
-            w_shr(u, k);
-            w_half_k(x1, k, P);
-        }
-        while (!(v[0] & 1)) {
-            const int k = w_ctz(v);
-            w_shr(v, k);
-            w_half_k(x2, k, P);
-        }
-        if (w_is_one(u) || w_is_one(v)) break;
-        if (w_ge(u, v)) {
-            w_sub(u, v);
-            w_submod(x1, x2, P2);
-        } else {
-            w_sub(v, u);
-            w_submod(x2, x1, P2);
-        }
+    for (int i = 0; i < BW; i++) {
+        a[i] = w_uni(a[i]);
+        b[i] = P[i];
+        u[i] = 0;
+        v[i] = 0;
     }
-    fp x = fp_from_w(w_is_one(u) ? x1 : x2);  // A^-1 (plain), < 2p
+    u[0] = 1;
+    for (int it = 0; it < 64 && !w_is_zero(a); it++) {
+        int n = w_bitlen(a);
+        const int nb = w_bitlen(b);
+        n = n > nb ? n : nb;
+        n = n > 62 ? n : 62;
+        uint64_t xa = ((uint64_t)w_bits32(a, n - 32) << 30) | (a[0] & ((1u << 30) - 1u));
+        uint64_t xb = ((uint64_t)w_bits32(b, n - 32) << 30) | (b[0] & ((1u << 30) - 1u));
+        int64_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+        for (int i = 0; i < 30; i++) {
+            if (xa & 1) {
+                if (xa < xb) {
+                    const uint64_t t = xa;
+                    xa = xb;
+                    xb = t;
+                    int64_t s = f0;
+                    f0 = f1;
+                    f1 = s;
+                    s = g0;
+                    g0 = g1;
+                    g1 = s;
+                }
+                xa -= xb;
+                f0 -= f1;
+                g0 -= g1;
+            }
+            xa >>= 1;
+            f1 *= 2;
+            g1 *= 2;
+        }
+        uint32_t ta[BW + 1], tb[BW + 1];
+        w_lin2(ta, f0, a, g0, b);
+        w_lin2(tb, f1, a, g1, b);
+        if (w_neg13(ta)) {
+            f0 = -f0;
+            g0 = -g0;
+        }
+        if (w_neg13(tb)) {
+            f1 = -f1;
+            g1 = -g1;
+        }
+        w_shr30(a, ta);
+        w_shr30(b, tb);
+        uint32_t nu[BW];
+        w_lin2_modp(nu, f0, u, g0, v, P);
+        w_lin2_modp(v, f1, u, g1, v, P);
+        for (int i = 0; i < BW; i++) u[i] = nu[i];
+    }
+    fp r = fp_from_w(v);  // y^-1 (plain, canonical) for y = the Montgomery integer x R
     fp r3;
     {
         const uint32_t c[NL] = BLS_R3;
         for (int j = 0; j < NL; j++) r3.l[j] = c[j];
     }
-    return fp_mul(x, r3);  // A^-1 R^3 / R = (a R)^-1 R^2 = a^-1 R: the Montgomery form of a^-1
+    return fp_mul(r, r3);  // y^-1 R^3 / R = (x R)^-1 R^2 = x^-1 R: the Montgomery form of x^-1
 }
 
 // sqrt for p = 3 mod 4; false if a is not a square

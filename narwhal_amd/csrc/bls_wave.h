@@ -18,17 +18,20 @@
 // every lane precede its writes (one wave: LDS operations execute in order; the host form runs
 // the lanes' reads first, then their writes).
 #pragma once
+#include <cassert>
+
 #include "bls381.h"
 
 namespace bls {
 namespace wave {
 
-struct Stage {
-    uint16_t nl, nap, nan, nbp, nbn, flags, rec_len;
-    uint32_t off;
-};
+// a program: its first lane record (u16 index into T_DATA), its stages, the first stage's lanes.
+// A stage's records follow the previous stage's, and every record carries its stage's header (lanes,
+// A's and B's term counts) and the next stage's lanes, so the interpreter walks a program from
+// the records alone.
 struct Prog {
-    uint16_t first, n;
+    uint32_t off;
+    uint16_t n, nl0;
 };
 
 }  // namespace wave
@@ -46,6 +49,18 @@ namespace bls {
 namespace wave {
 
 constexpr int SW = NL;  // words per slot
+// the slot words as the interpreter addresses them: LDS on the device (explicit, so the one
+// out-of-line copy of the stage loop issues LDS instructions), plain memory on the host
+#ifdef BLS_WAVE_DEV
+typedef __attribute__((address_space(3))) uint32_t wword;
+typedef __attribute__((address_space(3))) uint64_t wword2;
+#else
+typedef uint32_t wword;
+typedef uint64_t wword2;
+#endif
+// the wave's LDS: NSLOTS slots, then P << k (k < 16) for the combinations' offsets
+constexpr int KP_WORDS = 16 * NL;
+constexpr int WM_WORDS = SW * NSLOTS + KP_WORDS;
 
 // A lane's record in registers: REC u16 words (five 16-byte loads).  [0] destination slot, [1]
 // flags (1 product, 2 reduce, 4 A signed, 8 B signed), [2] k+1 of A's 2^k p (0 none), [3] k+1 of
@@ -56,6 +71,21 @@ struct Rec {
     uint32_t w[REC / 2];
 };
 NWV_HD uint32_t rec_u16(const Rec& r, int i) { return (r.w[i >> 1] >> ((i & 1) * 16)) & 0xffffu; }
+// the stage header at the record's end
+struct Hdr {
+    int nl, nap, nan, nbp, nbn, nl_next;
+};
+NWV_HD Hdr rec_hdr(const Rec& r) {
+    const uint32_t a = r.w[REC / 2 - 2], b = r.w[REC / 2 - 1];  // (nl | na << 16), (nb | nl_next << 16)
+    Hdr h;
+    h.nl = (int)(a & 0xffffu);
+    h.nap = (int)((a >> 16) & 0xffu);
+    h.nan = (int)(a >> 24);
+    h.nbp = (int)(b & 0xffu);
+    h.nbn = (int)((b >> 8) & 0xffu);
+    h.nl_next = (int)(b >> 16);
+    return h;
+}
 NWV_HD Rec load_rec(const uint16_t* p) {
     Rec r;
     const uint4* q = reinterpret_cast<const uint4*>(p);
@@ -70,45 +100,102 @@ NWV_HD Rec load_rec(const uint16_t* p) {
     return r;
 }
 
-// the n terms of a section into 32-bit limb sums
-template <int BASE>
-NWV_HD void acc_terms(const uint32_t* wm, const Rec& r, int n, uint32_t* a) {
+// A combination's limb sums: the offset 2^k p (when the lane has negative terms) is stored in a
+// redundant form whose limbs 0..12 are each >= 2^31 - 8 >= the most that 8 units of negative
+// terms can take from a limb (T_KP: P << k with 8 borrowed from each next limb), so every limb
+// sum below the top is a non-negative 32-bit value (< 2^32 with <= 7 positive units; <= 16 units
+// without negative terms) and only the top limb can be negative (the value never is).
+//
+// n terms of a section (n wave-uniform: one switch, then every LDS read in flight at once -- one
+// wave per SIMD has nothing else to hide their latency behind -- then the sums)
+template <int BASE, int N>
+NWV_HD void acc_n(const wword* wm, const Rec& r, uint32_t* a) {
+    uint32_t x[N][NL];
+    int sh[N];
 #pragma unroll
-    for (int t = 0; t < TMAX; t++) {
-        if (t < n) {
-            const uint32_t w = rec_u16(r, BASE + t);
-            const uint32_t* x = wm + SW * (w & 0xfffu);
-            const int sh = (int)(w >> 12);
+    for (int u = 0; u < N; u++) {
+        const uint32_t w = rec_u16(r, BASE + u);
+        // a slot is 56 bytes at an 8-byte aligned offset: seven 8-byte reads
+        const wword2* p = reinterpret_cast<const wword2*>(wm + SW * (w & 0xfffu));
+        sh[u] = (int)(w >> 12);
 #pragma unroll
-            for (int j = 0; j < NL; j++) a[j] += x[j] << sh;
+        for (int j = 0; j < NL / 2; j++) {
+            const uint64_t q = p[j];
+            x[u][2 * j] = (uint32_t)q;
+            x[u][2 * j + 1] = (uint32_t)(q >> 32);
         }
     }
+#pragma unroll
+    for (int u = 0; u < N; u++)
+#pragma unroll
+        for (int j = 0; j < NL; j++) a[j] += x[u][j] << sh[u];
 }
-
-// a combination: positive terms + 2^k p - negative terms, one carry pass (signed when the lane
-// has negative terms), normalised limbs
 template <int BASE>
-NWV_HD fp lin_comb(const uint32_t* wm, const Rec& r, int np, int nn, uint32_t k1, bool sgn) {
-    uint32_t a[NL], b[NL];
-#pragma unroll
-    for (int j = 0; j < NL; j++) a[j] = b[j] = 0;
-    acc_terms<BASE>(wm, r, np, a);
-    acc_terms<BASE + TMAX>(wm, r, nn, b);
-    if (k1) {
-        const uint32_t* kp = T_KP[k1 - 1];
-#pragma unroll
-        for (int j = 0; j < NL; j++) a[j] += kp[j];
+NWV_HD void acc_terms(const wword* wm, const Rec& r, int n, uint32_t* a) {
+    switch (n) {
+        case 1: acc_n<BASE, 1>(wm, r, a); break;
+        case 2: acc_n<BASE, 2>(wm, r, a); break;
+        case 3: acc_n<BASE, 3>(wm, r, a); break;
+        case 4: acc_n<BASE, 4>(wm, r, a); break;
+        case 5: acc_n<BASE, 5>(wm, r, a); break;
+        case 6: acc_n<BASE, 6>(wm, r, a); break;
+        case 7: acc_n<BASE, 7>(wm, r, a); break;
+        case 8: acc_n<BASE, 8>(wm, r, a); break;
+        default: break;
     }
+}
+// the limb sums of a combination: positive terms + 2^k p - negative terms
+template <int BASE>
+NWV_HD void comb_sums(const wword* wm, const Rec& r, int np, int nn, uint32_t k1, uint32_t* a) {
+    if (k1) {
+        const wword* kp = wm + SW * NSLOTS + NL * (k1 - 1);
+#pragma unroll
+        for (int j = 0; j < NL; j++) a[j] = kp[j];
+    } else {
+#pragma unroll
+        for (int j = 0; j < NL; j++) a[j] = 0;
+    }
+    acc_terms<BASE>(wm, r, np, a);
+    if (nn) {
+        uint32_t b[NL];
+#pragma unroll
+        for (int j = 0; j < NL; j++) b[j] = 0;
+        acc_terms<BASE + TMAX>(wm, r, nn, b);
+#pragma unroll
+        for (int j = 0; j < NL; j++) a[j] -= b[j];
+    }
+}
+// normalised limbs (< 2^28): one sequential carry pass (the top limb takes the rest)
+NWV_HD fp carry_seq(const uint32_t* a) {
     fp v;
     uint32_t c = 0;
 #pragma unroll
     for (int j = 0; j < NL - 1; j++) {
-        const uint32_t d = a[j] - b[j] + c;
+        const uint32_t d = a[j] + c;
         v.l[j] = d & LM;
-        c = sgn ? (uint32_t)((int32_t)d >> 28) : d >> 28;
+        c = d >> 28;
     }
-    v.l[NL - 1] = a[NL - 1] - b[NL - 1] + c;
+    v.l[NL - 1] = a[NL - 1] + c;
     return v;
+}
+// a product operand: limbs below 2^28 + 16, each from its own sum and the one below (no carry
+// chain); fp_mul takes such limbs.  A negative top limb (possible only for a value within 2^-24 of
+// a multiple of 2^364) takes the sequential pass.
+NWV_HD fp carry_par(const uint32_t* a) {
+    fp v;
+    v.l[0] = a[0] & LM;
+#pragma unroll
+    for (int j = 1; j < NL - 1; j++) v.l[j] = (a[j] & LM) + (a[j - 1] >> 28);
+    v.l[NL - 1] = a[NL - 1] + (a[NL - 2] >> 28);
+    if ((int32_t)v.l[NL - 1] < 0) v = carry_seq(a);
+    return v;
+}
+// a combination as a normalised value (the tests' and the G1/G2 helpers' form)
+template <int BASE>
+NWV_HD fp lin_comb(const wword* wm, const Rec& r, int np, int nn, uint32_t k1, bool) {
+    uint32_t a[NL];
+    comb_sums<BASE>(wm, r, np, nn, k1, a);
+    return carry_seq(a);
 }
 
 // x - q p with q = floor(top limb * QM / 2^32) <= x / p: the result is < 1.1 p (< 2p)
@@ -130,14 +217,18 @@ NWV_HD fp quick_reduce(const fp& x) {
     return r;
 }
 
-NWV_HD fp lane_value(const uint32_t* wm, const Stage& h, const Rec& r) {
+NWV_HD fp lane_value(const wword* wm, const Hdr& h, const Rec& r) {
     const uint32_t fl = rec_u16(r, 1);
-    fp v = lin_comb<4>(wm, r, h.nap, h.nan, rec_u16(r, 2), (fl & 4) != 0);
+    uint32_t a[NL];
+    comb_sums<4>(wm, r, h.nap, h.nan, rec_u16(r, 2), a);
+    fp v;
     if (fl & 1) {
-        const fp b = lin_comb<4 + 2 * TMAX>(wm, r, h.nbp, h.nbn, rec_u16(r, 3), (fl & 8) != 0);
-        v = fp_mul(v, b);
-    } else if (fl & 2) {
-        v = quick_reduce(v);
+        uint32_t b[NL];
+        comb_sums<4 + 2 * TMAX>(wm, r, h.nbp, h.nbn, rec_u16(r, 3), b);
+        v = fp_mul(carry_par(a), carry_par(b));
+    } else {
+        v = carry_seq(a);
+        if (fl & 2) v = quick_reduce(v);
     }
     return v;
 }
@@ -149,34 +240,43 @@ __device__ __forceinline__ void wsync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// the program's stages; each lane's record for the next stage is loaded while this one runs (a
+// lane past a stage's last record loads the last one: every record holds the header).  One copy
+// of the interpreter per kernel (not inlined at every call site): the kernels stay within the
+// instruction cache.
+__device__ __attribute__((noinline)) void wave_run(uint32_t* wm_generic, int lane, uint32_t off, int n, int nl) {
+    wword* wm = (wword*)wm_generic;
+    const uint16_t* base = T_DATA + off;
+    Rec cur = load_rec(base + (uint32_t)min(lane, nl - 1) * REC);
+#pragma unroll 1
+    for (int s = 0; s < n; s++) {
+        Hdr h = rec_hdr(cur);
+        h.nap = __builtin_amdgcn_readfirstlane(h.nap);  // wave-uniform: term counts in SGPRs
+        h.nan = __builtin_amdgcn_readfirstlane(h.nan);
+        h.nbp = __builtin_amdgcn_readfirstlane(h.nbp);
+        h.nbn = __builtin_amdgcn_readfirstlane(h.nbn);
+        const int nl_next = __builtin_amdgcn_readfirstlane(h.nl_next);
+        const uint16_t* nbase = base + (uint32_t)nl * REC;
+        Rec nxt = cur;
+        if (s + 1 < n) nxt = load_rec(nbase + (uint32_t)min(lane, nl_next - 1) * REC);
+        if (lane < nl) {
+            const uint32_t dst = rec_u16(cur, 0);
+            const fp v = lane_value(wm, h, cur);
+#pragma unroll
+            for (int j = 0; j < NL; j++) wm[SW * dst + j] = v.l[j];
+        }
+        wsync();
+        base = nbase;
+        nl = nl_next;
+        cur = nxt;
+    }
+}
 struct Wave {
     uint32_t* wm;
     int lane;
     __device__ void sync() const { wsync(); }
-    // the program's stages; each lane's record for the next stage is loaded while this one runs
-    __device__ void run(Prog p) const {
-        const int end = p.first + p.n;
-        Stage h = T_STAGES[p.first];
-        Rec cur = load_rec(T_DATA + h.off + (uint32_t)min(lane, (int)h.nl) * REC);
-#pragma unroll 1
-        for (int s = p.first; s < end; s++) {
-            Stage hn = h;
-            Rec nxt = cur;
-            if (s + 1 < end) {
-                hn = T_STAGES[s + 1];
-                nxt = load_rec(T_DATA + hn.off + (uint32_t)min(lane, (int)hn.nl) * REC);
-            }
-            if (lane < h.nl) {
-                const uint32_t dst = rec_u16(cur, 0);
-                const fp v = lane_value(wm, h, cur);
-#pragma unroll
-                for (int j = 0; j < NL; j++) wm[SW * dst + j] = v.l[j];
-            }
-            wsync();
-            h = hn;
-            cur = nxt;
-        }
-    }
+    __device__ void run(Prog p) const { wave_run(wm, lane, p.off, p.n, p.nl0); }
+    __device__ void run(Prog p, Prog) const { run(p); }
     // up to 128 words of global memory fetched into registers ahead of use (a prefetch), and
     // written into slots later
     struct Pre {
@@ -237,18 +337,26 @@ struct Wave {
     uint32_t* wm;
     int lane = 0;
     void sync() const {}
+    void run(Prog p, Prog) const { run(p); }
     void run(Prog p) const {
         fp out[64];
         uint32_t dst[64];
-        for (int s = p.first; s < p.first + p.n; s++) {
-            const Stage h = T_STAGES[s];
-            for (int l = 0; l < h.nl; l++) {  // every lane's reads ...
-                const Rec r = load_rec(T_DATA + h.off + (uint32_t)l * REC);
+        const uint16_t* base = T_DATA + p.off;
+        int nl = p.nl0;
+        for (int s = 0; s < (int)p.n; s++) {
+            int nl_next = 0;
+            for (int l = 0; l < nl; l++) {  // every lane's reads ...
+                const Rec r = load_rec(base + (uint32_t)l * REC);
+                const Hdr h = rec_hdr(r);
+                assert(h.nl == nl);
+                nl_next = h.nl_next;
                 dst[l] = rec_u16(r, 0);
                 out[l] = lane_value(wm, h, r);
             }
-            for (int l = 0; l < h.nl; l++)  // ... then its writes
+            for (int l = 0; l < nl; l++)  // ... then its writes
                 for (int j = 0; j < NL; j++) wm[SW * dst[l] + j] = out[l].l[j];
+            base += (uint32_t)nl * REC;
+            nl = nl_next;
         }
     }
     struct Pre {
@@ -292,11 +400,12 @@ struct Wave {
 };
 #endif
 
-// slot 0 = 0, then the constant table
+// slot 0 = 0, then the constant table; P << k past the slots
 template <class W>
 NWV_HD void init_slots(const W& w) {
     w.zero(0, 1);
     w.put_words(1, &T_CONSTS[0][0], NCONSTS);
+    w.put_words(NSLOTS, &T_KP[0][0], 16);
     w.sync();
 }
 
@@ -305,8 +414,9 @@ template <class W>
 NWV_HD void cyc_exp_x(const W& w, Prog mul_base) {
 #pragma unroll 1
     for (int b = 62; b >= 0; b--) {
-        w.run(P_CYC_SQR_F);
-        if ((BLS_X_ABS >> b) & 1) w.run(mul_base);
+        const bool m = (BLS_X_ABS >> b) & 1;
+        w.run(P_CYC_SQR_F, m ? mul_base : P_CYC_SQR_F);
+        if (m) w.run(mul_base, P_CYC_SQR_F);
     }
 }
 
@@ -315,8 +425,9 @@ template <class W>
 NWV_HD void g1_chain(const W& w, uint64_t k) {
 #pragma unroll 1
     for (int b = 62; b >= 0; b--) {
-        w.run(P_G1_DBL_U);
-        if ((k >> b) & 1) w.run(P_G1_ADD_UV);
+        const bool a = (k >> b) & 1;
+        w.run(P_G1_DBL_U, a ? P_G1_ADD_UV : P_G1_DBL_U);
+        if (a) w.run(P_G1_ADD_UV, P_G1_DBL_U);
     }
 }
 
@@ -376,8 +487,8 @@ NWV_HD bool pairing_check(const W& w, const uint32_t* qlines) {
             la = w.fetch(&T_G2_LINES[k + 1][0][0], LW);
             if (qlines) lb = w.fetch(qlines + (size_t)(k + 1) * LW, LW);
         }
-        const bool add = steps[k] == 'a';
-        w.run(qlines ? (add ? P_ML_ADD_FIXED : P_ML_DBL_FIXED) : (add ? P_ML_ADD_STEP : P_ML_DBL_STEP));
+        const Prog pd = qlines ? P_ML_DBL_FIXED : P_ML_DBL_STEP, pa = qlines ? P_ML_ADD_FIXED : P_ML_ADD_STEP;
+        w.run(steps[k] == 'a' ? pa : pd, k + 1 < NSTEPS && steps[k + 1] == 'a' ? pa : k + 1 < NSTEPS ? pd : P_CONJ_F);
     }
     w.run(P_CONJ_F);
     final_exp(w);

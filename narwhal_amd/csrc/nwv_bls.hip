@@ -345,7 +345,7 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_pairing_raw(uint32_t n, const
 
 // ---- the wave engine (bls_wave.h): one 64-lane wave per item ------------------------------------
 #define BLSW_IDX()                                        \
-    __shared__ uint32_t wm[wave::SW * wave::NSLOTS];      \
+    __shared__ uint32_t wm[wave::WM_WORDS];                   \
     const uint32_t i = blockIdx.x;                        \
     if (i >= n) return;                                   \
     const wave::Wave w{wm, (int)threadIdx.x}

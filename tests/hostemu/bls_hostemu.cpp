@@ -176,7 +176,7 @@ int bh_rlc_batch(size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_
 
 // ---- the wave engine (bls_wave.h) on the host: the same interpreter and stage tables -----------
 static wave::Wave host_wave() {
-    static thread_local std::vector<uint32_t> wm(wave::SW * wave::NSLOTS);
+    static thread_local std::vector<uint32_t> wm(wave::WM_WORDS);
     wave::Wave w;
     w.wm = wm.data();
     return w;

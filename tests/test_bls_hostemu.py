@@ -259,10 +259,11 @@ def test_wave_pipeline_fast_aggregate_verify(emu):
 
 
 def test_fp_inv_variable_time(emu):
-    """the binary extended-Euclid inversion (variable time: public inputs) against a^(p-2)"""
+    """the batched binary-GCD inversion (variable time: public inputs) against a^(p-2)"""
     rnd = random.Random(56)
     p = C.p
-    vals = [1, 2, p - 1, p - 2, (p + 1) // 2, 1 << 380, (1 << 381) % p] + [rnd.randrange(1, p) for _ in range(200)]
+    vals = [1, 2, 3, p - 1, p - 2, (p + 1) // 2, 1 << 62, (1 << 62) - 1, 1 << 380, (1 << 381) % p]
+    vals += [rnd.randrange(1, p) for _ in range(500)] + [rnd.randrange(1, 1 << rnd.randrange(1, 380)) for _ in range(100)]
     o = _buf(48)
     for a in vals:
         emu.bh_fp_inv_vt(a.to_bytes(48, "big"), o)

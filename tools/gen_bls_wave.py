@@ -274,7 +274,7 @@ def mat12(x): return (mat6(x[0]), mat6(x[1]))
 
 def M(x):
     """materialise x (identity on plain integers)"""
-    return mat(x) if isinstance(x, E) else x
+    return mat(x) if isinstance(x, E) and x.f else x
 
 
 def f6_mul(a, b, m=True):
@@ -738,10 +738,14 @@ def compile_prog(prog):
                 nxt += 1
             live.append((last_use.get(a.id, si), a.slot))
     max_slot = nxt
-    # 7. the lane records
+    # 7. the lane records.  In a stage with products a combination lane is a product by 1 (R mod p,
+    # the Montgomery one): the wave then runs one code path (no divergence), and the result is
+    # below 2p
+    one = CTX.consts[mont(1)]
     out_stages = []
     for st in stages:
         lanes = []
+        anymul = any(a.kind == "mul" for a in st)
         for a in st:
             ba, ka = _lin_bound(a.a)
             rec = {"dst": a.slot, "mul": a.kind == "mul", "reduce": a.reduce, "ka": ka, "kb": -1,
@@ -750,6 +754,9 @@ def compile_prog(prog):
                 _, kb = _lin_bound(a.b)
                 rec["kb"] = kb
                 rec["b"] = _terms(a.b)
+            elif anymul:
+                assert ba < (1 << 392)
+                rec.update(mul=True, reduce=False, b=([(one.slot, 0)], []))
             lanes.append(rec)
         out_stages.append(lanes)
     cp = Compiled(prog.name, out_stages)
@@ -775,6 +782,19 @@ def _terms(f):
 def kp_limbs(k):
     v = P << k
     return [(v >> (LB * j)) & LM if j < NL - 1 else v >> (LB * j) for j in range(NL)]
+
+
+def kp_redundant(k):
+    """the limbs r_j = s_j + 8 2^28 [j < 13] - 8 [j > 0] of P << k (s_j its normalised limbs): the
+    same value, limbs 0..12 in [2^31 - 8, 2^31 + 2^28), the top one s_13 - 8 >= 0"""
+    s = _limbs(P << k)
+    r = [s[j] + (8 << LB if j < NL - 1 else 0) - (8 if j > 0 else 0) for j in range(NL)]
+    assert sum(x << (LB * j) for j, x in enumerate(r)) == P << k
+    assert all((1 << 31) - 8 <= x < (1 << 32) for x in r[:-1]) and r[-1] >= 0
+    # the worst limb sums: <= 7 positive units on top of it stay below 2^32, 8 negative units
+    # (each limb < 2^28) never take it below 0
+    assert all(x + 7 * LM < (1 << 32) and x - 8 * LM >= 0 for x in r[:-1])
+    return r
 
 
 def simulate(cp, wm):
@@ -1003,13 +1023,14 @@ def _p_inv_b(io):
 
 
 # ---- Miller-loop steps -------------------------------------------------------------------------
-def _mlstep(io, add, fixed_b):
+def _mlstep(io, add, fixed_b, fused):
     """one Miller-loop step for the two pairs of a verification, e(-sig, g2) e(H, apk):
       pair A: P_A = (x, y) affine, its line (l0, l1, l4) for this step precomputed (LA; g2 is
               fixed);
       pair B: P_B = (X : Y : Z) homogeneous; either its line precomputed too (LB: a cached key's
               table, fixed_b) or computed here from the running T (Jacobian) and Q_B;
-    f <- f^2 lA lB (doubling step) or f lA lB (addition step).  Pair B's line is evaluated times Z
+    f <- f^2 lA lB (doubling step) or f lA lB (addition step), as (f^2 (lA lB)) when fused (the
+    lines' product runs beside the square: fewer stages) or ((f^2 lA) lB).  Pair B's line is evaluated times Z
     (l0 Z + l1 X v + l4 Y v w: a factor in Fp* that the final exponentiation maps to 1)."""
     f = f12_of(io, "F")
     if fixed_b:
@@ -1026,16 +1047,35 @@ def _mlstep(io, add, fixed_b):
         f = f12_sqr(f)
     xa, ya = io.fp("PA", 0), io.fp("PA", 1)
     la0, la1, la4 = f2_of(io, "LA", 0), f2_of(io, "LA", 1), f2_of(io, "LA", 2)
-    f = f12_mul_014(f, la0, f2_mul_fp(la1, xa), f2_mul_fp(la4, ya))
     xb, yb, zb = io.fp("PB", 0), io.fp("PB", 1), io.fp("PB", 2)
-    f = f12_mul_014(f, f2_mul_fp(l0, zb), f2_mul_fp(l1, xb), f2_mul_fp(l4, yb))
+    lA = (la0, f2_mul_fp(la1, xa), f2_mul_fp(la4, ya))
+    lB = (f2_mul_fp(l0, zb), f2_mul_fp(l1, xb), f2_mul_fp(l4, yb))
+    if fused:
+        # f (lA lB): the two lines' product is formed beside f's square, then one Fp12 product
+        f = f12_mul(f, mat12(line_mul(lA, lB)))
+    else:
+        f = f12_mul_014(f12_mul_014(f, *lA), *lB)
     put12(io, "F", f)
 
 
-program("ml_dbl_step")(lambda io: _mlstep(io, False, False))
-program("ml_add_step")(lambda io: _mlstep(io, True, False))
-program("ml_dbl_fixed")(lambda io: _mlstep(io, False, True))
-program("ml_add_fixed")(lambda io: _mlstep(io, True, True))
+def line_mul(a, b):
+    """(a0 + a1 v + a4 v w)(b0 + b1 v + b4 v w): an Fp12 whose c1.c0 is zero (6 Fp2 products)"""
+    a0, a1, a4 = a
+    b0, b1, b4 = b
+    t00, t11, t44 = f2_mul(a0, b0), f2_mul(a1, b1), f2_mul(a4, b4)
+    c00 = f2_add(t00, f2_mul_xi(t44))
+    c01 = f2_sub(f2_sub(f2_mul(f2_add(a0, a1), f2_add(b0, b1)), t00), t11)
+    c11 = f2_sub(f2_sub(f2_mul(f2_add(a0, a4), f2_add(b0, b4)), t00), t44)
+    c12 = f2_sub(f2_sub(f2_mul(f2_add(a1, a4), f2_add(b1, b4)), t11), t44)
+    z = a0[0] * 0
+    return ((c00, c01, t11), ((z, z), c11, c12))
+
+
+# the fused form (f^2 (lA lB)) where it has fewer stages: every step but the computed addition
+program("ml_dbl_step")(lambda io: _mlstep(io, False, False, True))
+program("ml_add_step")(lambda io: _mlstep(io, True, False, False))
+program("ml_dbl_fixed")(lambda io: _mlstep(io, False, True, True))
+program("ml_add_fixed")(lambda io: _mlstep(io, True, True, True))
 
 
 def _lines(io, add):
@@ -1396,6 +1436,7 @@ def emit(compiled, path):
     for name in names:
         cp = compiled[name]
         first = len(stages)
+        prev_hdr = None
         for st in cp.stages:
             nap = max(len(r["a"][0]) for r in st)
             nan = max(len(r["a"][1]) for r in st)
@@ -1407,6 +1448,7 @@ def emit(compiled, path):
             off = len(data)
             anymul = any(r["mul"] for r in st)
             anyred = any(r["reduce"] for r in st)
+            hdr_at = len(data)
             for r in st:
                 rec = [r["dst"], (1 if r["mul"] else 0) | (2 if r["reduce"] else 0) |
                        (4 if r["a"][1] else 0) | (8 if (r["b"] and r["b"][1]) else 0),
@@ -1418,11 +1460,19 @@ def emit(compiled, path):
                     return out + [0] * (TMAX - len(out))
                 rec += terms(r["a"][0]) + terms(r["a"][1])
                 rec += terms(r["b"][0]) + terms(r["b"][1]) if r["mul"] else [0] * (2 * TMAX)
-                rec += [0] * (rec_len - len(rec))
-                assert all(0 <= x < 65536 for x in rec)
+                rec += [0] * (rec_len - 4 - len(rec))
+                # the stage header, in every lane's record: lanes, A's and B's term counts, the
+                # next stage's lanes (its records follow this stage's)
+                rec += [len(st), nap | nan << 8, nbp | nbn << 8, 0]
+                assert len(rec) == rec_len and all(0 <= x < 65536 for x in rec)
                 data += rec
+            if prev_hdr is not None:
+                for k in range(prev_hdr[1]):
+                    data[prev_hdr[0] + k * REC + REC - 1] = len(st)
+            prev_hdr = (hdr_at, len(st))
+            assert 1 <= len(st) <= LANES
             stages.append((len(st), nap, nan, nbp, nbn, (1 if anymul else 0) | (2 if anyred else 0), rec_len, off))
-        progs.append((name, first, len(cp.stages)))
+        progs.append((name, first, len(cp.stages), stages[first][7], stages[first][0]))
         max_slot = max(max_slot, cp.max_slot)
     consts = sorted(CTX.consts.values(), key=lambda a: a.id)
     la = line_table(G2X, G2Y)
@@ -1440,22 +1490,21 @@ def emit(compiled, path):
     L.append(f"constexpr int NSTAGES = {len(stages)};")
     L.append(f"constexpr int NSTEPS = {len(la)};  // Miller-loop steps over |x|")
     L.append(f"constexpr uint32_t QM = {QM}u;  // floor(2^32 / (p_13 + 1)), the quick reduction's multiplier")
-    L.append(f"constexpr int REC = {REC};  // u16 words per lane record: header 4, then A+ A- B+ B- x {TMAX}")
+    L.append(f"constexpr int REC = {REC};  // u16 words per lane record: header 4, A+ A- B+ B- x {TMAX}, stage header 4")
     L.append(f"constexpr int TMAX = {TMAX};")
-    for name, first, n in progs:
-        L.append(f"constexpr Prog P_{name.upper()} = {{{first}, {n}}};")
+    L.append("// program: its first record (u16 index into T_DATA), stages, the first stage's lanes")
+    for name, first, n, off, nl0 in progs:
+        L.append(f"constexpr Prog P_{name.upper()} = {{{off}u, {n}, {nl0}}};")
     L.append("#define BLS_WAVE_STEPS_STR \"" + "".join(miller_steps()) + "\"")
     L.append("BLS_WAVE_TABLE uint32_t T_CONSTS[NCONSTS][14] = {")
     for a in consts:
         L.append("    {" + ", ".join(f"0x{x:07x}u" for x in _limbs(a.value)) + "},")
     L.append("};")
-    L.append("BLS_WAVE_TABLE uint32_t T_KP[16][14] = {  // P << k, normalised limbs")
+    L.append("// P << k in a redundant form: 8 borrowed from every limb above the lowest, so limbs 0..12 are")
+    L.append("// >= 2^31 - 8 (a combination's limb sums stay non-negative under 8 units of negative terms)")
+    L.append("BLS_WAVE_TABLE uint32_t T_KP[16][14] = {")
     for k in range(16):
-        L.append("    {" + ", ".join(f"0x{x:07x}u" for x in _limbs(P << k)) + "},")
-    L.append("};")
-    L.append("BLS_WAVE_TABLE Stage T_STAGES[NSTAGES] = {")
-    for st in stages:
-        L.append("    {" + ", ".join(str(x) for x in st) + "},")
+        L.append("    {" + ", ".join(f"0x{x:08x}u" for x in kp_redundant(k)) + "},")
     L.append("};")
     data += [0] * (2 * REC)  # the last lane's record may be read past its end by a prefetch
     L.append(f"BLS_WAVE_TABLE uint16_t T_DATA[{len(data)}] __attribute__((aligned(16))) = {{")
@@ -1488,6 +1537,7 @@ def build_all():
         body(TraceIO(prog))
         CTX.prog = None
         traced.append((prog, body))
+    CTX.cst(1)  # the Montgomery one (combination lanes of product stages multiply by it)
     REGS.layout(len(CTX.consts))
     for i, a in enumerate(sorted(CTX.consts.values(), key=lambda a: a.id)):
         a.slot = 1 + i
