@@ -41,6 +41,14 @@ hostemu: tests/_build/libhostemu.so tests/_build/libsvcstub.so tests/_build/libb
 tests/_build/libblsemu.so: tests/hostemu/bls_hostemu.cpp $(BLS_SRC)
 	@mkdir -p tests/_build
 	$(HIPCC) -std=c++17 -O2 --offload-host-only -x hip -fPIC -shared -o $@ tests/hostemu/bls_hostemu.cpp
+# the same build under AddressSanitizer + UndefinedBehaviorSanitizer (host code only):
+#   make blsemu-asan && tools/run_blsemu_asan.sh
+tests/_build/libblsemu_asan.so: tests/hostemu/bls_hostemu.cpp $(BLS_SRC)
+	@mkdir -p tests/_build
+	$(HIPCC) -std=c++17 -O1 -g --offload-host-only -x hip -fPIC -shared -fno-omit-frame-pointer \
+		-fno-gpu-sanitize -fsanitize=address,undefined -fno-sanitize-recover=all -shared-libsan \
+		-o $@ tests/hostemu/bls_hostemu.cpp
+blsemu-asan: tests/_build/libblsemu_asan.so
 # the batching service's host logic over a stubbed engine (tests/test_service_host.py)
 tests/_build/libsvcstub.so: tests/hostemu/service_stub.cpp narwhal_amd/csrc/nwv_service.cpp include/nwv_service.h
 	@mkdir -p tests/_build
@@ -59,4 +67,4 @@ clean:
 	rm -rf narwhal_amd/lib tests/_build
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib oracle hostemu tools clean
+.PHONY: blsemu-asan all lib oracle hostemu tools clean

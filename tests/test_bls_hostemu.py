@@ -19,7 +19,8 @@ r = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
 
 @pytest.fixture(scope="module")
 def emu():
-    path = os.path.join(ROOT, "tests", "_build", "libblsemu.so")
+    # NWV_BLSEMU_LIB: another build of the same code (the sanitizer build, tools/run_blsemu_asan.sh)
+    path = os.environ.get("NWV_BLSEMU_LIB") or os.path.join(ROOT, "tests", "_build", "libblsemu.so")
     if not os.path.exists(path):
         subprocess.run(["make", "-C", ROOT, "tests/_build/libblsemu.so"], check=True)
     L = ctypes.CDLL(path)
