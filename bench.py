@@ -58,6 +58,18 @@ MADS_DECOMPRESS = (OPS_MSM_POINTS[0] * MADS_PER_MUL + OPS_MSM_POINTS[1] * MADS_P
 MADS_MIXED_ADD = 7 * MADS_PER_MUL                          # per bucket entry (affine Niels)
 MADS_ADD = 9 * MADS_PER_MUL                                # extended + extended
 MADS_DBL = 4 * MADS_PER_MUL + 4 * MADS_PER_SQ              # projective doubling
+# SHA-512 (sha512.h), 32-bit VALU instructions per 128-byte block: a round is 34 (two 64-bit
+# rotations x3 as v_alignbit pairs, two v_xor3 pairs, two v_bitop3 pairs, six 64-bit adds), a
+# message-schedule step 22 (four rotations, a shift, two v_xor3 pairs, three 64-bit adds); 80
+# rounds + 64 steps + the state update.  Counted against the v_mad_u64_u32 roofline at the
+# guide's 2:1 issue ratio (a 32-bit form issues in half the time of a 64-bit-result form)
+SHA512_VALU_PER_BLOCK = 80 * 34 + 64 * 22 + 16
+
+
+def sha512_blocks(nbytes):
+    return (nbytes + 17 + 127) // 128
+
+
 OPS_STRAUS = (1155, 524)     # k_ed_straus: half-size scalars, 132 doublings (ed25519_lane.h)
 # guide-derived VALU peaks (MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32 x 2.4 GHz, a wave64 VALU
 # instruction issues over 2 cycles): 78.6 T lane-ops/s for full-rate 32-bit forms; the 64-bit
@@ -306,7 +318,7 @@ def issue_floor(kernels, n, kms, peak, launch):
             "frac": floor_s / (kms * 1e-3), "source": sorted(srcs)}
 
 
-def kernel_rooflines(kt, stats, n, na, peak):
+def kernel_rooflines(kt, stats, n, na, peak, mlen):
     """roofline of every kernel of the batch MSM from its single-stream, event-timed duration"""
     mad_peak = peak["v_mad_u64_u32_per_s"] / 1e12 if peak else None
     nw, nwz, buckets, E = stats["windows"], stats["windows_z"], stats["buckets"], stats["entries"]
@@ -335,13 +347,19 @@ def kernel_rooflines(kt, stats, n, na, peak):
                      "traffic": tr["bytes"] if tr else None,
                      "traffic_over_algorithmic": (tr["bytes"] / nbytes) if tr and nbytes else None}
 
-    valu("k_msm_prep", ["k_msm_prep"], MADS_DECOMPRESS * (na + n),
+    sha_blocks = sha512_blocks(64 + mlen)
+    sha_eq = SHA512_VALU_PER_BLOCK * sha_blocks // 2
+    valu("k_msm_prep", ["k_msm_prep"], MADS_DECOMPRESS * (na + n) + sha_eq * n,
          f"{MADS_DECOMPRESS} multiply-adds per decompressed point (24 mul + 257 sq) x {na + n} points "
-         "(R_i and the A points); the SHA-512 hashing in the same grid is not counted (a lower bound)")
+         f"(R_i and the A points), plus SHA-512(R || A || M) per signature: {sha_blocks} blocks x "
+         f"{SHA512_VALU_PER_BLOCK} 32-bit VALU instructions = {sha_eq} multiply-add equivalents "
+         f"(2 : 1 issue) x {n} signatures")
     mem("k_msm_hist", ["k_msm_hist"], 2 * digit_slots + 4 * cnt_len,
         f"read the i16 digit rows ({digit_slots} slots), write {cnt_len} u32 counts")
-    mem("k_msm_wscan", ["k_msm_wscan"], 12 * cnt_len,
-        f"read the {cnt_len} counts twice (totals, then offsets) and write them back as offsets")
+    mem("k_msm_wscan", ["k_msm_wscan"], 8 * cnt_len,
+        f"read the {cnt_len} counts and write them back as offsets (unique bytes: the workgroup's "
+        "second pass re-reads its window's counts from L2, and k_msm_hist has just written them, so "
+        "part of the first read can come from the MALL too)")
     mem("k_msm_scatter", ["k_msm_scatter"], 2 * digit_slots + 4 * cnt_len + 4 * E,
         f"read the digit rows and the {cnt_len} bucket offsets, write {E} u32 entries")
     valu("k_msm_bucket", ["k_msm_bucket"], MADS_MIXED_ADD * E,
@@ -655,7 +673,7 @@ def run_firehose(args, eng, rank, world, dist):
         return None
     # rank 0's sub-shard MSM against the integer roofline (event-timed kernels of one sub-shard)
     sub_n = firehose_pass.last_sub
-    per = kernel_rooflines(kt, firehose_pass.last_stats, sub_n, sub_n, valu_peak())
+    per = kernel_rooflines(kt, firehose_pass.last_stats, sub_n, sub_n, valu_peak(), 32)
     roof = dict(per["k_msm_prep"], kernel="k_msm_prep", selected_by="largest VALU kernel of the bulk phase",
                 kernel_share=per["k_msm_prep"]["kernel_ms"] / sum(kt.values()), subshard_sigs=sub_n)
     return {
@@ -841,7 +859,7 @@ def main():
     peak = valu_peak()
     if args.mode == 1:
         na = args.keys or args.n
-        per = kernel_rooflines(kt, stats, args.n, na, peak)
+        per = kernel_rooflines(kt, stats, args.n, na, peak, args.msg_len)
         # the dominant kernel of the THROUGHPUT regime: the most VALU work (issue floor) -- with
         # batches in flight the latency-bound tail overlaps other batches' work; by single-stream
         # time when no PMC pass of today's kernels is committed for this size
