@@ -108,9 +108,13 @@ NWV_HD Rec load_rec(const uint16_t* p) {
 //
 // n terms of a section (n wave-uniform: one switch, then every LDS read in flight at once -- one
 // wave per SIMD has nothing else to hide their latency behind -- then the sums)
+// Limb sums are kept as seven packed pairs (limb 2j in the low half of a 64-bit word, 2j+1 in the
+// high half): a slot's 8-byte LDS words are already such pairs, a term is seven 64-bit
+// shift-and-adds (v_lshl_add_u64), and no half ever carries into the next (every limb sum stays
+// below 2^32, and a term's shift of <= 3 keeps a 28-bit limb inside its half).
 template <int BASE, int N>
-NWV_HD void acc_n(const wword* wm, const Rec& r, uint32_t* a) {
-    uint32_t x[N][NL];
+NWV_HD void acc_n(const wword* wm, const Rec& r, uint64_t* a) {
+    uint64_t x[N][NL / 2];
     int sh[N];
 #pragma unroll
     for (int u = 0; u < N; u++) {
@@ -119,19 +123,15 @@ NWV_HD void acc_n(const wword* wm, const Rec& r, uint32_t* a) {
         const wword2* p = reinterpret_cast<const wword2*>(wm + SW * (w & 0xfffu));
         sh[u] = (int)(w >> 12);
 #pragma unroll
-        for (int j = 0; j < NL / 2; j++) {
-            const uint64_t q = p[j];
-            x[u][2 * j] = (uint32_t)q;
-            x[u][2 * j + 1] = (uint32_t)(q >> 32);
-        }
+        for (int j = 0; j < NL / 2; j++) x[u][j] = p[j];
     }
 #pragma unroll
     for (int u = 0; u < N; u++)
 #pragma unroll
-        for (int j = 0; j < NL; j++) a[j] += x[u][j] << sh[u];
+        for (int j = 0; j < NL / 2; j++) a[j] += x[u][j] << sh[u];
 }
 template <int BASE>
-NWV_HD void acc_terms(const wword* wm, const Rec& r, int n, uint32_t* a) {
+NWV_HD void acc_terms(const wword* wm, const Rec& r, int n, uint64_t* a) {
     switch (n) {
         case 1: acc_n<BASE, 1>(wm, r, a); break;
         case 2: acc_n<BASE, 2>(wm, r, a); break;
@@ -144,25 +144,36 @@ NWV_HD void acc_terms(const wword* wm, const Rec& r, int n, uint32_t* a) {
         default: break;
     }
 }
-// the limb sums of a combination: positive terms + 2^k p - negative terms
+// the limb sums of a combination: positive terms + 2^k p - negative terms (the subtraction per
+// 32-bit limb: with the redundant offset no limb below the top goes negative)
 template <int BASE>
-NWV_HD void comb_sums(const wword* wm, const Rec& r, int np, int nn, uint32_t k1, uint32_t* a) {
+NWV_HD void comb_sums(const wword* wm, const Rec& r, int np, int nn, uint32_t k1, uint32_t* out) {
+    uint64_t a[NL / 2];
     if (k1) {
-        const wword* kp = wm + SW * NSLOTS + NL * (k1 - 1);
+        const wword2* kp = reinterpret_cast<const wword2*>(wm + SW * NSLOTS + NL * (k1 - 1));
 #pragma unroll
-        for (int j = 0; j < NL; j++) a[j] = kp[j];
+        for (int j = 0; j < NL / 2; j++) a[j] = kp[j];
     } else {
 #pragma unroll
-        for (int j = 0; j < NL; j++) a[j] = 0;
+        for (int j = 0; j < NL / 2; j++) a[j] = 0;
     }
     acc_terms<BASE>(wm, r, np, a);
     if (nn) {
-        uint32_t b[NL];
+        uint64_t b[NL / 2];
 #pragma unroll
-        for (int j = 0; j < NL; j++) b[j] = 0;
+        for (int j = 0; j < NL / 2; j++) b[j] = 0;
         acc_terms<BASE + TMAX>(wm, r, nn, b);
 #pragma unroll
-        for (int j = 0; j < NL; j++) a[j] -= b[j];
+        for (int j = 0; j < NL / 2; j++) {
+            out[2 * j] = (uint32_t)a[j] - (uint32_t)b[j];
+            out[2 * j + 1] = (uint32_t)(a[j] >> 32) - (uint32_t)(b[j] >> 32);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < NL / 2; j++) {
+            out[2 * j] = (uint32_t)a[j];
+            out[2 * j + 1] = (uint32_t)(a[j] >> 32);
+        }
     }
 }
 // normalised limbs (< 2^28): one sequential carry pass (the top limb takes the rest)
@@ -244,21 +255,26 @@ __device__ __forceinline__ void wsync() {
 // lane past a stage's last record loads the last one: every record holds the header).  One copy
 // of the interpreter per kernel (not inlined at every call site): the kernels stay within the
 // instruction cache.
-__device__ __attribute__((noinline)) void wave_run(uint32_t* wm_generic, int lane, uint32_t off, int n, int nl) {
+__device__ __attribute__((noinline)) void wave_run(uint32_t* wm_generic, int lane, uint32_t off, int n, int nl0,
+                                                   int reps) {
     wword* wm = (wword*)wm_generic;
-    const uint16_t* base = T_DATA + off;
-    Rec cur = load_rec(base + (uint32_t)min(lane, nl - 1) * REC);
+    const uint16_t* base0 = T_DATA + off;
+    const uint16_t* base = base0;
+    int nl = nl0;
+    Rec cur = load_rec(base0 + (uint32_t)min(lane, nl0 - 1) * REC);
+    const int total = n * reps;
 #pragma unroll 1
-    for (int s = 0; s < n; s++) {
+    for (int t = 0, s = 0; t < total; t++) {
         Hdr h = rec_hdr(cur);
         h.nap = __builtin_amdgcn_readfirstlane(h.nap);  // wave-uniform: term counts in SGPRs
         h.nan = __builtin_amdgcn_readfirstlane(h.nan);
         h.nbp = __builtin_amdgcn_readfirstlane(h.nbp);
         h.nbn = __builtin_amdgcn_readfirstlane(h.nbn);
-        const int nl_next = __builtin_amdgcn_readfirstlane(h.nl_next);
-        const uint16_t* nbase = base + (uint32_t)nl * REC;
+        const bool wrap = s + 1 == n;  // the program's last stage: the next one is its first again
+        const int nl_next = wrap ? nl0 : __builtin_amdgcn_readfirstlane(h.nl_next);
+        const uint16_t* nbase = wrap ? base0 : base + (uint32_t)nl * REC;
         Rec nxt = cur;
-        if (s + 1 < n) nxt = load_rec(nbase + (uint32_t)min(lane, nl_next - 1) * REC);
+        if (t + 1 < total) nxt = load_rec(nbase + (uint32_t)min(lane, nl_next - 1) * REC);
         if (lane < nl) {
             const uint32_t dst = rec_u16(cur, 0);
             const fp v = lane_value(wm, h, cur);
@@ -269,14 +285,15 @@ __device__ __attribute__((noinline)) void wave_run(uint32_t* wm_generic, int lan
         base = nbase;
         nl = nl_next;
         cur = nxt;
+        s = wrap ? 0 : s + 1;
     }
 }
 struct Wave {
     uint32_t* wm;
     int lane;
     __device__ void sync() const { wsync(); }
-    __device__ void run(Prog p) const { wave_run(wm, lane, p.off, p.n, p.nl0); }
-    __device__ void run(Prog p, Prog) const { run(p); }
+    // the program `reps` times over (one call: runs of squarings / doublings)
+    __device__ void run(Prog p, int reps = 1) const { wave_run(wm, lane, p.off, p.n, p.nl0, reps); }
     // up to 128 words of global memory fetched into registers ahead of use (a prefetch), and
     // written into slots later
     struct Pre {
@@ -337,7 +354,9 @@ struct Wave {
     uint32_t* wm;
     int lane = 0;
     void sync() const {}
-    void run(Prog p, Prog) const { run(p); }
+    void run(Prog p, int reps) const {
+        for (int r = 0; r < reps; r++) run(p);
+    }
     void run(Prog p) const {
         fp out[64];
         uint32_t dst[64];
@@ -409,26 +428,34 @@ NWV_HD void init_slots(const W& w) {
     w.sync();
 }
 
+// the square-and-multiply chain of a 64-bit k (top bit 63) below its top bit: each run of
+// squarings (doublings) up to the next set bit is one interpreter call
+template <class W>
+NWV_HD void exp_chain(const W& w, uint64_t k, Prog sq, Prog mul) {
+    int b = 62;
+    while (b >= 0) {
+        int r = 0;
+        while (b - r >= 0 && !((k >> (b - r)) & 1)) r++;
+        if (b - r < 0) {  // trailing zeros: squarings only
+            w.run(sq, r);
+            break;
+        }
+        w.run(sq, r + 1);  // the zeros, then the set bit's squaring
+        w.run(mul);
+        b -= r + 1;
+    }
+}
+
 // F <- F^|x| by cyclotomic squarings (F starts as the base, which is also in register `base`)
 template <class W>
 NWV_HD void cyc_exp_x(const W& w, Prog mul_base) {
-#pragma unroll 1
-    for (int b = 62; b >= 0; b--) {
-        const bool m = (BLS_X_ABS >> b) & 1;
-        w.run(P_CYC_SQR_F, m ? mul_base : P_CYC_SQR_F);
-        if (m) w.run(mul_base, P_CYC_SQR_F);
-    }
+    exp_chain(w, BLS_X_ABS, P_CYC_SQR_F, mul_base);
 }
 
 // U <- [k] V (U = V on entry; k's top bit is bit 63), complete formulas (exact on every point)
 template <class W>
 NWV_HD void g1_chain(const W& w, uint64_t k) {
-#pragma unroll 1
-    for (int b = 62; b >= 0; b--) {
-        const bool a = (k >> b) & 1;
-        w.run(P_G1_DBL_U, a ? P_G1_ADD_UV : P_G1_DBL_U);
-        if (a) w.run(P_G1_ADD_UV, P_G1_DBL_U);
-    }
+    exp_chain(w, k, P_G1_DBL_U, P_G1_ADD_UV);
 }
 
 // F <- F^(3 (p^12 - 1) / r), the final_exp of bls381.h; the one Fp inversion runs on lane 0
@@ -488,7 +515,7 @@ NWV_HD bool pairing_check(const W& w, const uint32_t* qlines) {
             if (qlines) lb = w.fetch(qlines + (size_t)(k + 1) * LW, LW);
         }
         const Prog pd = qlines ? P_ML_DBL_FIXED : P_ML_DBL_STEP, pa = qlines ? P_ML_ADD_FIXED : P_ML_ADD_STEP;
-        w.run(steps[k] == 'a' ? pa : pd, k + 1 < NSTEPS && steps[k + 1] == 'a' ? pa : k + 1 < NSTEPS ? pd : P_CONJ_F);
+        w.run(steps[k] == 'a' ? pa : pd);
     }
     w.run(P_CONJ_F);
     final_exp(w);

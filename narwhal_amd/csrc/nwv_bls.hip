@@ -73,7 +73,10 @@ struct KeyTab {
     const int32_t* sc;
     const uint32_t* rs;
     const int32_t* ss;
+    const uint32_t* lines;  // cached keys' Miller-loop line tables (KL_WORDS per slot), or null
 };
+// words of a registered key's line table: (l0, l1, l4) of every Miller-loop step (w_key_lines)
+constexpr size_t KL_WORDS = (size_t)wave::NSTEPS * 6 * wave::SW;
 __device__ inline const uint32_t* key_rec(const KeyTab& t, uint32_t k) {
     return k < KC_CAP ? t.rc + (size_t)G2_REC_WORDS * k : t.rs + (size_t)G2_REC_WORDS * (k - KC_CAP);
 }
@@ -376,18 +379,34 @@ __global__ __launch_bounds__(64) void k_blsw_sub(uint32_t n, const uint32_t* rec
 // (run beside the signature's G1 check: the status join puts that check first)
 // H: homogeneous records (k_blsw_h2c) or affine ones (k_bls_h2c_g, h_hom = 0); apk: Jacobian
 // records (k_blsw_apk)
+// (a one-key item whose key is in the cache takes the key's precomputed line table: the Miller
+// loop then only evaluates lines, no G2 arithmetic)
 __global__ __launch_bounds__(64) void k_blsw_pair(uint32_t n, const uint32_t* srec, const int32_t* st_dec,
                                                   const uint32_t* hrec, int h_hom, const uint32_t* arec,
-                                                  const int32_t* st_apk, int32_t* st_pair) {
+                                                  const int32_t* st_apk, KeyTab kt, const uint32_t* pk_off,
+                                                  const uint32_t* pk_cnt, const uint32_t* pk_idx, int32_t* st_pair) {
     BLSW_IDX();
     int32_t s = ST_VERIFY_FAIL;
-    if (st_dec[i] == ST_OK && st_apk[i] == ST_OK)
+    if (st_dec[i] == ST_OK && st_apk[i] == ST_OK) {
+        const uint32_t* ql = nullptr;
+        if (kt.lines && pk_cnt[i] == 1) {
+            const uint32_t k = pk_idx[pk_off[i]];
+            if (k < KC_CAP) ql = kt.lines + KL_WORDS * k;
+        }
         s = w_pairing_check_g(w, srec + (size_t)G1_REC_WORDS * i,
                               hrec + (size_t)(h_hom ? G1H_REC_WORDS : G1_REC_WORDS) * i, h_hom != 0,
-                              arec + (size_t)G2J_WORDS * i, true, nullptr)
+                              arec + (size_t)G2J_WORDS * i, true, ql)
                 ? ST_OK
                 : ST_VERIFY_FAIL;
+    }
     if (threadIdx.x == 0) st_pair[i] = s;
+}
+// the line tables of newly registered keys: one wave per key (slots[i] = its cache slot)
+__global__ __launch_bounds__(64) void k_blsw_key_lines(uint32_t n, const uint32_t* slots, const uint32_t* rc,
+                                                       uint32_t* lines) {
+    BLSW_IDX();
+    const uint32_t k = slots[i];
+    w_key_lines(w, rc + (size_t)G2_REC_WORDS * k, lines + KL_WORDS * k);
 }
 // the key sum of item i on a wave: lane j adds the item's keys j, j + 64, ... (Jacobian, jac_add:
 // exact in every case), then a six-level tree through LDS.  The status is that of the item's first
@@ -513,6 +532,8 @@ struct HBuf {
 struct BlsKeyCache {
     std::shared_mutex mu;
     DBuf rec, st;  // KC_CAP x G2_REC_WORDS u32 records, KC_CAP int32 statuses
+    DBuf lines;    // line tables of slots [0, used): KL_WORDS u32 each (grown as keys register)
+    uint32_t lines_slots = 0;
     std::unordered_map<std::string, uint32_t> slot;
     uint32_t used = 0;
 };
@@ -706,6 +727,25 @@ int keycache_register(BlsDev& d, size_t n_keys, const uint8_t* keys) {
                        reinterpret_cast<const uint32_t*>(w + o_dst), reinterpret_cast<const uint32_t*>(w + o_rec),
                        static_cast<uint32_t*>(d.kc.rec.p), static_cast<int32_t*>(d.kc.st.p));
     BLS_HIP(hipGetLastError());
+    // the new slots' Miller-loop line tables (the table grows by whole copies: registration is rare)
+    const uint32_t need = d.kc.used + (uint32_t)nv;
+    if (need > d.kc.lines_slots) {
+        uint32_t cap = std::max<uint32_t>(need, std::max<uint32_t>(2 * d.kc.lines_slots, 256u));
+        cap = std::min<uint32_t>(cap, (uint32_t)KC_CAP);
+        DBuf nb;
+        if ((rc = nb.ensure(4 * KL_WORDS * cap))) return rc;
+        if (d.kc.used)
+            BLS_HIP(hipMemcpyAsync(nb.p, d.kc.lines.p, 4 * KL_WORDS * d.kc.used, hipMemcpyDeviceToDevice,
+                                   lane->stream));
+        BLS_HIP(hipStreamSynchronize(lane->stream));
+        std::swap(d.kc.lines.p, nb.p);
+        std::swap(d.kc.lines.cap, nb.cap);
+        d.kc.lines_slots = cap;
+    }
+    hipLaunchKernelGGL(k_blsw_key_lines, dim3((unsigned)nv), dim3(64), 0, lane->stream, (uint32_t)nv,
+                       reinterpret_cast<const uint32_t*>(w + o_dst), static_cast<const uint32_t*>(d.kc.rec.p),
+                       static_cast<uint32_t*>(d.kc.lines.p));
+    BLS_HIP(hipGetLastError());
     BLS_HIP(hipStreamSynchronize(lane->stream));
     for (size_t k = 0; k < nv; k++) d.kc.slot.emplace(fresh[src[k]], dst[k]);  // published after the copy
     d.kc.used += (uint32_t)nv;
@@ -803,7 +843,8 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     uint8_t* w = static_cast<uint8_t*>(L.work.p);
     KeyTab kt{cached ? static_cast<const uint32_t*>(d.kc.rec.p) : nullptr,
               cached ? static_cast<const int32_t*>(d.kc.st.p) : nullptr, reinterpret_cast<uint32_t*>(w + w_krec),
-              reinterpret_cast<int32_t*>(w + w_kst)};
+              reinterpret_cast<int32_t*>(w + w_kst),
+              cached && d.kc.lines_slots ? static_cast<const uint32_t*>(d.kc.lines.p) : nullptr};
     auto* srec = reinterpret_cast<uint32_t*>(w + w_srec);
     auto* hrec = reinterpret_cast<uint32_t*>(w + w_hrec);
     auto* arec = reinterpret_cast<uint32_t*>(w + w_arec);
@@ -895,7 +936,9 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
         BLS_HIP(hipEventRecord(L.ev[7], s0));
         hipLaunchKernelGGL(k_blsw_pair, dim3((unsigned)n), dim3(64), 0, s0, (uint32_t)n, (const uint32_t*)srec,
                            (const int32_t*)sdec, wave_small ? (const uint32_t*)hh : (const uint32_t*)hrec,
-                           wave_small ? 1 : 0, (const uint32_t*)ajrec, (const int32_t*)sapk, spair);
+                           wave_small ? 1 : 0, (const uint32_t*)ajrec, (const int32_t*)sapk, kt,
+                           reinterpret_cast<const uint32_t*>(in + o_off), reinterpret_cast<const uint32_t*>(in + o_cnt),
+                           reinterpret_cast<const uint32_t*>(in + o_idx), spair);
         BLS_HIP(hipEventRecord(L.ev[8], s0));
         BLS_HIP(hipStreamWaitEvent(s0, L.ev[13], 0));
         hipLaunchKernelGGL(k_blsw_status, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n,
