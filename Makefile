@@ -5,7 +5,8 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 BLS_SRC := narwhal_amd/csrc/nwv_bls.hip narwhal_amd/csrc/bls381.h narwhal_amd/csrc/bls_verify.h narwhal_amd/csrc/bls_group.h \
-	narwhal_amd/csrc/bls381_consts.h narwhal_amd/csrc/bls381_iso.h include/nwv_bls.h
+	narwhal_amd/csrc/bls381_consts.h narwhal_amd/csrc/bls381_iso.h narwhal_amd/csrc/bls_wave.h \
+	narwhal_amd/csrc/bls_wave_prog.h include/nwv_bls.h
 CSRC := $(filter-out $(BLS_SRC),$(wildcard narwhal_amd/csrc/*.h narwhal_amd/csrc/*.hip narwhal_amd/csrc/*.cpp)) \
 	include/nwv.h include/nwv_types.h include/nwv_service.h
 

@@ -910,7 +910,7 @@ def main():
         configs["C4"], cdata["C4"] = CL.leg_c4(eng)
         configs["C5"], cdata["C5"] = CL.leg_c5(eng)
         # the reference's default scheme, BLS12-381 (GPU legs, oracle checks, CPU baseline)
-        configs["BLS"] = CL.leg_bls(eng, threads, cpu=not args.no_cpu_baseline)
+        configs["BLS"] = CL.leg_bls(eng, threads, cpu=not args.no_cpu_baseline, peak=peak)
         if not args.no_cpu_baseline:
             for k, v in cpu_baseline_configs(configs, cdata, threads).items():
                 configs[k]["cpu_baseline"] = v

@@ -95,6 +95,20 @@ def load():
     return lib
 
 
+def bls_source_hash():
+    """sha256 (16 hex digits) over the BLS12-381 device sources (nwv_bls.hip, bls*.h and the wave
+    tables bls_wave_prog.h): committed BLS rocprofv3 --pmc summaries carry it"""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    fs = glob.glob(os.path.join(_HERE, "csrc", "bls*.h")) + [os.path.join(_HERE, "csrc", "nwv_bls.hip")]
+    for f in sorted(fs):
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def kernel_source_hash():
     """sha256 (16 hex digits) over the Ed25519 / BLAKE2b device-code sources (narwhal_amd/csrc/*.hip,
     *.h; the BLS12-381 translation unit nwv_bls.hip and its bls*.h headers are not part of those

@@ -428,8 +428,78 @@ def _bls_round_items(b, sks, rnd, certs, quorum):
     return aggs, signers, digests
 
 
+def bls_pairing_products(fixed_lines=True):
+    """Fp products of one pairing check on the wave engine (narwhal_amd/csrc/bls_wave.h
+    pairing_check + final_exp, the program counts tools/gen_bls_wave.py writes to
+    bls_wave_counts.json; multiplications by one of combination lanes not counted), and the
+    v_mad_u64_u32 of one product (14 x 14 limb products + 14 reduction rows of 14)"""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "narwhal_amd", "csrc",
+                           "bls_wave_counts.json")) as f:
+        meta = json.load(f)
+    pc = {k: v["products"] for k, v in meta["programs"].items()}
+    kind = "fixed" if fixed_lines else "step"
+    ml = sum(pc[f"ml_{'add' if c == 'a' else 'dbl'}_{kind}"] for c in meta["steps"])
+    xbits = bin(meta["x_abs"])[3:]  # below the top bit
+    exp_x = len(xbits) * pc["cyc_sqr_F"]
+    fe = (pc["inv_a"] + pc["inv_b"] + pc["easy1"] + pc["easy2"] + 5 * exp_x
+          + xbits.count("1") * (pc["mul_F_M"] + 2 * pc["mul_F_A"] + pc["mul_F_B"] + pc["mul_F_C"])
+          + pc["mulconj_F_M"] + pc["mulconj_F_A"] + pc["conjmulfrob_F_A"] + pc["conjmulfrob2_F_B"]
+          + pc["mulconj2_F_B"] + pc["cycsqrM_mul_M_to_G"] + pc["mul_F_G"])
+    return {"miller_loop": ml, "final_exp": fe, "total": ml + fe, "mads_per_product": meta["mads_per_product"]}
+
+
+def bls_pmc(n_items, kernel="k_blsw_pair"):
+    """(counters, source) of `kernel` from the newest committed BLS rocprofv3 --pmc summary
+    (tools/gpurun/r4_bls_prof.sh -> profiles/*bls_pmc*.json) whose bls_source_hash is HEAD's and
+    whose size is n_items; else (None, None)"""
+    import glob
+    import json
+    import os
+    from narwhal_amd._lib import bls_source_hash
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    want = bls_source_hash()
+    for f in sorted(glob.glob(os.path.join(root, "profiles", "*bls_pmc*.json")), reverse=True):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if d.get("n") == n_items and d.get("bls_source_hash") == want and kernel in d.get("kernels", {}):
+            return d["kernels"][kernel], os.path.relpath(f, root)
+    return None, None
+
+
+def bls_roofline(n_items, pairing_ms, peak, fixed_lines=True):
+    """the dominant BLS kernel (k_blsw_pair: every item's pairing check on its own wave) against
+    the measured v_mad_u64_u32 rate; with a committed PMC pass of HEAD's BLS sources also its VALU
+    issue floor (instructions at the measured rates) and HBM traffic"""
+    mad_peak_ts = (peak["v_mad_u64_u32_per_s"] / 1e12) if peak else None
+    c = bls_pairing_products(fixed_lines)
+    mads = c["total"] * c["mads_per_product"] * n_items
+    a = mads / (pairing_ms * 1e-3) / 1e12 if pairing_ms > 0 else None
+    pmc, src = bls_pmc(n_items)
+    floor = traffic = None
+    if pmc and peak and "SQ_INSTS_VALU" in pmc and "SQ_INSTS_VALU_INT64" in pmc and pairing_ms > 0:
+        v, i64 = pmc["SQ_INSTS_VALU"], pmc["SQ_INSTS_VALU_INT64"]
+        fs = i64 * 64 / peak["v_mad_u64_u32_per_s"] + (v - i64) * 64 / peak["v_add_u32_per_s"]
+        floor = {"valu_insts_per_launch": v, "int64_insts": i64, "floor_ms": fs * 1e3, "frac": fs / (pairing_ms * 1e-3),
+                 "source": src}
+    if pmc and "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
+        traffic = 2 * pmc["FETCH_SIZE"] * 1024 + pmc["WRITE_SIZE"] * 1024
+    return {"kernel": "k_blsw_pair", "bound": "valu", "achieved": a, "unit": "T v_mad_u64_u32/s", "peak": mad_peak_ts,
+            "frac": (a / mad_peak_ts) if (a and mad_peak_ts) else None, "kernel_ms": pairing_ms,
+            "mads_per_launch": mads, "items": n_items, "issue_floor": floor, "traffic": traffic,
+            "pmc_source": src,
+            "algorithmic": f"{c['total']} Fp products per pairing check ({c['miller_loop']} Miller loop with "
+                           f"{'precomputed' if fixed_lines else 'computed'} key lines, {c['final_exp']} final "
+                           f"exponentiation; tools/gen_bls_wave.py counts) x {c['mads_per_product']} multiply-adds x "
+                           f"{n_items} items"}
+
+
 def leg_bls(eng, threads=1, certs=100, quorum=67, committee=100, reps=20, throughput_n=16384, single_reps=200,
-            dag_rounds=20, concurrency=8, cpu=True):
+            dag_rounds=20, concurrency=8, cpu=True, peak=None):
     """SURVEY §8 row f4, the reference's default scheme (crypto/src/lib.rs:29-33 -> BLS12-381
     min_sig), host -> host, synthetic keys / messages (signatures and aggregates made on the GPU),
     the committee registered in the key cache (epoch start):
@@ -477,6 +547,18 @@ def leg_bls(eng, threads=1, certs=100, quorum=67, committee=100, reps=20, throug
         assert rc == 0
     assert b.verify(pks[0], m + b"!", s1) == _lib.NWV_ERR_SIGNATURE
     out["single_verify"] = dict(_pcts(t1), kernel_ms=b.last_kernel_ms())
+    # AggregateAuthenticator::aggregate of a quorum's votes (Certificate::new_unsafe,
+    # types/src/primary.rs:476-477): `quorum` compressed signatures -> their sum
+    vs = b.sign(sks[:quorum], [m] * quorum)
+    ta = []
+    for i in range(single_reps + 3):
+        t0 = time.perf_counter()
+        rc, agg_sig, _ = b.aggregate(vs)
+        if i >= 3:
+            ta.append(time.perf_counter() - t0)
+        assert rc == 0
+    assert b.aggregate_verify(agg_sig, pks[:quorum], m) == 0
+    out["aggregate"] = dict(_pcts(ta), signatures=quorum)
     # concurrent single verifies: one thread, then `concurrency` threads, for the same wall time
     sig_k = b.sign(sks[:concurrency], [m] * concurrency)
 
@@ -517,6 +599,7 @@ def leg_bls(eng, threads=1, certs=100, quorum=67, committee=100, reps=20, throug
         out["throughput"] = {"items": n, "ms_host_to_host": float(np.median(t2)) * 1e3,
                              "verifies_per_s": n / float(np.median(t2)), "path": b.last_path(),
                              "kernel_ms": {k: float(np.median([x[k] for x in km2])) for k in km2[0]}}
+        out["roofline"] = bls_roofline(n, out["throughput"]["kernel_ms"]["pairing_check"], peak)
         sample = sorted(rnd.choice(n, 48, replace=False).tolist())
         tp_check = ([sigs[k] for k in sample], [[kidx[k]] for k in sample], [msgs[k] for k in sample])
     out["dag_round"] = leg_bls_dag(eng, b, sks, pks, rnd, dag_rounds)

@@ -24,6 +24,7 @@ program whose bounds could break the limb arithmetic (int32 limb sums, product <
 Usage: python3 tools/gen_bls_wave.py [--check]   (--check: verify every program numerically and
 against independent big-integer arithmetic, write nothing)
 """
+import json
 import os
 import random
 import sys
@@ -1521,6 +1522,17 @@ def emit(compiled, path):
     L.append("}  // namespace bls")
     with open(path, "w") as f:
         f.write("\n".join(L) + "\n")
+    # per-program Fp product counts (the algorithmic work: combination lanes multiplied by one are
+    # not counted) for bench.py's roofline
+    counts = {name: {"stages": len(compiled[name].stages),
+                     "products": sum(1 for a in compiled[name].order if a.kind == "mul"),
+                     "product_lanes": sum(1 for st in compiled[name].stages for r in st if r["mul"])}
+              for name in names}
+    meta = {"generated_by": "tools/gen_bls_wave.py", "mads_per_product": 2 * NL * NL, "steps": "".join(miller_steps()),
+            "x_abs": X_ABS, "programs": counts}
+    with open(os.path.join(os.path.dirname(path), "bls_wave_counts.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+        f.write("\n")
     return len(stages), len(data)
 
 

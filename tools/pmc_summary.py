@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--note", default="")
     ap.add_argument("--launch-list", default="", help="comma-separated kernels of the profiled pipeline")
+    ap.add_argument("--bls", action="store_true", help="a BLS12-381 pass: record the BLS sources' hash")
     a = ap.parse_args()
     sums = collections.defaultdict(lambda: collections.defaultdict(float))
     cnt = collections.defaultdict(lambda: collections.defaultdict(set))
@@ -31,9 +32,11 @@ def main():
                     sums[k][c] += v
                     cnt[k][c].add(did)
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    from narwhal_amd._lib import kernel_source_hash
+    from narwhal_amd._lib import bls_source_hash, kernel_source_hash
     out = {"n": a.n, "note": a.note, "kernels": {}, "kernel_source_hash": kernel_source_hash(),
            "launch_list": a.launch_list.split(",") if a.launch_list else None}
+    if a.bls:
+        out["bls_source_hash"] = bls_source_hash()
     for k, cs in sums.items():
         out["kernels"][k] = {c: v / max(1, len(cnt[k][c])) for c, v in cs.items()}
     with open(a.out, "w") as fh:
