@@ -84,10 +84,11 @@ extern "C" __global__ void __launch_bounds__(256) k_ed_points(
     atomicOr(flags + i, f);
 }
 
-extern "C" __global__ void __launch_bounds__(256) k_ed_straus(
-    uint64_t n, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ kbuf,
-    const uint32_t* __restrict__ tables, const uint32_t* __restrict__ flags,
-    const uint32_t* __restrict__ btab, uint64_t* __restrict__ verdict) {
+template <bool PF>
+__device__ __forceinline__ void ed_straus_body(uint64_t n, const uint8_t* __restrict__ sig,
+                                               const uint8_t* __restrict__ kbuf, const uint32_t* __restrict__ tables,
+                                               const uint32_t* __restrict__ flags, const uint32_t* __restrict__ btab,
+                                               uint64_t* __restrict__ verdict) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63;
     bool ok = false;
@@ -95,11 +96,26 @@ extern "C" __global__ void __launch_bounds__(256) k_ed_straus(
         uint32_t Sw[8], k[8];
         load_words8(sig + 64 * i + 32, Sw);
         load_words8(kbuf + 32 * i, k);
-        const bool eq = lane_straus_check(k, Sw, tables + i * LANE_SCRATCH_WORDS, btab);
+        const bool eq = lane_straus_check<PF>(k, Sw, tables + i * LANE_SCRATCH_WORDS, btab);
         ok = eq && flags[i] == FLAGS_ALL;
     }
     const uint64_t mask = __ballot(ok);
     if (lane == 0 && i - lane < n) verdict[i >> 6] = mask;
+}
+extern "C" __global__ void __launch_bounds__(256) k_ed_straus(
+    uint64_t n, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ kbuf,
+    const uint32_t* __restrict__ tables, const uint32_t* __restrict__ flags,
+    const uint32_t* __restrict__ btab, uint64_t* __restrict__ verdict) {
+    ed_straus_body<false>(n, sig, kbuf, tables, flags, btab, verdict);
+}
+// the same with each window's A / R table entries loaded one window ahead (more registers, fewer
+// waves per SIMD): the default (C4 2.34 -> 2.29 ms, tools/gpurun/r4_c4_pf.sh); NWV_STRAUS_PF=0
+// selects k_ed_straus
+extern "C" __global__ void __launch_bounds__(256) k_ed_straus_pf(
+    uint64_t n, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ kbuf,
+    const uint32_t* __restrict__ tables, const uint32_t* __restrict__ flags,
+    const uint32_t* __restrict__ btab, uint64_t* __restrict__ verdict) {
+    ed_straus_body<true>(n, sig, kbuf, tables, flags, btab, verdict);
 }
 
 // RFC 8032: a = clamp(SHA-512(seed)[0..32]), prefix = [32..64], A = [a]B,

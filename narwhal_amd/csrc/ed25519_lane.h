@@ -236,6 +236,7 @@ NWV_HD int take_top5(uint32_t y[5], int w) {
 // [8]([w]B - [m]R + [cu]A) == identity, w = m s mod l, m = |v|, c = -1 (v > 0) or +1 (v < 0):
 // the cofactored check [8]([s]B - R - [k]A) == identity on half-size scalars (header comment).
 // tbl: entries 0..8 = j A, R_ENTRY + j = j R; btab: BTAB_WORDS (j B, identity, j 2^128 B).
+template <bool PF = false>
 NWV_HD bool lane_straus_check_half(const uint32_t k[8], const uint32_t Sw[8], const uint32_t* tbl,
                                    const uint32_t* btab) {
     uint32_t yu[5], ym[5], ylo[5], yhi[5];
@@ -254,15 +255,40 @@ NWV_HD bool lane_straus_check_half(const uint32_t k[8], const uint32_t Sw[8], co
     const uint32_t* bt128 = btab + BASE128_TABLE_OFFSET;
     ge_p2 r = ge_p2_identity();
     ge_p1p1 t;
+    // the lane's A and R table entries of a window are loaded one window ahead: the loads of
+    // window i - 1 are issued once window i's have been consumed, so they complete behind the B
+    // additions and the next four doublings instead of stalling the addition that needs them
+    // (two 40-word entries in registers)
+    // (PF; without it each addition reads its entry when it needs it)
+    uint32_t ea[PF ? 40 : 1], er[PF ? 40 : 1];
+    int ad = 0, rd = 0;
+    if (PF) {
+        ad = vneg ? take_top5(yu, 4) : -take_top5(yu, 4);
+        rd = -take_top5(ym, 4);
+        load_cached_entry(tbl + (ad < 0 ? -ad : ad) * CACHED_ENTRY_WORDS, ad < 0, ea);
+        load_cached_entry(rt + (rd < 0 ? -rd : rd) * CACHED_ENTRY_WORDS, rd < 0, er);
+    }
 #pragma unroll 1
     for (int i = 32; i >= 0; i--) {
         ge_p3 p = (i == 32) ? ge_p3_identity() : ge_p1p1_to_p3(dbl4(r));
-        const int du = take_top5(yu, 4);
-        const int ad = vneg ? du : -du;  // A's coefficient: -u (v > 0) or +u (v < 0)
-        t = ge_add_entry(p, tbl + (ad < 0 ? -ad : ad) * CACHED_ENTRY_WORDS, ad < 0);
-        const int rd = -take_top5(ym, 4);  // R's coefficient: -m
-        p = ge_p1p1_to_p3(t);
-        t = ge_add_entry(p, rt + (rd < 0 ? -rd : rd) * CACHED_ENTRY_WORDS, rd < 0);
+        if (PF) {
+            t = ge_add_loaded(p, ea);
+            p = ge_p1p1_to_p3(t);
+            t = ge_add_loaded(p, er);
+            if (i > 0) {
+                ad = vneg ? take_top5(yu, 4) : -take_top5(yu, 4);
+                rd = -take_top5(ym, 4);
+                load_cached_entry(tbl + (ad < 0 ? -ad : ad) * CACHED_ENTRY_WORDS, ad < 0, ea);
+                load_cached_entry(rt + (rd < 0 ? -rd : rd) * CACHED_ENTRY_WORDS, rd < 0, er);
+            }
+        } else {
+            const int du = take_top5(yu, 4);
+            ad = vneg ? du : -du;  // A's coefficient: -u (v > 0) or +u (v < 0)
+            t = ge_add_entry(p, tbl + (ad < 0 ? -ad : ad) * CACHED_ENTRY_WORDS, ad < 0);
+            rd = -take_top5(ym, 4);  // R's coefficient: -m
+            p = ge_p1p1_to_p3(t);
+            t = ge_add_entry(p, rt + (rd < 0 ? -rd : rd) * CACHED_ENTRY_WORDS, rd < 0);
+        }
         if ((i & 1) == 0) {
             const int dl = take_top5(ylo, 8), dh = take_top5(yhi, 8);
             p = ge_p1p1_to_p3(t);
@@ -308,9 +334,10 @@ NWV_HD uint32_t lane_points(const uint32_t Aw[8], const uint32_t Rw[8], uint32_t
     return lane_point_R(Rw, tbl) | lane_point_A(Aw, tbl);
 }
 // phase 3: [8]([s]B - [k]A - R) == identity, on half-size scalars
+template <bool PF = false>
 NWV_HD bool lane_straus_check(const uint32_t k[8], const uint32_t Sw[8], const uint32_t* tbl,
                               const uint32_t* btab) {
-    return lane_straus_check_half(k, Sw, tbl, btab);
+    return lane_straus_check_half<PF>(k, Sw, tbl, btab);
 }
 
 // Full single verification.  tbl: lane scratch (LANE_SCRATCH_WORDS words).

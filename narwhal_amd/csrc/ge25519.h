@@ -107,6 +107,24 @@ NWV_HD ge_p1p1 ge_add_entry(const ge_p3& p, const uint32_t* e, bool neg) {
     fe MM = fe_mul(fe_sub(p.Y, p.X), load_fe(e + (neg ? 0 : 10)));
     return ge_p1p1{fe_sub(PP, MM), fe_add(PP, MM), fe_add(ZZ2, TT2d), fe_sub(ZZ2, TT2d)};
 }
+// the 40 words of a cached entry that p + (neg ? -Q : Q) reads (Y+X, Y-X swapped and -2dT for -Q)
+NWV_HD void load_cached_entry(const uint32_t* e, bool neg, uint32_t out[40]) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        out[i] = e[(neg ? 10 : 0) + i];
+        out[10 + i] = e[(neg ? 0 : 10) + i];
+        out[20 + i] = e[20 + i];
+        out[30 + i] = e[(neg ? 40 : 30) + i];
+    }
+}
+// p + Q', Q' the words load_cached_entry fetched
+NWV_HD ge_p1p1 ge_add_loaded(const ge_p3& p, const uint32_t q[40]) {
+    fe TT2d = fe_mul(p.T, load_fe(q + 30));
+    fe ZZ2 = fe_mul(p.Z, load_fe(q + 20));
+    fe PP = fe_mul(fe_add(p.Y, p.X), load_fe(q));
+    fe MM = fe_mul(fe_sub(p.Y, p.X), load_fe(q + 10));
+    return ge_p1p1{fe_sub(PP, MM), fe_add(PP, MM), fe_add(ZZ2, TT2d), fe_sub(ZZ2, TT2d)};
+}
 // p + (neg ? -Q : Q), Q a precomp entry (mixed addition)
 NWV_HD ge_p1p1 ge_madd_entry(const ge_p3& p, const uint32_t* e, bool neg) {
     fe Txy2d = fe_mul(p.T, load_fe(e + (neg ? 30 : 20)));

@@ -398,7 +398,11 @@ int ed_launch(Lane& d, EdBuffers& b, size_t n, hipStream_t stream, hipEvent_t* e
         hipLaunchKernelGGL(k_ed_points, grid2, blk, 0, stream, (uint64_t)n, b.pk.as<uint8_t>(),
                            b.sig.as<uint8_t>(), b.tables.as<uint32_t>(), b.flags.as<uint32_t>());
     if (ev) NWV_HIP(hipEventRecord(ev[2], stream));
-    hipLaunchKernelGGL(k_ed_straus, grid, blk, 0, stream, (uint64_t)n, b.sig.as<uint8_t>(),
+    static const bool straus_pf = [] {
+        const char* e = std::getenv("NWV_STRAUS_PF");  // the prefetching form unless NWV_STRAUS_PF=0
+        return !(e && e[0] == '0');
+    }();
+    hipLaunchKernelGGL(straus_pf ? k_ed_straus_pf : k_ed_straus, grid, blk, 0, stream, (uint64_t)n, b.sig.as<uint8_t>(),
                        b.kbuf.as<uint8_t>(), b.tables.as<uint32_t>(), b.flags.as<uint32_t>(),
                        d.btab().as<uint32_t>(), b.verdict.as<uint64_t>());
     if (ev) NWV_HIP(hipEventRecord(ev[3], stream));

@@ -5,6 +5,7 @@
 #define NWV_HD __host__ __device__ inline
 #define NWV_COUNT_OPS 1
 unsigned long long nwv_count_mul = 0, nwv_count_sq = 0;
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -137,6 +138,8 @@ int he_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_
     uint32_t f = lane_hash(Aw, Rw, Sw, m.data(), len, k);
     f |= lane_points(Aw, Rw, tbl.data());
     const bool eq = lane_straus_check(k, Sw, tbl.data(), g_btab.data());
+    // the prefetching form (k_ed_straus_pf) must agree on every input
+    if (lane_straus_check<true>(k, Sw, tbl.data(), g_btab.data()) != eq) std::abort();
     return (eq && f == FLAGS_ALL) ? 1 : 0;
 }
 
