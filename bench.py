@@ -774,6 +774,9 @@ def main():
     ap.add_argument("--single-steps", type=int, default=8,
                     help="single-stream steps timed after the run (step latency, per-kernel times)")
     ap.add_argument("--h2h-seconds", type=float, default=2.0)
+    ap.add_argument("--headline-only", action="store_true",
+                    help="only the timed headline steps (no 1K latency, host-to-host, configs or CPU baseline): "
+                         "a rocprofv3 trace of this run is the headline alone")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -853,9 +856,13 @@ def main():
     dt, kt, stats = h["dt"], h["kt"], h["stats"]
     value = args.n * args.steps / dt
     threads = usable_cpus()
-    lat = latency_1k(eng, h["data"], args.latency_reps)
-    lat["device_breakdown"] = kernels_1k(eng, h["data"]) if args.mode == 1 else None
-    h2h = host_to_host(eng, h["data"], 4, args.h2h_seconds) if args.h2h_seconds > 0 else None
+    if args.headline_only:
+        args.no_configs = args.no_cpu_baseline = True
+        lat, h2h = None, None
+    else:
+        lat = latency_1k(eng, h["data"], args.latency_reps)
+        lat["device_breakdown"] = kernels_1k(eng, h["data"]) if args.mode == 1 else None
+        h2h = host_to_host(eng, h["data"], 4, args.h2h_seconds) if args.h2h_seconds > 0 else None
     peak = valu_peak()
     if args.mode == 1:
         na = args.keys or args.n
