@@ -309,7 +309,8 @@ NWV_HD bool w_pairing_check(const W& w, const uint32_t* sig_rec, const uint32_t*
 // stage programs.  out: X, Y, Z (x = X / Z, y = Y / Z) and an identity flag (3 NL + 1 words).
 constexpr int G1H_REC_WORDS = 3 * NL + 1;
 template <class W>
-NWV_HD void w_hash_to_g1(const W& w, const uint8_t* msg, uint32_t n, const uint8_t* dst, uint32_t dl, uint32_t* out) {
+NWV_HD void w_hash_to_g1(const W& w, const uint8_t* msg, uint32_t n, const uint8_t* dst, uint32_t dl, uint32_t* out,
+                         bool clear = true) {
     using namespace wave;
     init_slots(w);
     w.lanes(2, [&](int j) {
@@ -324,7 +325,7 @@ NWV_HD void w_hash_to_g1(const W& w, const uint8_t* msg, uint32_t n, const uint8
     });
     w.sync();
     w.run(P_ISO2_ADD);
-    g1_chain(w, BLS_H_EFF);
+    if (clear) g1_chain(w, BLS_H_EFF);  // (else U holds the sum of the two maps)
     w.get_words(REG_U, out, 3);
     w.sync();
     const bool inf = fp_is_zero(w.get(REG_U + 2));

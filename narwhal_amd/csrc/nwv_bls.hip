@@ -74,6 +74,7 @@ struct KeyTab {
     const uint32_t* rs;
     const int32_t* ss;
     const uint32_t* lines;  // cached keys' Miller-loop line tables (KL_WORDS per slot), or null
+    const uint32_t* hrc;    // cached keys' [h_eff] pk records (G2_REC_WORDS per slot), or null
 };
 // words of a registered key's line table: (l0, l1, l4) of every Miller-loop step (w_key_lines)
 constexpr size_t KL_WORDS = (size_t)wave::NSTEPS * 6 * wave::SW;
@@ -179,9 +180,11 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_apk_g(uint32_t n, KeyTab kt, 
 }
 // H(msg_i) on a group: lanes 0-3 map hash_to_field's u_0, lanes 4-7 u_1 (side by side), lane 4
 // hands its point to lane 0 through the group's LDS area, lane 0 adds and clears the cofactor
+// (kmode[i] = 1: item i's cofactor clearing is on its key side -- H0 = the maps' sum, see
+// k_bls_key_heff; kmode may be null)
 __global__ __launch_bounds__(BLS_LANES) void k_bls_h2c_g(uint32_t n, const uint8_t* msg, const uint64_t* off,
                                                          const uint32_t* len, const uint8_t* dst, uint32_t dl,
-                                                         uint32_t* rec) {
+                                                         uint32_t* rec, const uint32_t* kmode) {
     BLS_GIDX();
     const jac<fp> q = h2c_map(msg + off[i], len[i], dst, dl, (g.slot & 4) ? 1 : 0);
     g_sync();
@@ -189,7 +192,8 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_h2c_g(uint32_t n, const uint8
     g_sync();
     const jac<fp> q1 = ld_g1j(g.xa);
     if (g.slot != 0) return;
-    const jac<fp> h = jac_mul64(jac_add(q, q1), BLS_H_EFF);
+    const jac<fp> h0 = jac_add(q, q1);
+    const jac<fp> h = kmode && kmode[i] ? h0 : jac_mul64(h0, BLS_H_EFF);
     fp x = fp_zero(), y = fp_zero();
     if (!h.inf) g1_to_affine(x, y, h);
     st_g1(rec + (size_t)G1_REC_WORDS * i, x, y, h.inf);
@@ -354,9 +358,10 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_pairing_raw(uint32_t n, const
     const wave::Wave w{wm, (int)threadIdx.x}
 // H(msg_i), homogeneous
 __global__ __launch_bounds__(64) void k_blsw_h2c(uint32_t n, const uint8_t* msg, const uint64_t* off,
-                                                 const uint32_t* len, const uint8_t* dst, uint32_t dl, uint32_t* hrec) {
+                                                 const uint32_t* len, const uint8_t* dst, uint32_t dl, uint32_t* hrec,
+                                                 const uint32_t* kmode) {
     BLSW_IDX();
-    w_hash_to_g1(w, msg + off[i], len[i], dst, dl, hrec + (size_t)G1H_REC_WORDS * i);
+    w_hash_to_g1(w, msg + off[i], len[i], dst, dl, hrec + (size_t)G1H_REC_WORDS * i, !(kmode && kmode[i]));
 }
 // signature decode only (one lane per item); the G1 check runs beside the pairing (k_blsw_sub)
 __global__ __launch_bounds__(BLS_LANES) void k_blsw_sigdec(uint32_t n, const uint8_t* sig, uint32_t* rec, int32_t* st) {
@@ -384,15 +389,13 @@ __global__ __launch_bounds__(64) void k_blsw_sub(uint32_t n, const uint32_t* rec
 __global__ __launch_bounds__(64) void k_blsw_pair(uint32_t n, const uint32_t* srec, const int32_t* st_dec,
                                                   const uint32_t* hrec, int h_hom, const uint32_t* arec,
                                                   const int32_t* st_apk, KeyTab kt, const uint32_t* pk_off,
-                                                  const uint32_t* pk_cnt, const uint32_t* pk_idx, int32_t* st_pair) {
+                                                  const uint32_t* pk_cnt, const uint32_t* pk_idx, const uint32_t* kmode,
+                                                  int32_t* st_pair) {
     BLSW_IDX();
     int32_t s = ST_VERIFY_FAIL;
     if (st_dec[i] == ST_OK && st_apk[i] == ST_OK) {
         const uint32_t* ql = nullptr;
-        if (kt.lines && pk_cnt[i] == 1) {
-            const uint32_t k = pk_idx[pk_off[i]];
-            if (k < KC_CAP) ql = kt.lines + KL_WORDS * k;
-        }
+        if (kt.lines && kmode && kmode[i] && pk_cnt[i] == 1) ql = kt.lines + KL_WORDS * pk_idx[pk_off[i]];
         s = w_pairing_check_g(w, srec + (size_t)G1_REC_WORDS * i,
                               hrec + (size_t)(h_hom ? G1H_REC_WORDS : G1_REC_WORDS) * i, h_hom != 0,
                               arec + (size_t)G2J_WORDS * i, true, ql)
@@ -401,7 +404,21 @@ __global__ __launch_bounds__(64) void k_blsw_pair(uint32_t n, const uint32_t* sr
     }
     if (threadIdx.x == 0) st_pair[i] = s;
 }
-// the line tables of newly registered keys: one wave per key (slots[i] = its cache slot)
+// [h_eff] pk of newly registered keys (lane per key, affine records): the hash's cofactor clearing
+// moves onto the key side -- e(H0, [h_eff] pk) = e([h_eff] H0, pk) for H0 in E(Fp), as the
+// reduced pairing sees only H0's G1 component (tests/test_bls_hostemu.py
+// test_wave_cofactor_on_key_side) -- so a cached key's item skips the 64-bit G1 chain on H
+__global__ __launch_bounds__(BLS_LANES) void k_bls_key_heff(uint32_t n, const uint32_t* slots, const uint32_t* rc,
+                                                            uint32_t* hrc) {
+    BLS_IDX();
+    const uint32_t k = slots[i];
+    fp2 x, y;
+    ld_g2(rc + (size_t)G2_REC_WORDS * k, x, y);
+    g2_to_affine(x, y, jac_mul64(jac_from_affine(x, y), BLS_H_EFF));
+    st_g2(hrc + (size_t)G2_REC_WORDS * k, x, y, false);
+}
+// the line tables of newly registered keys (of their [h_eff] pk): one wave per key (slots[i] = its
+// cache slot)
 __global__ __launch_bounds__(64) void k_blsw_key_lines(uint32_t n, const uint32_t* slots, const uint32_t* rc,
                                                        uint32_t* lines) {
     BLSW_IDX();
@@ -414,7 +431,8 @@ __global__ __launch_bounds__(64) void k_blsw_key_lines(uint32_t n, const uint32_
 // The sum stays Jacobian (G2J_WORDS record: the Miller-loop programs take a Jacobian Q), so there
 // is no inversion; a one-key item copies its validated record with Z = 1.
 __global__ __launch_bounds__(64) void k_blsw_apk(uint32_t n, KeyTab kt, const uint32_t* pk_off, const uint32_t* pk_cnt,
-                                                 const uint32_t* pk_idx, uint32_t* rec, int32_t* st_apk) {
+                                                 const uint32_t* pk_idx, const uint32_t* kmode, uint32_t* rec,
+                                                 int32_t* st_apk) {
     __shared__ uint32_t xa[32 * G2J_WORDS];
     const uint32_t i = blockIdx.x;
     if (i >= n) return;
@@ -422,10 +440,13 @@ __global__ __launch_bounds__(64) void k_blsw_apk(uint32_t n, KeyTab kt, const ui
     const uint32_t cnt = pk_cnt[i];
     const uint32_t* idx = pk_idx + pk_off[i];
     uint32_t* out = rec + (size_t)G2J_WORDS * i;
+    // key-side items (every key cached) sum the keys' [h_eff] pk records
+    KeyTab kq = kt;
+    if (kmode && kmode[i]) kq.rc = kt.hrc;
     if (cnt == 1) {
         const uint32_t k = idx[0];
-        const int32_t ks = key_st(kt, k);
-        const uint32_t* kr = key_rec(kt, k);
+        const int32_t ks = key_st(kq, k);
+        const uint32_t* kr = key_rec(kq, k);
         const fp one = k_one();
         for (int wd = lane; wd < G2J_WORDS; wd += 64) {
             uint32_t v = 0;
@@ -443,12 +464,12 @@ __global__ __launch_bounds__(64) void k_blsw_apk(uint32_t n, KeyTab kt, const ui
     uint32_t first_bad = 0xffffffffu;
     for (uint32_t j = (uint32_t)lane; j < cnt; j += 64) {
         const uint32_t k = idx[j];
-        if (key_st(kt, k) != ST_OK) {
+        if (key_st(kq, k) != ST_OK) {
             first_bad = j;
             break;
         }
         fp2 x, y;
-        ld_g2(key_rec(kt, k), x, y);
+        ld_g2(key_rec(kq, k), x, y);
         acc = jac_add(acc, jac_from_affine(x, y));
     }
     for (int m = 32; m >= 1; m >>= 1) first_bad = min(first_bad, (uint32_t)__shfl_xor((int)first_bad, m));
@@ -462,7 +483,7 @@ __global__ __launch_bounds__(64) void k_blsw_apk(uint32_t n, KeyTab kt, const ui
     if (lane != 0) return;
     int32_t status = ST_OK;
     if (cnt == 0) status = ST_AGGR_MISMATCH;
-    else if (first_bad != 0xffffffffu) status = key_st(kt, idx[first_bad]);
+    else if (first_bad != 0xffffffffu) status = key_st(kq, idx[first_bad]);
     else if (acc.inf) status = ST_PK_INFINITY;
     if (status != ST_OK) {
         acc.inf = true;
@@ -532,6 +553,7 @@ struct HBuf {
 struct BlsKeyCache {
     std::shared_mutex mu;
     DBuf rec, st;  // KC_CAP x G2_REC_WORDS u32 records, KC_CAP int32 statuses
+    DBuf hrec;     // KC_CAP x G2_REC_WORDS: [h_eff] pk of each slot
     DBuf lines;    // line tables of slots [0, used): KL_WORDS u32 each (grown as keys register)
     uint32_t lines_slots = 0;
     std::unordered_map<std::string, uint32_t> slot;
@@ -679,7 +701,8 @@ int keycache_register(BlsDev& d, size_t n_keys, const uint8_t* keys) {
     if (lane.rc()) return lane.rc();
     std::unique_lock<std::shared_mutex> g(d.kc.mu);
     int rc;
-    if ((rc = d.kc.rec.ensure((size_t)4 * G2_REC_WORDS * KC_CAP)) || (rc = d.kc.st.ensure((size_t)4 * KC_CAP)))
+    if ((rc = d.kc.rec.ensure((size_t)4 * G2_REC_WORDS * KC_CAP)) || (rc = d.kc.st.ensure((size_t)4 * KC_CAP)) ||
+        (rc = d.kc.hrec.ensure((size_t)4 * G2_REC_WORDS * KC_CAP)))
         return rc;
     std::vector<std::string> fresh;
     std::vector<uint8_t> fk;
@@ -742,8 +765,11 @@ int keycache_register(BlsDev& d, size_t n_keys, const uint8_t* keys) {
         std::swap(d.kc.lines.cap, nb.cap);
         d.kc.lines_slots = cap;
     }
-    hipLaunchKernelGGL(k_blsw_key_lines, dim3((unsigned)nv), dim3(64), 0, lane->stream, (uint32_t)nv,
+    hipLaunchKernelGGL(k_bls_key_heff, dim3(kBlocks(nv)), dim3(BLS_LANES), 0, lane->stream, (uint32_t)nv,
                        reinterpret_cast<const uint32_t*>(w + o_dst), static_cast<const uint32_t*>(d.kc.rec.p),
+                       static_cast<uint32_t*>(d.kc.hrec.p));
+    hipLaunchKernelGGL(k_blsw_key_lines, dim3((unsigned)nv), dim3(64), 0, lane->stream, (uint32_t)nv,
+                       reinterpret_cast<const uint32_t*>(w + o_dst), static_cast<const uint32_t*>(d.kc.hrec.p),
                        static_cast<uint32_t*>(d.kc.lines.p));
     BLS_HIP(hipGetLastError());
     BLS_HIP(hipStreamSynchronize(lane->stream));
@@ -811,6 +837,15 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     }
     std::vector<uint32_t> remap(n_idx);
     for (size_t t = 0; t < n_idx; t++) remap[t] = ktab[pk_idx[t]];
+    // key-side cofactor clearing (wave path): items whose keys are all in the cache use the keys'
+    // [h_eff] pk records and line tables, and their hash skips the h_eff chain
+    const bool kside = wavem && cached && d.kc.lines_slots;
+    std::vector<uint32_t> kmode(kside ? n : 0);
+    for (size_t i = 0; i < kmode.size(); i++) {
+        bool all = pk_cnt[i] > 0;
+        for (uint32_t j = 0; j < pk_cnt[i] && all; j++) all = remap[pk_off[i] + j] < KC_CAP;
+        kmode[i] = all ? 1u : 0u;
+    }
     const size_t n_dec = fill_slot.size();  // keys decoded by this call
     uint8_t seed[32];
     nwv_internal_fill_seed(nullptr, seed);  // the batch coefficients' key: OS entropy per call
@@ -821,7 +856,7 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
                  o_idx = a.add(n_idx ? (const void*)remap.data() : zero, 4 * n_idx + 4),
                  o_msg = a.add(msg_bytes ? (const void*)msg_base : zero, msg_bytes + 1),
                  o_moff = a.add(msg_off, 8 * n), o_mlen = a.add(msg_len, 4 * n), o_dst = a.add(dst, dl),
-                 o_seed = a.add(seed, 32);
+                 o_seed = a.add(seed, 32), o_kmode = a.add(kside ? (const void*)kmode.data() : zero, 4 * kmode.size() + 4);
     if ((rc = L.stage.ensure(al256(a.total) + 64)) || (rc = L.in.ensure(a.total))) return rc;
     uint8_t* h = static_cast<uint8_t*>(L.stage.p);
     for (size_t k = 0; k < a.parts.size(); k++)
@@ -844,7 +879,9 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     KeyTab kt{cached ? static_cast<const uint32_t*>(d.kc.rec.p) : nullptr,
               cached ? static_cast<const int32_t*>(d.kc.st.p) : nullptr, reinterpret_cast<uint32_t*>(w + w_krec),
               reinterpret_cast<int32_t*>(w + w_kst),
-              cached && d.kc.lines_slots ? static_cast<const uint32_t*>(d.kc.lines.p) : nullptr};
+              cached && d.kc.lines_slots ? static_cast<const uint32_t*>(d.kc.lines.p) : nullptr,
+              cached ? static_cast<const uint32_t*>(d.kc.hrec.p) : nullptr};
+    const uint32_t* km = kside ? reinterpret_cast<const uint32_t*>(in + o_kmode) : nullptr;
     auto* srec = reinterpret_cast<uint32_t*>(w + w_srec);
     auto* hrec = reinterpret_cast<uint32_t*>(w + w_hrec);
     auto* arec = reinterpret_cast<uint32_t*>(w + w_arec);
@@ -891,7 +928,7 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     if (wavem)
         hipLaunchKernelGGL(k_blsw_apk, dim3((unsigned)n), dim3(64), 0, s1, (uint32_t)n, kt,
                            reinterpret_cast<const uint32_t*>(in + o_off), reinterpret_cast<const uint32_t*>(in + o_cnt),
-                           reinterpret_cast<const uint32_t*>(in + o_idx), ajrec, sapk);
+                           reinterpret_cast<const uint32_t*>(in + o_idx), km, ajrec, sapk);
     else
         hipLaunchKernelGGL(k_bls_apk_g, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s1, (uint32_t)n, kt,
                            reinterpret_cast<const uint32_t*>(in + o_off), reinterpret_cast<const uint32_t*>(in + o_cnt),
@@ -903,11 +940,11 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     if (wave_small)
         hipLaunchKernelGGL(k_blsw_h2c, dim3((unsigned)n), dim3(64), 0, s2, (uint32_t)n, in + o_msg,
                            reinterpret_cast<const uint64_t*>(in + o_moff),
-                           reinterpret_cast<const uint32_t*>(in + o_mlen), in + o_dst, (uint32_t)dl, hh);
+                           reinterpret_cast<const uint32_t*>(in + o_mlen), in + o_dst, (uint32_t)dl, hh, km);
     else
         hipLaunchKernelGGL(k_bls_h2c_g, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s2, (uint32_t)n, in + o_msg,
                            reinterpret_cast<const uint64_t*>(in + o_moff),
-                           reinterpret_cast<const uint32_t*>(in + o_mlen), in + o_dst, (uint32_t)dl, hrec);
+                           reinterpret_cast<const uint32_t*>(in + o_mlen), in + o_dst, (uint32_t)dl, hrec, km);
     BLS_HIP(hipEventRecord(L.ev[6], s2));
     BLS_HIP(hipEventRecord(L.ev[11], s2));
     if (wavem) {
@@ -938,7 +975,7 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
                            (const int32_t*)sdec, wave_small ? (const uint32_t*)hh : (const uint32_t*)hrec,
                            wave_small ? 1 : 0, (const uint32_t*)ajrec, (const int32_t*)sapk, kt,
                            reinterpret_cast<const uint32_t*>(in + o_off), reinterpret_cast<const uint32_t*>(in + o_cnt),
-                           reinterpret_cast<const uint32_t*>(in + o_idx), spair);
+                           reinterpret_cast<const uint32_t*>(in + o_idx), km, spair);
         BLS_HIP(hipEventRecord(L.ev[8], s0));
         BLS_HIP(hipStreamWaitEvent(s0, L.ev[13], 0));
         hipLaunchKernelGGL(k_blsw_status, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n,

@@ -278,6 +278,42 @@ int bh_w2_fast_aggregate_verify(const uint8_t* sig, size_t n_pks, const uint8_t*
     return w_pairing_check_h(w, srec, hrec, arec, nullptr) ? ST_OK : ST_VERIFY_FAIL;
 }
 
+// the same check with the cofactor clearing moved from H onto the key sum:
+// e(H0, [h_eff] apk) for H0 = iso(SSWU(u0)) + iso(SSWU(u1)) (not cleared); mode 1 = computed lines,
+// 2 = the line table of [h_eff] apk
+int bh_w3_fast_aggregate_verify(const uint8_t* sig, size_t n_pks, const uint8_t* pks, const uint8_t* msg, size_t n,
+                                const uint8_t* dst, size_t dl, int mode) {
+    int32_t st = bh_w_sig_status(sig);
+    if (st != ST_OK) return st;
+    uint32_t srec[G1_REC_WORDS], hrec[G1H_REC_WORDS], arec[G2_REC_WORDS];
+    fp x, y;
+    bool inf;
+    g1_decompress(x, y, inf, sig);
+    st_g1(srec, inf ? fp_zero() : x, inf ? fp_zero() : y, inf);
+    if (n_pks == 0) return ST_AGGR_MISMATCH;
+    std::vector<uint32_t> krec(G2_REC_WORDS * n_pks), idx(n_pks);
+    std::vector<int32_t> kst(n_pks);
+    for (size_t i = 0; i < n_pks; i++) {
+        kst[i] = key_decode(pks + 96 * i, krec.data() + G2_REC_WORDS * i);
+        idx[i] = (uint32_t)i;
+    }
+    st = apk_record(krec.data(), kst.data(), idx.data(), (uint32_t)n_pks, arec);
+    if (st != ST_OK) return st;
+    fp2 ax, ay;
+    ld_g2(arec, ax, ay);
+    const jac<fp2> hq = jac_mul64(jac_from_affine(ax, ay), BLS_H_EFF);
+    g2_to_affine(ax, ay, hq);
+    st_g2(arec, ax, ay, false);
+    const wave::Wave w = host_wave();
+    w_hash_to_g1(w, msg, (uint32_t)n, dst, (uint32_t)dl, hrec, false);
+    std::vector<uint32_t> tab;
+    if (mode == 2) {
+        tab.resize((size_t)wave::NSTEPS * 6 * NL);
+        w_key_lines(w, arec, tab.data());
+    }
+    return w_pairing_check_h(w, srec, hrec, arec, mode == 2 ? tab.data() : nullptr) ? ST_OK : ST_VERIFY_FAIL;
+}
+
 // the variable-time inversion of the wave engine's final exponentiation (plain big-endian in / out)
 void bh_fp_inv_vt(const uint8_t* a, uint8_t* out) {
     fp x;

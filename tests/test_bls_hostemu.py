@@ -40,6 +40,7 @@ def emu():
     L.bh_w_hash_to_g1.argtypes = [c, sz, c, sz, vp]
     L.bh_w_sig_status.argtypes = [c]
     L.bh_w2_fast_aggregate_verify.argtypes = [c, sz, c, c, sz, c, sz]
+    L.bh_w3_fast_aggregate_verify.argtypes = [c, sz, c, c, sz, c, sz, ctypes.c_int]
     L.bh_fp_inv_vt.argtypes = [c, vp]
     return L
 
@@ -271,3 +272,27 @@ def test_fp_inv_variable_time(emu):
         assert int.from_bytes(o.raw, "big") == pow(a, p - 2, p), hex(a)
     emu.bh_fp_inv_vt(bytes(48), o)
     assert o.raw == bytes(48)
+
+
+def test_wave_cofactor_on_key_side(emu):
+    """e(H0, [h_eff] apk) == e([h_eff] H0, apk): the hash's cofactor clearing moved onto the key sum
+    (H0 = the two maps' sum, not cleared), with computed lines and with the line table of
+    [h_eff] apk -- statuses equal the oracle's on valid items, wrong messages, wrong key sets,
+    signatures outside G1 and the identity"""
+    rnd = random.Random(58)
+    sks = [rnd.randrange(1, r).to_bytes(32, "big") for _ in range(3)]
+    pks = [B.keygen(k)[1] for k in sks]
+    cases = []
+    for t in range(6):
+        m = rnd.randbytes(rnd.choice([0, 1, 32, 100]))
+        _, agg = B.aggregate([B.sign(k, m) for k in sks])
+        cases += [(agg, pks, m), (agg, pks, m + b"?"), (agg, pks[:2], m)]
+        one = B.sign(sks[t % 3], m)
+        cases += [(one, [pks[t % 3]], m), (one, [pks[(t + 1) % 3]], m)]
+    cases += [(C.not_in_g1(), pks, b"m"), (C.IDENTITY_G1, pks, b"m")]
+    for sig, ks, msg in cases:
+        want = B.fast_aggregate_verify(sig, ks, msg)
+        for mode in (1, 2):
+            got = emu.bh_w3_fast_aggregate_verify(sig, len(ks), b"".join(ks), msg, len(msg), B.DST_NUL,
+                                                  len(B.DST_NUL), mode)
+            assert got == want, (mode, len(ks), len(msg))
