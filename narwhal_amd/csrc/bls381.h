@@ -195,18 +195,36 @@ NWV_HD fp fp_from_mont(const fp& a) {
     one.l[0] = 1;
     return fp_canon(fp_mul(a, one));
 }
-// a^e for a constant exponent given as 12 little-endian 32-bit words (wave-uniform control flow)
+// a^e for a constant exponent given as 12 little-endian 32-bit words (wave-uniform control flow):
+// sliding windows of up to 5 bits over the odd powers a, a^3, .., a^31 -- for the 379-bit square
+// root / inversion exponents 379 squarings + 67 products + 16 for the table, against 228 products
+// bit by bit
 BLS_NOINLINE fp fp_pow(const fp& a, const uint32_t* e) {
+    fp t[16];
+    t[0] = a;
+    const fp a2 = fp_sqr(a);
+    for (int k = 1; k < 16; k++) t[k] = fp_mul(t[k - 1], a2);
+    auto bit = [&](int i) -> uint32_t { return (e[i >> 5] >> (i & 31)) & 1u; };
+    int i = 383;
+    while (i >= 0 && !bit(i)) i--;
     fp acc = k_one();
     bool started = false;
-    for (int w = 11; w >= 0; w--)
-        for (int b = 31; b >= 0; b--) {
-            if (started) acc = fp_sqr(acc);
-            if ((e[w] >> b) & 1) {
-                acc = started ? fp_mul(acc, a) : a;
-                started = true;
-            }
+    while (i >= 0) {
+        if (!bit(i)) {
+            acc = fp_sqr(acc);
+            i--;
+            continue;
         }
+        int j = i - 4 < 0 ? 0 : i - 4;
+        while (!bit(j)) j++;  // the window ends on a set bit (bit i is set)
+        uint32_t v = 0;
+        for (int k = i; k >= j; k--) v = (v << 1) | bit(k);
+        if (started)
+            for (int k = i; k >= j; k--) acc = fp_sqr(acc);
+        acc = started ? fp_mul(acc, t[v >> 1]) : t[v >> 1];
+        started = true;
+        i = j - 1;
+    }
     return acc;
 }
 NWV_HD fp fp_inv(const fp& a) {
