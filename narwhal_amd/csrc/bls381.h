@@ -344,14 +344,17 @@ NWV_HD bool w_is_zero(const uint32_t* a) {
     for (int i = 0; i < BW; i++) o |= a[i];
     return o == 0;
 }
-BLS_NOINLINE fp fp_inv_vt(const fp& x) {
+// UNI: x is the same on every lane of the wave (the final exponentiation's norm): the steps then
+// run on the scalar unit.  Otherwise every lane inverts its own x.
+template <bool UNI>
+BLS_NOINLINE fp fp_inv_vt_t(const fp& x) {
     const fp xc = fp_canon(x);
     if (fp_is_zero(xc)) return fp_zero();
     uint32_t a[BW], b[BW], u[BW], v[BW], P[BW];
     w_from_fp(a, xc);
     w_from_fp(P, k_p());
     for (int i = 0; i < BW; i++) {
-        a[i] = w_uni(a[i]);
+        a[i] = UNI ? w_uni(a[i]) : a[i];
         b[i] = P[i];
         u[i] = 0;
         v[i] = 0;
@@ -412,6 +415,8 @@ BLS_NOINLINE fp fp_inv_vt(const fp& x) {
     }
     return fp_mul(r, r3);  // y^-1 R^3 / R = (x R)^-1 R^2 = x^-1 R: the Montgomery form of x^-1
 }
+NWV_HD fp fp_inv_vt(const fp& x) { return fp_inv_vt_t<false>(x); }
+NWV_HD fp fp_inv_vt_uniform(const fp& x) { return fp_inv_vt_t<true>(x); }
 
 // sqrt for p = 3 mod 4; false if a is not a square
 NWV_HD bool fp_sqrt(fp& r, const fp& a) {
@@ -798,6 +803,18 @@ NWV_HD void g1_to_affine(fp& x, fp& y, const jac<fp>& a) {
 }
 NWV_HD void g2_to_affine(fp2& x, fp2& y, const jac<fp2>& a) {
     const fp2 zi = f2_inv(a.z), zi2 = f2_sqr(zi);
+    x = f2_mul(a.x, zi2);
+    y = f2_mul(a.y, f2_mul(zi2, zi));
+}
+// the same for public points (verification, aggregation, keys): the variable-time inversion
+NWV_HD void g1_to_affine_vt(fp& x, fp& y, const jac<fp>& a) {
+    const fp zi = fp_inv_vt(a.z), zi2 = fp_sqr(zi);
+    x = fp_mul(a.x, zi2);
+    y = fp_mul(a.y, fp_mul(zi2, zi));
+}
+NWV_HD void g2_to_affine_vt(fp2& x, fp2& y, const jac<fp2>& a) {
+    const fp n = fp_inv_vt(fp_add(fp_sqr(a.z.c0), fp_sqr(a.z.c1)));
+    const fp2 zi = {fp_mul(a.z.c0, n), fp_neg(fp_mul(a.z.c1, n))}, zi2 = f2_sqr(zi);
     x = f2_mul(a.x, zi2);
     y = f2_mul(a.y, f2_mul(zi2, zi));
 }

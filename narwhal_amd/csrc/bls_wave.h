@@ -463,7 +463,7 @@ template <class W>
 NWV_HD void final_exp(const W& w) {
     w.run(P_INV_A);
     const fp n = w.get(REG_N);
-    w.put_fp(REG_N + 1, fp_inv_vt(n));
+    w.put_fp(REG_N + 1, fp_inv_vt_uniform(n));  // every lane holds the same norm
     w.sync();
     w.run(P_INV_B);
     w.run(P_EASY1);

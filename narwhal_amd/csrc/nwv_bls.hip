@@ -195,7 +195,7 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_h2c_g(uint32_t n, const uint8
     const jac<fp> h0 = jac_add(q, q1);
     const jac<fp> h = kmode && kmode[i] ? h0 : jac_mul64(h0, BLS_H_EFF);
     fp x = fp_zero(), y = fp_zero();
-    if (!h.inf) g1_to_affine(x, y, h);
+    if (!h.inf) g1_to_affine_vt(x, y, h);
     st_g1(rec + (size_t)G1_REC_WORDS * i, x, y, h.inf);
 }
 // the item's status in the oracle's order: the signature's, then the keys'
@@ -276,6 +276,11 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_sig_jac(uint32_t n, const uin
     p.z = k_one();
     st_g1j(srec + (size_t)G1J_REC_WORDS * i, p);
 }
+// st[i] <- the decode status when it is a failure, else the G1 check's
+__global__ __launch_bounds__(BLS_LANES) void k_bls_st_join(uint32_t n, const int32_t* dec, int32_t* st) {
+    BLS_IDX();
+    if (dec[i] != ST_OK) st[i] = dec[i];
+}
 __global__ void k_bls_g1_sum_out(uint32_t n, const int32_t* st, const uint32_t* srec, uint8_t* out48, int32_t* out_st) {
     if (blockIdx.x || threadIdx.x) return;
     for (uint32_t k = 0; k < n; k++)
@@ -285,7 +290,7 @@ __global__ void k_bls_g1_sum_out(uint32_t n, const int32_t* st, const uint32_t* 
         }
     const jac<fp> acc = ld_g1j(srec);
     fp x = fp_zero(), y = fp_zero();
-    if (!acc.inf) g1_to_affine(x, y, acc);
+    if (!acc.inf) g1_to_affine_vt(x, y, acc);
     g1_compress(out48, x, y, acc.inf);
     *out_st = ST_OK;
 }
@@ -414,7 +419,7 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_key_heff(uint32_t n, const ui
     const uint32_t k = slots[i];
     fp2 x, y;
     ld_g2(rc + (size_t)G2_REC_WORDS * k, x, y);
-    g2_to_affine(x, y, jac_mul64(jac_from_affine(x, y), BLS_H_EFF));
+    g2_to_affine_vt(x, y, jac_mul64(jac_from_affine(x, y), BLS_H_EFF));
     st_g2(hrc + (size_t)G2_REC_WORDS * k, x, y, false);
 }
 // the line tables of newly registered keys (of their [h_eff] pk): one wave per key (slots[i] = its
@@ -1163,13 +1168,26 @@ int nwv_bls_aggregate(nwv_ctx* ctx, size_t n, const uint8_t* sigs48, uint8_t out
     if ((rc = lane.rc())) return rc;
     BlsLane& L = *lane;
     const size_t w_rec = 0, w_st = al256(4 * G1_REC_WORDS * n), w_j = al256(w_st + 4 * n),
-                 w_out = al256(w_j + 4 * G1J_REC_WORDS * n), w_ost = w_out + 64, w_end = w_ost + 8;
+                 w_out = al256(w_j + 4 * G1J_REC_WORDS * n), w_ost = w_out + 64, w_st2 = al256(w_ost + 8),
+                 w_end = w_st2 + 4 * n;
     if ((rc = L.in.ensure(48 * n)) || (rc = L.work.ensure(w_end)) || (rc = L.stage.ensure(128))) return rc;
     uint8_t* w = static_cast<uint8_t*>(L.work.p);
     auto* srec = reinterpret_cast<uint32_t*>(w + w_j);
     BLS_HIP(hipMemcpyAsync(L.in.p, sigs48, 48 * n, hipMemcpyHostToDevice, L.stream));
-    hipLaunchKernelGGL(k_bls_sigs, dim3(kBlocks(n)), dim3(BLS_LANES), 0, L.stream, (uint32_t)n,
-                       (const uint8_t*)L.in.p, reinterpret_cast<uint32_t*>(w + w_rec), reinterpret_cast<int32_t*>(w + w_st));
+    if (n <= 1024) {  // decode on one lane each, the G1 checks on a wave each
+        auto* sdec = reinterpret_cast<int32_t*>(w + w_st2);
+        hipLaunchKernelGGL(k_blsw_sigdec, dim3(kBlocks(n)), dim3(BLS_LANES), 0, L.stream, (uint32_t)n,
+                           (const uint8_t*)L.in.p, reinterpret_cast<uint32_t*>(w + w_rec), sdec);
+        hipLaunchKernelGGL(k_blsw_sub, dim3((unsigned)n), dim3(64), 0, L.stream, (uint32_t)n,
+                           reinterpret_cast<const uint32_t*>(w + w_rec), (const int32_t*)sdec,
+                           reinterpret_cast<int32_t*>(w + w_st));
+        hipLaunchKernelGGL(k_bls_st_join, dim3(kBlocks(n)), dim3(BLS_LANES), 0, L.stream, (uint32_t)n,
+                           (const int32_t*)sdec, reinterpret_cast<int32_t*>(w + w_st));
+    } else {
+        hipLaunchKernelGGL(k_bls_sigs, dim3(kBlocks(n)), dim3(BLS_LANES), 0, L.stream, (uint32_t)n,
+                           (const uint8_t*)L.in.p, reinterpret_cast<uint32_t*>(w + w_rec),
+                           reinterpret_cast<int32_t*>(w + w_st));
+    }
     hipLaunchKernelGGL(k_bls_sig_jac, dim3(kBlocks(n)), dim3(BLS_LANES), 0, L.stream, (uint32_t)n,
                        reinterpret_cast<const uint32_t*>(w + w_rec), srec);
     for (uint32_t m = (uint32_t)n; m > 1; m = (m + 1) / 2)

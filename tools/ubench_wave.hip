@@ -70,7 +70,7 @@ __global__ __launch_bounds__(64) void k_piece(int which, int reps, uint32_t* out
             final_exp(w);
         } else if (which == 3) {
             const fp n = w.get(REG_N);
-            w.put_fp(REG_N + 1, fp_inv_vt(n));
+            w.put_fp(REG_N + 1, fp_inv_vt_uniform(n));
             w.sync();
         } else {
             ok ^= pairing_check(w, nullptr);
