@@ -911,8 +911,12 @@ BLS_NOINLINE void sha256_block(uint32_t* h, const uint32_t* blk) {
         0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
         0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
     uint32_t w[16];
+#pragma unroll
     for (int i = 0; i < 16; i++) w[i] = blk[i];
     uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+    // fully unrolled: the message schedule's indices and the round constants are compile-time
+    // (a rolled loop indexes w[] dynamically, which puts it in scratch memory)
+#pragma unroll
     for (int i = 0; i < 64; i++) {
         if (i >= 16) {
             const uint32_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
@@ -932,68 +936,108 @@ BLS_NOINLINE void sha256_block(uint32_t* h, const uint32_t* blk) {
     }
     h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
 }
-// A byte stream assembled from up to 4 segments, hashed block by block (segments are read with
-// byte loads; the hash is a small share of a hash_to_curve)
-struct seg { const uint8_t* p; uint32_t n; };
-NWV_HD uint8_t seg_byte(const seg* s, int ns, uint32_t k) {
-    for (int i = 0; i < ns; i++) {
-        if (k < s[i].n) return s[i].p[k];
-        k -= s[i].n;
-    }
-    return 0;
-}
-// SHA-256 of (prefix_blocks already absorbed into h, prefix_len bytes) || segments
-BLS_NOINLINE void sha256_segments(uint32_t* h, uint64_t prefix_len, const seg* s, int ns, uint8_t* out32) {
-    uint32_t total = 0;
-    for (int i = 0; i < ns; i++) total += s[i].n;
-    const uint64_t bits = (prefix_len + total) * 8;
+// SHA-256 of (`prefix` bytes already absorbed into h) || a byte stream of `total` bytes given by
+// byte(pos): words are assembled in registers (no byte arrays, whose dynamic indices would go to
+// scratch memory); out8 = the digest as eight big-endian words
+template <class B>
+NWV_HD void sha256_stream(uint32_t* h, uint32_t prefix, uint32_t total, B byte, uint32_t* out8) {
+    const uint64_t bits = (uint64_t)(prefix + total) * 8;
     const uint32_t nb = (total + 9 + 63) / 64;
     for (uint32_t blk = 0; blk < nb; blk++) {
         uint32_t w[16];
-        for (int i = 0; i < 16; i++) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
             uint32_t v = 0;
+#pragma unroll
             for (int k = 0; k < 4; k++) {
-                const uint32_t pos = 64 * blk + 4 * i + k;
-                uint8_t byte;
-                if (pos < total) byte = seg_byte(s, ns, pos);
-                else if (pos == total) byte = 0x80;
-                else if (blk == nb - 1 && pos >= 64 * blk + 56) byte = (uint8_t)(bits >> (8 * (64 * blk + 63 - pos)));
-                else byte = 0;
-                v = (v << 8) | byte;
+                const uint32_t pos = 64 * blk + 4 * j + k;
+                uint32_t b = 0;
+                if (pos < total) b = byte(pos);
+                else if (pos == total) b = 0x80u;
+                else if (blk == nb - 1 && 4 * j + k >= 56) b = (uint32_t)(bits >> (8 * (63 - (4 * j + k)))) & 0xffu;
+                v = (v << 8) | b;
             }
-            w[i] = v;
+            w[j] = v;
         }
         sha256_block(h, w);
     }
-    for (int i = 0; i < 8; i++)
-        for (int k = 0; k < 4; k++) out32[4 * i + k] = (uint8_t)(h[i] >> (24 - 8 * k));
+#pragma unroll
+    for (int i = 0; i < 8; i++) out8[i] = h[i];
 }
 NWV_HD void sha256_iv(uint32_t* h) {
     const uint32_t iv[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
     for (int i = 0; i < 8; i++) h[i] = iv[i];
 }
+// byte k (< 32) of eight big-endian words, by selects (no dynamic register indexing)
+NWV_HD uint32_t words_byte(const uint32_t* x, uint32_t k) {
+    const uint32_t q = k >> 2;
+    uint32_t v = x[0];
+#pragma unroll
+    for (int t = 1; t < 8; t++) v = q == (uint32_t)t ? x[t] : v;
+    return (v >> (24 - 8 * (k & 3))) & 0xffu;
+}
 
 // ------------------------------------------------------------------- hash_to_curve (G1)
-// expand_message_xmd (RFC 9380 §5.3.1), 128 output bytes; the 64-byte zero block Z_pad is the
-// first block of b_0's input: its compression is absorbed once per lane
-NWV_HD void expand_xmd_128(uint8_t* out, const uint8_t* msg, uint32_t n, const uint8_t* dst, uint32_t dl) {
+// expand_message_xmd (RFC 9380 §5.3.1), 128 output bytes as 32 big-endian words; the 64-byte zero
+// block Z_pad is the first block of b_0's input: its compression is absorbed once per lane
+NWV_HD void expand_xmd_128w(uint32_t* out, const uint8_t* msg, uint32_t n, const uint8_t* dst, uint32_t dl) {
     uint32_t h[8];
     sha256_iv(h);
     const uint32_t zero[16] = {0};
     sha256_block(h, zero);
-    const uint8_t lib[3] = {0, 128, 0};
-    const uint8_t dlb = (uint8_t)dl;
-    uint8_t b0[32], bi[32], x[33];
-    seg s0[4] = {{msg, n}, {lib, 3}, {dst, dl}, {&dlb, 1}};
-    sha256_segments(h, 64, s0, 4, b0);
+    uint32_t b0[8], bi[8];
+    // b_0 = H(Z_pad || msg || I2OSP(128, 2) || I2OSP(0, 1) || DST || I2OSP(len(DST), 1))
+    sha256_stream(h, 64, n + 3 + dl + 1,
+                  [&](uint32_t k) -> uint32_t {
+                      if (k < n) return msg[k];
+                      k -= n;
+                      if (k < 3) return k == 1 ? 128u : 0u;
+                      k -= 3;
+                      return k < dl ? (uint32_t)dst[k] : dl;
+                  },
+                  b0);
     for (int i = 1; i <= 4; i++) {
-        for (int k = 0; k < 32; k++) x[k] = i == 1 ? b0[k] : (uint8_t)(b0[k] ^ bi[k]);
-        x[32] = (uint8_t)i;
-        seg s1[3] = {{x, 33}, {dst, dl}, {&dlb, 1}};
+        // b_i = H((b_0 xor b_{i-1}) || I2OSP(i, 1) || DST || I2OSP(len(DST), 1))
+        uint32_t x[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) x[k] = i == 1 ? b0[k] : (b0[k] ^ bi[k]);
         sha256_iv(h);
-        sha256_segments(h, 0, s1, 3, bi);
-        for (int k = 0; k < 32; k++) out[32 * (i - 1) + k] = bi[k];
+        sha256_stream(h, 0, 33 + dl + 1,
+                      [&](uint32_t k) -> uint32_t {
+                          if (k < 32) return words_byte(x, k);
+                          if (k == 32) return (uint32_t)i;
+                          k -= 33;
+                          return k < dl ? (uint32_t)dst[k] : dl;
+                      },
+                      bi);
+#pragma unroll
+        for (int k = 0; k < 8; k++) out[8 * (i - 1) + k] = bi[k];
     }
+}
+NWV_HD void expand_xmd_128(uint8_t* out, const uint8_t* msg, uint32_t n, const uint8_t* dst, uint32_t dl) {
+    uint32_t w[32];
+    expand_xmd_128w(w, msg, n, dst, dl);
+    for (int i = 0; i < 32; i++)
+        for (int k = 0; k < 4; k++) out[4 * i + k] = (uint8_t)(w[i] >> (24 - 8 * k));
+}
+// 256 bits from eight big-endian words, as plain limbs
+NWV_HD fp plain_from_be256w(const uint32_t* w) {
+    uint32_t le[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) le[i] = w[7 - i];
+    fp r;
+#pragma unroll
+    for (int j = 0; j < NL; j++) {
+        const int bit = 28 * j, idx = bit >> 5, sh = bit & 31;
+        uint32_t v = idx < 8 ? le[idx] >> sh : 0u;
+        if (sh > 4 && idx + 1 < 8) v |= le[idx + 1] << (32 - sh);
+        r.l[j] = v & LM;
+    }
+    return r;
+}
+// 16 big-endian words (64 bytes) mod p, Montgomery form: hi * 2^256 + lo
+NWV_HD fp fp_from_be64w(const uint32_t* w) {
+    return fp_add(fp_mul(fp_to_mont(plain_from_be256w(w)), k_two256()), fp_to_mont(plain_from_be256w(w + 8)));
 }
 // 64 big-endian bytes mod p, Montgomery form: hi * 2^256 + lo
 NWV_HD fp fp_from_be64(const uint8_t* b) {
@@ -1071,9 +1115,9 @@ NWV_HD jac<fp> iso_map(const fp& x, const fp& y) {
 }
 // one of the two field elements of hash_to_field (j = 0, 1) mapped to E: iso(SSWU(u_j))
 BLS_NOINLINE jac<fp> h2c_map(const uint8_t* msg, uint32_t n, const uint8_t* dst, uint32_t dl, int j) {
-    uint8_t ub[128];
-    expand_xmd_128(ub, msg, n, dst, dl);
-    const fp u0 = fp_from_be64(ub), u1 = fp_from_be64(ub + 64);  // constant offsets, then a select
+    uint32_t uw[32];
+    expand_xmd_128w(uw, msg, n, dst, dl);
+    const fp u0 = fp_from_be64w(uw), u1 = fp_from_be64w(uw + 16);  // constant offsets, then a select
     fp x, y;
     map_sswu(x, y, fp_sel(j == 0, u0, u1));
     return iso_map(x, y);

@@ -314,9 +314,9 @@ NWV_HD void w_hash_to_g1(const W& w, const uint8_t* msg, uint32_t n, const uint8
     using namespace wave;
     init_slots(w);
     w.lanes(2, [&](int j) {
-        uint8_t ub[128];
-        expand_xmd_128(ub, msg, n, dst, dl);
-        const fp u0 = fp_from_be64(ub), u1 = fp_from_be64(ub + 64);  // constant offsets, then a select
+        uint32_t uw[32];
+        expand_xmd_128w(uw, msg, n, dst, dl);
+        const fp u0 = fp_from_be64w(uw), u1 = fp_from_be64w(uw + 16);  // constant offsets, then a select
         fp xn, xd, y;
         map_sswu_frac(xn, xd, y, fp_sel(j == 0, u0, u1));
         w.set(REG_S + 3 * j, xn);

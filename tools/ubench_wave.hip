@@ -176,6 +176,54 @@ __global__ __launch_bounds__(64) void k_parts(int which, int reps, uint32_t* out
     }
 }
 
+// the hash to G1 on a wave (no cofactor chain: the key-side form) and its lane-local pieces:
+// 0 the whole w_hash_to_g1, 1 expand_message_xmd on lanes 0-1, 2 map_sswu_frac on lanes 0-1,
+// 3 one fp_pow (the square-root exponent) on lane 0
+__global__ __launch_bounds__(64) void k_h2c(int which, int reps, uint32_t* out, unsigned long long* clk) {
+    __shared__ uint32_t wm[WM_WORDS];
+    const Wave w{wm, (int)threadIdx.x};
+    fill(w);
+    __shared__ uint8_t msg[64];
+    if (threadIdx.x < 64) msg[threadIdx.x] = (uint8_t)(threadIdx.x * 7 + 1);
+    const char dst[] = "BLS_SIG_BLS12381G1_XMD:SHA-256_SSWU_RO_NUL_";
+    __shared__ uint32_t rec[G1H_REC_WORDS];
+    w.sync();
+    uint32_t acc = 0;
+    const unsigned long long t0 = wall_clock64();
+#pragma unroll 1
+    for (int r = 0; r < reps; r++) {
+        if (which == 0) {
+            w_hash_to_g1(w, msg, 32, (const uint8_t*)dst, 43, rec, false);
+        } else if (which == 1) {
+            w.lanes(2, [&](int j) {
+                uint8_t ub[128];
+                expand_xmd_128(ub, msg + j, 32, (const uint8_t*)dst, 43);
+                acc += ub[5] + ub[77];
+            });
+        } else if (which == 2) {
+            w.lanes(2, [&](int j) {
+                fp xn, xd, y, u = k_one();
+                u.l[0] += (uint32_t)(r + j);
+                map_sswu_frac(xn, xd, y, u);
+                acc += xn.l[0] ^ y.l[3];
+            });
+        } else {
+            w.lanes(1, [&](int j) {
+                const uint32_t c1[12] = BLS_E_QR;
+                fp u = k_one();
+                u.l[0] += (uint32_t)(r + j);
+                acc += fp_pow(u, c1).l[2];
+            });
+        }
+        w.sync();
+    }
+    const unsigned long long t1 = wall_clock64();
+    if (threadIdx.x == 0) {
+        out[blockIdx.x] = rec[0] + acc;
+        clk[blockIdx.x] = t1 - t0;
+    }
+}
+
 typedef void (*kfn)(int, int, uint32_t*, unsigned long long*);
 
 int main(int argc, char** argv) {
@@ -192,7 +240,9 @@ int main(int argc, char** argv) {
               {"stage_copy_noload", k_stage, 0, 1000, 0}, {"stage_cyc_products_noload", k_stage, 1, 400, 0},
               {"stage_cyc_combos_noload", k_stage, 2, 1000, 0}, {"record_fetch_latency", k_stage, 3, 1000, 0},
               {"part_combos_only", k_parts, 0, 400, 0}, {"part_product_only", k_parts, 1, 400, 0},
-              {"part_comboA_product", k_parts, 2, 400, 0}};
+              {"part_comboA_product", k_parts, 2, 400, 0},
+              {"h2c_wave_no_cofactor", k_h2c, 0, 5, 0}, {"h2c_expand_xmd", k_h2c, 1, 20, 0},
+              {"h2c_map_sswu", k_h2c, 2, 5, 0}, {"fp_pow_sqrt_lane0", k_h2c, 3, 5, 0}};
     const int blocks_full = 256 * 4;  // a wave per SIMD
     uint32_t* out;
     unsigned long long* clk;
