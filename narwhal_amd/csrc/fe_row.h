@@ -17,9 +17,9 @@
 //            measured on gfx950 (tools/probe/dpp_probe.hip).
 //
 // Magnitudes: mul() takes operands with limbs a_k, b_k such that the column sums fit (checked
-// on the host): in practice "loose" limbs <= 2^17.7.  Its output has limbs < 2^16 + 2^11 on
-// lanes 1..15 and < 2^17 on lane 0 (three carry passes).  sub uses 8p, whose limbs (>= 2^18)
-// dominate any loose limb.
+// on the host): in practice "loose" limbs <= 2^17.7.  Its output has limbs < 2^16 + 2^12 (two
+// carry passes; round 3 ran a third that tightened this to 2^16 + 2^11).  sub uses 8p, whose
+// limbs (>= 2^18) dominate any loose limb.
 #pragma once
 #include "fe25519.h"
 
@@ -257,9 +257,11 @@ NWV_HD V mul_dpp(V a, V b, const RowConsts& k) {
     V64 acc = mad64(op[0], bs[0], zero64());
 #pragma unroll
     for (int r = 1; r < 16; r++) acc = mad64(op[r], bs[r], acc);
-    // first pass on the 64-bit columns (< 2^48): limb 15's carry x38 stays < 2^32
+    // first pass on the 64-bit columns (< 2^48): limb 15's carry x38 stays < 2^32; one more pass
+    // leaves limbs < 2^16 + 2^12 (operands of the next multiply, of sub's 8p and of carry32 all
+    // take that: a third pass, as before round 4, only tightened it to 2^16 + 2^11)
     const V x = lo16(acc) + ror1(mul32(shr16(acc), k.w15));
-    return carry32(carry32(x, k), k);
+    return carry32(x, k);
 }
 
 // The same product with the operands exchanged through LDS instead of 45 DPP moves: each row
@@ -285,7 +287,7 @@ NWV_HD V mul_lds(V a, V b, const RowConsts& k) {
 #pragma unroll
     for (int r = 1; r < 16; r++) acc = mad64(op[r], bs[r], acc);
     const V x = lo16(acc) + ror1(mul32(shr16(acc), k.w15));
-    return carry32(carry32(x, k), k);
+    return carry32(x, k);  // two passes (see mul_dpp)
 }
 
 // a * b mod p on every row: the LDS form when the wave has scratch (k.sc), else the DPP form
