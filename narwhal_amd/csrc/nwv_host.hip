@@ -10,6 +10,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <functional>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -685,37 +686,96 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     return NWV_OK;
 }
 
+// Persistent helper threads for the host-side staging copies (created once per process, on first
+// use): a call hands its piece loop to the pool and works on it too, instead of creating threads
+// per call (thread start-up was a visible share of a 40 MB staging).  One call uses the pool at a
+// time; a concurrent call finds it busy and copies alone.
+class StagePool {
+  public:
+    static StagePool& get() {
+        static StagePool* p = new StagePool();  // never destroyed: helpers may outlive static teardown
+        return *p;
+    }
+    // fn(helper) on the caller and on up to kHelpers pool threads; returns once every started
+    // helper has finished.  Returns false (fn not run) when the pool is busy.
+    template <class F>
+    bool run(F&& fn) {
+        std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
+        if (!busy.owns_lock()) return false;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            if (!started_) start();
+            job_ = std::function<void(bool)>(fn);
+            open_ = true;
+            taken_ = finished_ = 0;
+            gen_++;
+        }
+        cv_.notify_all();
+        fn(false);
+        std::unique_lock<std::mutex> g(mu_);
+        open_ = false;  // no helper starts on this job from now on
+        done_.wait(g, [&] { return finished_ == taken_; });
+        job_ = nullptr;
+        return true;
+    }
+
+  private:
+    static constexpr int kHelpers = 15;
+    void start() {
+        started_ = true;
+        for (int t = 0; t < kHelpers; t++) {
+            try {
+                std::thread(&StagePool::loop, this).detach();
+            } catch (...) {  // fewer helpers (never throw across the C ABI)
+                break;
+            }
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> g(mu_);
+        for (;;) {
+            cv_.wait(g, [&] { return gen_ != seen; });
+            seen = gen_;
+            if (!open_ || !job_) continue;
+            taken_++;
+            std::function<void(bool)> fn = job_;
+            g.unlock();
+            fn(true);
+            g.lock();
+            ++finished_;
+            done_.notify_all();
+        }
+    }
+    std::mutex run_mu_, mu_;
+    std::condition_variable cv_, done_;
+    std::function<void(bool)> job_;
+    uint64_t gen_ = 0;
+    int taken_ = 0, finished_ = 0;
+    bool open_ = false, started_ = false;
+};
+
 // Host-side packing copy into the pinned staging buffer: a 65,536 x 512 B batch is ~40 MB, which
 // one thread copies at a few GB/s (longer than the PCIe transfer and the batch MSM together), so
-// copies above 4 MiB are split over up to 8 host threads.
+// copies above 4 MiB are split into 2 MiB pieces over the staging pool.
 static void pack_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
-    constexpr size_t kMin = (size_t)4 << 20;
-    const size_t parts = std::min<size_t>(8, bytes / kMin);
-    if (parts < 2) {
+    constexpr size_t kMin = (size_t)4 << 20, kPiece = (size_t)2 << 20;
+    if (bytes < kMin) {
         std::memcpy(dst, src, bytes);
         return;
     }
-    const size_t step = ((bytes + parts - 1) / parts + 63) & ~(size_t)63;
-    std::vector<std::thread> th;
-    size_t done = step;  // bytes [0, done) are this thread's, the rest the helpers'
-    for (size_t k = 1; k < parts; k++) {
-        const size_t o = k * step;
-        if (o >= bytes) break;
-        try {
-            th.emplace_back([=] { std::memcpy(dst + o, src + o, std::min(step, bytes - o)); });
-        } catch (...) {  // no thread available: this thread copies the remainder (never throw
-            break;       // across the C ABI)
-        }
-        done = o + step;
-    }
-    std::memcpy(dst, src, std::min(step, bytes));
-    if (done < bytes) std::memcpy(dst + done, src + done, bytes - done);
-    for (auto& t : th) t.join();
+    const size_t np = (bytes + kPiece - 1) / kPiece;
+    std::atomic<size_t> next{0};
+    auto work = [&](bool) {
+        for (size_t k; (k = next.fetch_add(1)) < np;)
+            std::memcpy(dst + k * kPiece, src + k * kPiece, std::min(kPiece, bytes - k * kPiece));
+    };
+    if (!StagePool::get().run(work)) work(false);
 }
 
-// Large message regions: packing into pinned memory and the H2D DMA overlap.  Up to 8 host
-// threads take 2 MiB pieces in order, copy each into the pinned buffer and queue its DMA on
-// `stream` at once, so the copy engine starts on the first pieces while the rest are packed
+// Large message regions: packing into pinned memory and the H2D DMA overlap.  The caller and the
+// staging pool's threads take 2 MiB pieces in order, copy each into the pinned buffer and queue its
+// DMA on `stream` at once, so the copy engine starts on the first pieces while the rest are packed
 // (C4, 33.5 MB of messages: pack ~0.74 ms then DMA ~0.72 ms back to back before).
 struct PackSeg {
     size_t off;          // offset in the arena (host and device alike)
@@ -742,17 +802,7 @@ static int pack_copy_h2d(int ordinal, uint8_t* dev_base, uint8_t* host_base, con
                 err.store(1);
         }
     };
-    std::vector<std::thread> th;
-    const size_t helpers = std::min<size_t>(7, pieces.size() > 1 ? pieces.size() - 1 : 0);
-    for (size_t t = 0; t < helpers; t++) {
-        try {
-            th.emplace_back(work, true);
-        } catch (...) {  // fewer threads: the others (and this one) take the remaining pieces
-            break;
-        }
-    }
-    work(false);
-    for (auto& t : th) t.join();
+    if (pieces.size() < 2 || !StagePool::get().run(work)) work(false);
     return (err.load() || done.load() != pieces.size()) ? set_err(NWV_ERR_HIP, "pipelined staging copy") : NWV_OK;
 }
 
