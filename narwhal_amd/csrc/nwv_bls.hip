@@ -356,19 +356,18 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_pairing_raw(uint32_t n, const
 }
 
 // ---- the wave engine (bls_wave.h): one 64-lane wave per item ------------------------------------
-#define BLSW_IDX()                                        \
-    __shared__ uint32_t wm[wave::WM_WORDS];                   \
-    const uint32_t i = blockIdx.x;                        \
-    if (i >= n) return;                                   \
-    const wave::Wave w{wm, (int)threadIdx.x}
+#define BLSW_IDX()                        \
+    __shared__ uint32_t wm[wave::WM_WORDS]; \
+    const uint32_t i = blockIdx.x;          \
+    if (i >= n) return
 // H(msg_i), homogeneous
-__global__ __launch_bounds__(64) void k_blsw_h2c(uint32_t n, const uint8_t* msg, const uint64_t* off,
-                                                 const uint32_t* len, const uint8_t* dst, uint32_t dl, uint32_t* hrec,
-                                                 const uint32_t* kmode) {
-    BLSW_IDX();
+__device__ __forceinline__ void blsw_h2c_item(uint32_t* wm, uint32_t i, const uint8_t* msg, const uint64_t* off,
+                                              const uint32_t* len, const uint8_t* dst, uint32_t dl, uint32_t* hrec,
+                                              const uint32_t* kmode) {
+    const wave::Wave w{wm, (int)threadIdx.x};
     w_hash_to_g1(w, msg + off[i], len[i], dst, dl, hrec + (size_t)G1H_REC_WORDS * i, !(kmode && kmode[i]));
 }
-// signature decode only (one lane per item); the G1 check runs beside the pairing (k_blsw_sub)
+// signature decode only (one lane per item); the G1 check runs beside the pairing (k_blsw_pair_sub)
 __global__ __launch_bounds__(BLS_LANES) void k_blsw_sigdec(uint32_t n, const uint8_t* sig, uint32_t* rec, int32_t* st) {
     BLS_IDX();
     fp x, y;
@@ -378,25 +377,30 @@ __global__ __launch_bounds__(BLS_LANES) void k_blsw_sigdec(uint32_t n, const uin
     st_g1(rec + (size_t)G1_REC_WORDS * i, x, y, s == ST_OK && inf);
     st[i] = s;
 }
-__global__ __launch_bounds__(64) void k_blsw_sub(uint32_t n, const uint32_t* rec, const int32_t* st_dec, int32_t* st_sub) {
-    BLSW_IDX();
+__device__ __forceinline__ void blsw_sub_item(uint32_t* wm, uint32_t i, const uint32_t* rec, const int32_t* st_dec,
+                                              int32_t* st_sub) {
+    const wave::Wave w{wm, (int)threadIdx.x};
     const uint32_t* r = rec + (size_t)G1_REC_WORDS * i;
     int32_t s = ST_OK;
     if (st_dec[i] == ST_OK && !r[2 * NL]) s = w_g1_in_group(w, r) ? ST_OK : ST_NOT_IN_GROUP;
     if (threadIdx.x == 0) st_sub[i] = s;
 }
+__global__ __launch_bounds__(64) void k_blsw_sub(uint32_t n, const uint32_t* rec, const int32_t* st_dec, int32_t* st_sub) {
+    BLSW_IDX();
+    blsw_sub_item(wm, i, rec, st_dec, st_sub);
+}
 // e(-sig, g2) e(H, apk) == 1 for every item whose signature decoded and whose keys are valid
 // (run beside the signature's G1 check: the status join puts that check first)
-// H: homogeneous records (k_blsw_h2c) or affine ones (k_bls_h2c_g, h_hom = 0); apk: Jacobian
+// H: homogeneous records (k_blsw_pre) or affine ones (k_bls_h2c_g, h_hom = 0); apk: Jacobian
 // records (k_blsw_apk)
 // (a one-key item whose key is in the cache takes the key's precomputed line table: the Miller
 // loop then only evaluates lines, no G2 arithmetic)
-__global__ __launch_bounds__(64) void k_blsw_pair(uint32_t n, const uint32_t* srec, const int32_t* st_dec,
-                                                  const uint32_t* hrec, int h_hom, const uint32_t* arec,
-                                                  const int32_t* st_apk, KeyTab kt, const uint32_t* pk_off,
-                                                  const uint32_t* pk_cnt, const uint32_t* pk_idx, const uint32_t* kmode,
-                                                  int32_t* st_pair) {
-    BLSW_IDX();
+__device__ __forceinline__ void blsw_pair_item(uint32_t* wm, uint32_t i, const uint32_t* srec, const int32_t* st_dec,
+                                               const uint32_t* hrec, int h_hom, const uint32_t* arec,
+                                               const int32_t* st_apk, const KeyTab& kt, const uint32_t* pk_off,
+                                               const uint32_t* pk_cnt, const uint32_t* pk_idx, const uint32_t* kmode,
+                                               int32_t* st_pair) {
+    const wave::Wave w{wm, (int)threadIdx.x};
     int32_t s = ST_VERIFY_FAIL;
     if (st_dec[i] == ST_OK && st_apk[i] == ST_OK) {
         const uint32_t* ql = nullptr;
@@ -408,6 +412,28 @@ __global__ __launch_bounds__(64) void k_blsw_pair(uint32_t n, const uint32_t* sr
                 : ST_VERIFY_FAIL;
     }
     if (threadIdx.x == 0) st_pair[i] = s;
+}
+__global__ __launch_bounds__(64) void k_blsw_pair(uint32_t n, const uint32_t* srec, const int32_t* st_dec,
+                                                  const uint32_t* hrec, int h_hom, const uint32_t* arec,
+                                                  const int32_t* st_apk, KeyTab kt, const uint32_t* pk_off,
+                                                  const uint32_t* pk_cnt, const uint32_t* pk_idx, const uint32_t* kmode,
+                                                  int32_t* st_pair) {
+    BLSW_IDX();
+    blsw_pair_item(wm, i, srec, st_dec, hrec, h_hom, arec, st_apk, kt, pk_off, pk_cnt, pk_idx, kmode, st_pair);
+}
+// the pairing checks (blocks [0, n)) and the signatures' G1 checks (blocks [n, 2n)) as one launch:
+// independent waves, so the launch takes as long as the slower of the two per item
+__global__ __launch_bounds__(64) void k_blsw_pair_sub(uint32_t n, const uint32_t* srec, const int32_t* st_dec,
+                                                      const uint32_t* hrec, int h_hom, const uint32_t* arec,
+                                                      const int32_t* st_apk, KeyTab kt, const uint32_t* pk_off,
+                                                      const uint32_t* pk_cnt, const uint32_t* pk_idx,
+                                                      const uint32_t* kmode, int32_t* st_pair, int32_t* st_sub) {
+    __shared__ uint32_t wm[wave::WM_WORDS];
+    const uint32_t b = blockIdx.x;
+    if (b < n)
+        blsw_pair_item(wm, b, srec, st_dec, hrec, h_hom, arec, st_apk, kt, pk_off, pk_cnt, pk_idx, kmode, st_pair);
+    else if (b < 2 * n)
+        blsw_sub_item(wm, b - n, srec, st_dec, st_sub);
 }
 // [h_eff] pk of newly registered keys (lane per key, affine records): the hash's cofactor clearing
 // moves onto the key side -- e(H0, [h_eff] pk) = e([h_eff] H0, pk) for H0 in E(Fp), as the
@@ -428,6 +454,7 @@ __global__ __launch_bounds__(64) void k_blsw_key_lines(uint32_t n, const uint32_
                                                        uint32_t* lines) {
     BLSW_IDX();
     const uint32_t k = slots[i];
+    const wave::Wave w{wm, (int)threadIdx.x};
     w_key_lines(w, rc + (size_t)G2_REC_WORDS * k, lines + KL_WORDS * k);
 }
 // the key sum of item i on a wave: lane j adds the item's keys j, j + 64, ... (Jacobian, jac_add:
@@ -435,12 +462,9 @@ __global__ __launch_bounds__(64) void k_blsw_key_lines(uint32_t n, const uint32_
 // bad key in list order (else AGGR_MISMATCH for an empty list, PK_INFINITY for an identity sum).
 // The sum stays Jacobian (G2J_WORDS record: the Miller-loop programs take a Jacobian Q), so there
 // is no inversion; a one-key item copies its validated record with Z = 1.
-__global__ __launch_bounds__(64) void k_blsw_apk(uint32_t n, KeyTab kt, const uint32_t* pk_off, const uint32_t* pk_cnt,
-                                                 const uint32_t* pk_idx, const uint32_t* kmode, uint32_t* rec,
-                                                 int32_t* st_apk) {
-    __shared__ uint32_t xa[32 * G2J_WORDS];
-    const uint32_t i = blockIdx.x;
-    if (i >= n) return;
+__device__ __forceinline__ void blsw_apk_item(uint32_t* xa, uint32_t i, const KeyTab& kt, const uint32_t* pk_off,
+                                              const uint32_t* pk_cnt, const uint32_t* pk_idx, const uint32_t* kmode,
+                                              uint32_t* rec, int32_t* st_apk) {
     const int lane = (int)threadIdx.x;
     const uint32_t cnt = pk_cnt[i];
     const uint32_t* idx = pk_idx + pk_off[i];
@@ -496,6 +520,28 @@ __global__ __launch_bounds__(64) void k_blsw_apk(uint32_t n, KeyTab kt, const ui
     }
     st_g2j(out, acc);
     st_apk[i] = status;
+}
+__global__ __launch_bounds__(64) void k_blsw_apk(uint32_t n, KeyTab kt, const uint32_t* pk_off, const uint32_t* pk_cnt,
+                                                 const uint32_t* pk_idx, const uint32_t* kmode, uint32_t* rec,
+                                                 int32_t* st_apk) {
+    __shared__ uint32_t xa[32 * G2J_WORDS];
+    if (blockIdx.x >= n) return;
+    blsw_apk_item(xa, blockIdx.x, kt, pk_off, pk_cnt, pk_idx, kmode, rec, st_apk);
+}
+// hash to G1 (blocks [0, n)) and the key sums (blocks [n, 2n)) as one launch (one stream per
+// call side): independent waves, the LDS of the larger of the two
+__global__ __launch_bounds__(64) void k_blsw_pre(uint32_t n, const uint8_t* msg, const uint64_t* off,
+                                                 const uint32_t* len, const uint8_t* dst, uint32_t dl, uint32_t* hrec,
+                                                 KeyTab kt, const uint32_t* pk_off, const uint32_t* pk_cnt,
+                                                 const uint32_t* pk_idx, const uint32_t* kmode, uint32_t* arec,
+                                                 int32_t* st_apk) {
+    constexpr int LW = wave::WM_WORDS > 32 * G2J_WORDS ? wave::WM_WORDS : 32 * G2J_WORDS;
+    __shared__ uint32_t lds[LW];
+    const uint32_t b = blockIdx.x;
+    if (b < n)
+        blsw_h2c_item(lds, b, msg, off, len, dst, dl, hrec, kmode);
+    else if (b < 2 * n)
+        blsw_apk_item(lds, b - n, kt, pk_off, pk_cnt, pk_idx, kmode, arec, st_apk);
 }
 
 // the oracle's order: signature decode, its G1 check, the keys, the pairing equation
@@ -568,14 +614,15 @@ struct BlsKeyCache {
 // One call in flight: its streams, staging arena and scratch.  A device keeps a pool of these, so
 // concurrent callers run their pipelines side by side instead of queueing on one device lock.
 struct BlsLane {
-    hipStream_t stream = nullptr;                       // H2D, signatures, pairing check, D2H
-    hipStream_t side[3] = {nullptr, nullptr, nullptr};  // keys + key sums; hash to G1; G1 checks
+    hipStream_t stream = nullptr;              // H2D, signatures, pairing check, D2H
+    hipStream_t side[2] = {nullptr, nullptr};  // keys + key sums (+ hash to G1 on small wave calls); hash to G1
     HBuf stage;
     DBuf in, work;
-    // [0,1] keys, [1,2] key sums (side 0); [3,4] signatures (main; wave mode: decode on main, the
-    // G1 check on side 2); [5,6] hash to G1 (side 1); [7,8] pairing check (main); [9] inputs
-    // resident, [10] side 0 done, [11] side 1 done, [12] signatures decoded, [13] side 2 done
-    hipEvent_t ev[14] = {};
+    // [0,1] keys, [1,2] key sums (side 0); [3,4] signatures (main); [5,6] hash to G1 (side 1; side
+    // 0 on small wave calls); [7,8] pairing check (main); [9] inputs resident, [10] side 0 done,
+    // [11] side 1 done.  side[1] is created by the first call that needs it: a lane of small wave
+    // calls holds two streams, so eight lanes map one to one onto 16 hardware queues
+    hipEvent_t ev[12] = {};
     ~BlsLane() {
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
@@ -636,9 +683,7 @@ class LaneLease {
                 auto l = std::make_unique<BlsLane>();
                 if (hipSetDevice(d.ordinal) != hipSuccess ||
                     hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking) != hipSuccess ||
-                    hipStreamCreateWithFlags(&l->side[0], hipStreamNonBlocking) != hipSuccess ||
-                    hipStreamCreateWithFlags(&l->side[1], hipStreamNonBlocking) != hipSuccess ||
-                    hipStreamCreateWithFlags(&l->side[2], hipStreamNonBlocking) != hipSuccess) {
+                    hipStreamCreateWithFlags(&l->side[0], hipStreamNonBlocking) != hipSuccess) {
                     rc_ = nwv_internal_set_err(NWV_ERR_HIP, "bls stream");
                     return;
                 }
@@ -902,7 +947,7 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     auto* ssub = reinterpret_cast<int32_t*>(w + w_ssub);
     auto* spair = reinterpret_cast<int32_t*>(w + w_spair);
     auto* ajrec = reinterpret_cast<uint32_t*>(w + w_aj);
-    hipStream_t s0 = L.stream, s1 = L.side[0], s2 = L.side[1], s3 = L.side[2];
+    hipStream_t s0 = L.stream, s1 = L.side[0], s2 = L.side[1];
     // stage times of the completed call, its path and key counts -> the device's "last call"
     auto finish = [&](int path_done) -> int {
         const int pairs[5][2] = {{0, 1}, {3, 4}, {5, 6}, {1, 2}, {7, 8}};  // keys, sigs, h2c, apk, pairing
@@ -922,6 +967,48 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     BLS_HIP(hipMemcpyAsync(in, h, a.total, hipMemcpyHostToDevice, s0));
     BLS_HIP(hipEventRecord(L.ev[9], s0));
     BLS_HIP(hipStreamWaitEvent(s1, L.ev[9], 0));
+    if (wave_small) {
+        // a call of up to wave_max items on two streams (8 concurrent calls then fit 16 hardware
+        // queues one to one): side 0 decodes the keys the cache does not hold, then hashes to G1
+        // and sums the keys in one launch (k_blsw_pre); main decodes the signatures, then runs
+        // the pairing checks and the signatures' G1 checks in one launch (k_blsw_pair_sub)
+        BLS_HIP(hipEventRecord(L.ev[0], s1));
+        if (n_dec)
+            hipLaunchKernelGGL(k_bls_keys_fill, dim3(kBlocks(n_dec)), dim3(BLS_LANES), 0, s1, (uint32_t)n_dec,
+                               in + o_keys, reinterpret_cast<const uint32_t*>(in + o_kslot),
+                               const_cast<uint32_t*>(kt.rs), const_cast<int32_t*>(kt.ss));
+        BLS_HIP(hipEventRecord(L.ev[1], s1));
+        BLS_HIP(hipEventRecord(L.ev[5], s1));
+        hipLaunchKernelGGL(k_blsw_pre, dim3((unsigned)(2 * n)), dim3(64), 0, s1, (uint32_t)n, in + o_msg,
+                           reinterpret_cast<const uint64_t*>(in + o_moff), reinterpret_cast<const uint32_t*>(in + o_mlen),
+                           in + o_dst, (uint32_t)dl, hh, kt, reinterpret_cast<const uint32_t*>(in + o_off),
+                           reinterpret_cast<const uint32_t*>(in + o_cnt), reinterpret_cast<const uint32_t*>(in + o_idx),
+                           km, ajrec, sapk);
+        BLS_HIP(hipEventRecord(L.ev[2], s1));
+        BLS_HIP(hipEventRecord(L.ev[6], s1));
+        BLS_HIP(hipEventRecord(L.ev[10], s1));
+        BLS_HIP(hipEventRecord(L.ev[3], s0));
+        hipLaunchKernelGGL(k_blsw_sigdec, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, in + o_sigs, srec,
+                           sdec);
+        BLS_HIP(hipEventRecord(L.ev[4], s0));
+        BLS_HIP(hipStreamWaitEvent(s0, L.ev[10], 0));
+        BLS_HIP(hipEventRecord(L.ev[7], s0));
+        hipLaunchKernelGGL(k_blsw_pair_sub, dim3((unsigned)(2 * n)), dim3(64), 0, s0, (uint32_t)n,
+                           (const uint32_t*)srec, (const int32_t*)sdec, (const uint32_t*)hh, 1, (const uint32_t*)ajrec,
+                           (const int32_t*)sapk, kt, reinterpret_cast<const uint32_t*>(in + o_off),
+                           reinterpret_cast<const uint32_t*>(in + o_cnt), reinterpret_cast<const uint32_t*>(in + o_idx),
+                           km, spair, ssub);
+        BLS_HIP(hipEventRecord(L.ev[8], s0));
+        hipLaunchKernelGGL(k_blsw_status, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n,
+                           (const int32_t*)sdec, (const int32_t*)ssub, (const int32_t*)sapk, (const int32_t*)spair, st);
+        BLS_HIP(hipGetLastError());
+        BLS_HIP(hipMemcpyAsync(status, st, 4 * n, hipMemcpyDeviceToHost, s0));
+        BLS_HIP(hipStreamSynchronize(s0));
+        return finish(3);
+    }
+    if (!L.side[1] && hipStreamCreateWithFlags(&L.side[1], hipStreamNonBlocking) != hipSuccess)
+        return nwv_internal_set_err(NWV_ERR_HIP, "bls stream");
+    s2 = L.side[1];
     BLS_HIP(hipStreamWaitEvent(s2, L.ev[9], 0));
     // side 0: keys, key sums
     BLS_HIP(hipEventRecord(L.ev[0], s1));
@@ -942,47 +1029,26 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     BLS_HIP(hipEventRecord(L.ev[10], s1));
     // side 1: hash to G1 (every item: the statuses are not known yet)
     BLS_HIP(hipEventRecord(L.ev[5], s2));
-    if (wave_small)
-        hipLaunchKernelGGL(k_blsw_h2c, dim3((unsigned)n), dim3(64), 0, s2, (uint32_t)n, in + o_msg,
-                           reinterpret_cast<const uint64_t*>(in + o_moff),
-                           reinterpret_cast<const uint32_t*>(in + o_mlen), in + o_dst, (uint32_t)dl, hh, km);
-    else
-        hipLaunchKernelGGL(k_bls_h2c_g, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s2, (uint32_t)n, in + o_msg,
-                           reinterpret_cast<const uint64_t*>(in + o_moff),
-                           reinterpret_cast<const uint32_t*>(in + o_mlen), in + o_dst, (uint32_t)dl, hrec, km);
+    hipLaunchKernelGGL(k_bls_h2c_g, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s2, (uint32_t)n, in + o_msg,
+                       reinterpret_cast<const uint64_t*>(in + o_moff), reinterpret_cast<const uint32_t*>(in + o_mlen),
+                       in + o_dst, (uint32_t)dl, hrec, km);
     BLS_HIP(hipEventRecord(L.ev[6], s2));
     BLS_HIP(hipEventRecord(L.ev[11], s2));
     if (wavem) {
-        // main: signature decode; side 2: its G1 check; main: every item's pairing check beside
-        // it, then the statuses joined in the oracle's order
-        // (large calls: the one-lane-per-item decode + G1 check of the group path, which keeps
-        // every lane busy, and an all-Ok subgroup column)
+        // large wave calls: the one-lane-per-item decode + G1 check of the group path, which keeps
+        // every lane busy (an all-Ok subgroup column), then every item's pairing check on a wave
         BLS_HIP(hipEventRecord(L.ev[3], s0));
-        if (wave_small) {
-            hipLaunchKernelGGL(k_blsw_sigdec, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, in + o_sigs, srec,
-                               sdec);
-            BLS_HIP(hipEventRecord(L.ev[12], s0));
-            BLS_HIP(hipStreamWaitEvent(s3, L.ev[12], 0));
-            hipLaunchKernelGGL(k_blsw_sub, dim3((unsigned)n), dim3(64), 0, s3, (uint32_t)n, (const uint32_t*)srec,
-                               (const int32_t*)sdec, ssub);
-            BLS_HIP(hipEventRecord(L.ev[4], s3));
-        } else {
-            hipLaunchKernelGGL(k_bls_sigs, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, in + o_sigs, srec,
-                               sdec);
-            BLS_HIP(hipMemsetAsync(ssub, 0, 4 * n, s0));
-            BLS_HIP(hipEventRecord(L.ev[4], s0));
-        }
-        BLS_HIP(hipEventRecord(L.ev[13], wave_small ? s3 : s0));
+        hipLaunchKernelGGL(k_bls_sigs, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, in + o_sigs, srec, sdec);
+        BLS_HIP(hipMemsetAsync(ssub, 0, 4 * n, s0));
+        BLS_HIP(hipEventRecord(L.ev[4], s0));
         BLS_HIP(hipStreamWaitEvent(s0, L.ev[10], 0));
         BLS_HIP(hipStreamWaitEvent(s0, L.ev[11], 0));
         BLS_HIP(hipEventRecord(L.ev[7], s0));
         hipLaunchKernelGGL(k_blsw_pair, dim3((unsigned)n), dim3(64), 0, s0, (uint32_t)n, (const uint32_t*)srec,
-                           (const int32_t*)sdec, wave_small ? (const uint32_t*)hh : (const uint32_t*)hrec,
-                           wave_small ? 1 : 0, (const uint32_t*)ajrec, (const int32_t*)sapk, kt,
-                           reinterpret_cast<const uint32_t*>(in + o_off), reinterpret_cast<const uint32_t*>(in + o_cnt),
+                           (const int32_t*)sdec, (const uint32_t*)hrec, 0, (const uint32_t*)ajrec, (const int32_t*)sapk,
+                           kt, reinterpret_cast<const uint32_t*>(in + o_off), reinterpret_cast<const uint32_t*>(in + o_cnt),
                            reinterpret_cast<const uint32_t*>(in + o_idx), km, spair);
         BLS_HIP(hipEventRecord(L.ev[8], s0));
-        BLS_HIP(hipStreamWaitEvent(s0, L.ev[13], 0));
         hipLaunchKernelGGL(k_blsw_status, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n,
                            (const int32_t*)sdec, (const int32_t*)ssub, (const int32_t*)sapk, (const int32_t*)spair, st);
         BLS_HIP(hipGetLastError());
