@@ -58,10 +58,12 @@ tests/_build/libhostemu.so: tests/hostemu/hostemu.cpp $(CSRC)
 	@mkdir -p tests/_build
 	$(HIPCC) -std=c++17 -O1 --offload-host-only -x hip -DNWV_BOUNDS_CHECK -fPIC -shared -o $@ tests/hostemu/hostemu.cpp
 
-tools: tools/ubench_valu tools/ubench_field
+tools: tools/ubench_valu tools/ubench_field tools/ubench_wave
 tools/ubench_valu: tools/ubench_valu.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -o $@ $<
 tools/ubench_field: tools/ubench_field.hip narwhal_amd/csrc/fe25519.h
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
+tools/ubench_wave: tools/ubench_wave.hip $(BLS_SRC)
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 
 clean:

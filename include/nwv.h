@@ -68,6 +68,12 @@ typedef struct nwv_ctx nwv_ctx;
  * 8-lane group kernels (per item only after a rejection) instead of the default, every item's
  * own pairing check on one 64-lane wave (exact per-item statuses either way) */
 #define NWV_FLAG_BLS_BATCH 128u
+/* BLS12-381 (nwv_bls.h): signatures that passed a verify call of up to 1024 items on the wave path
+ * are kept decoded (and G1-checked) on the device, by their 48 bytes, in a ring of 65,536;
+ * nwv_bls_aggregate over signatures that are all in it sums the kept points instead of decoding
+ * and checking each again (the Core aggregates votes it has already verified).  This flag turns
+ * the ring off (every aggregate decodes and checks its signatures). */
+#define NWV_FLAG_NO_SIGCACHE 256u
 
 /* ------------------------------------------------------------------ lifecycle ----- */
 /* Process-wide context creation (created once, in Primary::spawn).

@@ -31,6 +31,7 @@ NWV_FLAG_MSM_SORT2 = 16
 NWV_FLAG_NO_MSM_REUSE = 32
 NWV_FLAG_BLS_PER_ITEM = 64
 NWV_FLAG_BLS_BATCH = 128
+NWV_FLAG_NO_SIGCACHE = 256
 NWV_RUN_TIMED = 0x100
 
 

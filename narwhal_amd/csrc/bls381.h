@@ -418,6 +418,139 @@ BLS_NOINLINE fp fp_inv_vt_t(const fp& x) {
 NWV_HD fp fp_inv_vt(const fp& x) { return fp_inv_vt_t<false>(x); }
 NWV_HD fp fp_inv_vt_uniform(const fp& x) { return fp_inv_vt_t<true>(x); }
 
+// The same inversion with a batch's four 12-word updates as independent rows: row r (0..3) applies
+// the matrix row r & 1 to (a, b) (r < 2: exact, / 2^30, made non-negative) or to (u, v) (r >= 2:
+// / 2^30 mod p), each with the batch's own coefficients; a negative (a, b) row then negates its
+// (u, v) row mod p (fp_inv_vt_t negates the coefficients first: the same value).  On the device the
+// rows run on four lanes at once (fp_inv_wave); inv_rows is the host form, one row after another.
+NWV_HD bool inv_row(int r, int64_t f0, int64_t g0, int64_t f1, int64_t g1, const uint32_t* a, const uint32_t* b,
+                    const uint32_t* u, const uint32_t* v, const uint32_t* P, uint32_t* o) {
+    const bool row1 = (r & 1) != 0, uv = (r & 2) != 0;
+    const int64_t F = row1 ? f1 : f0, G = row1 ? g1 : g0;
+    if (uv) {
+        w_lin2_modp(o, F, u, G, v, P);
+        return false;
+    }
+    uint32_t t[BW + 1];
+    w_lin2(t, F, a, G, b);
+    const bool neg = w_neg13(t);
+    w_shr30(o, t);
+    return neg;
+}
+// o <- p - o unless o = 0 (o in [0, p))
+NWV_HD void w_negp(uint32_t* o, const uint32_t* P) {
+    if (w_is_zero(o)) return;
+    int64_t c = 0;
+    for (int i = 0; i < BW; i++) {
+        c += (int64_t)P[i] - (int64_t)o[i];
+        o[i] = (uint32_t)c;
+        c >>= 32;
+    }
+}
+// the batch's 30 divsteps on the approximations of a and b -> the matrix [f0 g0; f1 g1]
+NWV_HD void inv_divsteps(const uint32_t* a, const uint32_t* b, int64_t& f0o, int64_t& g0o, int64_t& f1o,
+                         int64_t& g1o) {
+    int n = w_bitlen(a);
+    const int nb = w_bitlen(b);
+    n = n > nb ? n : nb;
+    n = n > 62 ? n : 62;
+    uint64_t xa = ((uint64_t)w_bits32(a, n - 32) << 30) | (a[0] & ((1u << 30) - 1u));
+    uint64_t xb = ((uint64_t)w_bits32(b, n - 32) << 30) | (b[0] & ((1u << 30) - 1u));
+    int32_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+#pragma unroll
+    for (int i = 0; i < 30; i++) {
+        const bool odd = (xa & 1) != 0;
+        const bool sw = odd && xa < xb;
+        const uint64_t ya = sw ? xb : xa, yb = sw ? xa : xb;
+        const int32_t h0 = sw ? f1 : f0, h1 = sw ? f0 : f1, k0 = sw ? g1 : g0, k1 = sw ? g0 : g1;
+        xa = odd ? ya - yb : ya;
+        xb = yb;
+        f0 = odd ? h0 - h1 : h0;
+        g0 = odd ? k0 - k1 : k0;
+        f1 = h1;
+        g1 = k1;
+        xa >>= 1;
+        f1 *= 2;
+        g1 *= 2;
+    }
+    f0o = f0;
+    g0o = g0;
+    f1o = f1;
+    g1o = g1;
+}
+NWV_HD fp inv_finish(const uint32_t* v) {
+    const fp r = fp_from_w(v);
+    fp r3;
+    {
+        const uint32_t c[NL] = BLS_R3;
+        for (int j = 0; j < NL; j++) r3.l[j] = c[j];
+    }
+    return fp_mul(r, r3);
+}
+inline fp inv_rows(const fp& x) {
+    const fp xc = fp_canon(x);
+    if (fp_is_zero(xc)) return fp_zero();
+    uint32_t a[BW], b[BW], u[BW], v[BW], P[BW];
+    w_from_fp(a, xc);
+    w_from_fp(P, k_p());
+    for (int i = 0; i < BW; i++) {
+        b[i] = P[i];
+        u[i] = v[i] = 0;
+    }
+    u[0] = 1;
+    for (int it = 0; it < 64 && !w_is_zero(a); it++) {
+        int64_t f0, g0, f1, g1;
+        inv_divsteps(a, b, f0, g0, f1, g1);
+        uint32_t o[4][BW];
+        bool neg[4];
+        for (int r = 0; r < 4; r++) neg[r] = inv_row(r, f0, g0, f1, g1, a, b, u, v, P, o[r]);
+        for (int r = 2; r < 4; r++)
+            if (neg[r - 2]) w_negp(o[r], P);
+        for (int i = 0; i < BW; i++) {
+            a[i] = o[0][i];
+            b[i] = o[1][i];
+            u[i] = o[2][i];
+            v[i] = o[3][i];
+        }
+    }
+    return inv_finish(v);
+}
+#if defined(__HIP_DEVICE_COMPILE__) || (defined(__HIPCC__) && !defined(BLS_GROUP_HOST_EMU))
+// every lane of the wave calls it with the same x: each lane runs the divsteps (uniform), lanes
+// 0..3 (and their copies r = lane & 3) compute the four rows at once, then read them back from
+// lanes 0..3
+__device__ __attribute__((noinline)) fp fp_inv_wave(const fp& x) {
+    const int r = (int)(threadIdx.x & 3);
+    fp xu;
+    for (int j = 0; j < NL; j++) xu.l[j] = __builtin_amdgcn_readfirstlane(x.l[j]);
+    const fp xc = fp_canon(xu);
+    if (fp_is_zero(xc)) return fp_zero();
+    uint32_t a[BW], b[BW], u[BW], v[BW], P[BW];
+    w_from_fp(a, xc);
+    w_from_fp(P, k_p());
+    for (int i = 0; i < BW; i++) {
+        b[i] = P[i];
+        u[i] = v[i] = 0;
+    }
+    u[0] = 1;
+    for (int it = 0; it < 64 && !w_is_zero(a); it++) {
+        int64_t f0, g0, f1, g1;
+        inv_divsteps(a, b, f0, g0, f1, g1);
+        uint32_t o[BW];
+        const bool neg = inv_row(r, f0, g0, f1, g1, a, b, u, v, P, o);
+        const int negs = (int)__builtin_amdgcn_readfirstlane(__ballot(neg) & 3u);  // rows 0, 1
+        if (r >= 2 && ((negs >> (r - 2)) & 1)) w_negp(o, P);
+        for (int i = 0; i < BW; i++) {
+            a[i] = __builtin_amdgcn_readlane(o[i], 0);
+            b[i] = __builtin_amdgcn_readlane(o[i], 1);
+            u[i] = __builtin_amdgcn_readlane(o[i], 2);
+            v[i] = __builtin_amdgcn_readlane(o[i], 3);
+        }
+    }
+    return inv_finish(v);
+}
+#endif
+
 // sqrt for p = 3 mod 4; false if a is not a square
 NWV_HD bool fp_sqrt(fp& r, const fp& a) {
     const uint32_t e[12] = BLS_E_SQRT;

@@ -381,5 +381,52 @@ NWV_HD bool w_pairing_check_h(const W& w, const uint32_t* sig_rec, const uint32_
     return w_pairing_check_g(w, sig_rec, hh_rec, true, apk_rec, false, qlines);
 }
 
+
+// ---- AggregateAuthenticator::aggregate (types/src/primary.rs:476-477) on a wave: g1_sum32 adds
+// G1SUM_N points with complete formulas (the identity and equal points need no branches); point k
+// sits in slots g1sum_slot(k) + 0..2 as (X : Y : Z) and the sum lands in U
+constexpr int G1P_WORDS = 3 * NL;  // a homogeneous partial sum (X, Y, Z)
+
+// the program's inputs: affine records (hom = 0: G1_REC_WORDS each, identity flagged; record j at
+// idx[j] when idx, else at j) or partial sums (hom = 1: G1P_WORDS each); inputs past m are the
+// identity.  The caller has run init_slots (the one comes from its constant slot).
+template <class W>
+NWV_HD void w_g1_sum_put(const W& w, const uint32_t* in, const uint32_t* idx, int hom, uint32_t first, uint32_t m) {
+    using namespace wave;
+    const uint32_t* one = w.wm + SW * SLOT_ONE;
+    for (int k = 0; k < G1SUM_N; k++) {
+        const uint32_t j = first + (uint32_t)k;
+        const int s = g1sum_slot(k);
+        if (j < m && hom) {
+            w.put_words(s, in + (size_t)G1P_WORDS * j, 3);
+            continue;
+        }
+        const uint32_t* r = j < m ? in + (size_t)G1_REC_WORDS * (idx ? idx[j] : j) : nullptr;
+        if (r && !r[2 * NL]) {
+            w.put_words(s, r, 2);
+            w.put_words(s + 2, one, 1);
+        } else {
+            w.zero(s, 3);
+            w.sync();
+            w.put_words(s + 1, one, 1);
+        }
+    }
+    w.sync();
+}
+
+// U (the program's sum) -> the 48-byte compressed point, x = X / Z, y = Y / Z (every lane calls
+// it: the inversion runs on the wave; lane 0 writes)
+template <class W>
+NWV_HD void w_g1_sum_compress(const W& w, uint8_t* out48) {
+    using namespace wave;
+    const fp X = w.get(REG_U), Y = w.get(REG_U + 1), Z = w.get(REG_U + 2);
+    if (fp_is_zero(Z)) {
+        if (w.lane == 0) g1_compress(out48, fp_zero(), fp_zero(), true);
+        return;
+    }
+    const fp zi = w.inv(Z);
+    if (w.lane == 0) g1_compress(out48, fp_mul(X, zi), fp_mul(Y, zi), false);
+}
+
 }  // namespace bls
 

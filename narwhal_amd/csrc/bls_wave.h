@@ -292,6 +292,8 @@ struct Wave {
     uint32_t* wm;
     int lane;
     __device__ void sync() const { wsync(); }
+    // x^-1 for a wave-uniform x (every lane calls it; the four update rows on four lanes)
+    __device__ fp inv(const fp& x) const { return fp_inv_wave(x); }
     // the program `reps` times over (one call: runs of squarings / doublings)
     __device__ void run(Prog p, int reps = 1) const { wave_run(wm, lane, p.off, p.n, p.nl0, reps); }
     // up to 128 words of global memory fetched into registers ahead of use (a prefetch), and
@@ -354,6 +356,7 @@ struct Wave {
     uint32_t* wm;
     int lane = 0;
     void sync() const {}
+    fp inv(const fp& x) const { return inv_rows(x); }
     void run(Prog p, int reps) const {
         for (int r = 0; r < reps; r++) run(p);
     }
@@ -427,6 +430,29 @@ NWV_HD void init_slots(const W& w) {
     w.put_words(NSLOTS, &T_KP[0][0], 16);
     w.sync();
 }
+#ifdef BLS_WAVE_DEV
+// the device form: every lane fetches all its words of both tables before storing any (one memory
+// round trip; put_words' loop waits for each 64-word load in turn)
+__device__ __forceinline__ void init_slots(const Wave& w) {
+    constexpr int NC = SW * NCONSTS, NK = 16 * SW, NT = (NC + NK + 63) / 64;
+    const uint32_t* c = &T_CONSTS[0][0];
+    const uint32_t* k = &T_KP[0][0];
+    uint32_t v[NT];
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+        const int i = w.lane + 64 * t;
+        v[t] = i < NC ? c[i] : i < NC + NK ? k[i - NC] : 0u;
+    }
+    if (w.lane < SW) w.wm[w.lane] = 0;
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+        const int i = w.lane + 64 * t;
+        if (i < NC) w.wm[SW + i] = v[t];
+        else if (i < NC + NK) w.wm[SW * NSLOTS + (i - NC)] = v[t];
+    }
+    w.sync();
+}
+#endif
 
 // the square-and-multiply chain of a 64-bit k (top bit 63) below its top bit: each run of
 // squarings (doublings) up to the next set bit is one interpreter call
@@ -463,7 +489,7 @@ template <class W>
 NWV_HD void final_exp(const W& w) {
     w.run(P_INV_A);
     const fp n = w.get(REG_N);
-    w.put_fp(REG_N + 1, fp_inv_vt_uniform(n));  // every lane holds the same norm
+    w.put_fp(REG_N + 1, w.inv(n));  // every lane holds the same norm
     w.sync();
     w.run(P_INV_B);
     w.run(P_EASY1);

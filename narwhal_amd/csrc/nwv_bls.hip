@@ -68,6 +68,7 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_rec_copy(uint32_t n, const ui
 // A call's key table: index k < KC_CAP names slot k of the device's key cache, k >= KC_CAP entry
 // k - KC_CAP of the call's scratch table (keys the cache does not hold, decoded by this call)
 constexpr uint32_t KC_CAP = 65536;
+constexpr uint32_t SC_CAP = 65536;  // the verified-signature ring (BlsSigCache)
 struct KeyTab {
     const uint32_t* rc;
     const int32_t* sc;
@@ -262,37 +263,10 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_final(const uint32_t* frec, i
     g_sync();
     if (g.slot == 0) *ok = r ? 1 : 0;
 }
-// AggregateAuthenticator::aggregate (Certificate::new_unsafe, types/src/primary.rs:476-477): the sum
-// of n decoded signatures as a tree over the lanes -- each decoded record becomes a Jacobian entry
-// (k_bls_sig_jac), ceil(log2 n) levels of k_bls_sfold add pairs, and one lane takes the first bad
-// status in list order and compresses the sum (k_bls_g1_sum_out)
-__global__ __launch_bounds__(BLS_LANES) void k_bls_sig_jac(uint32_t n, const uint32_t* rec, uint32_t* srec) {
-    BLS_IDX();
-    const uint32_t* r = rec + (size_t)G1_REC_WORDS * i;
-    jac<fp> p;
-    p.inf = r[2 * NL] != 0;  // a failed decode is stored as the identity (its status decides)
-    p.x = ld_fp(r);
-    p.y = ld_fp(r + NL);
-    p.z = k_one();
-    st_g1j(srec + (size_t)G1J_REC_WORDS * i, p);
-}
 // st[i] <- the decode status when it is a failure, else the G1 check's
 __global__ __launch_bounds__(BLS_LANES) void k_bls_st_join(uint32_t n, const int32_t* dec, int32_t* st) {
     BLS_IDX();
     if (dec[i] != ST_OK) st[i] = dec[i];
-}
-__global__ void k_bls_g1_sum_out(uint32_t n, const int32_t* st, const uint32_t* srec, uint8_t* out48, int32_t* out_st) {
-    if (blockIdx.x || threadIdx.x) return;
-    for (uint32_t k = 0; k < n; k++)
-        if (st[k] != ST_OK) {
-            *out_st = st[k];
-            return;
-        }
-    const jac<fp> acc = ld_g1j(srec);
-    fp x = fp_zero(), y = fp_zero();
-    if (!acc.inf) g1_to_affine_vt(x, y, acc);
-    g1_compress(out48, x, y, acc.inf);
-    *out_st = ST_OK;
 }
 __global__ __launch_bounds__(BLS_LANES) void k_bls_keygen(uint32_t n, const uint8_t* sk, uint8_t* pk) {
     BLS_IDX();
@@ -544,11 +518,98 @@ __global__ __launch_bounds__(64) void k_blsw_pre(uint32_t n, const uint8_t* msg,
         blsw_apk_item(lds, b - n, kt, pk_off, pk_cnt, pk_idx, kmode, arec, st_apk);
 }
 
+// AggregateAuthenticator::aggregate (types/src/primary.rs:476-477) on the wave engine: the g1_sum32
+// program adds 32 points per wave.  The inputs (w_g1_sum_put's forms: affine records, optionally
+// through a list of positions, or partial sums) are fetched in one batch -- every lane issues its
+// 21 words' loads before any is stored -- rather than point by point.
+__device__ __forceinline__ void blsw_sum_load(uint32_t* wm, const uint32_t* in, const uint32_t* idx, int hom,
+                                              uint32_t first, uint32_t m) {
+    using namespace wave;
+    const int lane = (int)threadIdx.x;
+    constexpr int PW = 3 * NL, TOT = G1SUM_N * PW, T = (TOT + 63) / 64;
+    static_assert(T <= 32, "one mask bit per word");
+    init_slots(Wave{wm, lane});
+    uint32_t v[T], one_at = 0;
+#pragma unroll
+    for (int t = 0; t < T; t++) {
+        const int wd = lane + 64 * t, k = wd / PW, c = (wd % PW) / NL, l = wd % NL;
+        const uint32_t j = first + (uint32_t)k;
+        uint32_t x = 0;
+        bool one = false;
+        if (wd < TOT) {
+            if (j >= m) {
+                one = c == 1;  // the identity (0 : 1 : 0)
+            } else if (hom) {
+                x = in[(size_t)PW * j + (wd % PW)];
+            } else {
+                const uint32_t* r = in + (size_t)G1_REC_WORDS * (idx ? idx[j] : j);
+                if (r[2 * NL]) one = c == 1;
+                else if (c < 2) x = r[c * NL + l];
+                else one = true;
+            }
+        }
+        v[t] = x;
+        one_at |= (one ? 1u : 0u) << t;
+    }
+#pragma unroll
+    for (int t = 0; t < T; t++) {
+        const int wd = lane + 64 * t, k = wd / PW;
+        if (wd < TOT)
+            wm[SW * g1sum_slot(k) + (wd % PW)] = (one_at >> t) & 1u ? wm[SW * SLOT_ONE + wd % NL] : v[t];
+    }
+    wsync();
+}
+__global__ __launch_bounds__(64) void k_blsw_g1_sum(uint32_t m, const uint32_t* in, const uint32_t* idx, int hom,
+                                                    uint32_t* part) {
+    __shared__ uint32_t wm[wave::WM_WORDS];
+    const uint32_t b = blockIdx.x;
+    if ((size_t)b * wave::G1SUM_N >= m) return;
+    blsw_sum_load(wm, in, idx, hom, b * wave::G1SUM_N, m);
+    const wave::Wave w{wm, (int)threadIdx.x};
+    w.run(wave::P_G1_SUM32);
+    w.get_words(wave::REG_U, part + (size_t)G1P_WORDS * b, 3);
+}
+// the last level (m <= G1SUM_N inputs, one block): the first bad status of the n_st items in list
+// order (st: null when every item is known good), else the compressed sum
+__global__ __launch_bounds__(64) void k_blsw_g1_sum_fin(uint32_t m, const uint32_t* in, const uint32_t* idx, int hom,
+                                                        uint32_t n_st, const int32_t* st, uint8_t* out48,
+                                                        int32_t* out_st) {
+    __shared__ uint32_t wm[wave::WM_WORDS];
+    const int lane = (int)threadIdx.x;
+    if (blockIdx.x) return;
+    if (st) {
+        uint32_t bad = 0xffffffffu;
+        for (uint32_t k = (uint32_t)lane; k < n_st; k += 64)
+            if (st[k] != ST_OK) {
+                bad = k;
+                break;
+            }
+        for (int o = 32; o >= 1; o >>= 1) bad = min(bad, (uint32_t)__shfl_xor((int)bad, o));
+        if (bad != 0xffffffffu) {
+            if (lane == 0) *out_st = st[bad];
+            return;
+        }
+    }
+    blsw_sum_load(wm, in, idx, hom, 0, m);
+    const wave::Wave w{wm, lane};
+    w.run(wave::P_G1_SUM32);
+    w_g1_sum_compress(w, out48);
+    if (lane == 0) *out_st = ST_OK;
+}
+
 // the oracle's order: signature decode, its G1 check, the keys, the pairing equation
+// (sc_rec: a verified signature's record is also kept in the signature ring at slot sc_base + i)
 __global__ __launch_bounds__(BLS_LANES) void k_blsw_status(uint32_t n, const int32_t* dec, const int32_t* sub,
-                                                           const int32_t* apk, const int32_t* pair, int32_t* st) {
+                                                           const int32_t* apk, const int32_t* pair, int32_t* st,
+                                                           const uint32_t* srec, uint32_t* sc_rec, uint32_t sc_base) {
     BLS_IDX();
-    st[i] = dec[i] != ST_OK ? dec[i] : sub[i] != ST_OK ? sub[i] : apk[i] != ST_OK ? apk[i] : pair[i];
+    const int32_t s = dec[i] != ST_OK ? dec[i] : sub[i] != ST_OK ? sub[i] : apk[i] != ST_OK ? apk[i] : pair[i];
+    st[i] = s;
+    if (sc_rec && s == ST_OK) {
+        uint32_t* d = sc_rec + (size_t)G1_REC_WORDS * ((sc_base + i) % SC_CAP);
+        const uint32_t* r = srec + (size_t)G1_REC_WORDS * i;
+        for (int k = 0; k < G1_REC_WORDS; k++) d[k] = r[k];
+    }
 }
 
 // ------------------------------------------------------------------------------- host side
@@ -632,12 +693,80 @@ struct BlsLane {
     }
 };
 
+// Signatures that passed a wave-path verify call of up to wave_max items, kept decoded (affine G1
+// records) by their 48 bytes: AggregateAuthenticator::aggregate over votes the Core has already
+// verified (primary/src/aggregators.rs VotesAggregator::append -> types/src/primary.rs:476) then
+// sums kept records instead of decoding and G1-checking each signature again.  A ring of SC_CAP
+// records: a verify call reserves n slots (unmapping what they held) under the unique lock before
+// its kernels run, k_blsw_status writes the verified records into them, and the call maps them
+// after its stream synchronises (a slot re-reserved meanwhile stays unmapped: `gen`).  An
+// aggregate holds the shared lock from its lookups until its stream synchronises, so no slot it
+// reads is reserved while its kernels run.
+struct Sig48 {
+    uint8_t b[48];
+    bool operator==(const Sig48& o) const { return std::memcmp(b, o.b, 48) == 0; }
+};
+struct Sig48Hash {
+    size_t operator()(const Sig48& s) const {  // the x coordinate's low 64 bits (big-endian bytes 40..47)
+        uint64_t h;
+        std::memcpy(&h, s.b + 40, 8);
+        return (size_t)(h * 0x9e3779b97f4a7c15ull);
+    }
+};
+struct BlsSigCache {
+    std::shared_mutex mu;
+    DBuf rec;  // SC_CAP x G1_REC_WORDS
+    std::unordered_map<Sig48, uint32_t, Sig48Hash> slot;
+    std::vector<Sig48> key;     // the signature slot s holds (when held[s])
+    std::vector<uint8_t> held;  // slot s is mapped
+    std::vector<uint64_t> gen;  // the reservation slot s belongs to
+    uint32_t next = 0;
+    uint64_t gens = 0;
+    // n slots from the ring's cursor, unmapped; -> the first slot (NWV_OK) and the reservation
+    int reserve(size_t n, uint32_t& base, uint64_t& g) {
+        std::unique_lock<std::shared_mutex> lk(mu);
+        if (!rec.p) {
+            int rc = rec.ensure((size_t)4 * G1_REC_WORDS * SC_CAP);
+            if (rc) return rc;
+            key.resize(SC_CAP);
+            held.assign(SC_CAP, 0);
+            gen.assign(SC_CAP, 0);
+            slot.reserve(SC_CAP);
+        }
+        base = next;
+        g = ++gens;
+        for (size_t i = 0; i < n; i++) {
+            const uint32_t t = (uint32_t)((base + i) % SC_CAP);
+            if (held[t]) {
+                auto it = slot.find(key[t]);
+                if (it != slot.end() && it->second == t) slot.erase(it);
+                held[t] = 0;
+            }
+            gen[t] = g;
+        }
+        next = (uint32_t)((base + n) % SC_CAP);
+        return NWV_OK;
+    }
+    // the call's verified signatures (status OK) mapped to their slots
+    void publish(size_t n, const uint8_t* sigs, const int32_t* status, uint32_t base, uint64_t g) {
+        std::unique_lock<std::shared_mutex> lk(mu);
+        for (size_t i = 0; i < n; i++) {
+            const uint32_t t = (uint32_t)((base + i) % SC_CAP);
+            if (status[i] != ST_OK || gen[t] != g) continue;
+            std::memcpy(key[t].b, sigs + 48 * i, 48);
+            held[t] = 1;
+            slot[key[t]] = t;
+        }
+    }
+};
+
 constexpr size_t kMaxLanes = 8;
 
 struct BlsDev {
     int ordinal = -1;
     uint32_t flags = 0;  // the context's nwv_init flags
     BlsKeyCache kc;
+    BlsSigCache sc;
     std::mutex pool_mu;
     std::condition_variable pool_cv;
     std::vector<std::unique_ptr<BlsLane>> lanes;
@@ -999,11 +1128,18 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
                            reinterpret_cast<const uint32_t*>(in + o_cnt), reinterpret_cast<const uint32_t*>(in + o_idx),
                            km, spair, ssub);
         BLS_HIP(hipEventRecord(L.ev[8], s0));
+        // verified signatures stay decoded in the device's ring (BlsSigCache) for aggregates
+        const bool keep = !(d.flags & NWV_FLAG_NO_SIGCACHE);
+        uint32_t sc_base = 0;
+        uint64_t sc_gen = 0;
+        if (keep && (rc = d.sc.reserve(n, sc_base, sc_gen))) return rc;
         hipLaunchKernelGGL(k_blsw_status, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n,
-                           (const int32_t*)sdec, (const int32_t*)ssub, (const int32_t*)sapk, (const int32_t*)spair, st);
+                           (const int32_t*)sdec, (const int32_t*)ssub, (const int32_t*)sapk, (const int32_t*)spair, st,
+                           (const uint32_t*)srec, keep ? static_cast<uint32_t*>(d.sc.rec.p) : nullptr, sc_base);
         BLS_HIP(hipGetLastError());
         BLS_HIP(hipMemcpyAsync(status, st, 4 * n, hipMemcpyDeviceToHost, s0));
         BLS_HIP(hipStreamSynchronize(s0));
+        if (keep) d.sc.publish(n, sigs, status, sc_base, sc_gen);
         return finish(3);
     }
     if (!L.side[1] && hipStreamCreateWithFlags(&L.side[1], hipStreamNonBlocking) != hipSuccess)
@@ -1050,7 +1186,8 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
                            reinterpret_cast<const uint32_t*>(in + o_idx), km, spair);
         BLS_HIP(hipEventRecord(L.ev[8], s0));
         hipLaunchKernelGGL(k_blsw_status, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n,
-                           (const int32_t*)sdec, (const int32_t*)ssub, (const int32_t*)sapk, (const int32_t*)spair, st);
+                           (const int32_t*)sdec, (const int32_t*)ssub, (const int32_t*)sapk, (const int32_t*)spair, st,
+                           (const uint32_t*)srec, nullptr, 0u);
         BLS_HIP(hipGetLastError());
         BLS_HIP(hipMemcpyAsync(status, st, 4 * n, hipMemcpyDeviceToHost, s0));
         BLS_HIP(hipStreamSynchronize(s0));
@@ -1233,12 +1370,64 @@ int nwv_bls_aggregate(nwv_ctx* ctx, size_t n, const uint8_t* sigs48, uint8_t out
     LaneLease lane(*d);
     if ((rc = lane.rc())) return rc;
     BlsLane& L = *lane;
-    const size_t w_rec = 0, w_st = al256(4 * G1_REC_WORDS * n), w_j = al256(w_st + 4 * n),
-                 w_out = al256(w_j + 4 * G1J_REC_WORDS * n), w_ost = w_out + 64, w_st2 = al256(w_ost + 8),
-                 w_end = w_st2 + 4 * n;
+    // scratch: records, statuses, the sum tree's two partial-sum levels, the output, decode statuses
+    const size_t n_part = (n + wave::G1SUM_N - 1) / wave::G1SUM_N + 1;
+    const size_t w_rec = 0, w_st = al256(4 * G1_REC_WORDS * n), w_pa = al256(w_st + 4 * n),
+                 w_pb = al256(w_pa + 4 * G1P_WORDS * n_part), w_out = al256(w_pb + 4 * G1P_WORDS * n_part),
+                 w_ost = w_out + 64, w_st2 = al256(w_ost + 8), w_end = w_st2 + 4 * n;
     if ((rc = L.in.ensure(48 * n)) || (rc = L.work.ensure(w_end)) || (rc = L.stage.ensure(128))) return rc;
     uint8_t* w = static_cast<uint8_t*>(L.work.p);
-    auto* srec = reinterpret_cast<uint32_t*>(w + w_j);
+    // the sum of the records at `in` (through the positions idx_d when given) as a tree of
+    // k_blsw_g1_sum levels; the last (one block) takes the first bad status of st_d when given
+    auto sum_tree = [&](const uint32_t* in, const uint32_t* idx_d, const int32_t* st_d) {
+        uint32_t m = (uint32_t)n;
+        const uint32_t* src = in;
+        int hom = 0, flip = 0;
+        while (m > (uint32_t)wave::G1SUM_N) {
+            const uint32_t nb = (m + wave::G1SUM_N - 1) / wave::G1SUM_N;
+            auto* dst = reinterpret_cast<uint32_t*>(w + (flip ? w_pb : w_pa));
+            hipLaunchKernelGGL(k_blsw_g1_sum, dim3(nb), dim3(64), 0, L.stream, m, src, idx_d, hom, dst);
+            src = dst;
+            idx_d = nullptr;
+            hom = 1;
+            m = nb;
+            flip ^= 1;
+        }
+        hipLaunchKernelGGL(k_blsw_g1_sum_fin, dim3(1), dim3(64), 0, L.stream, m, src, idx_d, hom,
+                           st_d ? (uint32_t)n : 0u, st_d, w + w_out, reinterpret_cast<int32_t*>(w + w_ost));
+    };
+    auto fetch = [&]() -> int {
+        BLS_HIP(hipGetLastError());
+        uint8_t* hs = static_cast<uint8_t*>(L.stage.p);
+        BLS_HIP(hipMemcpyAsync(hs, w + w_out, 64 + 8, hipMemcpyDeviceToHost, L.stream));
+        BLS_HIP(hipStreamSynchronize(L.stream));
+        int32_t st;
+        std::memcpy(&st, hs + 64, 4);
+        if (status_or_null) *status_or_null = st;
+        if (st != NWV_BLS_OK) return NWV_ERR_SIGNATURE;
+        std::memcpy(out48, hs, 48);
+        return NWV_OK;
+    };
+    // every signature verified by an earlier call: sum the ring's records (no decode, no G1 check)
+    if (!(d->flags & NWV_FLAG_NO_SIGCACHE)) {
+        std::shared_lock<std::shared_mutex> hold(d->sc.mu);
+        if (d->sc.rec.p && n <= SC_CAP) {
+            std::vector<uint32_t> pos(n);
+            bool all = true;
+            Sig48 k;
+            for (size_t i = 0; i < n && all; i++) {
+                std::memcpy(k.b, sigs48 + 48 * i, 48);
+                auto it = d->sc.slot.find(k);
+                if (it == d->sc.slot.end()) all = false;
+                else pos[i] = it->second;
+            }
+            if (all) {
+                BLS_HIP(hipMemcpyAsync(L.in.p, pos.data(), 4 * n, hipMemcpyHostToDevice, L.stream));
+                sum_tree(static_cast<const uint32_t*>(d->sc.rec.p), static_cast<const uint32_t*>(L.in.p), nullptr);
+                return fetch();
+            }
+        }
+    }
     BLS_HIP(hipMemcpyAsync(L.in.p, sigs48, 48 * n, hipMemcpyHostToDevice, L.stream));
     if (n <= 1024) {  // decode on one lane each, the G1 checks on a wave each
         auto* sdec = reinterpret_cast<int32_t*>(w + w_st2);
@@ -1254,23 +1443,8 @@ int nwv_bls_aggregate(nwv_ctx* ctx, size_t n, const uint8_t* sigs48, uint8_t out
                            (const uint8_t*)L.in.p, reinterpret_cast<uint32_t*>(w + w_rec),
                            reinterpret_cast<int32_t*>(w + w_st));
     }
-    hipLaunchKernelGGL(k_bls_sig_jac, dim3(kBlocks(n)), dim3(BLS_LANES), 0, L.stream, (uint32_t)n,
-                       reinterpret_cast<const uint32_t*>(w + w_rec), srec);
-    for (uint32_t m = (uint32_t)n; m > 1; m = (m + 1) / 2)
-        hipLaunchKernelGGL(k_bls_sfold, dim3(kBlocks(m / 2)), dim3(BLS_LANES), 0, L.stream, m, srec);
-    hipLaunchKernelGGL(k_bls_g1_sum_out, dim3(1), dim3(1), 0, L.stream, (uint32_t)n,
-                       reinterpret_cast<const int32_t*>(w + w_st), (const uint32_t*)srec, w + w_out,
-                       reinterpret_cast<int32_t*>(w + w_ost));
-    BLS_HIP(hipGetLastError());
-    uint8_t* hs = static_cast<uint8_t*>(L.stage.p);
-    BLS_HIP(hipMemcpyAsync(hs, w + w_out, 64 + 8, hipMemcpyDeviceToHost, L.stream));
-    BLS_HIP(hipStreamSynchronize(L.stream));
-    int32_t st;
-    std::memcpy(&st, hs + 64, 4);
-    if (status_or_null) *status_or_null = st;
-    if (st != NWV_BLS_OK) return NWV_ERR_SIGNATURE;
-    std::memcpy(out48, hs, 48);
-    return NWV_OK;
+    sum_tree(reinterpret_cast<const uint32_t*>(w + w_rec), nullptr, reinterpret_cast<const int32_t*>(w + w_st));
+    return fetch();
 }
 
 int nwv_bls_verify_batch_empty_fail(nwv_ctx* ctx, const uint8_t* msg, size_t msg_len, const uint8_t* pks,

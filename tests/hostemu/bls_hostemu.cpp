@@ -320,6 +320,57 @@ void bh_fp_inv_vt(const uint8_t* a, uint8_t* out) {
     be_to_mont(x, a);
     mont_to_be(out, fp_inv_vt(x));
 }
+// the row form (fp_inv_wave's order of updates, one row after another)
+void bh_fp_inv_rows(const uint8_t* a, uint8_t* out) {
+    fp x;
+    be_to_mont(x, a);
+    mont_to_be(out, inv_rows(x));
+}
+
+// AggregateAuthenticator::aggregate as the device runs it: statuses in list order (decode, then
+// the wave G1 check), the records summed 32 at a time by g1_sum32 into partial sums, the partials
+// summed the same way, U compressed (first = 0: records straight; first = 1: through a reversed
+// position list, as the verified-signature ring is read)
+int bh_w_aggregate(size_t n, const uint8_t* sigs, uint8_t* out48, int through_idx) {
+    if (n == 0) return ST_AGGR_MISMATCH;
+    std::vector<uint32_t> rec(G1_REC_WORDS * n), pos(n);
+    for (size_t i = 0; i < n; i++) {
+        const int32_t st = bh_w_sig_status(sigs + 48 * i);
+        if (st != ST_OK) return st;
+        fp x, y;
+        bool inf;
+        g1_decompress(x, y, inf, sigs + 48 * i);
+        const size_t at = through_idx ? n - 1 - i : i;  // record i stored at position `at`
+        st_g1(rec.data() + G1_REC_WORDS * at, inf ? fp_zero() : x, inf ? fp_zero() : y, inf);
+        pos[i] = (uint32_t)at;
+    }
+    const wave::Wave w = host_wave();
+    const uint32_t* src = rec.data();
+    const uint32_t* idx = through_idx ? pos.data() : nullptr;
+    int hom = 0;
+    size_t m = n;
+    std::vector<uint32_t> part;
+    while (m > (size_t)wave::G1SUM_N) {
+        const size_t nb = (m + wave::G1SUM_N - 1) / wave::G1SUM_N;
+        std::vector<uint32_t> nxt(G1P_WORDS * nb);
+        for (size_t b = 0; b < nb; b++) {
+            wave::init_slots(w);
+            w_g1_sum_put(w, src, idx, hom, (uint32_t)(b * wave::G1SUM_N), (uint32_t)m);
+            w.run(wave::P_G1_SUM32);
+            w.get_words(wave::REG_U, nxt.data() + G1P_WORDS * b, 3);
+        }
+        part.swap(nxt);
+        src = part.data();
+        idx = nullptr;
+        hom = 1;
+        m = nb;
+    }
+    wave::init_slots(w);
+    w_g1_sum_put(w, src, idx, hom, 0, (uint32_t)m);
+    w.run(wave::P_G1_SUM32);
+    w_g1_sum_compress(w, out48);
+    return ST_OK;
+}
 
 }  // extern "C"
 

@@ -42,6 +42,8 @@ def emu():
     L.bh_w2_fast_aggregate_verify.argtypes = [c, sz, c, c, sz, c, sz]
     L.bh_w3_fast_aggregate_verify.argtypes = [c, sz, c, c, sz, c, sz, ctypes.c_int]
     L.bh_fp_inv_vt.argtypes = [c, vp]
+    L.bh_w_aggregate.argtypes = [sz, c, vp, ctypes.c_int]
+    L.bh_fp_inv_rows.argtypes = [c, vp]
     return L
 
 
@@ -267,11 +269,12 @@ def test_fp_inv_variable_time(emu):
     vals = [1, 2, 3, p - 1, p - 2, (p + 1) // 2, 1 << 62, (1 << 62) - 1, 1 << 380, (1 << 381) % p]
     vals += [rnd.randrange(1, p) for _ in range(500)] + [rnd.randrange(1, 1 << rnd.randrange(1, 380)) for _ in range(100)]
     o = _buf(48)
-    for a in vals:
-        emu.bh_fp_inv_vt(a.to_bytes(48, "big"), o)
-        assert int.from_bytes(o.raw, "big") == pow(a, p - 2, p), hex(a)
-    emu.bh_fp_inv_vt(bytes(48), o)
-    assert o.raw == bytes(48)
+    for inv in (emu.bh_fp_inv_vt, emu.bh_fp_inv_rows):  # the row form: the wave's (fp_inv_wave) updates
+        for a in vals:
+            inv(a.to_bytes(48, "big"), o)
+            assert int.from_bytes(o.raw, "big") == pow(a, p - 2, p), hex(a)
+        inv(bytes(48), o)
+        assert o.raw == bytes(48)
 
 
 def test_wave_cofactor_on_key_side(emu):
@@ -296,3 +299,26 @@ def test_wave_cofactor_on_key_side(emu):
             got = emu.bh_w3_fast_aggregate_verify(sig, len(ks), b"".join(ks), msg, len(msg), B.DST_NUL,
                                                   len(B.DST_NUL), mode)
             assert got == want, (mode, len(ks), len(msg))
+
+
+def test_wave_aggregate_matches_oracle(emu):
+    """AggregateAuthenticator::aggregate by the g1_sum32 tree (nwv_bls.hip k_blsw_g1_sum /
+    k_blsw_g1_sum_fin) against the oracle's sum: one point, a partial block, exactly 32, two tree
+    levels (67 = the quorum of 100), 1,100 (three levels), repeated and opposite points (the
+    complete formulas' doubling and identity cases), the identity signature, and a bad signature
+    mid-list; straight records and records read through a position list"""
+    rnd = random.Random(31)
+    base = [B.g1_compress(B.g1_mul(B.g1_gen(), rnd.randrange(1, r))) for _ in range(40)]
+    neg = bytes([base[3][0] ^ 0x20]) + base[3][1:]  # -P: the sign bit flipped
+    ident = bytes([0xc0]) + bytes(47)
+    cases = [base[:1], base[:5], base[:32], base[:33], (base * 2)[:67], [base[0]] * 4, [base[3], neg],
+             [base[3], neg, base[4]], [ident, base[1]], [ident], (base * 28)[:1100]]
+    for sigs in cases:
+        want_rc, want = B.aggregate(sigs)
+        for through in (0, 1):
+            o = _buf(48)
+            st = emu.bh_w_aggregate(len(sigs), b"".join(sigs), o, through)
+            assert st == want_rc and o.raw == want, (len(sigs), through)
+    bad = base[:10] + [C.not_in_g1()] + base[10:40]
+    o = _buf(48)
+    assert emu.bh_w_aggregate(len(bad), b"".join(bad), o, 0) == B.aggregate(bad)[0] == B.ORB_NOT_IN_GROUP

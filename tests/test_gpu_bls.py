@@ -321,3 +321,46 @@ def test_committee_shape_100(bls, bls_batch, bls_per_item, path):
     assert bls.last_path() == EXPECT_PATH[path][0]
     got = bls.verify_many(keys, [i[0] for i in items[:6]], [i[1] for i in items[:6]], [i[2] for i in items[:6]])
     assert list(got) == [0] * 6
+
+
+@pytest.fixture(scope="module")
+def bls_nosig():
+    """a context under NWV_FLAG_NO_SIGCACHE: every aggregate decodes and G1-checks its signatures"""
+    import narwhal_amd
+    from narwhal_amd import _lib
+    from narwhal_amd.bls import Bls
+    e = narwhal_amd.Engine(device=0, flags=_lib.NWV_FLAG_NO_SIGCACHE)
+    yield Bls(e)
+    e.close()
+
+
+def test_aggregate_verified_signatures(bls, bls_nosig):
+    """AggregateAuthenticator::aggregate over votes already verified (the Core's quorum of 67 of
+    100): signatures that passed a verify call are summed from the device's ring (k_blsw_g1_sum
+    through the ring positions), others are decoded and checked first; both equal the oracle, as
+    do a context without the ring, repeated signatures, a not-yet-verified signature among
+    verified ones, a bad one, and 1,100 signatures (three tree levels)"""
+    from narwhal_amd import _lib
+    sks, pks = _committee(bls, 100, 41)
+    d = bytes(range(7, 39))
+    sigs = bls.sign(sks, [d] * 100)
+    got = bls.verify_many(pks, sigs[:67], [[k] for k in range(67)], [d] * 67)
+    assert list(got) == [0] * 67
+    for b in (bls, bls_nosig):
+        for sub in (sigs[:67], sigs[:1], sigs[:32], sigs[:33], sigs[5:9] * 3, sigs[:66] + [sigs[80]]):
+            rc, agg, st = b.aggregate(sub)
+            want_rc, want = B.aggregate(sub)
+            assert (rc, st) == (_lib.NWV_OK, want_rc) and agg == want
+        rc, _, st = b.aggregate(sigs[:20] + [C.not_in_g1()] + sigs[20:40])
+        assert rc == _lib.NWV_ERR_SIGNATURE and st == B.ORB_NOT_IN_GROUP
+    rnd = random.Random(43)
+    many = bls.sign([sks[k % 100] for k in range(1100)], [bytes([k % 251]) * 32 for k in range(1100)])
+    for lo in range(0, 1100, 550):
+        keys = [[k % 100] for k in range(lo, lo + 550)]
+        assert list(bls.verify_many(pks, many[lo:lo + 550], keys,
+                                    [bytes([k % 251]) * 32 for k in range(lo, lo + 550)])) == [0] * 550
+    order = list(range(1100))
+    rnd.shuffle(order)
+    sub = [many[k] for k in order]
+    rc, agg, st = bls.aggregate(sub)
+    assert rc == _lib.NWV_OK and agg == B.aggregate(sub)[1]

@@ -1363,6 +1363,21 @@ def _p_phi(io):
     io.put("S", 3, Y + y * Z)
 
 
+# the aggregate's sum (AggregateAuthenticator::aggregate): 32 homogeneous points in the Fp12 and line
+# registers (unused outside the pairing), a five-level tree of complete additions -> U
+SUM_IN = [(r, i) for r in ("F", "G", "M", "A", "B", "C") for i in range(12)] + \
+         [(r, i) for r in ("LA", "LB", "W", "W2") for i in range(6)]
+SUM_N = len(SUM_IN) // 3
+
+
+@program("g1_sum32")
+def _p_sum32(io):
+    pts = [tuple(io.fp(*SUM_IN[3 * k + j]) for j in range(3)) for k in range(SUM_N)]
+    while len(pts) > 1:
+        pts = [g_add_complete(pts[2 * j], pts[2 * j + 1], None, F1) for j in range(len(pts) // 2)]
+    _put_g1(io, "U", pts[0])
+
+
 def g1_chain_int(vals, k, base_reg="V"):
     """U <- [k] V by the programs (MSB first; k's top bit set)"""
     for i in range(3):
@@ -1488,6 +1503,14 @@ def emit(compiled, path):
     L.append(f"constexpr int NCONSTS = {len(consts)};")
     for r in REGS.order:
         L.append(f"constexpr int REG_{r} = {REGS.regs[r][0]};")
+    L.append(f"constexpr int SLOT_ONE = {CTX.consts[mont(1)].slot};  // the Montgomery one (a constant slot)")
+    L.append(f"constexpr int G1SUM_N = {SUM_N};  // g1_sum32's inputs: point k at slots g1sum_slot(k) + 0..2 (X, Y, Z)")
+    firsts = [REGS.slot(*SUM_IN[3 * k]) for k in range(SUM_N)]
+    assert all(REGS.slot(*SUM_IN[3 * k + j]) == firsts[k] + j for k in range(SUM_N) for j in range(3))
+    cut = next(k for k in range(1, SUM_N) if firsts[k] != firsts[k - 1] + 3)  # two runs of slots
+    assert all(firsts[k] == firsts[cut] + 3 * (k - cut) for k in range(cut, SUM_N))
+    L.append(f"NWV_HD constexpr int g1sum_slot(int k) {{ return k < {cut} ? {firsts[0]} + 3 * k : "
+             f"{firsts[cut]} + 3 * (k - {cut}); }}")
     L.append(f"constexpr int NSTAGES = {len(stages)};")
     L.append(f"constexpr int NSTEPS = {len(la)};  // Miller-loop steps over |x|")
     L.append(f"constexpr uint32_t QM = {QM}u;  // floor(2^32 / (p_13 + 1)), the quick reduction's multiplier")

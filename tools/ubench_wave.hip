@@ -30,6 +30,7 @@ __host__ __device__ Prog prog_of(int which) {
         case 3: return P_ML_DBL_STEP;
         case 4: return P_ML_DBL_FIXED;
         case 5: return P_G1_DBL_U;
+        case 7: return P_G1_SUM32;
         default: return P_COPY_F_TO_M;
     }
 }
@@ -50,7 +51,8 @@ __global__ __launch_bounds__(64) void k_prog(int which, int reps, uint32_t* out,
 }
 
 // the pieces of one pairing check: 0 Miller loop (computed lines), 1 Miller loop (fixed lines),
-// 2 final exponentiation, 3 the Fp inversion of lane 0, 4 the whole check
+// 2 final exponentiation, 3 the Fp inversion of lane 0, 4 the whole check, 5 the inversion with
+// the update rows on four lanes (fp_inv_wave)
 __global__ __launch_bounds__(64) void k_piece(int which, int reps, uint32_t* out, unsigned long long* clk) {
     __shared__ uint32_t wm[WM_WORDS];
     const Wave w{wm, (int)threadIdx.x};
@@ -71,6 +73,10 @@ __global__ __launch_bounds__(64) void k_piece(int which, int reps, uint32_t* out
         } else if (which == 3) {
             const fp n = w.get(REG_N);
             w.put_fp(REG_N + 1, fp_inv_vt_uniform(n));
+            w.sync();
+        } else if (which == 5) {
+            const fp n = w.get(REG_N);
+            w.put_fp(REG_N + 1, fp_inv_wave(n));
             w.sync();
         } else {
             ok ^= pairing_check(w, nullptr);
@@ -234,9 +240,9 @@ int main(int argc, char** argv) {
     } ks[] = {{"cyc_sqr_F", k_prog, 0, 400, 2},        {"sqr_F", k_prog, 1, 200, 3},
               {"mul_F_M", k_prog, 2, 200, 3},          {"ml_dbl_step", k_prog, 3, 100, 9},
               {"ml_dbl_fixed", k_prog, 4, 100, 9},     {"g1_dbl_u", k_prog, 5, 200, 5},
-              {"copy_F_to_M", k_prog, 6, 400, 1},      {"miller_loop", k_piece, 0, 2, 0},
+              {"copy_F_to_M", k_prog, 6, 400, 1},      {"g1_sum32", k_prog, 7, 50, 18},      {"miller_loop", k_piece, 0, 2, 0},
               {"miller_loop_fixed", k_piece, 1, 2, 0}, {"final_exp", k_piece, 2, 2, 0},
-              {"fp_inv_vt_lane0", k_piece, 3, 20, 0},  {"pairing_check", k_piece, 4, 2, 0},
+              {"fp_inv_vt_lane0", k_piece, 3, 20, 0},  {"fp_inv_wave", k_piece, 5, 20, 0},  {"pairing_check", k_piece, 4, 2, 0},
               {"stage_copy_noload", k_stage, 0, 1000, 0}, {"stage_cyc_products_noload", k_stage, 1, 400, 0},
               {"stage_cyc_combos_noload", k_stage, 2, 1000, 0}, {"record_fetch_latency", k_stage, 3, 1000, 0},
               {"part_combos_only", k_parts, 0, 400, 0}, {"part_product_only", k_parts, 1, 400, 0},
