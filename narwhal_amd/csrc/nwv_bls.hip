@@ -518,25 +518,28 @@ __global__ __launch_bounds__(64) void k_blsw_pre(uint32_t n, const uint8_t* msg,
         blsw_apk_item(lds, b - n, kt, pk_off, pk_cnt, pk_idx, kmode, arec, st_apk);
 }
 
-// AggregateAuthenticator::aggregate (types/src/primary.rs:476-477) on the wave engine: the g1_sum32
-// program adds 32 points per wave.  The inputs (w_g1_sum_put's forms: affine records, optionally
-// through a list of positions, or partial sums) are fetched in one batch -- every lane issues its
-// 21 words' loads before any is stored -- rather than point by point.
+// AggregateAuthenticator::aggregate (types/src/primary.rs:476-477) on the wave engine: a wave adds
+// up to 32 points with the smallest g1_sum program that holds them (2, 4, ... 32 inputs: one level
+// of complete additions, about three stages, per doubling).  The inputs (w_g1_sum_put's forms:
+// affine records, optionally through a list of positions, or partial sums) are fetched in one
+// batch -- every lane issues all its loads before any is stored -- rather than point by point.
+// points [first, first + k) of the input (k <= G1SUM_N; those at or past m are the identity)
 __device__ __forceinline__ void blsw_sum_load(uint32_t* wm, const uint32_t* in, const uint32_t* idx, int hom,
-                                              uint32_t first, uint32_t m) {
+                                              uint32_t first, uint32_t m, uint32_t k) {
     using namespace wave;
     const int lane = (int)threadIdx.x;
-    constexpr int PW = 3 * NL, TOT = G1SUM_N * PW, T = (TOT + 63) / 64;
+    constexpr int PW = 3 * NL, T = (G1SUM_N * PW + 63) / 64;
     static_assert(T <= 32, "one mask bit per word");
+    const int tot = (int)k * PW;
     init_slots(Wave{wm, lane});
     uint32_t v[T], one_at = 0;
 #pragma unroll
     for (int t = 0; t < T; t++) {
-        const int wd = lane + 64 * t, k = wd / PW, c = (wd % PW) / NL, l = wd % NL;
-        const uint32_t j = first + (uint32_t)k;
+        const int wd = lane + 64 * t, q = wd / PW, c = (wd % PW) / NL, l = wd % NL;
+        const uint32_t j = first + (uint32_t)q;
         uint32_t x = 0;
         bool one = false;
-        if (wd < TOT) {
+        if (wd < tot) {
             if (j >= m) {
                 one = c == 1;  // the identity (0 : 1 : 0)
             } else if (hom) {
@@ -553,21 +556,23 @@ __device__ __forceinline__ void blsw_sum_load(uint32_t* wm, const uint32_t* in, 
     }
 #pragma unroll
     for (int t = 0; t < T; t++) {
-        const int wd = lane + 64 * t, k = wd / PW;
-        if (wd < TOT)
-            wm[SW * g1sum_slot(k) + (wd % PW)] = (one_at >> t) & 1u ? wm[SW * SLOT_ONE + wd % NL] : v[t];
+        const int wd = lane + 64 * t;
+        if (wd < tot)
+            wm[SW * g1sum_slot(wd / PW) + (wd % PW)] = (one_at >> t) & 1u ? wm[SW * SLOT_ONE + wd % NL] : v[t];
     }
     wsync();
 }
+// block b: points [b per, b per + per) (per <= G1SUM_N) -> partial sum b
 __global__ __launch_bounds__(64) void k_blsw_g1_sum(uint32_t m, const uint32_t* in, const uint32_t* idx, int hom,
-                                                    uint32_t* part) {
+                                                    uint32_t* part, uint32_t per) {
     __shared__ uint32_t wm[wave::WM_WORDS];
-    const uint32_t b = blockIdx.x;
-    if ((size_t)b * wave::G1SUM_N >= m) return;
-    blsw_sum_load(wm, in, idx, hom, b * wave::G1SUM_N, m);
+    const uint32_t first = blockIdx.x * per;
+    if (first >= m) return;
+    const uint32_t cnt = min(per, m - first);
+    blsw_sum_load(wm, in, idx, hom, first, m, g1_sum_width(cnt));
     const wave::Wave w{wm, (int)threadIdx.x};
-    w.run(wave::P_G1_SUM32);
-    w.get_words(wave::REG_U, part + (size_t)G1P_WORDS * b, 3);
+    w.run(g1_sum_prog(cnt));
+    w.get_words(wave::REG_U, part + (size_t)G1P_WORDS * blockIdx.x, 3);
 }
 // the last level (m <= G1SUM_N inputs, one block): the first bad status of the n_st items in list
 // order (st: null when every item is known good), else the compressed sum
@@ -590,9 +595,9 @@ __global__ __launch_bounds__(64) void k_blsw_g1_sum_fin(uint32_t m, const uint32
             return;
         }
     }
-    blsw_sum_load(wm, in, idx, hom, 0, m);
+    blsw_sum_load(wm, in, idx, hom, 0, m, g1_sum_width(m));
     const wave::Wave w{wm, lane};
-    w.run(wave::P_G1_SUM32);
+    w.run(g1_sum_prog(m));
     w_g1_sum_compress(w, out48);
     if (lane == 0) *out_st = ST_OK;
 }
@@ -1371,7 +1376,7 @@ int nwv_bls_aggregate(nwv_ctx* ctx, size_t n, const uint8_t* sigs48, uint8_t out
     if ((rc = lane.rc())) return rc;
     BlsLane& L = *lane;
     // scratch: records, statuses, the sum tree's two partial-sum levels, the output, decode statuses
-    const size_t n_part = (n + wave::G1SUM_N - 1) / wave::G1SUM_N + 1;
+    const size_t n_part = (n + wave::G1SUM_N - 1) / wave::G1SUM_N + wave::G1SUM_N + 1;  // g1_sum_per
     const size_t w_rec = 0, w_st = al256(4 * G1_REC_WORDS * n), w_pa = al256(w_st + 4 * n),
                  w_pb = al256(w_pa + 4 * G1P_WORDS * n_part), w_out = al256(w_pb + 4 * G1P_WORDS * n_part),
                  w_ost = w_out + 64, w_st2 = al256(w_ost + 8), w_end = w_st2 + 4 * n;
@@ -1384,9 +1389,10 @@ int nwv_bls_aggregate(nwv_ctx* ctx, size_t n, const uint8_t* sigs48, uint8_t out
         const uint32_t* src = in;
         int hom = 0, flip = 0;
         while (m > (uint32_t)wave::G1SUM_N) {
-            const uint32_t nb = (m + wave::G1SUM_N - 1) / wave::G1SUM_N;
+            const uint32_t per = g1_sum_per(m);
+            const uint32_t nb = (m + per - 1) / per;
             auto* dst = reinterpret_cast<uint32_t*>(w + (flip ? w_pb : w_pa));
-            hipLaunchKernelGGL(k_blsw_g1_sum, dim3(nb), dim3(64), 0, L.stream, m, src, idx_d, hom, dst);
+            hipLaunchKernelGGL(k_blsw_g1_sum, dim3(nb), dim3(64), 0, L.stream, m, src, idx_d, hom, dst, per);
             src = dst;
             idx_d = nullptr;
             hom = 1;

@@ -351,12 +351,13 @@ int bh_w_aggregate(size_t n, const uint8_t* sigs, uint8_t* out48, int through_id
     size_t m = n;
     std::vector<uint32_t> part;
     while (m > (size_t)wave::G1SUM_N) {
-        const size_t nb = (m + wave::G1SUM_N - 1) / wave::G1SUM_N;
+        const size_t per = g1_sum_per((uint32_t)m), nb = (m + per - 1) / per;
         std::vector<uint32_t> nxt(G1P_WORDS * nb);
         for (size_t b = 0; b < nb; b++) {
+            const uint32_t cnt = (uint32_t)(m - b * per < per ? m - b * per : per);
             wave::init_slots(w);
-            w_g1_sum_put(w, src, idx, hom, (uint32_t)(b * wave::G1SUM_N), (uint32_t)m);
-            w.run(wave::P_G1_SUM32);
+            w_g1_sum_put(w, src, idx, hom, (uint32_t)(b * per), (uint32_t)m, g1_sum_width(cnt));
+            w.run(g1_sum_prog(cnt));
             w.get_words(wave::REG_U, nxt.data() + G1P_WORDS * b, 3);
         }
         part.swap(nxt);
@@ -366,8 +367,8 @@ int bh_w_aggregate(size_t n, const uint8_t* sigs, uint8_t* out48, int through_id
         m = nb;
     }
     wave::init_slots(w);
-    w_g1_sum_put(w, src, idx, hom, 0, (uint32_t)m);
-    w.run(wave::P_G1_SUM32);
+    w_g1_sum_put(w, src, idx, hom, 0, (uint32_t)m, g1_sum_width((uint32_t)m));
+    w.run(g1_sum_prog((uint32_t)m));
     w_g1_sum_compress(w, out48);
     return ST_OK;
 }

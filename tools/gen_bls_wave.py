@@ -1370,12 +1370,17 @@ SUM_IN = [(r, i) for r in ("F", "G", "M", "A", "B", "C") for i in range(12)] + \
 SUM_N = len(SUM_IN) // 3
 
 
-@program("g1_sum32")
-def _p_sum32(io):
-    pts = [tuple(io.fp(*SUM_IN[3 * k + j]) for j in range(3)) for k in range(SUM_N)]
+def _sum_tree(io, n):
+    pts = [tuple(io.fp(*SUM_IN[3 * k + j]) for j in range(3)) for k in range(n)]
     while len(pts) > 1:
         pts = [g_add_complete(pts[2 * j], pts[2 * j + 1], None, F1) for j in range(len(pts) // 2)]
     _put_g1(io, "U", pts[0])
+
+
+# the same tree over the first 2, 4, 8, 16 or all 32 input points (a level of fewer partial sums
+# takes the smallest that holds them)
+for _n in (2, 4, 8, 16, 32):
+    program(f"g1_sum{_n}")(lambda io, n=_n: _sum_tree(io, n))
 
 
 def g1_chain_int(vals, k, base_reg="V"):
