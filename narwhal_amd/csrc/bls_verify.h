@@ -382,19 +382,18 @@ NWV_HD bool w_pairing_check_h(const W& w, const uint32_t* sig_rec, const uint32_
 }
 
 
-// ---- AggregateAuthenticator::aggregate (types/src/primary.rs:476-477) on a wave: g1_sum32 adds
+// ---- AggregateAuthenticator::aggregate (types/src/primary.rs:476-477) on a wave: g1_sum16 adds
 // G1SUM_N points with complete formulas (the identity and equal points need no branches); point k
 // sits in slots g1sum_slot(k) + 0..2 as (X : Y : Z) and the sum lands in U
 constexpr int G1P_WORDS = 3 * NL;  // a homogeneous partial sum (X, Y, Z)
 // the smallest sum program over cnt points (1 <= cnt <= G1SUM_N) and its input count
-NWV_HD uint32_t g1_sum_width(uint32_t cnt) { return cnt <= 2 ? 2u : cnt <= 4 ? 4u : cnt <= 8 ? 8u : cnt <= 16 ? 16u : 32u; }
+NWV_HD uint32_t g1_sum_width(uint32_t cnt) { return cnt <= 2 ? 2u : cnt <= 4 ? 4u : cnt <= 8 ? 8u : 16u; }
 NWV_HD wave::Prog g1_sum_prog(uint32_t cnt) {
     const uint32_t k = g1_sum_width(cnt);
-    return k == 2 ? wave::P_G1_SUM2 : k == 4 ? wave::P_G1_SUM4 : k == 8 ? wave::P_G1_SUM8 : k == 16 ? wave::P_G1_SUM16 : wave::P_G1_SUM32;
+    return k == 2 ? wave::P_G1_SUM2 : k == 4 ? wave::P_G1_SUM4 : k == 8 ? wave::P_G1_SUM8 : wave::P_G1_SUM16;
 }
-// points a wave takes at a level of m inputs (m > G1SUM_N): 16 while the next level stays within
-// one wave's 32 (fewer additions per wave on the critical path), else 32
-NWV_HD uint32_t g1_sum_per(uint32_t m) { return m <= 16u * wave::G1SUM_N ? 16u : (uint32_t)wave::G1SUM_N; }
+// points a wave takes at a level of m > G1SUM_N inputs
+NWV_HD uint32_t g1_sum_per(uint32_t) { return (uint32_t)wave::G1SUM_N; }
 
 // the program's inputs: affine records (hom = 0: G1_REC_WORDS each, identity flagged; record j at
 // idx[j] when idx, else at j) or partial sums (hom = 1: G1P_WORDS each); inputs past m are the

@@ -58,9 +58,13 @@ typedef __attribute__((address_space(3))) uint64_t wword2;
 typedef uint32_t wword;
 typedef uint64_t wword2;
 #endif
-// the wave's LDS: NSLOTS slots, then P << k (k < 16) for the combinations' offsets
+// the wave's LDS: P << k (k < 16, the combinations' offsets) just BELOW slot 0, then the slots:
+// a kernel allocates KP_WORDS + SW x (its programs' slots) words and works from wm = base +
+// KP_WORDS, so kernels that run only the pairing and G1-check programs (NSLOTS_PAIR slots) take
+// less LDS -- more resident waves -- than those that also run the hash's isogeny map (NSLOTS)
 constexpr int KP_WORDS = 16 * NL;
-constexpr int WM_WORDS = SW * NSLOTS + KP_WORDS;
+constexpr int WM_WORDS = KP_WORDS + SW * NSLOTS;
+constexpr int WM_WORDS_PAIR = KP_WORDS + SW * NSLOTS_PAIR;
 
 // A lane's record in registers: REC u16 words (five 16-byte loads).  [0] destination slot, [1]
 // flags (1 product, 2 reduce, 4 A signed, 8 B signed), [2] k+1 of A's 2^k p (0 none), [3] k+1 of
@@ -150,7 +154,7 @@ template <int BASE>
 NWV_HD void comb_sums(const wword* wm, const Rec& r, int np, int nn, uint32_t k1, uint32_t* out) {
     uint64_t a[NL / 2];
     if (k1) {
-        const wword2* kp = reinterpret_cast<const wword2*>(wm + SW * NSLOTS + NL * (k1 - 1));
+        const wword2* kp = reinterpret_cast<const wword2*>(wm - KP_WORDS + NL * (k1 - 1));
 #pragma unroll
         for (int j = 0; j < NL / 2; j++) a[j] = kp[j];
     } else {
@@ -427,7 +431,7 @@ template <class W>
 NWV_HD void init_slots(const W& w) {
     w.zero(0, 1);
     w.put_words(1, &T_CONSTS[0][0], NCONSTS);
-    w.put_words(NSLOTS, &T_KP[0][0], 16);
+    w.put_words(-16, &T_KP[0][0], 16);  // below slot 0
     w.sync();
 }
 #ifdef BLS_WAVE_DEV
@@ -448,7 +452,7 @@ __device__ __forceinline__ void init_slots(const Wave& w) {
     for (int t = 0; t < NT; t++) {
         const int i = w.lane + 64 * t;
         if (i < NC) w.wm[SW + i] = v[t];
-        else if (i < NC + NK) w.wm[SW * NSLOTS + (i - NC)] = v[t];
+        else if (i < NC + NK) w.wm[(i - NC) - KP_WORDS] = v[t];
     }
     w.sync();
 }
@@ -510,7 +514,8 @@ NWV_HD void final_exp(const W& w) {
     cyc_exp_x(w, P_MUL_F_C);
     w.run(P_CONJMULFROB2_F_B);
     w.run(P_MULCONJ2_F_B);
-    w.run(P_CYCSQRM_MUL_M_TO_G);
+    w.run(P_CYCSQR_M_TO_G);
+    w.run(P_MUL_G_M);
     w.run(P_MUL_F_G);
 }
 

@@ -330,9 +330,13 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_pairing_raw(uint32_t n, const
 }
 
 // ---- the wave engine (bls_wave.h): one 64-lane wave per item ------------------------------------
-#define BLSW_IDX()                        \
-    __shared__ uint32_t wm[wave::WM_WORDS]; \
-    const uint32_t i = blockIdx.x;          \
+// a wave's LDS for programs of up to NS slots: wm points at slot 0 (P << k sits below it)
+#define BLSW_LDS(NS)                                            \
+    __shared__ uint32_t wm_lds[wave::KP_WORDS + wave::SW * (NS)]; \
+    uint32_t* const wm = wm_lds + wave::KP_WORDS
+#define BLSW_IDX()                    \
+    BLSW_LDS(wave::NSLOTS_PAIR);      \
+    const uint32_t i = blockIdx.x;    \
     if (i >= n) return
 // H(msg_i), homogeneous
 __device__ __forceinline__ void blsw_h2c_item(uint32_t* wm, uint32_t i, const uint8_t* msg, const uint64_t* off,
@@ -402,7 +406,7 @@ __global__ __launch_bounds__(64) void k_blsw_pair_sub(uint32_t n, const uint32_t
                                                       const int32_t* st_apk, KeyTab kt, const uint32_t* pk_off,
                                                       const uint32_t* pk_cnt, const uint32_t* pk_idx,
                                                       const uint32_t* kmode, int32_t* st_pair, int32_t* st_sub) {
-    __shared__ uint32_t wm[wave::WM_WORDS];
+    BLSW_LDS(wave::NSLOTS_PAIR);
     const uint32_t b = blockIdx.x;
     if (b < n)
         blsw_pair_item(wm, b, srec, st_dec, hrec, h_hom, arec, st_apk, kt, pk_off, pk_cnt, pk_idx, kmode, st_pair);
@@ -513,13 +517,13 @@ __global__ __launch_bounds__(64) void k_blsw_pre(uint32_t n, const uint8_t* msg,
     __shared__ uint32_t lds[LW];
     const uint32_t b = blockIdx.x;
     if (b < n)
-        blsw_h2c_item(lds, b, msg, off, len, dst, dl, hrec, kmode);
+        blsw_h2c_item(lds + wave::KP_WORDS, b, msg, off, len, dst, dl, hrec, kmode);
     else if (b < 2 * n)
         blsw_apk_item(lds, b - n, kt, pk_off, pk_cnt, pk_idx, kmode, arec, st_apk);
 }
 
 // AggregateAuthenticator::aggregate (types/src/primary.rs:476-477) on the wave engine: a wave adds
-// up to 32 points with the smallest g1_sum program that holds them (2, 4, ... 32 inputs: one level
+// up to 16 points with the smallest g1_sum program that holds them (2, 4, 8, 16 inputs: one level
 // of complete additions, about three stages, per doubling).  The inputs (w_g1_sum_put's forms:
 // affine records, optionally through a list of positions, or partial sums) are fetched in one
 // batch -- every lane issues all its loads before any is stored -- rather than point by point.
@@ -565,7 +569,7 @@ __device__ __forceinline__ void blsw_sum_load(uint32_t* wm, const uint32_t* in, 
 // block b: points [b per, b per + per) (per <= G1SUM_N) -> partial sum b
 __global__ __launch_bounds__(64) void k_blsw_g1_sum(uint32_t m, const uint32_t* in, const uint32_t* idx, int hom,
                                                     uint32_t* part, uint32_t per) {
-    __shared__ uint32_t wm[wave::WM_WORDS];
+    BLSW_LDS(wave::NSLOTS);
     const uint32_t first = blockIdx.x * per;
     if (first >= m) return;
     const uint32_t cnt = min(per, m - first);
@@ -579,7 +583,7 @@ __global__ __launch_bounds__(64) void k_blsw_g1_sum(uint32_t m, const uint32_t* 
 __global__ __launch_bounds__(64) void k_blsw_g1_sum_fin(uint32_t m, const uint32_t* in, const uint32_t* idx, int hom,
                                                         uint32_t n_st, const int32_t* st, uint8_t* out48,
                                                         int32_t* out_st) {
-    __shared__ uint32_t wm[wave::WM_WORDS];
+    BLSW_LDS(wave::NSLOTS);
     const int lane = (int)threadIdx.x;
     if (blockIdx.x) return;
     if (st) {
@@ -1376,7 +1380,7 @@ int nwv_bls_aggregate(nwv_ctx* ctx, size_t n, const uint8_t* sigs48, uint8_t out
     if ((rc = lane.rc())) return rc;
     BlsLane& L = *lane;
     // scratch: records, statuses, the sum tree's two partial-sum levels, the output, decode statuses
-    const size_t n_part = (n + wave::G1SUM_N - 1) / wave::G1SUM_N + wave::G1SUM_N + 1;  // g1_sum_per
+    const size_t n_part = (n + wave::G1SUM_N - 1) / wave::G1SUM_N + 1;  // g1_sum_per
     const size_t w_rec = 0, w_st = al256(4 * G1_REC_WORDS * n), w_pa = al256(w_st + 4 * n),
                  w_pb = al256(w_pa + 4 * G1P_WORDS * n_part), w_out = al256(w_pb + 4 * G1P_WORDS * n_part),
                  w_ost = w_out + 64, w_st2 = al256(w_ost + 8), w_end = w_st2 + 4 * n;

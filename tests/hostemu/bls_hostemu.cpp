@@ -175,10 +175,12 @@ int bh_rlc_batch(size_t n, const uint8_t* sigs, const uint8_t* pks, const uint8_
 }
 
 // ---- the wave engine (bls_wave.h) on the host: the same interpreter and stage tables -----------
+// the device's layout: P << k below slot 0, then NSLOTS slots (the pairing kernels' NSLOTS_PAIR is
+// a prefix of it; tests/test_bls_hostemu.py runs under AddressSanitizer too)
 static wave::Wave host_wave() {
     static thread_local std::vector<uint32_t> wm(wave::WM_WORDS);
     wave::Wave w;
-    w.wm = wm.data();
+    w.wm = wm.data() + wave::KP_WORDS;
     return w;
 }
 static void f12_from_be(const uint8_t* in, uint32_t* slots) {
@@ -328,7 +330,7 @@ void bh_fp_inv_rows(const uint8_t* a, uint8_t* out) {
 }
 
 // AggregateAuthenticator::aggregate as the device runs it: statuses in list order (decode, then
-// the wave G1 check), the records summed 32 at a time by g1_sum32 into partial sums, the partials
+// the wave G1 check), the records summed 16 at a time by the g1_sum programs into partial sums, the partials
 // summed the same way, U compressed (first = 0: records straight; first = 1: through a reversed
 // position list, as the verified-signature ring is read)
 int bh_w_aggregate(size_t n, const uint8_t* sigs, uint8_t* out48, int through_idx) {

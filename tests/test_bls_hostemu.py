@@ -302,9 +302,9 @@ def test_wave_cofactor_on_key_side(emu):
 
 
 def test_wave_aggregate_matches_oracle(emu):
-    """AggregateAuthenticator::aggregate by the g1_sum32 tree (nwv_bls.hip k_blsw_g1_sum /
-    k_blsw_g1_sum_fin) against the oracle's sum: one point, a partial block, exactly 32, two tree
-    levels (67 = the quorum of 100), 1,100 (three levels), repeated and opposite points (the
+    """AggregateAuthenticator::aggregate by the g1_sum trees (nwv_bls.hip k_blsw_g1_sum /
+    k_blsw_g1_sum_fin) against the oracle's sum: one point, a partial block, 32 and 33 (two tree
+    levels), 67 (the quorum of 100), 1,100 (three levels), repeated and opposite points (the
     complete formulas' doubling and identity cases), the identity signature, and a bad signature
     mid-list; straight records and records read through a position list"""
     rnd = random.Random(31)

@@ -446,7 +446,7 @@ def bls_pairing_products(fixed_lines=True):
     fe = (pc["inv_a"] + pc["inv_b"] + pc["easy1"] + pc["easy2"] + 5 * exp_x
           + xbits.count("1") * (pc["mul_F_M"] + 2 * pc["mul_F_A"] + pc["mul_F_B"] + pc["mul_F_C"])
           + pc["mulconj_F_M"] + pc["mulconj_F_A"] + pc["conjmulfrob_F_A"] + pc["conjmulfrob2_F_B"]
-          + pc["mulconj2_F_B"] + pc["cycsqrM_mul_M_to_G"] + pc["mul_F_G"])
+          + pc["mulconj2_F_B"] + pc["cycsqr_M_to_G"] + pc["mul_G_M"] + pc["mul_F_G"])
     return {"miller_loop": ml, "final_exp": fe, "total": ml + fe, "mads_per_product": meta["mads_per_product"]}
 
 

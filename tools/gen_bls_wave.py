@@ -989,10 +989,16 @@ def _p_e2(io):
     put12(io, "F", f12_mul(f12_frob2(f), f))
 
 
-@program("cycsqrM_mul_M_to_G")   # G <- cyc_sqr(M) M
-def _p_g(io):
-    m = f12_of(io, "M")
-    put12(io, "G", f12_mul(f12_cyc_sqr3(m), m))
+# G <- cyc_sqr(M) M as two programs: fused, its 84 temporaries made it the largest of the pairing
+# check's programs (281 slots), and the pairing kernels' LDS follows their largest program
+@program("cycsqr_M_to_G")
+def _p_g1(io):
+    put12(io, "G", f12_cyc_sqr(f12_of(io, "M")))
+
+
+@program("mul_G_M")
+def _p_g2(io):
+    put12(io, "G", f12_mul(f12_of(io, "G"), f12_of(io, "M")))
 
 
 @program("inv_a")
@@ -1176,7 +1182,8 @@ def final_exp_seq(vals, run=_run_int, inv=None):
     exp_x("C")
     run("conjmulfrob2_F_B", vals)    # c = conj(acc) frob2(b) conj(b)
     run("mulconj2_F_B", vals)
-    run("cycsqrM_mul_M_to_G", vals)  # c (cyc_sqr(m) m)
+    run("cycsqr_M_to_G", vals)       # c (cyc_sqr(m) m)
+    run("mul_G_M", vals)
     run("mul_F_G", vals)
 
 
@@ -1363,10 +1370,11 @@ def _p_phi(io):
     io.put("S", 3, Y + y * Z)
 
 
-# the aggregate's sum (AggregateAuthenticator::aggregate): 32 homogeneous points in the Fp12 and line
-# registers (unused outside the pairing), a five-level tree of complete additions -> U
-SUM_IN = [(r, i) for r in ("F", "G", "M", "A", "B", "C") for i in range(12)] + \
-         [(r, i) for r in ("LA", "LB", "W", "W2") for i in range(6)]
+# the aggregate's sum (AggregateAuthenticator::aggregate): 16 homogeneous points in four Fp12
+# registers (unused outside the pairing), a four-level tree of complete additions -> U.  Sixteen,
+# not more: a 32-point tree needs 349 slots against the pairing programs' 307, and every wave
+# kernel's LDS (hence the pairing kernel's occupancy) follows the largest program.
+SUM_IN = [(r, i) for r in ("F", "G", "M", "A") for i in range(12)]
 SUM_N = len(SUM_IN) // 3
 
 
@@ -1377,9 +1385,9 @@ def _sum_tree(io, n):
     _put_g1(io, "U", pts[0])
 
 
-# the same tree over the first 2, 4, 8, 16 or all 32 input points (a level of fewer partial sums
-# takes the smallest that holds them)
-for _n in (2, 4, 8, 16, 32):
+# the same tree over the first 2, 4, 8 or all 16 input points (a level of fewer partial sums takes
+# the smallest that holds them)
+for _n in (2, 4, 8, 16):
     program(f"g1_sum{_n}")(lambda io, n=_n: _sum_tree(io, n))
 
 
@@ -1505,17 +1513,19 @@ def emit(compiled, path):
     L.append("namespace bls {")
     L.append("namespace wave {")
     L.append(f"constexpr int NSLOTS = {max_slot};")
+    # the pairing check's and the G1 check's programs (every program but the hash's isogeny map and
+    # the aggregate's sums): the pairing kernels give a wave this many slots
+    pair_max = max(compiled[nm].max_slot for nm in names if nm != "iso2_add" and not nm.startswith("g1_sum"))
+    L.append(f"constexpr int NSLOTS_PAIR = {pair_max};")
     L.append(f"constexpr int NCONSTS = {len(consts)};")
     for r in REGS.order:
         L.append(f"constexpr int REG_{r} = {REGS.regs[r][0]};")
     L.append(f"constexpr int SLOT_ONE = {CTX.consts[mont(1)].slot};  // the Montgomery one (a constant slot)")
-    L.append(f"constexpr int G1SUM_N = {SUM_N};  // g1_sum32's inputs: point k at slots g1sum_slot(k) + 0..2 (X, Y, Z)")
+    L.append(f"constexpr int G1SUM_N = {SUM_N};  // g1_sum programs' inputs: point k at slots g1sum_slot(k) + 0..2 (X, Y, Z)")
     firsts = [REGS.slot(*SUM_IN[3 * k]) for k in range(SUM_N)]
     assert all(REGS.slot(*SUM_IN[3 * k + j]) == firsts[k] + j for k in range(SUM_N) for j in range(3))
-    cut = next(k for k in range(1, SUM_N) if firsts[k] != firsts[k - 1] + 3)  # two runs of slots
-    assert all(firsts[k] == firsts[cut] + 3 * (k - cut) for k in range(cut, SUM_N))
-    L.append(f"NWV_HD constexpr int g1sum_slot(int k) {{ return k < {cut} ? {firsts[0]} + 3 * k : "
-             f"{firsts[cut]} + 3 * (k - {cut}); }}")
+    assert all(firsts[k] == firsts[0] + 3 * k for k in range(SUM_N))  # one run of slots
+    L.append(f"NWV_HD constexpr int g1sum_slot(int k) {{ return {firsts[0]} + 3 * k; }}")
     L.append(f"constexpr int NSTAGES = {len(stages)};")
     L.append(f"constexpr int NSTEPS = {len(la)};  // Miller-loop steps over |x|")
     L.append(f"constexpr uint32_t QM = {QM}u;  // floor(2^32 / (p_13 + 1)), the quick reduction's multiplier")

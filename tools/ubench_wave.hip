@@ -30,13 +30,14 @@ __host__ __device__ Prog prog_of(int which) {
         case 3: return P_ML_DBL_STEP;
         case 4: return P_ML_DBL_FIXED;
         case 5: return P_G1_DBL_U;
-        case 7: return P_G1_SUM32;
+        case 7: return P_G1_SUM16;
         default: return P_COPY_F_TO_M;
     }
 }
 
 __global__ __launch_bounds__(64) void k_prog(int which, int reps, uint32_t* out, unsigned long long* clk) {
-    __shared__ uint32_t wm[WM_WORDS];
+    __shared__ uint32_t wm_lds[WM_WORDS];
+    uint32_t* const wm = wm_lds + KP_WORDS;
     const Wave w{wm, (int)threadIdx.x};
     fill(w);
     const Prog p = prog_of(which);
@@ -54,7 +55,8 @@ __global__ __launch_bounds__(64) void k_prog(int which, int reps, uint32_t* out,
 // 2 final exponentiation, 3 the Fp inversion of lane 0, 4 the whole check, 5 the inversion with
 // the update rows on four lanes (fp_inv_wave)
 __global__ __launch_bounds__(64) void k_piece(int which, int reps, uint32_t* out, unsigned long long* clk) {
-    __shared__ uint32_t wm[WM_WORDS];
+    __shared__ uint32_t wm_lds[WM_WORDS];
+    uint32_t* const wm = wm_lds + KP_WORDS;
     const Wave w{wm, (int)threadIdx.x};
     fill(w);
     const unsigned long long t0 = wall_clock64();
@@ -93,7 +95,8 @@ __global__ __launch_bounds__(64) void k_piece(int which, int reps, uint32_t* out
 // 1 the product stage of cyc_sqr_F, 2 its combination stage; 3 only the record loads (a dependent
 // chain: the latency of a lane record fetch)
 __global__ __launch_bounds__(64) void k_stage(int which, int reps, uint32_t* out, unsigned long long* clk) {
-    __shared__ uint32_t wm[WM_WORDS];
+    __shared__ uint32_t wm_lds[WM_WORDS];
+    uint32_t* const wm = wm_lds + KP_WORDS;
     const Wave w{wm, (int)threadIdx.x};
     fill(w);
     const int lane = threadIdx.x;
@@ -140,7 +143,8 @@ __global__ __launch_bounds__(64) void k_stage(int which, int reps, uint32_t* out
 // the product stage of cyc_sqr_F split into its parts, repeated: 0 both combinations only (no
 // product), 1 the product only (operands read as two plain slots), 2 combination A + product
 __global__ __launch_bounds__(64) void k_parts(int which, int reps, uint32_t* out, unsigned long long* clk) {
-    __shared__ uint32_t wm[WM_WORDS];
+    __shared__ uint32_t wm_lds[WM_WORDS];
+    uint32_t* const wm = wm_lds + KP_WORDS;
     const Wave w{wm, (int)threadIdx.x};
     fill(w);
     const int lane = threadIdx.x;
@@ -186,7 +190,8 @@ __global__ __launch_bounds__(64) void k_parts(int which, int reps, uint32_t* out
 // 0 the whole w_hash_to_g1, 1 expand_message_xmd on lanes 0-1, 2 map_sswu_frac on lanes 0-1,
 // 3 one fp_pow (the square-root exponent) on lane 0
 __global__ __launch_bounds__(64) void k_h2c(int which, int reps, uint32_t* out, unsigned long long* clk) {
-    __shared__ uint32_t wm[WM_WORDS];
+    __shared__ uint32_t wm_lds[WM_WORDS];
+    uint32_t* const wm = wm_lds + KP_WORDS;
     const Wave w{wm, (int)threadIdx.x};
     fill(w);
     __shared__ uint8_t msg[64];
@@ -240,7 +245,7 @@ int main(int argc, char** argv) {
     } ks[] = {{"cyc_sqr_F", k_prog, 0, 400, 2},        {"sqr_F", k_prog, 1, 200, 3},
               {"mul_F_M", k_prog, 2, 200, 3},          {"ml_dbl_step", k_prog, 3, 100, 9},
               {"ml_dbl_fixed", k_prog, 4, 100, 9},     {"g1_dbl_u", k_prog, 5, 200, 5},
-              {"copy_F_to_M", k_prog, 6, 400, 1},      {"g1_sum32", k_prog, 7, 50, 18},      {"miller_loop", k_piece, 0, 2, 0},
+              {"copy_F_to_M", k_prog, 6, 400, 1},      {"g1_sum16", k_prog, 7, 50, 13},      {"miller_loop", k_piece, 0, 2, 0},
               {"miller_loop_fixed", k_piece, 1, 2, 0}, {"final_exp", k_piece, 2, 2, 0},
               {"fp_inv_vt_lane0", k_piece, 3, 20, 0},  {"fp_inv_wave", k_piece, 5, 20, 0},  {"pairing_check", k_piece, 4, 2, 0},
               {"stage_copy_noload", k_stage, 0, 1000, 0}, {"stage_cyc_products_noload", k_stage, 1, 400, 0},
