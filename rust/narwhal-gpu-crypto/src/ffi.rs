@@ -41,6 +41,8 @@ pub const NWV_FLAG_MSM_SORT2: u32 = 16;
 pub const NWV_FLAG_NO_MSM_REUSE: u32 = 32;
 pub const NWV_FLAG_BLS_PER_ITEM: u32 = 64;
 pub const NWV_FLAG_BLS_BATCH: u32 = 128;
+/// BLS12-381: no verified-signature ring (every aggregate decodes and G1-checks its signatures)
+pub const NWV_FLAG_NO_SIGCACHE: u32 = 256;
 
 // per-item BLS12-381 statuses (include/nwv_bls.h)
 pub const NWV_BLS_OK: i32 = 0;
