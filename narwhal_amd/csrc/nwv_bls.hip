@@ -607,15 +607,15 @@ __global__ __launch_bounds__(64) void k_blsw_g1_sum_fin(uint32_t m, const uint32
 }
 
 // the oracle's order: signature decode, its G1 check, the keys, the pairing equation
-// (sc_rec: a verified signature's record is also kept in the signature ring at slot sc_base + i)
+// (sc_rec: a verified signature's record is also kept in the signature ring, at slot sc_slot[i])
 __global__ __launch_bounds__(BLS_LANES) void k_blsw_status(uint32_t n, const int32_t* dec, const int32_t* sub,
                                                            const int32_t* apk, const int32_t* pair, int32_t* st,
-                                                           const uint32_t* srec, uint32_t* sc_rec, uint32_t sc_base) {
+                                                           const uint32_t* srec, uint32_t* sc_rec, const uint32_t* sc_slot) {
     BLS_IDX();
     const int32_t s = dec[i] != ST_OK ? dec[i] : sub[i] != ST_OK ? sub[i] : apk[i] != ST_OK ? apk[i] : pair[i];
     st[i] = s;
     if (sc_rec && s == ST_OK) {
-        uint32_t* d = sc_rec + (size_t)G1_REC_WORDS * ((sc_base + i) % SC_CAP);
+        uint32_t* d = sc_rec + (size_t)G1_REC_WORDS * sc_slot[i];
         const uint32_t* r = srec + (size_t)G1_REC_WORDS * i;
         for (int k = 0; k < G1_REC_WORDS; k++) d[k] = r[k];
     }
@@ -708,7 +708,8 @@ struct BlsLane {
 // sums kept records instead of decoding and G1-checking each signature again.  A ring of SC_CAP
 // records: a verify call reserves n slots (unmapping what they held) under the unique lock before
 // its kernels run, k_blsw_status writes the verified records into them, and the call maps them
-// after its stream synchronises (a slot re-reserved meanwhile stays unmapped: `gen`).  An
+// after its stream synchronises.  A reserved slot stays `busy` until its call maps or releases
+// it, and the cursor steps over busy slots, so no two calls in flight ever write one slot.  An
 // aggregate holds the shared lock from its lookups until its stream synchronises, so no slot it
 // reads is reserved while its kernels run.
 struct Sig48 {
@@ -728,44 +729,56 @@ struct BlsSigCache {
     std::unordered_map<Sig48, uint32_t, Sig48Hash> slot;
     std::vector<Sig48> key;     // the signature slot s holds (when held[s])
     std::vector<uint8_t> held;  // slot s is mapped
-    std::vector<uint64_t> gen;  // the reservation slot s belongs to
+    std::vector<uint8_t> busy;  // reserved by a call still in flight
     uint32_t next = 0;
-    uint64_t gens = 0;
-    // n slots from the ring's cursor, unmapped; -> the first slot (NWV_OK) and the reservation
-    int reserve(size_t n, uint32_t& base, uint64_t& g) {
+    // n free slots from the ring's cursor (busy ones skipped: at most kMaxLanes x 1,024 are),
+    // unmapped and marked busy -> out
+    int reserve(size_t n, std::vector<uint32_t>& out) {
         std::unique_lock<std::shared_mutex> lk(mu);
         if (!rec.p) {
             int rc = rec.ensure((size_t)4 * G1_REC_WORDS * SC_CAP);
             if (rc) return rc;
             key.resize(SC_CAP);
             held.assign(SC_CAP, 0);
-            gen.assign(SC_CAP, 0);
+            busy.assign(SC_CAP, 0);
             slot.reserve(SC_CAP);
         }
-        base = next;
-        g = ++gens;
+        out.clear();
         for (size_t i = 0; i < n; i++) {
-            const uint32_t t = (uint32_t)((base + i) % SC_CAP);
+            uint32_t t = next;
+            while (busy[t]) t = (t + 1) % SC_CAP;
             if (held[t]) {
                 auto it = slot.find(key[t]);
                 if (it != slot.end() && it->second == t) slot.erase(it);
                 held[t] = 0;
             }
-            gen[t] = g;
+            busy[t] = 1;
+            out.push_back(t);
+            next = (t + 1) % SC_CAP;
         }
-        next = (uint32_t)((base + n) % SC_CAP);
         return NWV_OK;
     }
-    // the call's verified signatures (status OK) mapped to their slots
-    void publish(size_t n, const uint8_t* sigs, const int32_t* status, uint32_t base, uint64_t g) {
+    // the call's verified signatures (status OK) mapped to their slots (status null: the call
+    // failed, its slots are only released)
+    void publish(size_t n, const uint8_t* sigs, const int32_t* status, const std::vector<uint32_t>& slots) {
         std::unique_lock<std::shared_mutex> lk(mu);
-        for (size_t i = 0; i < n; i++) {
-            const uint32_t t = (uint32_t)((base + i) % SC_CAP);
-            if (status[i] != ST_OK || gen[t] != g) continue;
+        for (size_t i = 0; i < slots.size() && i < n; i++) {
+            const uint32_t t = slots[i];
+            busy[t] = 0;
+            if (!status || status[i] != ST_OK) continue;
             std::memcpy(key[t].b, sigs + 48 * i, 48);
             held[t] = 1;
             slot[key[t]] = t;
         }
+    }
+};
+// a call's reserved ring slots, released unless the call publishes them
+struct SigSlots {
+    BlsSigCache* sc = nullptr;
+    std::vector<uint32_t> slots;
+    size_t n = 0;
+    ~SigSlots() {
+        if (sc) sc->publish(n, nullptr, nullptr, slots);
     }
 };
 
@@ -1035,6 +1048,15 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
         kmode[i] = all ? 1u : 0u;
     }
     const size_t n_dec = fill_slot.size();  // keys decoded by this call
+    // verified signatures stay decoded in the device's ring (BlsSigCache) for aggregates
+    // (n <= 1,024 whatever NWV_BLS_WAVE_MAX says: kMaxLanes calls hold at most 8,192 busy slots)
+    const bool keep = wave_small && n <= 1024 && !(d.flags & NWV_FLAG_NO_SIGCACHE);
+    SigSlots kept;
+    if (keep) {
+        if ((rc = d.sc.reserve(n, kept.slots))) return rc;
+        kept.sc = &d.sc;
+        kept.n = n;
+    }
     uint8_t seed[32];
     nwv_internal_fill_seed(nullptr, seed);  // the batch coefficients' key: OS entropy per call
     Arena a;
@@ -1044,7 +1066,8 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
                  o_idx = a.add(n_idx ? (const void*)remap.data() : zero, 4 * n_idx + 4),
                  o_msg = a.add(msg_bytes ? (const void*)msg_base : zero, msg_bytes + 1),
                  o_moff = a.add(msg_off, 8 * n), o_mlen = a.add(msg_len, 4 * n), o_dst = a.add(dst, dl),
-                 o_seed = a.add(seed, 32), o_kmode = a.add(kside ? (const void*)kmode.data() : zero, 4 * kmode.size() + 4);
+                 o_seed = a.add(seed, 32), o_kmode = a.add(kside ? (const void*)kmode.data() : zero, 4 * kmode.size() + 4),
+                 o_scs = a.add(keep ? (const void*)kept.slots.data() : zero, 4 * kept.slots.size() + 4);
     if ((rc = L.stage.ensure(al256(a.total) + 64)) || (rc = L.in.ensure(a.total))) return rc;
     uint8_t* h = static_cast<uint8_t*>(L.stage.p);
     for (size_t k = 0; k < a.parts.size(); k++)
@@ -1137,18 +1160,18 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
                            reinterpret_cast<const uint32_t*>(in + o_cnt), reinterpret_cast<const uint32_t*>(in + o_idx),
                            km, spair, ssub);
         BLS_HIP(hipEventRecord(L.ev[8], s0));
-        // verified signatures stay decoded in the device's ring (BlsSigCache) for aggregates
-        const bool keep = !(d.flags & NWV_FLAG_NO_SIGCACHE);
-        uint32_t sc_base = 0;
-        uint64_t sc_gen = 0;
-        if (keep && (rc = d.sc.reserve(n, sc_base, sc_gen))) return rc;
+        // (the verified records into the ring slots this call reserved)
         hipLaunchKernelGGL(k_blsw_status, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n,
                            (const int32_t*)sdec, (const int32_t*)ssub, (const int32_t*)sapk, (const int32_t*)spair, st,
-                           (const uint32_t*)srec, keep ? static_cast<uint32_t*>(d.sc.rec.p) : nullptr, sc_base);
+                           (const uint32_t*)srec, keep ? static_cast<uint32_t*>(d.sc.rec.p) : nullptr,
+                           reinterpret_cast<const uint32_t*>(in + o_scs));
         BLS_HIP(hipGetLastError());
         BLS_HIP(hipMemcpyAsync(status, st, 4 * n, hipMemcpyDeviceToHost, s0));
         BLS_HIP(hipStreamSynchronize(s0));
-        if (keep) d.sc.publish(n, sigs, status, sc_base, sc_gen);
+        if (keep) {
+            d.sc.publish(n, sigs, status, kept.slots);
+            kept.sc = nullptr;
+        }
         return finish(3);
     }
     if (!L.side[1] && hipStreamCreateWithFlags(&L.side[1], hipStreamNonBlocking) != hipSuccess)
@@ -1196,7 +1219,7 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
         BLS_HIP(hipEventRecord(L.ev[8], s0));
         hipLaunchKernelGGL(k_blsw_status, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n,
                            (const int32_t*)sdec, (const int32_t*)ssub, (const int32_t*)sapk, (const int32_t*)spair, st,
-                           (const uint32_t*)srec, nullptr, 0u);
+                           (const uint32_t*)srec, nullptr, nullptr);
         BLS_HIP(hipGetLastError());
         BLS_HIP(hipMemcpyAsync(status, st, 4 * n, hipMemcpyDeviceToHost, s0));
         BLS_HIP(hipStreamSynchronize(s0));
