@@ -74,6 +74,10 @@ typedef struct nwv_ctx nwv_ctx;
  * and checking each again (the Core aggregates votes it has already verified).  This flag turns
  * the ring off (every aggregate decodes and checks its signatures). */
 #define NWV_FLAG_NO_SIGCACHE 256u
+/* diagnostic / tests: small batch MSMs (at most NWV_MSM_ROW_PREP_MAX points to decompress, env,
+ * default 8192) run each point's decompression power on a 16-lane row (k_msm_prep's row form,
+ * latency-bound batches); this flag keeps every batch on the lane-local decompression */
+#define NWV_FLAG_NO_ROW_PREP 512u
 
 /* ------------------------------------------------------------------ lifecycle ----- */
 /* Process-wide context creation (created once, in Primary::spawn).

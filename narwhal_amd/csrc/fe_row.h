@@ -45,6 +45,7 @@ __device__ __forceinline__ V shr16(V64 x) { return (uint32_t)(x >> 16); }
 __device__ __forceinline__ V sel(M m, V a, V b) { return m ? b : a; }
 __device__ __forceinline__ M row_is(int q) { return ((__lane_id() >> 4) & 3) == (uint32_t)q; }
 __device__ __forceinline__ M limb_is(int k) { return (__lane_id() & 15) == (uint32_t)k; }
+__device__ __forceinline__ M limb_lt(int k) { return (__lane_id() & 15) < (uint32_t)k; }
 template <int R>
 __device__ __forceinline__ V shr(V x) { return (V)__builtin_amdgcn_mov_dpp((int)x, 0x110 + R, 0xF, 0xF, true); }
 template <int R>
@@ -52,6 +53,9 @@ __device__ __forceinline__ V shl(V x) { return (V)__builtin_amdgcn_mov_dpp((int)
 template <int R>
 __device__ __forceinline__ V share(V x) { return (V)__builtin_amdgcn_mov_dpp((int)x, 0x150 + R, 0xF, 0xF, true); }
 __device__ __forceinline__ V ror1(V x) { return (V)__builtin_amdgcn_mov_dpp((int)x, 0x121, 0xF, 0xF, true); }
+// row_ror:R -- lane k of a row gets lane (k - R) mod 16 of the same row
+template <int R>
+__device__ __forceinline__ V ror(V x) { return (V)__builtin_amdgcn_mov_dpp((int)x, 0x120 + R, 0xF, 0xF, true); }
 // v_permlane16_swap: old.rows(1,3) <-> src.rows(0,2);  v_permlane32_swap: old.rows(2,3) <-> src.rows(0,1)
 __device__ __forceinline__ void swap16(V& a, V& b) {
     const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
@@ -153,6 +157,7 @@ inline V shr16(V64 x) { V r; NWV_ROW_FOR { row_check(x.l[i] >> 48 == 0); r.l[i] 
 inline V sel(M m, V a, V b) { V r; NWV_ROW_FOR r.l[i] = m.l[i] ? b.l[i] : a.l[i]; return r; }
 inline M row_is(int q) { M m; NWV_ROW_FOR m.l[i] = ((i >> 4) & 3) == q; return m; }
 inline M limb_is(int k) { M m; NWV_ROW_FOR m.l[i] = (i & 15) == k; return m; }
+inline M limb_lt(int k) { M m; NWV_ROW_FOR m.l[i] = (i & 15) < k; return m; }
 template <int R>
 inline V shr(V x) { V r; NWV_ROW_FOR r.l[i] = (i & 15) >= R ? x.l[i - R] : 0u; return r; }
 template <int R>
@@ -160,6 +165,8 @@ inline V shl(V x) { V r; NWV_ROW_FOR r.l[i] = (i & 15) + R <= 15 ? x.l[i + R] : 
 template <int R>
 inline V share(V x) { V r; NWV_ROW_FOR r.l[i] = x.l[(i & ~15) + R]; return r; }
 inline V ror1(V x) { V r; NWV_ROW_FOR r.l[i] = x.l[(i & ~15) + (((i & 15) + 15) & 15)]; return r; }
+template <int R>
+inline V ror(V x) { V r; NWV_ROW_FOR r.l[i] = x.l[(i & ~15) + (((i & 15) + 16 - R) & 15)]; return r; }
 inline void swap16(V& a, V& b) {
     V ra = a, rb = b;
     NWV_ROW_FOR {
@@ -203,6 +210,7 @@ struct RowConsts {
     V k8p;  // limb k of 8p: 8 * (0xFFED | 0xFFFF | 0x7FFF)
     M r1, r2, r3;
     uint32_t* sc = nullptr;  // 192 words of LDS for this wave: operands of mul() go through LDS
+    int rot = 0;             // mul() by row rotations (mul_ror; 2: two multiply-add chains) instead of LDS or shifts
 };
 NWV_HD RowConsts row_consts() {
     RowConsts c;
@@ -290,8 +298,79 @@ NWV_HD V mul_lds(V a, V b, const RowConsts& k) {
     return carry32(x, k);  // two passes (see mul_dpp)
 }
 
-// a * b mod p on every row: the LDS form when the wave has scratch (k.sc), else the DPP form
-NWV_HD V mul(V a, V b, const RowConsts& k) { return k.sc ? mul_lds(a, b, k) : mul_dpp(a, b, k); }
+// The same product with each wrapped operand made by ONE instruction: op_R = ror<R>(a) x w_R,
+// w_R = 38 on limbs k < R (the wrapped ones), else 1 -- a row_ror DPP source folded into
+// v_mul_u32_u24 -- and b_R by one row_newbcast move.  No LDS round trip, 31 operand instructions.
+NWV_HD V mul_ror(V a, V b, const RowConsts& k) {
+    V op[16], bs[16];
+    op[0] = a;
+    bs[0] = share<0>(b);
+#define NWV_ROW_OPERANDS(R)                                         \
+    op[R] = mul24(ror<R>(a), sel(limb_lt(R), bc(1), bc(38)));       \
+    bs[R] = share<R>(b);
+    NWV_ROW_OPERANDS(1) NWV_ROW_OPERANDS(2) NWV_ROW_OPERANDS(3) NWV_ROW_OPERANDS(4)
+    NWV_ROW_OPERANDS(5) NWV_ROW_OPERANDS(6) NWV_ROW_OPERANDS(7) NWV_ROW_OPERANDS(8)
+    NWV_ROW_OPERANDS(9) NWV_ROW_OPERANDS(10) NWV_ROW_OPERANDS(11) NWV_ROW_OPERANDS(12)
+    NWV_ROW_OPERANDS(13) NWV_ROW_OPERANDS(14) NWV_ROW_OPERANDS(15)
+#undef NWV_ROW_OPERANDS
+    V64 acc;
+    if (k.rot == 2) {  // two interleaved multiply-add chains
+        V64 a0 = mad64(op[0], bs[0], zero64()), a1 = mad64(op[1], bs[1], zero64());
+#pragma unroll
+        for (int r = 2; r < 16; r += 2) {
+            a0 = mad64(op[r], bs[r], a0);
+            a1 = mad64(op[r + 1], bs[r + 1], a1);
+        }
+        acc = add64(a0, a1);
+    } else {
+        acc = mad64(op[0], bs[0], zero64());
+#pragma unroll
+        for (int r = 1; r < 16; r++) acc = mad64(op[r], bs[r], acc);
+    }
+    const V x = lo16(acc) + ror1(mul32(shr16(acc), k.w15));
+    return carry32(x, k);  // two passes (see mul_dpp)
+}
+
+// a * b mod p on every row: the rotation form (k.rot), the LDS form when the wave has scratch
+// (k.sc), else the shift form
+NWV_HD V mul(V a, V b, const RowConsts& k) {
+    return k.rot ? mul_ror(a, b, k) : k.sc ? mul_lds(a, b, k) : mul_dpp(a, b, k);
+}
+
+// x^(2^n) on every row
+NWV_HD V row_sqn(V x, int n, const RowConsts& k) {
+#pragma unroll 1
+    for (int i = 0; i < n; i++) x = mul(x, x, k);
+    return x;
+}
+
+// x^((p-5)/8) on every row: fe_pow22501 and fe_pow_p58's addition chain (fe25519.h), 250
+// squarings and 11 multiplies, each one row product (the decompression's power, ge25519.h, for
+// latency-bound small batches: a rotation-form round is ~0.17 us against ~0.27 us for one
+// lane-local squaring)
+NWV_HD V row_pow_p58(V x, const RowConsts& k) {
+    const V t0 = mul(x, x, k);
+    const V t1 = row_sqn(t0, 2, k);
+    const V t2 = mul(x, t1, k);
+    const V t3 = mul(t0, t2, k);
+    const V t4 = mul(t3, t3, k);
+    const V t5 = mul(t2, t4, k);
+    const V t6 = row_sqn(t5, 5, k);
+    const V t7 = mul(t6, t5, k);
+    const V t8 = row_sqn(t7, 10, k);
+    const V t9 = mul(t8, t7, k);
+    const V t10 = row_sqn(t9, 20, k);
+    const V t11 = mul(t10, t9, k);
+    const V t12 = row_sqn(t11, 10, k);
+    const V t13 = mul(t12, t7, k);
+    const V t14 = row_sqn(t13, 50, k);
+    const V t15 = mul(t14, t13, k);
+    const V t16 = row_sqn(t15, 100, k);
+    const V t17 = mul(t16, t15, k);
+    const V t18 = row_sqn(t17, 50, k);
+    const V t19 = mul(t18, t13, k);
+    return mul(row_sqn(t19, 2, k), x, k);
+}
 
 // ---- points: every row holds the whole point (X, Y, Z, T one V each) ------------------------
 
@@ -358,10 +437,15 @@ NWV_HD void row_horner(const uint32_t* cq, const uint32_t* top, const Layout& la
 //   W = sum_{k < m} 2^k T_k + U  ->  d = T_{m-1};  d = [2] d + T_k (k = m-2 .. 0);  d = d + U;
 //   d = [2^post] d.
 // planes: [m + 1][4][16] row limbs of cached points (Y+X | Y-X | 2dT | 2Z): T_0 .. T_{m-1}, then
-// U.  Row 0 writes d's X | Y | Z | T limbs to out[0..64).  sc: optional LDS scratch (mul_lds).
-NWV_HD void row_planes_chain(const uint32_t* planes, int m, int post, uint32_t* out, uint32_t* sc = nullptr) {
+// U.  Row 0 writes d's X | Y | Z | T limbs to out[0..64).  Multiplies by row rotations (mul_ror,
+// the fastest form on gfx950: 0.340 us per doubling against 0.418 with the LDS exchange and 0.383
+// with DPP shifts, profiles/round5_ubench_row.jsonl); rot = 0 selects the LDS form when sc (192
+// words) is given, else the shift form (host-emulation cross-checks).
+NWV_HD RowP3 row_planes_chain(const uint32_t* planes, int m, int post, uint32_t* out, uint32_t* sc = nullptr,
+                              int rot = 1) {
     RowConsts k = row_consts();
-    k.sc = sc;  // 192 words of LDS: the multiplies exchange operands through it (mul_lds)
+    k.rot = rot;
+    k.sc = rot ? nullptr : sc;
     const V lane = lane_id() & 63u;
     const V limb = lane & 15u;
     // d = identity (X = 0, Y = Z = 1, T = 0), then the planes from the top
@@ -374,6 +458,43 @@ NWV_HD void row_planes_chain(const uint32_t* planes, int m, int post, uint32_t* 
     d = row_add_cached(d, ld(planes, bc(64u * (uint32_t)m) + lane), k);
 #pragma unroll 1
     for (int i = 0; i < post; i++) d = row_dbl(d, k);
+    if (out) {
+        const M r0 = row_is(0);
+        st(out, limb, d.X, r0);
+        st(out, limb + bc(16), d.Y, r0);
+        st(out, limb + bc(32), d.Z, r0);
+        st(out, limb + bc(48), d.T, r0);
+    }
+    return d;
+}
+
+// 2d mod p in radix-2^16 limbs
+NWV_HD V row_d2() {
+    const uint32_t c[16] = {61785, 9906, 39828, 60374, 45398, 33411, 5274, 224,
+                            53552, 61171, 33010, 6542, 64743, 22239, 55772, 9222};
+    V x = bc(c[0]);
+#pragma unroll
+    for (int i = 1; i < 16; i++) x = sel(limb_is(i), x, bc(c[i]));
+    return x;
+}
+
+// cached form of an extended point held on every row: row 0 Y+X, row 1 Y-X, row 2 2dT, row 3
+// 2Z -- one row product (rows 0, 1 multiply by 1, row 2 by 2d, row 3 by 2)
+NWV_HD V row_to_cached(const RowP3& d, const RowConsts& k) {
+    const V in = carry32(rowsel(k, d.Y + d.X, sub(d.Y, d.X, k), d.T, d.Z), k);
+    const V l0 = sel(limb_is(0), bc(0), bc(1));
+    return mul(in, rowsel(k, l0, l0, row_d2(), l0 + l0), k);
+}
+
+// One step of the MSM tail's final sum: acc (X | Y | Z | T limbs, 64 words) + q (cached row form,
+// lane-major: row r's limbs at 16 r) -> out (X | Y | Z | T limbs, row 0 writes them)
+NWV_HD void row_ladder_step(const uint32_t* acc, const uint32_t* q, uint32_t* out, int rot = 1) {
+    RowConsts k = row_consts();
+    k.rot = rot;
+    const V lane = lane_id() & 63u;
+    const V limb = lane & 15u;
+    RowP3 d{ld(acc, limb), ld(acc, limb + bc(16)), ld(acc, limb + bc(32)), ld(acc, limb + bc(48))};
+    d = row_add_cached(d, ld(q, lane), k);
     const M r0 = row_is(0);
     st(out, limb, d.X, r0);
     st(out, limb + bc(16), d.Y, r0);

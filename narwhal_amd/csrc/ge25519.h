@@ -190,18 +190,26 @@ NWV_HD void words_pin(uint32_t w[8]) {
 // sqrt_ratio_i(u, v) with u = y^2 - 1, v = d y^2 + 1 inlined.  Only the 8 input words and the
 // exponentiation state are live across the 250-squaring chain: y, u, v and u v^3 are
 // recomputed after it (5 multiplies) instead of occupying 40 VGPRs through it.
+// The decompression in three pieces, so that the exponentiation can run elsewhere (on 16-lane
+// rows for small batches, k_msm_prep): the prelude u v^7, the power (u v^7)^((p-5)/8), the rest.
+NWV_HD fe ge_decompress_pre(const uint32_t w[8]) {
+    fe y, u, v;
+    ge_uv_from_words(w, y, u, v);
+    fe v3 = fe_mul(fe_sq(v), v);
+    return fe_mul(u, fe_mul(fe_sq(v3), v));
+}
+NWV_HD bool ge_decompress_post(const uint32_t w_in[8], fe pw, ge_p3& out);
 NWV_HD bool ge_decompress(const uint32_t w_in[8], ge_p3& out) {
     uint32_t w[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) w[i] = w_in[i];
-    fe pw;
-    {
-        fe y, u, v;
-        ge_uv_from_words(w, y, u, v);
-        fe v3 = fe_mul(fe_sq(v), v);
-        fe uv7 = fe_mul(u, fe_mul(fe_sq(v3), v));
-        pw = fe_pow_p58(uv7);
-    }
+    const fe pw = fe_pow_p58(ge_decompress_pre(w));
+    return ge_decompress_post(w, pw, out);
+}
+NWV_HD bool ge_decompress_post(const uint32_t w_in[8], fe pw, ge_p3& out) {
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) w[i] = w_in[i];
     fe_pin(pw);
     words_pin(w);
     fe y, u, v;

@@ -745,8 +745,13 @@ struct BlsSigCache {
         }
         out.clear();
         for (size_t i = 0; i < n; i++) {
-            uint32_t t = next;
-            while (busy[t]) t = (t + 1) % SC_CAP;
+            uint32_t t = next, seen = 0;
+            while (busy[t] && ++seen < SC_CAP) t = (t + 1) % SC_CAP;
+            if (busy[t]) {  // only after failed calls abandoned their slots (SigSlots)
+                for (uint32_t u : out) busy[u] = 0;
+                out.clear();
+                return nwv_internal_set_err(NWV_ERR_HIP, "bls signature ring: no free slot");
+            }
             if (held[t]) {
                 auto it = slot.find(key[t]);
                 if (it != slot.end() && it->second == t) slot.erase(it);
@@ -772,13 +777,19 @@ struct BlsSigCache {
         }
     }
 };
-// a call's reserved ring slots, released unless the call publishes them
+// a call's reserved ring slots, released unless the call publishes them.  A call that fails
+// after its kernels were queued may still have k_blsw_status writing into them: the release
+// first waits for the call's stream, and if that wait fails too the slots stay busy (abandoned)
+// so no other call can ever map a slot a late write may still land in.
 struct SigSlots {
     BlsSigCache* sc = nullptr;
     std::vector<uint32_t> slots;
     size_t n = 0;
+    hipStream_t stream = nullptr;  // the stream k_blsw_status writes the slots on
     ~SigSlots() {
-        if (sc) sc->publish(n, nullptr, nullptr, slots);
+        if (!sc) return;
+        if (stream && hipStreamSynchronize(stream) != hipSuccess) return;  // abandoned, see above
+        sc->publish(n, nullptr, nullptr, slots);
     }
 };
 
@@ -1109,6 +1120,7 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     auto* spair = reinterpret_cast<int32_t*>(w + w_spair);
     auto* ajrec = reinterpret_cast<uint32_t*>(w + w_aj);
     hipStream_t s0 = L.stream, s1 = L.side[0], s2 = L.side[1];
+    kept.stream = s0;
     // stage times of the completed call, its path and key counts -> the device's "last call"
     auto finish = [&](int path_done) -> int {
         const int pairs[5][2] = {{0, 1}, {3, 4}, {5, 6}, {1, 2}, {7, 8}};  // keys, sigs, h2c, apk, pairing

@@ -129,7 +129,7 @@ struct PinnedBuf {
 struct EdBuffers {
     DevBuf pk, sig, msg, off, len, kbuf, flags, tables, verdict;
     DevBuf m_scal, m_partial, m_state, m_pts, m_digits, m_cnt, m_tiles, m_entries, m_kstart, m_hpart,
-        m_bsum, m_wsum, m_tpart, m_ctr, m_stamps, m_bpt, m_mid, m_kst2, m_segkey;
+        m_bsum, m_wsum, m_tpart, m_ctr, m_stamps, m_mid, m_kst2, m_segkey;
     // keyed batches: distinct keys (m x 32), CSR of signatures by key, per-signature z_i k_i
     DevBuf keys, koff, ksig, m_ascal;
     DevBuf kslot;  // keyed batches over the key cache: each distinct key's cache slot
@@ -139,7 +139,7 @@ struct EdBuffers {
     void release() {
         for (DevBuf* b : {&pk, &sig, &msg, &off, &len, &kbuf, &flags, &tables, &verdict, &m_scal,
                           &m_partial, &m_state, &m_pts, &m_digits, &m_cnt, &m_tiles, &m_entries,
-                          &m_kstart, &m_hpart, &m_bsum, &m_wsum, &m_tpart, &m_ctr, &m_stamps, &m_bpt, &m_mid, &m_kst2, &m_segkey, &keys, &koff, &ksig, &m_ascal,
+                          &m_kstart, &m_hpart, &m_bsum, &m_wsum, &m_tpart, &m_ctr, &m_stamps, &m_mid, &m_kst2, &m_segkey, &keys, &koff, &ksig, &m_ascal,
                           &kslot, &in})
             b->release();
         nkeys_distinct = 0;
@@ -511,7 +511,7 @@ size_t msm_na(const EdBuffers& b, size_t n) {
     return b.kc_split ? 2 * b.nkeys_distinct + 1 : b.nkeys_distinct;
 }
 
-constexpr size_t MSM_CTR_BYTES = 256;  // k_msm_tail arrival counters (nw + 1 <= 49 words)
+constexpr size_t MSM_CTR_BYTES = 512;  // k_msm_tail arrival counters (128 words)
 
 int msm_alloc(EdBuffers& b, const MsmPlan& p, size_t n) {
     const size_t nblk = (n + 255) / 256;
@@ -529,9 +529,9 @@ int msm_alloc(EdBuffers& b, const MsmPlan& p, size_t n) {
         (rc = b.m_hpart.ensure((size_t)4 * P3_WORDS * p.nseg + 64)) ||
         (p.chunks == 1 && (rc = b.m_segkey.ensure((size_t)4 * p.nseg + 64))) ||
         (rc = b.m_bsum.ensure((size_t)4 * P3_WORDS * p.nkeys + 64)) ||
-        (rc = b.m_wsum.ensure((size_t)4 * P3_WORDS * p.lay.nw + 64)) ||
+        (rc = b.m_wsum.ensure((size_t)4 * 64 * (2 * p.lay.nw + 1) + 64)) ||
         (rc = b.m_tpart.ensure((size_t)4 * P3_WORDS * TAIL_PART_SLOTS * p.lay.nw * p.tail_S + 64)) ||
-        (rc = b.m_ctr.ensure(MSM_CTR_BYTES)) || (rc = b.m_bpt.ensure(4 * P3_WORDS + 64)))
+        (rc = b.m_ctr.ensure(MSM_CTR_BYTES)))
         return rc;
     return NWV_OK;
 }
@@ -577,11 +577,17 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
                            b.m_ascal.as<uint32_t>(), digits, b.m_partial.as<uint32_t>(), state,
                            b.kc_split ? 1u : 0u, b.m_ctr.as<uint32_t>(), reuse ? b.kbuf.as<uint32_t>() : nullptr,
                            reuse ? b.flags.as<uint32_t>() : nullptr};
-    const MsmPointArgs gp{(uint64_t)n, (uint64_t)na, b.kc_split ? 0 : (uint64_t)na,
-                          keyed ? b.keys.as<uint8_t>() : b.pk.as<uint8_t>(),
-                          b.sig.as<uint8_t>(), b.m_pts.as<uint32_t>(), state};
+    // decompression on 16-lane rows when the batch is small enough to be latency-bound
+    static const uint64_t row_prep_max = [] {
+        const char* e = std::getenv("NWV_MSM_ROW_PREP_MAX");
+        return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)8192;
+    }();
+    const uint64_t ndec = b.kc_split ? 0 : (uint64_t)na;
+    const bool rows = !(d.flags & NWV_FLAG_NO_ROW_PREP) && n + ndec <= row_prep_max;
+    const MsmPointArgs gp{(uint64_t)n, (uint64_t)na, ndec, keyed ? b.keys.as<uint8_t>() : b.pk.as<uint8_t>(),
+                          b.sig.as<uint8_t>(), b.m_pts.as<uint32_t>(), state, rows ? 1u : 0u};
     const size_t waves = (n + 63) / 64 + (na + 63) / 64;
-    const unsigned pblk = (unsigned)((64 * waves + 255) / 256);
+    const unsigned pblk = rows ? (unsigned)((n + ndec + 15) / 16) : (unsigned)((64 * waves + 255) / 256);
     const bool fused = !(d.flags & NWV_FLAG_MSM_SPLIT_PREP);
     if (fused)
         hipLaunchKernelGGL(k_msm_prep, dim3(nblk + pblk), dim3(256), 0, stream, gs, p.lay, gp, nblk);
@@ -664,7 +670,7 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     const uint32_t quad_max_c = n <= quad_max_n ? 256u : 0u;
     const MsmTailArgs ta{b.m_bsum.as<uint32_t>(), b.m_hpart.as<uint32_t>(), kst, E, p.nkeys, p.seg,
                          b.m_tpart.as<uint32_t>(), b.m_wsum.as<uint32_t>(),
-                         b.m_ctr.as<uint32_t>(), state, b.m_bpt.as<uint32_t>(), b.m_partial.as<uint32_t>(),
+                         b.m_ctr.as<uint32_t>(), state, b.m_partial.as<uint32_t>(),
                          d.gpu->comb.as<uint32_t>(), nblk, quad_max_c, state + 1, state + 2, p.tail_S, st_buf};
     // combine items per thread: (lg C + 1) x S_w over the windows (C = nb / S_w buckets per chunk)
     int items = 0;

@@ -76,6 +76,8 @@ static int lg2(int x) {
 }
 static bool tail_host(const MsmLayout& lay, const uint32_t* bs, uint32_t S) {
     ge_p3 tot = ge_p3_identity();
+    std::vector<uint32_t> ladder(64, 0);  // the final sum's accumulator (row limbs), the identity
+    ladder[16] = ladder[32] = 1;
     std::vector<ge_p3> scaled;
     for (int w = 0; w < lay.nw; w++) {
         const int nb = 1 << (lay.width[w] - 1);
@@ -103,14 +105,32 @@ static bool tail_host(const MsmLayout& lay, const uint32_t* bs, uint32_t S) {
             fe_to_limbs16(fe_carry(fe_add(pl.Z, pl.Z)), rows.data() + 64 * k + 48);
         }
         std::vector<uint32_t> sc(192);
-        rowf::row_planes_chain(rows.data(), m, lay.pos[w] + 3, out.data(), (w & 1) ? sc.data() : nullptr);
+        // the windows cycle through the three multiply forms (rotations, as on the device; LDS; shifts)
+        const int rot = w % 3 == 0 ? 1 : 0;
+        const rowf::RowP3 d = rowf::row_planes_chain(rows.data(), m, lay.pos[w] + 3, out.data(),
+                                                     (w % 3 == 1) ? sc.data() : nullptr, rot);
         const ge_p3 ws{fe_from_limbs16(out.data()), fe_from_limbs16(out.data() + 16), fe_from_limbs16(out.data() + 32),
                        fe_from_limbs16(out.data() + 48)};
         scaled.push_back(ws);
         tot = p3_add(tot, ws);
+        // the kernel's final sum: each window's cached row form, one ladder step per window
+        rowf::RowConsts k = rowf::row_consts();
+        k.rot = rot;
+        k.sc = (w % 3 == 1) ? sc.data() : nullptr;
+        const rowf::V c = rowf::row_to_cached(d, k);
+        std::vector<uint32_t> q(64), nxt(64);
+        for (int i = 0; i < 64; i++) q[i] = c.l[i];
+        rowf::row_ladder_step(ladder.data(), q.data(), nxt.data(), rot);
+        ladder = nxt;
     }
-    // the kernel's last step: a binary tree of additions over the windows, identity padded to a
-    // power of two (k_msm_tail adds [8 b]B as one more item; here B is inside the MSM)
+    {
+        const fe X = fe_from_limbs16(ladder.data()), Y = fe_from_limbs16(ladder.data() + 16),
+                 Z = fe_from_limbs16(ladder.data() + 32);
+        const bool ladder_id = fe_is_zero(X) && fe_eq(Y, Z);
+        if (ladder_id != (fe_is_zero(tot.X) && fe_eq(tot.Y, tot.Z))) abort();  // ladder vs lane sum
+    }
+    // a binary tree of additions over the windows (identity padded to a power of two), the round-4
+    // kernel's final sum, against the sequential lane sum
     size_t P2 = 1;
     while (P2 < scaled.size()) P2 <<= 1;
     scaled.resize(P2, ge_p3_identity());
@@ -186,6 +206,46 @@ int he_decompress(const uint8_t* p, uint8_t* out_xy) {
     std::memcpy(out_xy, x, 32);
     std::memcpy(out_xy + 32, y, 32);
     return ok ? 1 : 0;
+}
+
+// k_msm_prep's row form of the decompression (msm_points_rows_block) on the emulated wave, four
+// points at a time: lane-local prelude, the power on 16-lane rows (form 0: DPP shifts, 1: LDS,
+// 2: row rotations as on the device), lane-local postlude.  Each point's MSM record (30 words) and
+// decode flag must equal the lane-local ge_decompress's; returns the number of points that differ.
+int he_row_decompress(const uint8_t* encs, int count, int form) {
+    int bad = 0;
+    std::vector<uint32_t> sh(64), sc(192);
+    for (int base = 0; base < count; base += 4) {
+        uint32_t w[4][8] = {};
+        for (int q = 0; q < 4; q++) {
+            if (base + q < count) words(encs + 32 * (base + q), w[q]);
+            fe_to_limbs16(ge_decompress_pre(w[q]), sh.data() + 16 * q);
+        }
+        rowf::RowConsts k = rowf::row_consts();
+        k.rot = form == 2 ? 1 : 0;
+        k.sc = form == 1 ? sc.data() : nullptr;
+        rowf::V x;
+        for (int i = 0; i < 64; i++) x.l[i] = sh[i];
+        const rowf::V pw = rowf::row_pow_p58(x, k);
+        for (int i = 0; i < 64; i++) sh[i] = pw.l[i];
+        for (int q = 0; q < 4 && base + q < count; q++) {
+            ge_p3 P, R;
+            const bool ok = ge_decompress_post(w[q], fe_from_limbs16(sh.data() + 16 * q), P);
+            const bool ok_ref = ge_decompress(w[q], R);
+            uint32_t e[MSM_PT_WORDS], e_ref[MSM_PT_WORDS];
+            msm_store_point(e, P);
+            msm_store_point(e_ref, R);
+            uint32_t fa[8], fb[8];
+            bool same = ok == ok_ref;
+            for (int c = 0; c < 3 && same; c++) {  // compare canonical coordinates of the record
+                fe_freeze(load_fe(e + 10 * c), fa);
+                fe_freeze(load_fe(e_ref + 10 * c), fb);
+                same = std::memcmp(fa, fb, 32) == 0;
+            }
+            bad += same ? 0 : 1;
+        }
+    }
+    return bad;
 }
 
 void he_sc_reduce(const uint8_t* in64, uint8_t* out32) {
@@ -512,7 +572,8 @@ void he_msm_point_counts(const uint8_t* pk, const uint8_t* sig, unsigned long lo
     counts[1] = nwv_count_sq;
 }
 
-// one field multiply on the emulated wave (the DPP form, or with use_lds the LDS-operand form): a, b
+// one field multiply on the emulated wave (use_lds 0: the DPP shift form, 1: the LDS-operand form,
+// 2: the row-rotation form): a, b
 // given as 16 loose limbs (same in every row); out = row 0's product limbs.  Returns 0 when the four
 // rows disagree.
 int he_row_mul(const uint32_t* a16, const uint32_t* b16, uint32_t* out16, int use_lds) {
@@ -523,7 +584,8 @@ int he_row_mul(const uint32_t* a16, const uint32_t* b16, uint32_t* out16, int us
     }
     std::vector<uint32_t> sc(192, 0xDEADBEEFu);
     rowf::RowConsts k = rowf::row_consts();
-    if (use_lds) k.sc = sc.data();
+    if (use_lds == 1) k.sc = sc.data();
+    k.rot = use_lds == 2;
     const rowf::V r = rowf::mul(a, b, k);
     for (int i = 0; i < 64; i++)
         if (r.l[i] != r.l[i & 15]) return 0;

@@ -364,3 +364,51 @@ def test_aggregate_verified_signatures(bls, bls_nosig):
     sub = [many[k] for k in order]
     rc, agg, st = bls.aggregate(sub)
     assert rc == _lib.NWV_OK and agg == B.aggregate(sub)[1]
+
+
+def test_ring_wraps_under_concurrent_verifies_and_aggregates(bls):
+    """the verified-signature ring (BlsSigCache, 65,536 slots) under load: 8 threads verify
+    1,024-signature calls until the ring has wrapped (73,728 reservations) while 2 threads
+    aggregate 67-signature subsets; every verify status is OK and every aggregate equals the
+    oracle's (a slot re-reserved while a call or an aggregate still used it would show up as a
+    wrong sum)"""
+    import threading
+    from narwhal_amd import _lib
+    sks, pks = _committee(bls, 100, 51)
+    msgs = [bytes([k % 251, k // 251]) * 16 for k in range(1024)]
+    sigs = bls.sign([sks[k % 100] for k in range(1024)], msgs)
+    keys = [[k % 100] for k in range(1024)]
+    errs = []
+    stop = threading.Event()
+
+    def verifier():
+        try:
+            for _ in range(9):
+                st = bls.verify_many(pks, sigs, keys, msgs)
+                if list(st) != [0] * 1024:
+                    errs.append(("verify", [int(x) for x in st if x][:4]))
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errs.append(("verify", repr(e)))
+
+    def aggregator(seed):
+        rnd = random.Random(seed)
+        try:
+            while not stop.is_set():
+                sub = [sigs[k] for k in rnd.sample(range(1024), 67)]
+                rc, agg, st = bls.aggregate(sub)
+                want_rc, want = B.aggregate(sub)
+                if (rc, st, agg) != (_lib.NWV_OK, want_rc, want):
+                    errs.append(("aggregate", rc, st))
+        except Exception as e:  # noqa: BLE001
+            errs.append(("aggregate", repr(e)))
+
+    vs = [threading.Thread(target=verifier) for _ in range(8)]
+    ags = [threading.Thread(target=aggregator, args=(s,)) for s in (1, 2)]
+    for t in vs + ags:
+        t.start()
+    for t in vs:
+        t.join()
+    stop.set()
+    for t in ags:
+        t.join()
+    assert not errs, errs[:5]

@@ -32,13 +32,14 @@ def lib(he):  # noqa: F811
     he.he_row_mul.argtypes = [vp, vp, vp, ctypes.c_int]
     he.he_row_horner.argtypes = [ctypes.c_int, vp, vp, vp, vp]
     he.he_decompress.argtypes = [ctypes.c_char_p, vp]
+    he.he_row_decompress.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
     return he
 
 
-@pytest.mark.parametrize("use_lds", [0, 1])
+@pytest.mark.parametrize("use_lds", [0, 1, 2])
 @pytest.mark.parametrize("bound", [2**16, 2**16 + 2**11, 2**17, int(2**17.7)])
 def test_row_mul_values_and_output_bounds(lib, bound, use_lds):
-    """both operand paths of the row multiply (DPP moves, or the LDS exchange the MSM tail uses)
+    """the three operand paths of the row multiply (DPP shifts, the LDS exchange, row rotations)
     give the product mod p with the documented output bounds"""
     rnd = random.Random(bound)
     cases = [[bound - 1] * 16, [0] * 16, [1] + [0] * 15]
@@ -102,3 +103,23 @@ def test_row_horner_torsion_is_identity(lib):
     pts = [TORSION[1]] * 8
     pts[3] = _random_point(lib, rnd)
     assert _horner(lib, widths, pts)[0] == 0
+
+
+@pytest.mark.parametrize("form", [0, 1, 2])
+def test_row_decompression_matches_lane_local(lib, form):
+    """k_msm_prep's row form (the decompression power on 16-lane rows, small batches) gives the
+    same MSM record and decode flag as the lane-local ge_decompress on random encodings (about
+    half do not decode), the 8-torsion encodings, y >= p, negative zero and the golden vectors'
+    keys and R values"""
+    import json
+    import os
+    rnd = random.Random(11 + form)
+    encs = [bytes(rnd.getrandbits(8) for _ in range(32)) for _ in range(40)]
+    encs += TORSION + [bytes(31) + b"\x80" * 1, (P).to_bytes(32, "little"), (P + 1).to_bytes(32, "little"),
+                       (2**255 - 1).to_bytes(32, "little"), ((1) | (1 << 255)).to_bytes(32, "little")]
+    g = os.path.join(os.path.dirname(__file__), "golden", "ed25519_vectors.json")
+    with open(g) as f:
+        vs = json.load(f)["vectors"]
+    for v in vs[:: max(1, len(vs) // 40)]:
+        encs += [bytes.fromhex(v["pk"]), bytes.fromhex(v["sig"])[:32]]
+    assert lib.he_row_decompress(b"".join(encs), len(encs), form) == 0
