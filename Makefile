@@ -6,7 +6,7 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 BLS_SRC := narwhal_amd/csrc/nwv_bls.hip narwhal_amd/csrc/bls381.h narwhal_amd/csrc/bls_verify.h narwhal_amd/csrc/bls_group.h \
 	narwhal_amd/csrc/bls381_consts.h narwhal_amd/csrc/bls381_iso.h narwhal_amd/csrc/bls_wave.h \
-	narwhal_amd/csrc/bls_wave_prog.h include/nwv_bls.h
+	narwhal_amd/csrc/bls_wave_prog.h narwhal_amd/csrc/bls_shard.h include/nwv_bls.h
 CSRC := $(filter-out $(BLS_SRC),$(wildcard narwhal_amd/csrc/*.h narwhal_amd/csrc/*.hip narwhal_amd/csrc/*.cpp)) \
 	include/nwv.h include/nwv_types.h include/nwv_service.h
 
@@ -37,7 +37,11 @@ narwhal_amd/lib/libnwv.so: narwhal_amd/lib/nwv_host.o narwhal_amd/lib/nwv_bls.o 
 oracle:
 	$(MAKE) -C oracle
 
-hostemu: tests/_build/libhostemu.so tests/_build/libsvcstub.so tests/_build/libblsemu.so
+hostemu: tests/_build/libhostemu.so tests/_build/libsvcstub.so tests/_build/libblsemu.so tests/_build/libblsshard.so
+# the BLS calls' split over a multi-device context (bls_shard.h) with a stub per-device verifier
+tests/_build/libblsshard.so: tests/hostemu/bls_shard_stub.cpp narwhal_amd/csrc/bls_shard.h
+	@mkdir -p tests/_build
+	g++ -O1 -g -std=c++17 -fPIC -shared -pthread -o $@ tests/hostemu/bls_shard_stub.cpp
 # the gfx950 BLS12-381 code compiled for the host (tests/test_bls_hostemu.py)
 tests/_build/libblsemu.so: tests/hostemu/bls_hostemu.cpp $(BLS_SRC)
 	@mkdir -p tests/_build

@@ -278,6 +278,34 @@ def pmc_file(n, launch):
     return None, None
 
 
+def rocprof_headline(kernels=("k_msm_prep", "k_msm_bucket", "k_msm_tail")):
+    """the newest committed rocprofv3 --kernel-trace --stats summary of the headline alone with ONE
+    batch in flight (profiles/*_headline_inflight1_rocprof_kernel_stats.csv) whose stored bench line
+    (*_headline_inflight1_bench_line.json, the same run) carries today's kernel_source_hash: its
+    per-kernel averages are single-stream kernel times, comparable with the line's kernel_ms
+    (tests/test_profiles_evidence.py); else None"""
+    import csv
+    import glob
+    from narwhal_amd._lib import kernel_source_hash
+    want = kernel_source_hash()
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_headline_inflight1_rocprof_kernel_stats.csv")),
+                    reverse=True):
+        line = f.replace("_rocprof_kernel_stats.csv", "_bench_line.json")
+        try:
+            with open(line) as fh:
+                bl = json.load(fh)
+            with open(f) as fh:
+                rows = {r["Name"]: r for r in csv.DictReader(fh)}
+        except (OSError, ValueError, KeyError):
+            continue
+        if bl.get("kernel_source_hash") != want:
+            continue
+        return {"source": os.path.relpath(f, ROOT), "bench_line": os.path.relpath(line, ROOT),
+                "avg_ms": {k: float(rows[k]["AverageNs"]) * 1e-6 for k in kernels if k in rows},
+                "line_kernel_ms": {k: bl.get("kernel_ms", {}).get(k) for k in kernels}}
+    return None
+
+
 def pmc_kernel(kernel, n, launch):
     """(counters, source) of `kernel` from pmc_file(n, launch), or (None, None)"""
     d, src = pmc_file(n, launch)
@@ -354,6 +382,15 @@ def kernel_rooflines(kt, stats, n, na, peak, mlen):
          f"(R_i and the A points), plus SHA-512(R || A || M) per signature: {sha_blocks} blocks x "
          f"{SHA512_VALU_PER_BLOCK} 32-bit VALU instructions = {sha_eq} multiply-add equivalents "
          f"(2 : 1 issue) x {n} signatures")
+    # the SHA-512 share is a count of compiled 32-bit instructions, not multiply-adds: the
+    # decompression-only figure (round 3's numerator, a lower bound) stays beside it
+    pr = out["k_msm_prep"]
+    pr["mads_sha512_equiv_per_launch"] = sha_eq * n
+    pr["mads_decompression_per_launch"] = MADS_DECOMPRESS * (na + n)
+    kms = pr["kernel_ms"]
+    a_dec = MADS_DECOMPRESS * (na + n) / (kms * 1e-3) / 1e12 if kms > 0 else None
+    pr["achieved_decompression_only"] = a_dec
+    pr["frac_decompression_only"] = (a_dec / mad_peak) if (a_dec and mad_peak) else None
     mem("k_msm_hist", ["k_msm_hist"], 2 * digit_slots + 4 * cnt_len,
         f"read the i16 digit rows ({digit_slots} slots), write {cnt_len} u32 counts")
     mem("k_msm_wscan", ["k_msm_wscan"], 8 * cnt_len,
@@ -891,6 +928,12 @@ def main():
             fl["note"] = ("VALU issue floor of one whole batch (every kernel of the launch list) against the "
                           "step time with batches in flight")
         roof["batch_issue_floor"] = fl
+        # the kernel trace this line's kernel times can be checked against (committed, same sources)
+        rp = rocprof_headline()
+        roof["rocprof_source"] = rp["source"] if rp else None
+        roof["rocprof_headline_inflight1"] = rp
+        pmc_src = (roof.get("issue_floor") or {}).get("source")
+        roof["pmc_source"] = pmc_src
     else:
         kms = kt.get("k_ed_straus", 0.0)
         m = (OPS_STRAUS[0] * MADS_PER_MUL + OPS_STRAUS[1] * MADS_PER_SQ) * args.n
@@ -926,7 +969,9 @@ def main():
                                                        c5["cpu_baseline"]["worker_batch_digests_ms_per_round"])
         del cdata
     result = base_line(args, 1, dt)
+    from narwhal_amd._lib import kernel_source_hash
     result.update({
+        "kernel_source_hash": kernel_source_hash(),
         "steady_state": h["steady"],
         "single_stream": {"ms_per_step": float(np.median(h["single"])),
                           "sigs_per_s": args.n / (float(np.median(h["single"])) * 1e-3)},

@@ -35,8 +35,9 @@ typedef struct nwv_service nwv_service;
 /* completion callback: called exactly once per submitted item, from a service thread, without
  * the service lock held.  It may submit further items asynchronously; the blocking calls
  * (nwv_service_verify_*, nwv_service_flush) on the SAME service return NWV_ERR_REENTRANT from
- * inside its callback (they would wait on the thread running it; blocking calls on another
- * service are allowed), and it must not call nwv_service_free. */
+ * inside its callback (they would wait on the thread running it), and so do blocking calls on
+ * another service whose callbacks are already waiting (directly or through others) on this one
+ * (a cycle of such waits could leave every flusher waiting); it must not call nwv_service_free. */
 typedef void (*nwv_done_fn)(void* user, int32_t result);
 
 /* max_batch: flush as soon as this many items are pending (>= 1); max_wait_us: flush when the
@@ -57,6 +58,22 @@ int nwv_service_verify_header(nwv_service* svc, const nwv_header* h, int32_t* re
 int nwv_service_verify_vote(nwv_service* svc, const nwv_vote* v, int32_t* result);
 int nwv_service_verify_certificate(nwv_service* svc, const nwv_certificate* c, int32_t* result);
 
+/* ---- the same service under BLS12-381, the reference's default scheme (crypto/src/lib.rs:29-33):
+ * the nwv_bls_* structs of nwv_types.h (96-byte keys, 48-byte signatures, one 48-byte aggregate
+ * per certificate); each flush is ONE nwv_bls_verify_mixed_many call (every digest in one BLAKE2b
+ * launch, every signature check -- header and vote signatures, certificates' aggregates -- in one
+ * nwv_bls_verify_many call).  A service is of one scheme: the other scheme's calls on it return
+ * NWV_ERR_ARG.  flush, stats and free are shared. */
+int nwv_service_create_bls(nwv_ctx* ctx, const nwv_bls_committee* committee, size_t max_batch, uint32_t max_wait_us,
+                           nwv_service** out);
+int nwv_service_set_committee_bls(nwv_service* svc, const nwv_bls_committee* committee);
+int nwv_service_submit_bls_header(nwv_service* svc, const nwv_bls_header* h, nwv_done_fn done, void* user);
+int nwv_service_submit_bls_vote(nwv_service* svc, const nwv_bls_vote* v, nwv_done_fn done, void* user);
+int nwv_service_submit_bls_certificate(nwv_service* svc, const nwv_bls_certificate* c, nwv_done_fn done,
+                                       void* user);
+int nwv_service_verify_bls_header(nwv_service* svc, const nwv_bls_header* h, int32_t* result);
+int nwv_service_verify_bls_vote(nwv_service* svc, const nwv_bls_vote* v, int32_t* result);
+int nwv_service_verify_bls_certificate(nwv_service* svc, const nwv_bls_certificate* c, int32_t* result);
 /* returns once every item submitted before the call has completed */
 int nwv_service_flush(nwv_service* svc);
 

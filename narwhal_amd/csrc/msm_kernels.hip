@@ -867,9 +867,9 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_bucket_q(
 // cdna_hip_programming.md Guideline 16, counter form) combines them with one more butterfly over
 // s, per plane: T_k = sum_s T_{s,k} (k < lg C), and the butterfly of the R_s gives the planes
 // k >= lg C and U.  Its wave 0 then runs, on 16-lane rows (fe_row.h), the m-step plane chain and
-// pos_w + 3 doublings ([8] folded in).  The final sum runs as a ladder over the windows beside
-// the chains (msm_tail_body); its last step tests the identity: *verdict = 1 iff accepted and no
-// failure flag is set.  ctr[0, 128) must be zero at launch (k_msm_prep's first workgroup clears it).
+// pos_w + 3 doublings ([8] folded in).  The final sum runs on one wave beside the chains
+// (msm_tail_body), which then tests the identity: *verdict = 1 iff accepted and no failure flag is
+// set.  ctr[0, 128) must be zero at launch (k_msm_prep's first workgroup clears it).
 struct MsmTailArgs {
     const uint32_t* bsum;  // [nkeys] bucket sums (P3): a bucket's first piece (k_msm_bucket[_q])
     const uint32_t* hpart;    // [nseg] continuation pieces of buckets spanning chunks
@@ -877,9 +877,9 @@ struct MsmTailArgs {
     const uint32_t* total;    // entry count E
     uint32_t nkeys, seg;      // seg: entries per bucket lane (T of k_msm_bucket[_q])
     uint32_t* part;        // [nw][S][TAIL_PART_SLOTS] chunk planes (P3): R_s, T_{s,0}, T_{s,1}, ...
-    uint32_t* wsc;         // [2 nw + 1] x 64 words: the final sum's partial sums acc_0..acc_nw (row
-                           // limbs X | Y | Z | T), then the scaled windows in cached row form
-    uint32_t* ctr;         // [0, nw): chunk arrivals; [64, 64 + nw): the final sum's steps
+    uint32_t* wsc;         // [2 nw + 1] x 64 words: (nw + 1) x 64 unused, then the scaled windows
+                           // in cached row form (the final sum's terms)
+    uint32_t* ctr;         // [0, nw): chunk arrivals; [64, 64 + nw): window w's term published
     const uint32_t* fail;
     const uint32_t* partial;   // k_msm_prep's per-workgroup sums of z_i s_i (nblk x 9 words)
     const uint32_t* comb;      // fixed-base comb table
@@ -1179,58 +1179,68 @@ __device__ __forceinline__ void msm_tail_body(const MsmLayout& lay, const MsmTai
     extern __shared__ uint32_t lds[];
     uint32_t* flag = lds + 256 * P3_WORDS;
     const int t = threadIdx.x;
-    // Final sum as a ladder in window order: acc_0 = [8 b]B, acc_{w+1} = acc_w + (scaled window w),
-    // each step one row-form addition (fe_row.h row_ladder_step) made by whichever of its two
-    // inputs arrives second (counter ctr[64 + w]), on wave 0 alone.  Window chains end in about
-    // window order (window w's chain is pos_w + 3 + its plane count long), so the steps run
-    // behind the chains and only one addition follows the top window's.  Round 4 summed all
-    // nw + 1 items after the last arrival with a 5-level quad-lane tree (13 us at 1,024).
-    uint32_t* acc = a.wsc;                                   // acc_i, i = 0..nw: X | Y | Z | T row limbs
-    const uint32_t* wc = a.wsc + (size_t)64 * (lay.nw + 1);  // window w's cached row form
-    uint32_t* sa = lds + 16 * P3_WORDS;                      // 3 x 64 words: acc_lw, wc_lw, result
-    int lw;
-    if (blockIdx.y == 0) {
-        // row 0: the basepoint term, one workgroup beside the windows
-        if (blockIdx.x != 0) return;
-        msm_bterm(a.partial, a.nblk, a.comb, sa);
-        if (t >= 64) return;
-        tail_st_coh(acc + t, sa[t]);
-        lw = 0;
-    } else {
+    // Final sum by ONE accumulating wave (the basepoint term's workgroup, dispatched first):
+    // acc = [8 b]B, then acc += (scaled window w) for w = 0 .. nw - 1 in window order, each a
+    // row-form addition (fe_row.h row_add_cached, ~0.4 us) with acc kept in registers.  Window w's
+    // last workgroup publishes its cached row form and sets ready[w] (ctr[64 + w]); the wave waits
+    // for each flag in turn.  Window chains end in about window order (window w's chain is
+    // pos_w + 3 + its plane count long), so the additions run behind the chains and one follows
+    // the top window's.  Round 4 summed all nw + 1 items after the last arrival with a 5-level
+    // quad-lane tree (13 us at 1,024 signatures); a hand-off ladder between workgroups cost ~1.7 us
+    // a step (cross-XCD atomics and loads) and fell behind the windows.
+    uint32_t* ready = a.ctr + 64;
+    uint32_t* sa = lds + 16 * P3_WORDS;  // 64 words
+    if (blockIdx.y != 0) {
         if (!msm_tail_window<PER>(lay, a, lds, flag)) return;
-        if (t >= 64) return;
-        lw = lay.nw - (int)blockIdx.y;
-    }
-    const int w = lw;  // stamp slot
-#pragma unroll 1
-    while (true) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's hand-off stores are done
-        uint32_t old = 0;
-        if (t == 0) old = __hip_atomic_fetch_add(a.ctr + 64 + lw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        old = __builtin_amdgcn_readfirstlane(old);
-        if (old == 0) return;  // the step's other input arrives later and makes it
-        const bool last = lw + 1 == lay.nw;
-        if (last) NWV_TAIL_STAMP(5);
-        sa[t] = tail_ld_coh(acc + (size_t)64 * lw + t);
-        sa[64 + t] = tail_ld_coh(wc + (size_t)64 * lw + t);
-        rowf::lds_order();
-        rowf::row_ladder_step(sa, sa + 64, sa + 128);
-        rowf::lds_order();
-        if (last) {
-            if (t == 0) {
-                const uint32_t* fin = sa + 128;
-                const bool ok = fe_is_zero(fe_from_limbs16(fin)) &&
-                                fe_eq(fe_from_limbs16(fin + 16), fe_from_limbs16(fin + 32)) && *a.fail == 0;
-                *a.verdict = ok ? 1u : 0u;
-                // per-run tally (runs of one batch are ordered on its stream: a plain increment)
-                if (a.runs) a.runs[ok ? 0 : 1] += 1u;
-            }
-            NWV_TAIL_STAMP(6);
-            return;
+        if (t < 64) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the cached row form has landed
+            if (t == 0) tail_st_coh(ready + (lay.nw - (int)blockIdx.y), 1u);
         }
-        tail_st_coh(acc + (size_t)64 * (lw + 1) + t, sa[128 + t]);
-        lw++;
+        return;
     }
+    if (blockIdx.x != 0) return;
+    msm_bterm(a.partial, a.nblk, a.comb, sa);
+    if (t >= 64) return;
+#if defined(__HIP_DEVICE_COMPILE__)  // (rowf's lane type is the host emulation's wave elsewhere)
+    const uint32_t* wc = a.wsc + (size_t)64 * (lay.nw + 1);  // window w's cached row form
+    rowf::RowConsts k = rowf::row_consts();
+    k.rot = 1;
+    const uint32_t limb = t & 15;
+    rowf::RowP3 d{sa[limb], sa[16 + limb], sa[32 + limb], sa[48 + limb]};
+    bool timed_out = false;
+#pragma unroll 1
+    for (int w = 0; w < lay.nw; w++) {
+        // a bounded wait (~0.5 s): a window that never publishes ends the kernel with a reject
+        uint32_t spins = 0;
+        while (tail_ld_coh(ready + w) == 0u && ++spins < (1u << 24)) __builtin_amdgcn_s_sleep(1);
+        if (spins >= (1u << 24)) {
+            timed_out = true;
+            break;
+        }
+        if (w == lay.nw - 1) NWV_TAIL_STAMP(5);
+        d = rowf::row_add_cached(d, tail_ld_coh(wc + (size_t)64 * w + t), k);
+    }
+    if (t < 16) {
+        sa[t] = d.X;
+        sa[16 + t] = d.Y;
+        sa[32 + t] = d.Z;
+    }
+    rowf::lds_order();
+    // the identity test X = 0 and Y = Z as two zero tests side by side: lane 0 X - 0, lane 1 Y - Z
+    // (the same instructions on both lanes, one freeze each)
+    const fe va = fe_from_limbs16(sa + (t == 1 ? 16 : 0));
+    const fe vb = fe_select(fe_from_limbs16(sa + 32), fe_zero(), t != 1);
+    const bool nz = !fe_is_zero(fe_sub(fe_carry(va), fe_carry(vb)));
+    const unsigned long long bad = __ballot(t < 2 && nz);
+    if (t == 0) {
+        const bool ok = !timed_out && bad == 0 && *a.fail == 0;
+        *a.verdict = ok ? 1u : 0u;
+        // per-run tally (runs of one batch are ordered on its stream: a plain increment)
+        if (a.runs) a.runs[ok ? 0 : 1] += 1u;
+    }
+    const int w = lay.nw - 1;  // stamp slot
+    NWV_TAIL_STAMP(6);
+#endif
 }
 
 extern "C" __global__ void __launch_bounds__(256) k_msm_tail(MsmLayout lay, MsmTailArgs a) { msm_tail_body<1>(lay, a); }

@@ -34,8 +34,11 @@
 #include "../../include/nwv.h"
 #include "../../include/nwv_bls.h"
 #include "bls_verify.h"
+#include "bls_shard.h"
 
 using namespace bls;
+using nwv::bls_for_ranges;
+using nwv::bls_shard_ranges;
 
 __attribute__((visibility("hidden"))) int nwv_internal_set_err(int code, const char* msg);
 extern "C" {  // defined in nwv_host.hip's extern "C" section
@@ -809,10 +812,18 @@ struct BlsDev {
     int last_path = 0;
     uint64_t last_keys[2] = {0, 0};  // key-list entries found in the cache, distinct keys decoded
 };
+// the BLS engine's state of one context: one BlsDev per device of the context (nwv_init with
+// several devices shards nwv_bls_verify_many by item index, bls_shard.h).  Diagnostic / test hook:
+// env NWV_BLS_DEVICE_REPLICAS=r gives every device r independent BlsDev shards (own key cache,
+// ring and lanes), so the split, the per-shard key registration and the status merge run on a
+// one-GPU box too.
+struct BlsCtx {
+    std::vector<BlsDev*> devs;
+};
 std::mutex g_mu;
-std::unordered_map<nwv_ctx*, BlsDev*> g_devs;
+std::unordered_map<nwv_ctx*, BlsCtx*> g_devs;
 
-int dev_of(nwv_ctx* ctx, BlsDev** out) {
+int ctx_of(nwv_ctx* ctx, BlsCtx** out) {
     if (!ctx) return nwv_internal_set_err(NWV_ERR_ARG, "null context");
     std::lock_guard<std::mutex> g(g_mu);
     auto it = g_devs.find(ctx);
@@ -820,14 +831,50 @@ int dev_of(nwv_ctx* ctx, BlsDev** out) {
         *out = it->second;
         return NWV_OK;
     }
-    const int ord = nwv_device_ordinal(ctx, 0);
-    if (ord < 0) return nwv_internal_set_err(NWV_ERR_NODEV, "context has no device");
-    auto* d = new BlsDev;
-    d->ordinal = ord;
-    d->flags = nwv_internal_ctx_flags(ctx);
-    g_devs[ctx] = d;
-    *out = d;
+    const int nd = nwv_device_count(ctx);
+    if (nd <= 0 || nwv_device_ordinal(ctx, 0) < 0) return nwv_internal_set_err(NWV_ERR_NODEV, "context has no device");
+    static const int replicas = [] {
+        const char* e = std::getenv("NWV_BLS_DEVICE_REPLICAS");
+        const int r = e ? std::atoi(e) : 1;
+        return r < 1 ? 1 : (r > 8 ? 8 : r);
+    }();
+    auto* c = new BlsCtx;
+    for (int k = 0; k < nd; k++)
+        for (int r = 0; r < replicas; r++) {
+            auto* d = new BlsDev;
+            d->ordinal = nwv_device_ordinal(ctx, k);
+            d->flags = nwv_internal_ctx_flags(ctx);
+            c->devs.push_back(d);
+        }
+    g_devs[ctx] = c;
+    *out = c;
     return NWV_OK;
+}
+
+// the context's first device (single-device entry points: aggregate, keygen, sign, hash, pairing)
+int dev_of(nwv_ctx* ctx, BlsDev** out) {
+    BlsCtx* c;
+    int rc = ctx_of(ctx, &c);
+    if (rc) return rc;
+    *out = c->devs[0];
+    return NWV_OK;
+}
+
+// fn(dev) on every device of the context (one host thread each), first nonzero rc in device order
+template <class Fn>
+int on_all_devices(BlsCtx& c, Fn fn) {
+    std::vector<std::pair<size_t, size_t>> r;
+    for (size_t k = 0; k < c.devs.size(); k++) r.push_back({k, k + 1});
+    std::vector<std::string> err(c.devs.size());
+    const int rc = bls_for_ranges(r, [&](size_t k, size_t, size_t) {
+        const int e = fn(*c.devs[k]);
+        if (e) err[k] = nwv_last_error();
+        return e;
+    });
+    if (rc)
+        for (size_t k = 0; k < err.size(); k++)
+            if (!err[k].empty()) return nwv_internal_set_err(rc, err[k].c_str());
+    return rc;
 }
 
 // a lane of the device's pool for the duration of one call (created on demand, at most kMaxLanes)
@@ -1292,7 +1339,10 @@ __attribute__((visibility("hidden"))) void nwv_bls_ctx_release(nwv_ctx* ctx) {
     std::lock_guard<std::mutex> g(g_mu);
     auto it = g_devs.find(ctx);
     if (it == g_devs.end()) return;
-    (void)hipSetDevice(it->second->ordinal);
+    for (BlsDev* d : it->second->devs) {
+        (void)hipSetDevice(d->ordinal);
+        delete d;
+    }
     delete it->second;
     g_devs.erase(it);
 }
@@ -1319,11 +1369,34 @@ int nwv_bls_verify_many(nwv_ctx* ctx, size_t n_keys, const uint8_t* keys, size_t
     if (n_idx && !pk_idx) return nwv_internal_set_err(NWV_ERR_ARG, "null pk_idx");
     for (size_t k = 0; k < n_idx; k++)
         if (pk_idx[k] >= n_keys) return nwv_internal_set_err(NWV_ERR_ARG, "key index out of range");
-    BlsDev* d;
-    int rc = dev_of(ctx, &d);
+    BlsCtx* c;
+    int rc = ctx_of(ctx, &c);
     if (rc) return rc;
-    return verify_on(*d, n_keys, keys, n, sigs, pk_off, pk_cnt, pk_idx, n_idx, msg_base, msg_off, msg_len, msg_bytes,
-                     dst, dst_len, status);
+    // items split by index over the context's devices (bls_shard.h); small calls stay on device 0
+    static const size_t shard_min = [] {
+        const char* e = std::getenv("NWV_BLS_SHARD_MIN");
+        return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)256;
+    }();
+    const auto ranges = bls_shard_ranges(n, c->devs.size(), shard_min);
+    if (ranges.size() == 1)
+        return verify_on(*c->devs[0], n_keys, keys, n, sigs, pk_off, pk_cnt, pk_idx, n_idx, msg_base, msg_off, msg_len,
+                         msg_bytes, dst, dst_len, status);
+    std::vector<std::string> err(ranges.size());
+    rc = bls_for_ranges(ranges, [&](size_t k, size_t lo, size_t hi) -> int {
+        size_t ni = 0, mb = 0;  // the range's own key-index and message extents
+        for (size_t i = lo; i < hi; i++) {
+            ni = std::max<size_t>(ni, (size_t)pk_off[i] + pk_cnt[i]);
+            mb = std::max<size_t>(mb, msg_off[i] + msg_len[i]);
+        }
+        const int e = verify_on(*c->devs[k], n_keys, keys, hi - lo, sigs + 48 * lo, pk_off + lo, pk_cnt + lo, pk_idx,
+                                ni, msg_base, msg_off + lo, msg_len + lo, mb, dst, dst_len, status + lo);
+        if (e) err[k] = nwv_last_error();
+        return e;
+    });
+    if (rc)  // the failing range's message, on the caller's thread
+        for (size_t k = 0; k < err.size(); k++)
+            if (!err[k].empty()) return nwv_internal_set_err(rc, err[k].c_str());
+    return rc;
 }
 
 int nwv_bls_last_kernel_ms(nwv_ctx* ctx, double out_ms[5]) {
@@ -1358,19 +1431,22 @@ int nwv_bls_last_keys(nwv_ctx* ctx, uint64_t out[2]) {
 int nwv_bls_keycache_register(nwv_ctx* ctx, size_t n_keys, const uint8_t* keys) {
     if (n_keys && !keys) return nwv_internal_set_err(NWV_ERR_ARG, "null argument");
     if (n_keys > KC_CAP) return nwv_internal_set_err(NWV_ERR_ARG, "more keys than the cache holds");
-    BlsDev* d;
-    int rc = dev_of(ctx, &d);
+    BlsCtx* c;
+    int rc = ctx_of(ctx, &c);
     if (rc) return rc;
-    return n_keys ? keycache_register(*d, n_keys, keys) : NWV_OK;
+    // every device verifies its own item range against its own cache
+    return n_keys ? on_all_devices(*c, [&](BlsDev& d) { return keycache_register(d, n_keys, keys); }) : NWV_OK;
 }
 
 int nwv_bls_keycache_reset(nwv_ctx* ctx) {
-    BlsDev* d;
-    int rc = dev_of(ctx, &d);
+    BlsCtx* c;
+    int rc = ctx_of(ctx, &c);
     if (rc) return rc;
-    std::unique_lock<std::shared_mutex> g(d->kc.mu);  // waits for calls that read the records
-    d->kc.slot.clear();
-    d->kc.used = 0;
+    for (BlsDev* d : c->devs) {
+        std::unique_lock<std::shared_mutex> g(d->kc.mu);  // waits for calls that read the records
+        d->kc.slot.clear();
+        d->kc.used = 0;
+    }
     return NWV_OK;
 }
 

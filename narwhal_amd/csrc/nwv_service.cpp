@@ -24,7 +24,8 @@ namespace {
 using Clock = std::chrono::steady_clock;
 
 // committee (config/src/lib.rs:488-551) owned by the service; items keep the one current at
-// their submission
+// their submission.  Ed25519 committees hold 32-byte keys, BLS12-381 ones 96-byte keys (the two
+// C structs differ only in that).
 struct OwnedCommittee {
     std::vector<uint8_t> keys;
     std::vector<uint64_t> stakes;
@@ -32,18 +33,25 @@ struct OwnedCommittee {
     std::vector<std::vector<uint32_t>> ids;
     std::vector<const uint32_t*> id_ptr;
     nwv_committee view{};
+    nwv_bls_committee bview{};
 
-    explicit OwnedCommittee(const nwv_committee& c)
-        : keys(c.keys, c.keys + 32 * c.n), stakes(c.stakes, c.stakes + c.n), ids(c.n), id_ptr(c.n, nullptr) {
-        n_workers.assign(c.n, 0);
-        for (size_t i = 0; i < c.n; i++) {
-            const uint32_t k = c.n_workers ? c.n_workers[i] : 0;
-            n_workers[i] = k;
-            if (k && c.worker_ids && c.worker_ids[i]) ids[i].assign(c.worker_ids[i], c.worker_ids[i] + k);
+    OwnedCommittee(size_t n, const uint8_t* k, size_t key_bytes, const uint64_t* st, uint64_t epoch,
+                   const uint32_t* nw, const uint32_t* const* wid)
+        : keys(k, k + key_bytes * n), stakes(st, st + n), ids(n), id_ptr(n, nullptr) {
+        n_workers.assign(n, 0);
+        for (size_t i = 0; i < n; i++) {
+            const uint32_t c = nw ? nw[i] : 0;
+            n_workers[i] = c;
+            if (c && wid && wid[i]) ids[i].assign(wid[i], wid[i] + c);
             id_ptr[i] = ids[i].empty() ? nullptr : ids[i].data();
         }
-        view = nwv_committee{c.n, keys.data(), stakes.data(), c.epoch, n_workers.data(), id_ptr.data()};
+        view = nwv_committee{n, keys.data(), stakes.data(), epoch, n_workers.data(), id_ptr.data()};
+        bview = nwv_bls_committee{n, keys.data(), stakes.data(), epoch, n_workers.data(), id_ptr.data()};
     }
+    explicit OwnedCommittee(const nwv_committee& c)
+        : OwnedCommittee(c.n, c.keys, 32, c.stakes, c.epoch, c.n_workers, c.worker_ids) {}
+    explicit OwnedCommittee(const nwv_bls_committee& c)
+        : OwnedCommittee(c.n, c.keys, 96, c.stakes, c.epoch, c.n_workers, c.worker_ids) {}
 };
 
 enum Kind { HEADER = 0, VOTE = 1, CERT = 2 };
@@ -56,6 +64,9 @@ struct Item {
     nwv_header h{};
     nwv_vote v{};
     nwv_certificate c{};
+    nwv_bls_header bh{};  // BLS12-381 services
+    nwv_bls_vote bv{};
+    nwv_bls_certificate bc{};
     nwv_done_fn done = nullptr;
     void* user = nullptr;
     Clock::time_point t;
@@ -88,7 +99,32 @@ void copy_header(Item* it, const nwv_header& h, size_t at, size_t wat, nwv_heade
     if (!h.n_parents) out.parents = nullptr;
 }
 
-bool header_ok(const nwv_header* h) {
+// the BLS12-381 header layout (96-byte author, 48-byte signature)
+size_t bls_header_bytes(const nwv_bls_header& h) { return 96 + 32 * h.n_payload + 32 * h.n_parents + 32 + 48; }
+void copy_bls_header(Item* it, const nwv_bls_header& h, size_t at, size_t wat, nwv_bls_header& out) {
+    uint8_t* b = it->bytes.data() + at;
+    auto put = [&](const uint8_t* src, size_t n) {
+        if (n && src) std::memcpy(b, src, n);
+        else if (n) std::memset(b, 0, n);
+        const uint8_t* r = b;
+        b += n;
+        return r;
+    };
+    out = h;
+    out.author = put(h.author, 96);
+    out.payload_digests = put(h.payload_digests, 32 * h.n_payload);
+    out.parents = put(h.parents, 32 * h.n_parents);
+    out.id = put(h.id, 32);
+    out.signature = put(h.signature, 48);
+    uint32_t* w = it->words.data() + wat;
+    if (h.n_payload && h.payload_workers) std::memcpy(w, h.payload_workers, 4 * h.n_payload);
+    out.payload_workers = h.n_payload ? w : nullptr;
+    if (!h.n_payload) out.payload_digests = nullptr;
+    if (!h.n_parents) out.parents = nullptr;
+}
+
+template <class H>
+bool header_ok(const H* h) {
     return h && h->author && h->id && h->signature && (!h->n_payload || (h->payload_digests && h->payload_workers)) &&
            (!h->n_parents || h->parents);
 }
@@ -113,8 +149,9 @@ void waiter_done(void* user, int32_t r) {
 // callback may submit asynchronously, but a blocking call on THAT service (nwv_service_verify_*,
 // nwv_service_flush) would wait for batches that this very thread -- or, with both flushers inside
 // callbacks, no thread -- would ever verify: such calls return NWV_ERR_REENTRANT instead of
-// deadlocking.  Blocking calls on another service (or the engine) are not refused.  Set and
-// restored by an RAII guard, so a callback that unwinds cannot leave it set.
+// deadlocking.  Blocking calls on another service are refused only when they would close a cycle
+// of such waits (WaitEdge below).  Set and restored by an RAII guard, so a callback that unwinds
+// cannot leave it set.
 thread_local const nwv_service* tl_cb_svc = nullptr;
 struct CallbackScope {
     const nwv_service* prev;
@@ -122,10 +159,58 @@ struct CallbackScope {
     ~CallbackScope() { tl_cb_svc = prev; }
 };
 
+// Blocking calls made from callbacks across services: while a callback of service A waits on
+// service B, the edge A -> B is in a process-wide waits-for graph.  A wait that would close a
+// cycle (B's callbacks already wait, directly or through other services, on A) is refused with
+// NWV_ERR_REENTRANT: with every flusher of each service inside such a callback, none of them
+// would ever verify the batch another one waits for.
+std::mutex g_wait_mu;
+std::multiset<std::pair<const nwv_service*, const nwv_service*>> g_wait_edges;
+bool waits_reach(const nwv_service* from, const nwv_service* to) {  // g_wait_mu held
+    std::vector<const nwv_service*> stack{from};
+    std::set<const nwv_service*> seen;
+    while (!stack.empty()) {
+        const nwv_service* x = stack.back();
+        stack.pop_back();
+        if (x == to) return true;
+        if (!seen.insert(x).second) continue;
+        for (auto it = g_wait_edges.lower_bound({x, nullptr}); it != g_wait_edges.end() && it->first == x; ++it)
+            stack.push_back(it->second);
+    }
+    return false;
+}
+// registers the edge (callback's service -> target) for the duration of a blocking call
+struct WaitEdge {
+    const nwv_service* from = nullptr;
+    const nwv_service* to = nullptr;
+    int rc = NWV_OK;
+    explicit WaitEdge(const nwv_service* target) {
+        if (!tl_cb_svc || !target) return;  // not inside a callback: nothing can wait on this thread
+        if (tl_cb_svc == target) {
+            rc = NWV_ERR_REENTRANT;
+            return;
+        }
+        std::lock_guard<std::mutex> g(g_wait_mu);
+        if (waits_reach(target, tl_cb_svc)) {
+            rc = NWV_ERR_REENTRANT;
+            return;
+        }
+        from = tl_cb_svc;
+        to = target;
+        g_wait_edges.insert({from, to});
+    }
+    ~WaitEdge() {
+        if (!from) return;
+        std::lock_guard<std::mutex> g(g_wait_mu);
+        g_wait_edges.erase(g_wait_edges.find({from, to}));
+    }
+};
+
 template <class Submit>
 int verify_blocking(const nwv_service* svc, Submit submit, int32_t* result) {
     if (!result) return NWV_ERR_ARG;
-    if (svc && tl_cb_svc == svc) return NWV_ERR_REENTRANT;
+    WaitEdge edge(svc);
+    if (edge.rc) return edge.rc;
     Waiter w;
     const int rc = submit(&w);
     if (rc) return rc;
@@ -139,6 +224,7 @@ int verify_blocking(const nwv_service* svc, Submit submit, int32_t* result) {
 
 struct nwv_service {
     nwv_ctx* ctx = nullptr;
+    bool bls = false;  // BLS12-381 service (nwv_service_create_bls): one nwv_bls_verify_mixed_many per flush
     size_t max_batch = 1;
     std::chrono::microseconds max_wait{0};
     std::mutex mu;
@@ -183,17 +269,33 @@ void nwv_service::run() {
         }
         if (!pending.empty()) cv_work.notify_one();  // the rest may be another flusher's
         lk.unlock();
-        std::vector<nwv_header> H;
-        std::vector<nwv_vote> V;
-        std::vector<nwv_certificate> C;
-        for (auto& it : batch) {
-            if (it->kind == HEADER) H.push_back(it->h);
-            else if (it->kind == VOTE) V.push_back(it->v);
-            else C.push_back(it->c);
+        size_t nh = 0, nv = 0, nc = 0;
+        for (auto& it : batch) (it->kind == HEADER ? nh : it->kind == VOTE ? nv : nc)++;
+        std::vector<int32_t> rh(nh), rv(nv), rc(nc);
+        int rc_call;
+        if (bls) {
+            std::vector<nwv_bls_header> H;
+            std::vector<nwv_bls_vote> V;
+            std::vector<nwv_bls_certificate> C;
+            for (auto& it : batch) {
+                if (it->kind == HEADER) H.push_back(it->bh);
+                else if (it->kind == VOTE) V.push_back(it->bv);
+                else C.push_back(it->bc);
+            }
+            rc_call = nwv_bls_verify_mixed_many(ctx, &com_b->bview, nh, H.data(), rh.data(), nv, V.data(), rv.data(),
+                                                nc, C.data(), rc.data());
+        } else {
+            std::vector<nwv_header> H;
+            std::vector<nwv_vote> V;
+            std::vector<nwv_certificate> C;
+            for (auto& it : batch) {
+                if (it->kind == HEADER) H.push_back(it->h);
+                else if (it->kind == VOTE) V.push_back(it->v);
+                else C.push_back(it->c);
+            }
+            rc_call = nwv_verify_mixed_many(ctx, &com_b->view, nh, H.data(), rh.data(), nv, V.data(), rv.data(), nc,
+                                            C.data(), rc.data());
         }
-        std::vector<int32_t> rh(H.size()), rv(V.size()), rc(C.size());
-        const int rc_call = nwv_verify_mixed_many(ctx, &com_b->view, H.size(), H.data(), rh.data(), V.size(),
-                                                  V.data(), rv.data(), C.size(), C.data(), rc.data());
         size_t ih = 0, iv = 0, ic = 0;
         {
             CallbackScope scope(this);
@@ -229,8 +331,12 @@ int nwv_service::submit(std::unique_ptr<Item> it, nwv_done_fn done, void* user) 
 
 extern "C" {
 
-int nwv_service_create(nwv_ctx* ctx, const nwv_committee* committee, size_t max_batch, uint32_t max_wait_us,
-                       nwv_service** out) {
+}  // extern "C"
+
+namespace {
+template <class Committee>
+int service_create(nwv_ctx* ctx, const Committee* committee, size_t max_batch, uint32_t max_wait_us, bool bls,
+                   nwv_service** out) {
     if (!out) return NWV_ERR_ARG;
     *out = nullptr;
     if (!ctx || !committee || !committee->keys || !committee->stakes || max_batch == 0) return NWV_ERR_ARG;
@@ -238,6 +344,7 @@ int nwv_service_create(nwv_ctx* ctx, const nwv_committee* committee, size_t max_
     if (!s) return NWV_ERR_OOM;
     try {
         s->ctx = ctx;
+        s->bls = bls;
         s->max_batch = max_batch;
         s->max_wait = std::chrono::microseconds(max_wait_us);
         s->com = std::make_shared<const OwnedCommittee>(*committee);
@@ -257,9 +364,9 @@ int nwv_service_create(nwv_ctx* ctx, const nwv_committee* committee, size_t max_
     *out = s;
     return NWV_OK;
 }
-
-int nwv_service_set_committee(nwv_service* svc, const nwv_committee* committee) {
-    if (!svc || !committee || !committee->keys || !committee->stakes) return NWV_ERR_ARG;
+template <class Committee>
+int set_committee(nwv_service* svc, const Committee* committee, bool bls) {
+    if (!svc || !committee || !committee->keys || !committee->stakes || svc->bls != bls) return NWV_ERR_ARG;
     try {
         auto c = std::make_shared<const OwnedCommittee>(*committee);
         std::lock_guard<std::mutex> g(svc->mu);
@@ -269,9 +376,27 @@ int nwv_service_set_committee(nwv_service* svc, const nwv_committee* committee) 
     }
     return NWV_OK;
 }
+}  // namespace
+
+extern "C" {
+
+int nwv_service_create(nwv_ctx* ctx, const nwv_committee* committee, size_t max_batch, uint32_t max_wait_us,
+                       nwv_service** out) {
+    return service_create(ctx, committee, max_batch, max_wait_us, false, out);
+}
+int nwv_service_create_bls(nwv_ctx* ctx, const nwv_bls_committee* committee, size_t max_batch, uint32_t max_wait_us,
+                           nwv_service** out) {
+    return service_create(ctx, committee, max_batch, max_wait_us, true, out);
+}
+int nwv_service_set_committee(nwv_service* svc, const nwv_committee* committee) {
+    return set_committee(svc, committee, false);
+}
+int nwv_service_set_committee_bls(nwv_service* svc, const nwv_bls_committee* committee) {
+    return set_committee(svc, committee, true);
+}
 
 int nwv_service_submit_header(nwv_service* svc, const nwv_header* h, nwv_done_fn done, void* user) {
-    if (!svc || !header_ok(h)) return NWV_ERR_ARG;
+    if (!svc || svc->bls || !header_ok(h)) return NWV_ERR_ARG;
     try {
         auto it = std::make_unique<Item>();
         it->kind = HEADER;
@@ -285,7 +410,7 @@ int nwv_service_submit_header(nwv_service* svc, const nwv_header* h, nwv_done_fn
 }
 
 int nwv_service_submit_vote(nwv_service* svc, const nwv_vote* v, nwv_done_fn done, void* user) {
-    if (!svc || !v || !v->id || !v->origin || !v->author || !v->signature) return NWV_ERR_ARG;
+    if (!svc || svc->bls || !v || !v->id || !v->origin || !v->author || !v->signature) return NWV_ERR_ARG;
     try {
         auto it = std::make_unique<Item>();
         it->kind = VOTE;
@@ -303,7 +428,7 @@ int nwv_service_submit_vote(nwv_service* svc, const nwv_vote* v, nwv_done_fn don
 }
 
 int nwv_service_submit_certificate(nwv_service* svc, const nwv_certificate* c, nwv_done_fn done, void* user) {
-    if (!svc || !c || !header_ok(&c->header) || (c->n_signed && !c->signed_authorities) ||
+    if (!svc || svc->bls || !c || !header_ok(&c->header) || (c->n_signed && !c->signed_authorities) ||
         (c->n_sigs && !c->aggregated_signature))
         return NWV_ERR_ARG;
     try {
@@ -327,6 +452,77 @@ int nwv_service_submit_certificate(nwv_service* svc, const nwv_certificate* c, n
     }
 }
 
+// ---- BLS12-381 items (96-byte keys, 48-byte signatures; a certificate's aggregate is one
+// 48-byte G1 point or NULL for AggregateSignature::default())
+int nwv_service_submit_bls_header(nwv_service* svc, const nwv_bls_header* h, nwv_done_fn done, void* user) {
+    if (!svc || !svc->bls || !header_ok(h)) return NWV_ERR_ARG;
+    try {
+        auto it = std::make_unique<Item>();
+        it->kind = HEADER;
+        it->bytes.resize(bls_header_bytes(*h));
+        it->words.resize(h->n_payload);
+        copy_bls_header(it.get(), *h, 0, 0, it->bh);
+        return svc->submit(std::move(it), done, user);
+    } catch (...) {
+        return NWV_ERR_OOM;
+    }
+}
+
+int nwv_service_submit_bls_vote(nwv_service* svc, const nwv_bls_vote* v, nwv_done_fn done, void* user) {
+    if (!svc || !svc->bls || !v || !v->id || !v->origin || !v->author || !v->signature) return NWV_ERR_ARG;
+    try {
+        auto it = std::make_unique<Item>();
+        it->kind = VOTE;
+        it->bytes.resize(32 + 96 + 96 + 48);
+        uint8_t* b = it->bytes.data();
+        std::memcpy(b, v->id, 32);
+        std::memcpy(b + 32, v->origin, 96);
+        std::memcpy(b + 128, v->author, 96);
+        std::memcpy(b + 224, v->signature, 48);
+        it->bv = nwv_bls_vote{b, v->round, v->epoch, b + 32, b + 128, b + 224};
+        return svc->submit(std::move(it), done, user);
+    } catch (...) {
+        return NWV_ERR_OOM;
+    }
+}
+
+int nwv_service_submit_bls_certificate(nwv_service* svc, const nwv_bls_certificate* c, nwv_done_fn done,
+                                       void* user) {
+    if (!svc || !svc->bls || !c || !header_ok(&c->header) || (c->n_signed && !c->signed_authorities))
+        return NWV_ERR_ARG;
+    try {
+        auto it = std::make_unique<Item>();
+        it->kind = CERT;
+        const size_t hb = bls_header_bytes(c->header);
+        it->bytes.resize(hb + 48);
+        it->words.resize(c->header.n_payload + c->n_signed);
+        copy_bls_header(it.get(), c->header, 0, 0, it->bc.header);
+        uint32_t* sa = it->words.data() + c->header.n_payload;
+        if (c->n_signed) std::memcpy(sa, c->signed_authorities, 4 * c->n_signed);
+        uint8_t* sg = it->bytes.data() + hb;
+        if (c->aggregated_signature) std::memcpy(sg, c->aggregated_signature, 48);
+        it->bc.n_signed = c->n_signed;
+        it->bc.signed_authorities = c->n_signed ? sa : nullptr;
+        it->bc.aggregated_signature = c->aggregated_signature ? sg : nullptr;
+        return svc->submit(std::move(it), done, user);
+    } catch (...) {
+        return NWV_ERR_OOM;
+    }
+}
+
+int nwv_service_verify_bls_header(nwv_service* svc, const nwv_bls_header* h, int32_t* result) {
+    return verify_blocking(svc, [&](Waiter* w) { return nwv_service_submit_bls_header(svc, h, waiter_done, w); },
+                           result);
+}
+int nwv_service_verify_bls_vote(nwv_service* svc, const nwv_bls_vote* v, int32_t* result) {
+    return verify_blocking(svc, [&](Waiter* w) { return nwv_service_submit_bls_vote(svc, v, waiter_done, w); },
+                           result);
+}
+int nwv_service_verify_bls_certificate(nwv_service* svc, const nwv_bls_certificate* c, int32_t* result) {
+    return verify_blocking(svc, [&](Waiter* w) { return nwv_service_submit_bls_certificate(svc, c, waiter_done, w); },
+                           result);
+}
+
 int nwv_service_verify_header(nwv_service* svc, const nwv_header* h, int32_t* result) {
     return verify_blocking(svc, [&](Waiter* w) { return nwv_service_submit_header(svc, h, waiter_done, w); }, result);
 }
@@ -340,7 +536,8 @@ int nwv_service_verify_certificate(nwv_service* svc, const nwv_certificate* c, i
 
 int nwv_service_flush(nwv_service* svc) {
     if (!svc) return NWV_ERR_ARG;
-    if (tl_cb_svc == svc) return NWV_ERR_REENTRANT;
+    WaitEdge edge(svc);
+    if (edge.rc) return edge.rc;
     std::unique_lock<std::mutex> lk(svc->mu);
     const uint64_t upto = svc->next_seq;
     svc->flush_upto = std::max(svc->flush_upto, upto);

@@ -28,6 +28,18 @@ _SIGS = {
     "nwv_service_verify_vote": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "nwv_service_verify_certificate": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)],
                                        ctypes.c_int),
+    "nwv_service_create_bls": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
+                                ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "nwv_service_set_committee_bls": ([ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "nwv_service_submit_bls_header": ([ctypes.c_void_p, ctypes.c_void_p, DONE_FN, ctypes.c_void_p], ctypes.c_int),
+    "nwv_service_submit_bls_vote": ([ctypes.c_void_p, ctypes.c_void_p, DONE_FN, ctypes.c_void_p], ctypes.c_int),
+    "nwv_service_submit_bls_certificate": ([ctypes.c_void_p, ctypes.c_void_p, DONE_FN, ctypes.c_void_p],
+                                           ctypes.c_int),
+    "nwv_service_verify_bls_header": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)],
+                                      ctypes.c_int),
+    "nwv_service_verify_bls_vote": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+    "nwv_service_verify_bls_certificate": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)],
+                                           ctypes.c_int),
     "nwv_service_flush": ([ctypes.c_void_p], ctypes.c_int),
     "nwv_service_stats": ([ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     "nwv_service_free": ([ctypes.c_void_p], None),
@@ -46,15 +58,23 @@ def bind(lib):
 
 
 class Service:
-    """One batching service over an Engine's context (or any nwv_ctx handle with lib)."""
+    """One batching service over an Engine's context (or any nwv_ctx handle with lib).
 
-    def __init__(self, engine, committee, max_batch=256, max_wait_us=200, lib=None, ctx=None):
+    scheme='bls': the reference's default scheme (crypto/src/lib.rs:29-33), BLS12-381 -- items are
+    types.Header / Vote with 96-byte keys and 48-byte signatures and types.BlsCertificate; each
+    flush is one nwv_bls_verify_mixed_many call (nwv_service_create_bls)."""
+
+    def __init__(self, engine, committee, max_batch=256, max_wait_us=200, lib=None, ctx=None, scheme="ed25519"):
+        if scheme not in ("ed25519", "bls"):
+            raise ValueError("scheme must be 'ed25519' or 'bls'")
         self.lib = bind(lib if lib is not None else _lib.load())
+        self.scheme = scheme
+        self._p = "bls_" if scheme == "bls" else ""
         self._keep = T._Keep()
         cc = committee._c(self._keep)
         h = ctypes.c_void_p()
-        rc = self.lib.nwv_service_create(ctx if ctx is not None else engine._h, ctypes.byref(cc), max_batch,
-                                         max_wait_us, ctypes.byref(h))
+        create = self.lib.nwv_service_create_bls if scheme == "bls" else self.lib.nwv_service_create
+        rc = create(ctx if ctx is not None else engine._h, ctypes.byref(cc), max_batch, max_wait_us, ctypes.byref(h))
         if rc:
             raise _lib.NwvError(rc, "nwv_service_create")
         self._h = h
@@ -75,7 +95,8 @@ class Service:
     def set_committee(self, committee):
         keep = T._Keep()
         cc = committee._c(keep)
-        rc = self.lib.nwv_service_set_committee(self._h, ctypes.byref(cc))
+        fn = self.lib.nwv_service_set_committee_bls if self.scheme == "bls" else self.lib.nwv_service_set_committee
+        rc = fn(self._h, ctypes.byref(cc))
         if rc:
             raise _lib.NwvError(rc, "nwv_service_set_committee")
 
@@ -89,15 +110,15 @@ class Service:
 
     def verify_header(self, header):
         keep = T._Keep()
-        return self._verify(self.lib.nwv_service_verify_header, header._c(keep))
+        return self._verify(getattr(self.lib, f"nwv_service_verify_{self._p}header"), header._c(keep))
 
     def verify_vote(self, vote):
         keep = T._Keep()
-        return self._verify(self.lib.nwv_service_verify_vote, vote._c(keep))
+        return self._verify(getattr(self.lib, f"nwv_service_verify_{self._p}vote"), vote._c(keep))
 
     def verify_certificate(self, cert):
         keep = T._Keep()
-        return self._verify(self.lib.nwv_service_verify_certificate, cert._c(keep))
+        return self._verify(getattr(self.lib, f"nwv_service_verify_{self._p}certificate"), cert._c(keep))
 
     # asynchronous forms: done(code) runs on a service thread
     def _submit(self, fn, st, done):
@@ -117,15 +138,15 @@ class Service:
 
     def submit_header(self, header, done):
         keep = T._Keep()
-        self._submit(self.lib.nwv_service_submit_header, header._c(keep), done)
+        self._submit(getattr(self.lib, f"nwv_service_submit_{self._p}header"), header._c(keep), done)
 
     def submit_vote(self, vote, done):
         keep = T._Keep()
-        self._submit(self.lib.nwv_service_submit_vote, vote._c(keep), done)
+        self._submit(getattr(self.lib, f"nwv_service_submit_{self._p}vote"), vote._c(keep), done)
 
     def submit_certificate(self, cert, done):
         keep = T._Keep()
-        self._submit(self.lib.nwv_service_submit_certificate, cert._c(keep), done)
+        self._submit(getattr(self.lib, f"nwv_service_submit_{self._p}certificate"), cert._c(keep), done)
 
     def flush(self):
         _lib._check(self.lib.nwv_service_flush(self._h))

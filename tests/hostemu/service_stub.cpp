@@ -33,6 +33,30 @@ int nwv_verify_mixed_many(nwv_ctx*, const nwv_committee* c, size_t nh, const nwv
     return NWV_OK;
 }
 
+// the BLS12-381 layer's stand-in, same rule (a certificate's code from its header's signature;
+// an aggregate holding no signature -> InvalidSignature)
+int nwv_bls_verify_mixed_many(nwv_ctx*, const nwv_bls_committee* c, size_t nh, const nwv_bls_header* h, int32_t* rh,
+                              size_t nv, const nwv_bls_vote* v, int32_t* rv, size_t nc, const nwv_bls_certificate* cs,
+                              int32_t* rc) {
+    g_calls++;
+    const long n = (long)(nh + nv + nc);
+    g_items += n;
+    long m = g_max.load();
+    while (n > m && !g_max.compare_exchange_weak(m, n)) {
+    }
+    if (g_delay_us) std::this_thread::sleep_for(std::chrono::microseconds(g_delay_us.load()));
+    if (g_fail) return NWV_ERR_HIP;
+    auto code = [&](uint64_t epoch, const uint8_t* sig) {
+        if (epoch != c->epoch) return NWV_DAG_INVALID_EPOCH;
+        return sig[0] == 0xFF ? NWV_DAG_INVALID_SIGNATURE : NWV_DAG_OK;
+    };
+    for (size_t i = 0; i < nh; i++) rh[i] = code(h[i].epoch, h[i].signature);
+    for (size_t i = 0; i < nv; i++) rv[i] = code(v[i].epoch, v[i].signature);
+    for (size_t i = 0; i < nc; i++)
+        rc[i] = cs[i].aggregated_signature ? code(cs[i].header.epoch, cs[i].header.signature) : NWV_DAG_INVALID_SIGNATURE;
+    return NWV_OK;
+}
+
 void stub_reset(long delay_us, long fail) {
     g_calls = 0;
     g_items = 0;

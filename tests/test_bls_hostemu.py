@@ -322,3 +322,16 @@ def test_wave_aggregate_matches_oracle(emu):
     bad = base[:10] + [C.not_in_g1()] + base[10:40]
     o = _buf(48)
     assert emu.bh_w_aggregate(len(bad), b"".join(bad), o, 0) == B.aggregate(bad)[0] == B.ORB_NOT_IN_GROUP
+
+
+def test_generated_wave_tables_match_generator():
+    """narwhal_amd/csrc/bls_wave_prog.h and bls_wave_counts.json are exactly what
+    tools/gen_bls_wave.py emits (its --check re-emits into a temporary directory and compares), after
+    checking every program against its formulas on Python integers"""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(root, "tools", "gen_bls_wave.py"), "--check"],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "match the generator" in p.stderr

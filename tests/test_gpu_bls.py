@@ -412,3 +412,19 @@ def test_ring_wraps_under_concurrent_verifies_and_aggregates(bls):
     for t in ags:
         t.join()
     assert not errs, errs[:5]
+
+
+def test_verify_many_sharded_over_devices():
+    """nwv_bls_verify_many over a multi-device context: the items split by index over three BLS
+    shards on this GPU (NWV_BLS_DEVICE_REPLICAS, the test hook of bls_shard.h), keys registered on
+    every shard, statuses merged in item order -- equal to the oracle with and without the cache"""
+    import subprocess
+    import sys
+    env = dict(os.environ, NWV_BLS_DEVICE_REPLICAS="3", NWV_BLS_SHARD_MIN="8")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "bls_shard_gpu_check.py")], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["shards"] == 3 and out["items"] > 48 and out["want_nonzero"] >= 7
+    assert out["registered_on_shard0"] == 100
+    assert out["cached_equal"] and out["uncached_equal"], out

@@ -200,3 +200,31 @@ def test_bls_core_drain(env):
             got[i] = code
     assert [got[i] for i in range(len(msgs))] == want
     assert d.calls >= 1 and d.largest <= 512
+
+
+def test_bls_service_concurrent_submitters(env):
+    """the in-library batching service in BLS mode (nwv_service_create_bls): 8 threads submit the
+    adversarial round's headers, votes and certificates with the blocking calls; each gets the
+    oracle's code for its own message, and the service coalesced them into few engine calls"""
+    import threading
+    from narwhal_amd.service import Service
+    headers, votes, certs = _adversarial(env)
+    want_h, want_v, want_c = _oracle_codes(env, headers, votes, certs)
+    msgs = [(h, w) for h, w in zip(headers, want_h)] + [(v, w) for v, w in zip(votes, want_v)] + \
+           [(c, w) for c, w in zip(certs, want_c)]
+    got = [None] * len(msgs)
+    with Service(env["eng"], env["com"], max_batch=64, max_wait_us=2000, scheme="bls") as svc:
+        def worker(lo):
+            for k in range(lo, len(msgs), 8):
+                m = msgs[k][0]
+                got[k] = (svc.verify_certificate(m) if isinstance(m, env["T"].BlsCertificate) else
+                          svc.verify_vote(m) if isinstance(m, env["T"].Vote) else svc.verify_header(m))
+
+        th = [threading.Thread(target=worker, args=(lo,)) for lo in range(8)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        st = svc.stats()
+    assert got == [w for _, w in msgs]
+    assert st["items"] == len(msgs) and st["calls"] < len(msgs)

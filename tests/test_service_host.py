@@ -265,3 +265,100 @@ def test_core_drain_policy():
     t0 = time.perf_counter()
     assert d2.drain(q) == [0, 1]  # a late message within the deadline joins the flush
     assert 0.15 < time.perf_counter() - t0 < 2.0  # then the deadline ends the drain
+
+
+def test_blocking_wait_that_closes_a_cycle_is_refused(lib):
+    """a callback of A blocks on B (edge A -> B); a callback of B that then blocks on A
+    would close the cycle A -> B -> A (with every flusher of both inside such callbacks nothing
+    would ever verify) -- it gets NWV_ERR_REENTRANT, while A's wait on B completes normally"""
+    from narwhal_amd import _lib
+    lib.stub_reset(200_000, 0)  # each engine call takes 200 ms: A's callback is inside B meanwhile
+    rnd = random.Random(8)
+    a = S.Service(None, _committee(0), max_batch=1, max_wait_us=0, lib=lib, ctx=ctypes.c_void_p(1))
+    b = S.Service(None, _committee(0), max_batch=1, max_wait_us=0, lib=lib, ctx=ctypes.c_void_p(1))
+    try:
+        a_inside, seen_a, seen_b, done = threading.Event(), [], [], threading.Event()
+
+        def cb_a(code):
+            a_inside.set()
+            seen_a.append(b.verify_vote(_vote(rnd, 0, False)))
+
+        def cb_b(code):
+            assert a_inside.wait(5)
+            time.sleep(0.05)
+            try:
+                a.verify_vote(_vote(rnd, 0, False))
+                seen_b.append("returned")
+            except _lib.NwvError as e:
+                seen_b.append(e.code)
+            done.set()
+
+        a.submit_header(_header(rnd, 0, False), cb_a)
+        b.submit_header(_header(rnd, 0, False), cb_b)
+        assert done.wait(10)
+        a.flush()
+        assert seen_b == [_lib.NWV_ERR_REENTRANT] and seen_a == [0]
+    finally:
+        lib.stub_reset(0, 0)
+        a.close()
+        b.close()
+
+
+def test_bls_service_codes_and_scheme_checks(lib):
+    """a BLS12-381 service (nwv_service_create_bls): concurrent submitters of 96-byte-key headers,
+    votes and certificates get their own codes through one nwv_bls_verify_mixed_many per flush (the
+    stub's rule; an aggregate holding no signature -> InvalidSignature), and the other scheme's
+    calls are refused on each kind of service"""
+    from narwhal_amd import _lib
+    lib.stub_reset(2000, 0)
+    rnd = random.Random(9)
+    keys = sorted(bytes([i + 1]) * 96 for i in range(4))
+    com = T.Committee(keys, [1] * 4, 0, [[0, 1]] * 4)
+
+    def header(epoch, bad):
+        return T.Header(rnd.randbytes(96), 1, epoch, [(rnd.randbytes(32), 0)], [rnd.randbytes(32)],
+                        rnd.randbytes(32), bytes([0xFF if bad else 1]) + rnd.randbytes(47))
+
+    def item(k):
+        kind = k % 3
+        epoch, bad = (1 if k % 7 == 0 else 0), (k % 5 == 0)
+        if kind == 0:
+            h = header(epoch, bad)
+            return h, (T.InvalidEpoch.code if epoch else T.InvalidSignature.code if bad else 0)
+        if kind == 1:
+            v = T.Vote(rnd.randbytes(32), 1, epoch, rnd.randbytes(96), rnd.randbytes(96),
+                       bytes([0xFF if bad else 2]) + rnd.randbytes(47))
+            return v, (T.InvalidEpoch.code if epoch else T.InvalidSignature.code if bad else 0)
+        none = k % 11 == 0
+        c = T.BlsCertificate(header(epoch, bad), [0, 1, 2], None if none else rnd.randbytes(48))
+        return c, (T.InvalidSignature.code if none else T.InvalidEpoch.code if epoch else
+                   T.InvalidSignature.code if bad else 0)
+
+    svc = S.Service(None, com, max_batch=16, max_wait_us=500, lib=lib, ctx=ctypes.c_void_p(1), scheme="bls")
+    ed = S.Service(None, _committee(0), max_batch=4, max_wait_us=0, lib=lib, ctx=ctypes.c_void_p(1))
+    try:
+        items = [item(k) for k in range(120)]
+        got = [None] * len(items)
+
+        def worker(lo):
+            for k in range(lo, len(items), 8):
+                got[k] = _verify(svc, items[k][0])
+
+        th = [threading.Thread(target=worker, args=(lo,)) for lo in range(8)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert got == [w for _, w in items]
+        st = svc.stats()
+        assert st["items"] == 120 and st["calls"] < 120
+        r = ctypes.c_int32(0)  # an Ed25519 item on the BLS service, a BLS item on the Ed25519 one
+        keep = T._Keep()
+        assert lib.nwv_service_verify_vote(svc._h, ctypes.byref(_vote(rnd, 0, False)._c(keep)),
+                                           ctypes.byref(r)) == _lib.NWV_ERR_ARG
+        assert lib.nwv_service_verify_bls_vote(ed._h, ctypes.byref(_vote(rnd, 0, False)._c(keep)),
+                                               ctypes.byref(r)) == _lib.NWV_ERR_ARG
+    finally:
+        lib.stub_reset(0, 0)
+        svc.close()
+        ed.close()

@@ -1643,8 +1643,19 @@ if __name__ == "__main__":
     check_g1_formulas()
     assert all(ls[0] != (0, 0) for ls in line_table(G2X, G2Y))  # identity signatures rely on it
     print("pairing and G1 formulas check", file=sys.stderr)
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "narwhal_amd", "csrc")
     if "--check" not in sys.argv:
-        out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "narwhal_amd", "csrc",
-                           "bls_wave_prog.h")
+        out = os.path.join(csrc, "bls_wave_prog.h")
         ns, nd = emit(compiled, out)
         print(f"wrote {out}: {ns} stages, {nd} record words", file=sys.stderr)
+    else:
+        # the committed header and counts must be exactly what the generator emits today
+        import tempfile
+        with tempfile.TemporaryDirectory() as td:
+            emit(compiled, os.path.join(td, "bls_wave_prog.h"))
+            for f in ("bls_wave_prog.h", "bls_wave_counts.json"):
+                with open(os.path.join(td, f), "rb") as a, open(os.path.join(csrc, f), "rb") as b:
+                    if a.read() != b.read():
+                        print(f"{f}: the committed file differs from the generator's output", file=sys.stderr)
+                        sys.exit(1)
+        print("committed bls_wave_prog.h and bls_wave_counts.json match the generator", file=sys.stderr)
