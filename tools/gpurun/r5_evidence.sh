@@ -5,7 +5,8 @@
 #   the default bench; the driver's 20-step bench; the headline alone under rocprofv3 with ONE
 #   batch in flight (its averages are single-stream kernel times: compare kernel_ms) and, under a
 #   different name, with 12 in flight (averages stretched by the overlap).
-# Afterwards (container): tools/gpurun/r5_collect.sh copies the summaries to profiles/round5_*.
+# Part 2 (r5_evidence2.sh, a separate call: the PMC summaries copied into profiles/ first) runs the
+# benches; afterwards (container) tools/gpurun/r5_collect.sh copies the summaries to profiles/round5_*.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -27,8 +28,4 @@ timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -d $O/bls_pmc2 -o pmc --output-fo
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d $O/bls_pmc3 -o pmc --output-format csv -- python3 tools/bls_pmc_driver.py 16384 1 > $O/bls_pmc3.log 2>&1 || exit $?
 python3 tools/pmc_summary.py --bls --n 16384 --note "round 5 at HEAD: BLS12-381 wave engine, 16,384 single-key items (registered committee keys), tools/bls_pmc_driver.py" --out $O/round5_bls_pmc_n16384.json $O/bls_pmc1 $O/bls_pmc2 $O/bls_pmc3 || exit $?
 cp $O/round5_bls_pmc_n16384.json profiles/ || exit $?
-timeout -k 10 700 python -u bench.py > $O/bench.json 2> $O/bench.err || exit $?
-timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/bench_s20.json 2> $O/bench_s20.err || exit $?
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof1 -o b --output-format csv -- python3 bench.py --steps 20 --warmup 5 --headline-only --inflight 1 --steady-steps 0 --single-steps 8 > $O/headline_inflight1_bench_line.json 2> $O/prof1.log || exit $?
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof12 -o b --output-format csv -- python3 bench.py --steps 20 --warmup 5 --headline-only --inflight 12 --steady-steps 0 --single-steps 8 > $O/headline_inflight12_bench_line.json 2> $O/prof12.log || exit $?
-echo ALLDONE
+echo PART1DONE
