@@ -113,7 +113,8 @@ __device__ __forceinline__ void msm_scalars_block(uint32_t blk, const MsmScalarA
     uint32_t* __restrict__ fail = g.fail;
     const int keyed = g.keyed;
     __shared__ uint32_t zs_lds[256 * 9];
-    const uint64_t i = (uint64_t)blk * 256 + threadIdx.x;
+    const uint32_t nt = blockDim.x;  // 256, or 64 when the call's decompression runs on rows
+    const uint64_t i = (uint64_t)blk * nt + threadIdx.x;
     uint32_t zs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (i < n) {
         uint32_t Aw[8], Rw[8], Sw[8], k[8], z[8], a[8];
@@ -143,11 +144,11 @@ __device__ __forceinline__ void msm_scalars_block(uint32_t blk, const MsmScalarA
 #pragma unroll
     for (int k = 0; k < 8; k++) zs_lds[threadIdx.x * 9 + k] = zs[k];
     __syncthreads();
-    // column sums: thread t < 8 adds word t of the 256 values (< 2^40), then thread 0 carries
+    // column sums: thread t < 8 adds word t of the nt values (< 2^40), then thread 0 carries
     __shared__ unsigned long long col[8];
     if (threadIdx.x < 8) {
         unsigned long long s = 0;
-        for (int r = 0; r < 256; r++) s += zs_lds[r * 9 + threadIdx.x];
+        for (uint32_t r = 0; r < nt; r++) s += zs_lds[r * 9 + threadIdx.x];
         col[threadIdx.x] = s;
     }
     __syncthreads();
@@ -166,7 +167,8 @@ __device__ __forceinline__ void msm_scalars_block(uint32_t blk, const MsmScalarA
         digits[(uint64_t)threadIdx.x * np + na] = 0;
         if (g.split) digits[(uint64_t)threadIdx.x * np + na - 1] = 0;
     }
-    if (blk == 0 && threadIdx.x < 128) g.tail_ctr[threadIdx.x] = 0u;  // (no memset launch)
+    if (blk == 0)  // (no memset launch)
+        for (uint32_t t = threadIdx.x; t < 128; t += nt) g.tail_ctr[t] = 0u;
 }
 
 // Keyed batches (ed25519_consensus groups batch entries by verification key): one workgroup per
@@ -268,7 +270,7 @@ extern "C" __global__ void __launch_bounds__(64) k_keycache_fill(uint32_t cnt, c
 // distinct keys of a keyed batch) into points [0, na).
 __device__ __forceinline__ void msm_points_block(uint32_t blk, const MsmPointArgs& g) {
     const uint64_t n = g.n, na = g.na;
-    const uint64_t t = (uint64_t)blk * 256 + threadIdx.x;
+    const uint64_t t = (uint64_t)blk * blockDim.x + threadIdx.x;
     const uint64_t rwaves = (n + 63) / 64;
     const bool is_r = (t >> 6) < rwaves;
     const uint64_t i = is_r ? t : t - 64 * rwaves;
@@ -288,16 +290,19 @@ __device__ __forceinline__ void msm_points_block(uint32_t blk, const MsmPointArg
 // per workgroup.  Point j of the call: R_j (into na + 1 + j) for j < n, then the A points (into
 // j - n).  Lanes 0..3 of a wave run their row's prelude (u v^7) and postlude (the square-root
 // checks, the sign, the record) lane-locally; the power's limbs go through 64 words of LDS.
-// The lane-local form runs one point per lane at ~0.27 us per squaring; a row at ~0.17 us per
-// product, so the prep of a 1,024-signature batch is bound by its hash role again.
+// The lane-local form runs one point per lane at ~0.27 us per squaring; a row at ~0.13 us per
+// product.  The call then launches k_msm_prep with 64-thread workgroups: four such waves on one
+// CU (one per SIMD) ran the decompression in 62 us against 52 us for single-wave workgroups
+// spread over the chip (512 waves, tools/ubench_prep.hip, profiles/round5_ubench_prep.jsonl).
 __device__ __forceinline__ void msm_points_rows_block(uint32_t blk, const MsmPointArgs& g) {
 #if defined(__HIP_DEVICE_COMPILE__)  // (rowf's lane type is the host emulation's wave elsewhere)
     __shared__ uint32_t rl[256];  // per wave: 4 rows x 16 limbs
     const uint64_t n = g.n, na = g.na, tot = n + g.ndec;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t wave = (uint64_t)blk * (blockDim.x >> 6) + wv;  // 4 points per wave
     uint32_t* sh = rl + 64 * wv;
-    const uint64_t j = ((uint64_t)blk * 4 + wv) * 4 + (lane & 3);
-    if (((uint64_t)blk * 4 + wv) * 4 >= tot) return;  // whole wave past the end (wave-uniform)
+    const uint64_t j = wave * 4 + (lane & 3);
+    if (wave * 4 >= tot) return;  // whole wave past the end (wave-uniform)
     uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (lane < 4) {
         if (j < tot) msm_load8(j < n ? g.sig + 64 * j : g.apk + 32 * (j - n), w);

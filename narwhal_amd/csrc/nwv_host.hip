@@ -514,7 +514,7 @@ size_t msm_na(const EdBuffers& b, size_t n) {
 constexpr size_t MSM_CTR_BYTES = 512;  // k_msm_tail arrival counters (128 words)
 
 int msm_alloc(EdBuffers& b, const MsmPlan& p, size_t n) {
-    const size_t nblk = (n + 255) / 256;
+    const size_t nblk = (n + 63) / 64;  // k_msm_prep's hash workgroups (64 or 256 threads)
     int rc;
     if ((b.nkeys_distinct && (rc = b.m_ascal.ensure(32 * n + 32))) || (rc = b.m_partial.ensure(36 * nblk + 36)) ||
         (rc = b.m_state.ensure(128)) ||
@@ -560,7 +560,6 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     // [0] fail flags, [1] verdict, [2..4) accepted / rejected run tally, [8..16) seed
     uint32_t* state = b.m_state.as<uint32_t>();
     if (seed32 && !state_ready) NWV_HIP(hipMemcpyAsync(state + 8, seed32, 32, hipMemcpyHostToDevice, stream));
-    const unsigned nblk = (unsigned)((n + 255) / 256);
     auto mark = [&](int k) -> int {
         if (ev) NWV_HIP(hipEventRecord(ev[k], stream));
         return NWV_OK;
@@ -586,13 +585,17 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     const bool rows = !(d.flags & NWV_FLAG_NO_ROW_PREP) && n + ndec <= row_prep_max;
     const MsmPointArgs gp{(uint64_t)n, (uint64_t)na, ndec, keyed ? b.keys.as<uint8_t>() : b.pk.as<uint8_t>(),
                           b.sig.as<uint8_t>(), b.m_pts.as<uint32_t>(), state, rows ? 1u : 0u};
+    // row form: single-wave workgroups (a wave alone on its CU decompresses faster than four
+    // waves of one workgroup sharing a CU), so the fused grid's hash role uses 64 threads too
+    const unsigned pthr = rows ? 64u : 256u;
     const size_t waves = (n + 63) / 64 + (na + 63) / 64;
-    const unsigned pblk = rows ? (unsigned)((n + ndec + 15) / 16) : (unsigned)((64 * waves + 255) / 256);
+    const unsigned sblk = (unsigned)((n + pthr - 1) / pthr);  // hash workgroups (k_msm_tail's partials)
+    const unsigned pblk = rows ? (unsigned)((n + ndec + 3) / 4) : (unsigned)((64 * waves + 255) / 256);
     const bool fused = !(d.flags & NWV_FLAG_MSM_SPLIT_PREP);
     if (fused)
-        hipLaunchKernelGGL(k_msm_prep, dim3(nblk + pblk), dim3(256), 0, stream, gs, p.lay, gp, nblk);
+        hipLaunchKernelGGL(k_msm_prep, dim3(sblk + pblk), dim3(pthr), 0, stream, gs, p.lay, gp, sblk);
     else
-        hipLaunchKernelGGL(k_msm_scalars, dim3(nblk), dim3(256), 0, stream, gs, p.lay);
+        hipLaunchKernelGGL(k_msm_scalars, dim3(sblk), dim3(pthr), 0, stream, gs, p.lay);
     const uint32_t* kc = b.kc_split ? d.gpu->kc.recs.as<uint32_t>() : nullptr;
     if (keyed)
         hipLaunchKernelGGL(k_msm_keysum, dim3((unsigned)b.nkeys_distinct), dim3(256), 0, stream, (uint64_t)n,
@@ -601,7 +604,7 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
                            state);
     if ((rc = mark(1))) return rc;
     if ((rc = mark(2))) return rc;
-    if (!fused) hipLaunchKernelGGL(k_msm_points, dim3(pblk), dim3(256), 0, stream, gp);
+    if (!fused) hipLaunchKernelGGL(k_msm_points, dim3(pblk), dim3(pthr), 0, stream, gp);
     if ((rc = mark(3))) return rc;
     const size_t lds_nb = (size_t)4 << (p.lay.cmax - 1);
     uint32_t* kst = b.m_kstart.as<uint32_t>();
@@ -671,7 +674,7 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     const MsmTailArgs ta{b.m_bsum.as<uint32_t>(), b.m_hpart.as<uint32_t>(), kst, E, p.nkeys, p.seg,
                          b.m_tpart.as<uint32_t>(), b.m_wsum.as<uint32_t>(),
                          b.m_ctr.as<uint32_t>(), state, b.m_partial.as<uint32_t>(),
-                         d.gpu->comb.as<uint32_t>(), nblk, quad_max_c, state + 1, state + 2, p.tail_S, st_buf};
+                         d.gpu->comb.as<uint32_t>(), sblk, quad_max_c, state + 1, state + 2, p.tail_S, st_buf};
     // combine items per thread: (lg C + 1) x S_w over the windows (C = nb / S_w buckets per chunk)
     int items = 0;
     for (int w = 0; w < p.lay.nw; w++) {

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstring>
+#include <unistd.h>
 #include "../narwhal_amd/csrc/fe_row.h"
 #include "../narwhal_amd/csrc/msm.h"
 
@@ -53,11 +54,13 @@ __global__ void __launch_bounds__(256) k_rowsq(uint32_t* out, long long* cyc, in
 
 // k_msm_prep's row decompression (msm_points_rows_block) on one wave, with cycle stamps after
 // the lane-local prelude, the row power and the postlude
-__global__ void __launch_bounds__(64) k_rowdec(uint32_t* out, long long* cyc) {
+__global__ void __launch_bounds__(64) k_rowdec(uint32_t* out, long long* cyc, int target) {
 #if defined(__HIP_DEVICE_COMPILE__)
     __shared__ uint32_t sh[64];
+    if ((int)blockIdx.x != target) return;  // one working block; the others land on other CUs
     const int lane = threadIdx.x;
     const long long t0 = clock64();
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
     uint32_t w[8];
     for (int i = 0; i < 8; i++) w[i] = 0x66666666u + (lane & 3) * 0x1111u;
     if (lane < 4) fe_to_limbs16(ge_decompress_pre(w), sh + 16 * lane);
@@ -77,10 +80,12 @@ __global__ void __launch_bounds__(64) k_rowdec(uint32_t* out, long long* cyc) {
         out[32 * lane + 31] = ok;
     }
     const long long t3 = clock64();
+    const unsigned long long r3 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {
         cyc[0] = t1 - t0;
         cyc[1] = t2 - t1;
         cyc[2] = t3 - t2;
+        cyc[3] = (long long)(r3 - r0);  // 100 MHz ticks
     }
 #endif
 }
@@ -126,14 +131,26 @@ int main() {
         printf("{\"sq_form\": \"%s\", \"waves\": %d, \"us_per_sq\": %.4f, \"cycles_per_sq\": %.1f}\n",
                v < 2 ? "ror" : "lds", nthr / 64, t * 1e3 / iters, (double)cc / iters);
     }
-    {
-        long long cc[3];
-        hipLaunchKernelGGL(k_rowdec, dim3(1), dim3(64), 0, 0, out, cyc);
+    // (a) the same CU twice (warm instruction cache), (b) a block index the kernel never ran on
+    // before: with 2,048 blocks it lands on a CU whose instruction cache holds none of this code
+    for (int idle = 0; idle < 4; idle++) {
+        long long cc[4];
+        const int target = idle < 2 ? 0 : 1000 + 37 * idle;
+        if (idle < 2) hipLaunchKernelGGL(k_rowdec, dim3(2048), dim3(64), 0, 0, out, cyc, target);
         hipDeviceSynchronize();
-        hipLaunchKernelGGL(k_rowdec, dim3(1), dim3(64), 0, 0, out, cyc);
-        hipDeviceSynchronize();
-        hipMemcpy(cc, cyc, 24, hipMemcpyDeviceToHost);
-        printf("{\"rowdec_cycles\": {\"prelude\": %lld, \"power\": %lld, \"postlude\": %lld}}\n", cc[0], cc[1], cc[2]);
+        if (idle == 1) usleep(20000);
+        hipEventRecord(e0);
+        hipLaunchKernelGGL(k_rowdec, dim3(2048), dim3(64), 0, 0, out, cyc, target);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float t;
+        hipEventElapsedTime(&t, e0, e1);
+        hipMemcpy(cc, cyc, 32, hipMemcpyDeviceToHost);
+        const long long tot = cc[0] + cc[1] + cc[2];
+        printf("{\"rowdec_case\": \"%s\", \"cycles\": {\"prelude\": %lld, \"power\": %lld, \"postlude\": %lld}, "
+               "\"in_kernel_us\": %.2f, \"clock_ghz\": %.3f, \"event_us\": %.2f}\n",
+               idle == 0 ? "warm" : idle == 1 ? "warm_after_20ms_idle" : "fresh_cu", cc[0], cc[1], cc[2],
+               cc[3] * 0.01, tot / (cc[3] * 10.0), t * 1e3);
     }
     const bool same = std::memcmp(h[0], h[1], sizeof(h[0])) == 0 && std::memcmp(h[0], h[2], sizeof(h[0])) == 0 &&
                       std::memcmp(h[0], h[3], sizeof(h[0])) == 0;
