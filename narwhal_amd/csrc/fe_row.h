@@ -372,6 +372,58 @@ NWV_HD V row_pow_p58(V x, const RowConsts& k) {
     return mul(row_sqn(t19, 2, k), x, k);
 }
 
+NWV_HD V row_d2();
+// a field constant given as 16 radix-2^16 limbs, lane k of every row holding limb k
+NWV_HD V row_const(const uint32_t c[16]) {
+    V x = bc(c[0]);
+#pragma unroll
+    for (int i = 1; i < 16; i++) x = sel(limb_is(i), x, bc(c[i]));
+    return x;
+}
+NWV_HD V row_d() {  // the curve's d = -121665 / 121666
+    const uint32_t c[16] = {30883, 4953, 19914, 30187, 55467, 16705, 2637, 112,
+                            59544, 30585, 16505, 36039, 65139, 11119, 27886, 20995};
+    return row_const(c);
+}
+NWV_HD V row_sqrtm1() {  // sqrt(-1) = 2^((p - 1) / 4)
+    const uint32_t c[16] = {41136, 18958, 6951, 50414, 58488, 44335, 6150, 12099,
+                            55207, 15867, 153, 11085, 57099, 20417, 9344, 11139};
+    return row_const(c);
+}
+
+// Point decompression (ge25519.h ge_decompress, CompressedEdwardsY::decompress) on rows, one
+// point per row, for latency-bound small batches: the prelude and the square-root test's
+// products as row products; only the canonical tests (zero, sign) and the record's conversion
+// stay lane-local (msm_points_rows_block).
+//   y: the encoding's low 255 bits as 16 limbs (values >= p accepted, reduced lazily)
+NWV_HD void row_dec_pre(V y, const RowConsts& k, V& u, V& v, V& uv3, V& uv7) {
+    const V one = sel(limb_is(0), bc(0), bc(1));
+    const V yy = mul(y, y, k);
+    u = carry32(sub(yy, one, k), k);          // y^2 - 1
+    v = carry32(mul(yy, row_d(), k) + one, k);  // d y^2 + 1
+    const V v3 = mul(mul(v, v, k), v, k);
+    uv3 = mul(u, v3, k);
+    uv7 = mul(uv3, mul(v3, v, k), k);  // u v^7 = (u v^3) v^4
+}
+// after pw = uv7^((p-5)/8): the candidate root r = u v^3 pw, r sqrt(-1), and the three values
+// whose zero tests decide the root: check - u, check + u, check + u sqrt(-1) (check = v r^2)
+NWV_HD void row_dec_mid(V uv3, V pw, V u, V v, const RowConsts& k, V& r, V& ri, V& c0, V& c1, V& c2) {
+    const V i = row_sqrtm1();
+    r = mul(uv3, pw, k);
+    ri = mul(r, i, k);
+    const V check = mul(v, mul(r, r, k), k);
+    c0 = carry32(sub(check, u, k), k);
+    c1 = carry32(check + u, k);
+    c2 = carry32(check + mul(u, i, k), k);
+}
+// the MSM record's coordinates (affine Niels, msm.h msm_store_point) from the root x (sign
+// applied, limbs < 2^16 + 2^12) and y: y + x, y - x, 2d x y
+NWV_HD void row_dec_record(V x, V y, const RowConsts& k, V& ypx, V& ymx, V& xy2d) {
+    ypx = carry32(y + x, k);
+    ymx = carry32(sub(y, x, k), k);
+    xy2d = mul(mul(x, y, k), row_d2(), k);
+}
+
 // ---- points: every row holds the whole point (X, Y, Z, T one V each) ------------------------
 
 struct RowP3 {

@@ -285,43 +285,71 @@ __device__ __forceinline__ void msm_points_block(uint32_t blk, const MsmPointArg
     if (!ok) atomicOr(g.fail, 2u);
 }
 
-// Small (latency-bound) batches: the same decompression with its power (250 squarings, 11
-// multiplies) on 16-lane rows (fe_row.h, rotation-form products), four points per wave, sixteen
-// per workgroup.  Point j of the call: R_j (into na + 1 + j) for j < n, then the A points (into
-// j - n).  Lanes 0..3 of a wave run their row's prelude (u v^7) and postlude (the square-root
-// checks, the sign, the record) lane-locally; the power's limbs go through 64 words of LDS.
-// The lane-local form runs one point per lane at ~0.27 us per squaring; a row at ~0.13 us per
-// product.  The call then launches k_msm_prep with 64-thread workgroups: four such waves on one
-// CU (one per SIMD) ran the decompression in 62 us against 52 us for single-wave workgroups
-// spread over the chip (512 waves, tools/ubench_prep.hip, profiles/round5_ubench_prep.jsonl).
+// Small (latency-bound) batches: the same decompression (ge25519.h ge_decompress) on 16-lane rows
+// (fe_row.h, rotation-form products), one point per row, four per wave.  Point j of the call:
+// R_j (into na + 1 + j) for j < n, then the A points (into j - n).  Every product -- the prelude
+// u v^7, the power (250 squarings, 11 multiplies), the root and its square-root test, the record's
+// 2d x y -- is a row product (~0.13 us) instead of a lane-local one (~0.3 us); only the canonical
+// tests (three zero tests side by side on lanes 0..2 of the row, the root's sign on lane 0) and the
+// record's conversion to ten-limb form (lanes 0..2, one coordinate each) are lane-local, handed
+// through 48 words of LDS per row.  The call launches k_msm_prep with 64-thread workgroups: four
+// such waves on one CU (one per SIMD) decompressed in 62 us against 52 us for single-wave
+// workgroups spread over the chip (512 waves, tools/ubench_prep.hip, profiles/round5_ubench_prep.jsonl).
 __device__ __forceinline__ void msm_points_rows_block(uint32_t blk, const MsmPointArgs& g) {
 #if defined(__HIP_DEVICE_COMPILE__)  // (rowf's lane type is the host emulation's wave elsewhere)
-    __shared__ uint32_t rl[256];  // per wave: 4 rows x 16 limbs
+    __shared__ uint32_t rl[4 * 192];  // per wave: 4 rows x 48 words
     const uint64_t n = g.n, na = g.na, tot = n + g.ndec;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, row = lane >> 4, limb = lane & 15;
     const uint64_t wave = (uint64_t)blk * (blockDim.x >> 6) + wv;  // 4 points per wave
-    uint32_t* sh = rl + 64 * wv;
-    const uint64_t j = wave * 4 + (lane & 3);
-    if (wave * 4 >= tot) return;  // whole wave past the end (wave-uniform)
-    uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (lane < 4) {
-        if (j < tot) msm_load8(j < n ? g.sig + 64 * j : g.apk + 32 * (j - n), w);
-        fe_to_limbs16(ge_decompress_pre(w), sh + 16 * lane);
-    }
-    rowf::lds_order();
+    if (wave * 4 >= tot) return;                                   // whole wave past the end (wave-uniform)
+    uint32_t* sh = rl + 192 * wv + 48 * row;                       // this row's 48 words
+    const uint64_t j = wave * 4 + row;
+    const bool live = j < tot;
+    // limb `limb` of the encoding; its bit 255 (the sign of x) cleared, kept per row
+    uint32_t y16 = 0u;
+    if (live) y16 = reinterpret_cast<const uint16_t*>(j < n ? g.sig + 64 * j : g.apk + 32 * (j - n))[limb];
+    const bool sign = (__shfl(y16, (lane & ~15) + 15) >> 15) != 0u;
+    if (limb == 15) y16 &= 0x7FFFu;
     rowf::RowConsts k = rowf::row_consts();
     k.rot = 1;
-    const uint32_t pw = rowf::row_pow_p58(sh[lane], k);
+    uint32_t u, v, uv3, uv7;
+    rowf::row_dec_pre(y16, k, u, v, uv3, uv7);
+    const uint32_t pw = rowf::row_pow_p58(uv7, k);
+    uint32_t r, ri, c0, c1, c2;
+    rowf::row_dec_mid(uv3, pw, u, v, k, r, ri, c0, c1, c2);
+    // square-root test: zero tests of check - u, check + u, check + u sqrt(-1) on lanes 0..2
+    sh[limb] = c0;
+    sh[16 + limb] = c1;
+    sh[32 + limb] = c2;
     rowf::lds_order();
-    sh[lane] = pw;
+    bool z = false;
+    if (limb < 3) z = fe_is_zero(fe_from_limbs16(sh + 16 * limb));
+    const uint32_t rz = (uint32_t)(__ballot(z) >> (16 * row)) & 7u;
+    const bool ok = (rz & 3u) != 0u;  // correct (check = u) or flipped (check = -u)
+    const uint32_t rr = (rz & 6u) ? ri : r;
+    // the root made non-negative, then negated by the sign bit: x = rr or -rr
     rowf::lds_order();
-    if (lane < 4 && j < tot) {
-        ge_p3 P;
-        const bool ok = ge_decompress_post(w, fe_from_limbs16(sh + 16 * lane), P);
+    sh[limb] = rr;
+    rowf::lds_order();
+    bool neg = false;
+    if (limb == 0) neg = fe_is_negative(fe_from_limbs16(sh));
+    const bool negr = ((__ballot(neg) >> (16 * row)) & 1u) != 0u;
+    const uint32_t x = negr != sign ? rowf::carry32(rowf::sub(0u, rr, k), k) : rr;
+    uint32_t ypx, ymx, xy2d;
+    rowf::row_dec_record(x, y16, k, ypx, ymx, xy2d);
+    rowf::lds_order();
+    sh[limb] = ypx;
+    sh[16 + limb] = ymx;
+    sh[32 + limb] = xy2d;
+    rowf::lds_order();
+    if (live && limb < 3) {
         uint32_t* e = g.pts + (size_t)MSM_PT_WORDS * (j < n ? na + 1 + j : j - n);
-        msm_store_point(e, P);
-        e[MSM_PT_WORDS - 1] = ok ? 0u : 1u;
-        if (!ok) atomicOr(g.fail, 2u);
+        store_fe(e + 10 * limb, fe_from_limbs16(sh + 16 * limb));
+        if (limb == 0) {
+            e[30] = 0u;
+            e[MSM_PT_WORDS - 1] = ok ? 0u : 1u;
+            if (!ok) atomicOr(g.fail, 2u);
+        }
     }
 #endif
 }

@@ -646,8 +646,8 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
         const char* e = std::getenv("NWV_BUCKET_QUAD_MAX_N");
         return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)4096;
     }();
-    if (n <= bucket_quad_max_n)
-        hipLaunchKernelGGL(k_msm_bucket_q, dim3((unsigned)((p.nseg + 63) / 64)), dim3(256), 0, stream, p.seg,
+    if (n <= bucket_quad_max_n)  // single-wave workgroups: spread over the CUs (see k_msm_prep's row form)
+        hipLaunchKernelGGL(k_msm_bucket_q, dim3((unsigned)((p.nseg + 15) / 16)), dim3(64), 0, stream, p.seg,
                            p.nkeys, E, ent, kst, b.m_pts.as<uint32_t>(), b.m_bsum.as<uint32_t>(),
                            b.m_hpart.as<uint32_t>(), seg_key, state);
     else

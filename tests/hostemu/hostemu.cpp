@@ -208,37 +208,76 @@ int he_decompress(const uint8_t* p, uint8_t* out_xy) {
     return ok ? 1 : 0;
 }
 
-// k_msm_prep's row form of the decompression (msm_points_rows_block) on the emulated wave, four
-// points at a time: lane-local prelude, the power on 16-lane rows (form 0: DPP shifts, 1: LDS,
-// 2: row rotations as on the device), lane-local postlude.  Each point's MSM record (30 words) and
-// decode flag must equal the lane-local ge_decompress's; returns the number of points that differ.
+// k_msm_prep's row form of the decompression (msm_kernels.hip msm_points_rows_block) on the
+// emulated wave, four points at a time (one per row): the prelude, the power, the root and its
+// square-root test and the record's 2d x y as row products (form 0: DPP shifts, 1: LDS, 2: row
+// rotations as on the device), the zero / sign tests and the record's conversion lane-local as on
+// lanes 0..2 of each row.  Each point's MSM record (30 words, canonical values compared) and decode
+// flag must equal the lane-local ge_decompress's; returns the number of points that differ.
 int he_row_decompress(const uint8_t* encs, int count, int form) {
     int bad = 0;
-    std::vector<uint32_t> sh(64), sc(192);
+    std::vector<uint32_t> sc(192);
     for (int base = 0; base < count; base += 4) {
-        uint32_t w[4][8] = {};
-        for (int q = 0; q < 4; q++) {
-            if (base + q < count) words(encs + 32 * (base + q), w[q]);
-            fe_to_limbs16(ge_decompress_pre(w[q]), sh.data() + 16 * q);
+        rowf::V y16;
+        bool sign[4] = {false, false, false, false};
+        for (int l = 0; l < 64; l++) {
+            const int q = l >> 4, limb = l & 15;
+            uint32_t v = 0;
+            if (base + q < count) v = (uint32_t)encs[32 * (base + q) + 2 * limb] | ((uint32_t)encs[32 * (base + q) + 2 * limb + 1] << 8);
+            if (limb == 15) {
+                sign[q] = (v >> 15) != 0;
+                v &= 0x7FFFu;
+            }
+            y16.l[l] = v;
         }
         rowf::RowConsts k = rowf::row_consts();
         k.rot = form == 2 ? 1 : 0;
         k.sc = form == 1 ? sc.data() : nullptr;
-        rowf::V x;
-        for (int i = 0; i < 64; i++) x.l[i] = sh[i];
-        const rowf::V pw = rowf::row_pow_p58(x, k);
-        for (int i = 0; i < 64; i++) sh[i] = pw.l[i];
+        rowf::V u, v, uv3, uv7, r, ri, c0, c1, c2;
+        rowf::row_dec_pre(y16, k, u, v, uv3, uv7);
+        const rowf::V pw = rowf::row_pow_p58(uv7, k);
+        rowf::row_dec_mid(uv3, pw, u, v, k, r, ri, c0, c1, c2);
+        auto limbs = [](const rowf::V& x, int q, uint32_t out[16]) {
+            for (int i = 0; i < 16; i++) out[i] = x.l[16 * q + i];
+        };
+        bool ok[4];
+        rowf::V rr = r;
+        for (int q = 0; q < 4; q++) {
+            uint32_t a[16];
+            bool z[3];
+            const rowf::V* cs[3] = {&c0, &c1, &c2};
+            for (int c = 0; c < 3; c++) {
+                limbs(*cs[c], q, a);
+                z[c] = fe_is_zero(fe_from_limbs16(a));
+            }
+            ok[q] = z[0] || z[1];
+            if (z[1] || z[2])
+                for (int i = 0; i < 16; i++) rr.l[16 * q + i] = ri.l[16 * q + i];
+        }
+        rowf::M flip;
+        const rowf::V nrr = rowf::carry32(rowf::sub(rowf::bc(0), rr, k), k);
+        for (int q = 0; q < 4; q++) {
+            uint32_t a[16];
+            limbs(rr, q, a);
+            const bool negr = fe_is_negative(fe_from_limbs16(a)) != 0;
+            for (int i = 0; i < 16; i++) flip.l[16 * q + i] = negr != sign[q];
+        }
+        const rowf::V x = rowf::sel(flip, rr, nrr);
+        rowf::V ypx, ymx, xy2d;
+        rowf::row_dec_record(x, y16, k, ypx, ymx, xy2d);
         for (int q = 0; q < 4 && base + q < count; q++) {
-            ge_p3 P, R;
-            const bool ok = ge_decompress_post(w[q], fe_from_limbs16(sh.data() + 16 * q), P);
-            const bool ok_ref = ge_decompress(w[q], R);
-            uint32_t e[MSM_PT_WORDS], e_ref[MSM_PT_WORDS];
-            msm_store_point(e, P);
+            uint32_t w[8];
+            words(encs + 32 * (base + q), w);
+            ge_p3 R;
+            const bool ok_ref = ge_decompress(w, R);
+            uint32_t e_ref[MSM_PT_WORDS];
             msm_store_point(e_ref, R);
-            uint32_t fa[8], fb[8];
-            bool same = ok == ok_ref;
-            for (int c = 0; c < 3 && same; c++) {  // compare canonical coordinates of the record
-                fe_freeze(load_fe(e + 10 * c), fa);
+            bool same = ok[q] == ok_ref;
+            const rowf::V* co[3] = {&ypx, &ymx, &xy2d};
+            for (int c = 0; c < 3 && same; c++) {  // canonical values of the record's coordinates
+                uint32_t a[16], fa[8], fb[8];
+                limbs(*co[c], q, a);
+                fe_freeze(fe_from_limbs16(a), fa);
                 fe_freeze(load_fe(e_ref + 10 * c), fb);
                 same = std::memcmp(fa, fb, 32) == 0;
             }
