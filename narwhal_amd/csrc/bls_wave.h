@@ -292,6 +292,108 @@ __device__ __attribute__((noinline)) void wave_run(uint32_t* wm_generic, int lan
         s = wrap ? 0 : s + 1;
     }
 }
+// k items on one wave (the throughput path): item j's slots in bank j (the one-item layout: P << k
+// below its slot 0), banks `bank` words apart.  A stage of nl lanes per item runs 64 / nl items per
+// pass (lane l: item l / nl of the pass, record l % nl), ceil(k / (64 / nl)) passes, then one wave
+// sync.  So the narrow stages -- the final exponentiation's cyclotomic squarings (18 products, then
+// 12 combinations), which are most of a pairing check's stages -- run k items for the instructions
+// of one, and a wide one (an Fp12 product's 54) takes k passes as k waves would.  The pairing
+// kernel's time did not move with 4 instead of 10 resident waves per CU (LDS padded per wave, 37.5
+// ms for 16,384 items either way, profiles/round5_bls_occupancy.txt): one wave per SIMD already
+// keeps its VALU busy, so fewer instructions per item is what raises throughput.
+__device__ __attribute__((noinline)) void wave_run_k(uint32_t* wm0_generic, uint32_t bank, int k, int lane,
+                                                     uint32_t off, int n, int nl0, int reps) {
+    wword* wm0 = (wword*)wm0_generic;
+    const uint16_t* base0 = T_DATA + off;
+    const uint16_t* base = base0;
+    int nl = nl0;
+    Rec cur = load_rec(base0 + (uint32_t)(lane % nl0) * REC);
+    const int total = n * reps;
+#pragma unroll 1
+    for (int t = 0, s = 0; t < total; t++) {
+        Hdr h = rec_hdr(cur);
+        h.nap = __builtin_amdgcn_readfirstlane(h.nap);
+        h.nan = __builtin_amdgcn_readfirstlane(h.nan);
+        h.nbp = __builtin_amdgcn_readfirstlane(h.nbp);
+        h.nbn = __builtin_amdgcn_readfirstlane(h.nbn);
+        const bool wrap = s + 1 == n;
+        const int nl_next = wrap ? nl0 : __builtin_amdgcn_readfirstlane(h.nl_next);
+        const uint16_t* nbase = wrap ? base0 : base + (uint32_t)nl * REC;
+        Rec nxt = cur;
+        if (t + 1 < total) nxt = load_rec(nbase + (uint32_t)(lane % nl_next) * REC);
+        const int ipp = 64 / nl, first = lane / nl;
+        if (first < ipp) {
+            const uint32_t dst = rec_u16(cur, 0);
+#pragma unroll 1
+            for (int item = first; item < k; item += ipp) {
+                wword* wm = wm0 + (uint32_t)item * bank;
+                const fp v = lane_value(wm, h, cur);
+#pragma unroll
+                for (int j = 0; j < NL; j++) wm[SW * dst + j] = v.l[j];
+            }
+        }
+        wsync();
+        base = nbase;
+        nl = nl_next;
+        cur = nxt;
+        s = wrap ? 0 : s + 1;
+    }
+}
+// The Wave interface over k banks (final_exp, exp_chain and cyc_exp_x run on it unchanged)
+struct WaveK {
+    uint32_t* wm;   // bank 0's slot 0
+    uint32_t bank;  // words from one bank to the next
+    int k;          // items
+    int lane;
+    __device__ uint32_t* bk(int j) const { return wm + (uint32_t)j * bank; }
+    __device__ void sync() const { wsync(); }
+    __device__ void run(Prog p, int reps = 1) const { wave_run_k(wm, bank, k, lane, p.off, p.n, p.nl0, reps); }
+    __device__ void zero(int slot, int n) const {
+        for (int j = 0; j < k; j++)
+            for (int w = lane; w < SW * n; w += 64) bk(j)[SW * slot + w] = 0;
+    }
+    __device__ void copy_slots(int dst, int src, int n) const {
+        for (int j = 0; j < k; j++)
+            for (int w = lane; w < SW * n; w += 64) bk(j)[SW * dst + w] = bk(j)[SW * src + w];
+    }
+    // item j's words (global or LDS) into its bank
+    __device__ void put_words(int j, int slot, const uint32_t* src, int n) const {
+        for (int w = lane; w < SW * n; w += 64) bk(j)[SW * slot + w] = src[w];
+    }
+    // a value every lane holds, written to item j's bank (j < 0: every bank) by lane 0
+    __device__ void put_fp(int j, int slot, const fp& v) const {
+        if (lane != 0) return;
+        for (int b = j < 0 ? 0 : j; b < (j < 0 ? k : j + 1); b++)
+            for (int i = 0; i < NL; i++) bk(b)[SW * slot + i] = v.l[i];
+    }
+    __device__ fp get(int j, int slot) const {
+        fp v;
+        for (int i = 0; i < NL; i++) v.l[i] = bk(j)[SW * slot + i];
+        return v;
+    }
+    // each item's inverse, one wave-wide inversion after another
+    __device__ void invert_slot(int dst, int src) const {
+        for (int j = 0; j < k; j++) {
+            const fp x = get(j, src);
+            put_fp(j, dst, fp_inv_wave(x));
+        }
+    }
+    // bit j set when item j's 12 F slots are the Fp12 one (lanes 12 j .. 12 j + 11, k <= 5)
+    __device__ uint32_t f_is_one_mask() const {
+        const int j = lane / 12, c = lane % 12;
+        bool bad = false;
+        if (j < k) {
+            const fp v = get(j, REG_F + c);
+            bad = c == 0 ? !fp_eq(v, k_one()) : !fp_is_zero(v);
+        }
+        const uint64_t b = __ballot(bad);
+        uint32_t ok = 0;
+        for (int i = 0; i < k; i++)
+            if (((b >> (12 * i)) & 0xfffull) == 0) ok |= 1u << i;
+        return ok;
+    }
+};
+
 struct Wave {
     uint32_t* wm;
     int lane;
@@ -344,6 +446,10 @@ struct Wave {
         for (int j = 0; j < NL; j++) v.l[j] = wm[SW * slot + j];
         return v;
     }
+    // n slots copied within the wave's LDS
+    __device__ void copy_slots(int dst, int src, int n) const { put_words(dst, wm + SW * src, n); }
+    // slot dst <- slot src ^ -1 (every lane reads the value; the four update rows on four lanes)
+    __device__ void invert_slot(int dst, int src) const { put_fp(dst, inv(get(src))); }
     // every lane: the 12 F slots == the Fp12 one
     __device__ bool f_is_one() const {
         bool ok = true;
@@ -416,6 +522,8 @@ struct Wave {
         for (int j = 0; j < NL; j++) v.l[j] = wm[SW * slot + j];
         return v;
     }
+    void copy_slots(int dst, int src, int n) const { put_words(dst, wm + SW * src, n); }
+    void invert_slot(int dst, int src) const { put_fp(dst, inv(get(src))); }
     bool f_is_one() const {
         for (int k = 0; k < 12; k++) {
             const fp v = get(REG_F + k);
@@ -492,8 +600,7 @@ NWV_HD void g1_chain(const W& w, uint64_t k) {
 template <class W>
 NWV_HD void final_exp(const W& w) {
     w.run(P_INV_A);
-    const fp n = w.get(REG_N);
-    w.put_fp(REG_N + 1, w.inv(n));  // every lane holds the same norm
+    w.invert_slot(REG_N + 1, REG_N);  // the norm's inverse (every lane reads the norm)
     w.sync();
     w.run(P_INV_B);
     w.run(P_EASY1);
@@ -530,7 +637,7 @@ NWV_HD bool pairing_check(const W& w, const uint32_t* qlines) {
     w.zero(REG_F, 12);
     w.sync();
     w.put_fp(REG_F, k_one());
-    w.put_words(REG_TB, w.wm + SW * REG_QB, 6);
+    w.copy_slots(REG_TB, REG_QB, 6);
     w.sync();
     const char* steps = BLS_WAVE_STEPS_STR;
     constexpr int LW = 6 * SW;  // words of a step's line

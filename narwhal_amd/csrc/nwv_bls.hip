@@ -394,6 +394,104 @@ __device__ __forceinline__ void blsw_pair_item(uint32_t* wm, uint32_t i, const u
     }
     if (threadIdx.x == 0) st_pair[i] = s;
 }
+// The throughput form: up to BLS_PACK_MAX items per wave (wave::WaveK: each item's slots in its
+// own LDS bank, the narrow stages of every item in one pass).  e(-sig, g2) e(H, apk) == 1 for each
+// item as blsw_pair_item; an item whose signature or keys failed gets VERIFY_FAIL whatever its bank
+// computed.  Precomputed key lines are used only when every item of the wave has them (the Miller
+// loop's program is one for the wave).
+constexpr int BLS_PACK_MAX = 4;
+__global__ __launch_bounds__(64) void k_blsw_pair_k(uint32_t n, uint32_t kper, const uint32_t* srec,
+                                                    const int32_t* st_dec, const uint32_t* hrec, int h_hom,
+                                                    const uint32_t* arec, const int32_t* st_apk, KeyTab kt,
+                                                    const uint32_t* pk_off, const uint32_t* pk_cnt,
+                                                    const uint32_t* pk_idx, const uint32_t* kmode, int32_t* st_pair) {
+    using namespace wave;
+    extern __shared__ uint32_t lds_k[];
+    const int lane = (int)threadIdx.x;
+    const uint32_t i0 = blockIdx.x * kper;
+    if (i0 >= n) return;
+    const int k = (int)(n - i0 < kper ? n - i0 : kper);
+    const uint32_t bankw = (uint32_t)(KP_WORDS + SW * NSLOTS_PAIR);
+    const WaveK w{lds_k + KP_WORDS, bankw, k, lane};
+    const uint32_t* sig[BLS_PACK_MAX];
+    const uint32_t* hr[BLS_PACK_MAX];
+    const uint32_t* ql[BLS_PACK_MAX];
+    bool fixed = true;
+    for (int j = 0; j < k; j++) {
+        const uint32_t i = i0 + j;
+        sig[j] = srec + (size_t)G1_REC_WORDS * i;
+        hr[j] = hrec + (size_t)(h_hom ? G1H_REC_WORDS : G1_REC_WORDS) * i;
+        ql[j] = (kt.lines && kmode && kmode[i] && pk_cnt[i] == 1) ? kt.lines + KL_WORDS * pk_idx[pk_off[i]] : nullptr;
+        fixed = fixed && ql[j] != nullptr;
+    }
+    // every bank: slot 0, the constants, P << k below slot 0; then each item's points
+    for (int j = 0; j < k; j++) init_slots(Wave{w.bk(j), lane});
+    w.zero(REG_PA, 2);
+    w.zero(REG_PB, 3);
+    w.zero(REG_QB, 6);
+    w.sync();
+    for (int j = 0; j < k; j++) {
+        const uint32_t i = i0 + j;
+        if (!sig[j][2 * NL]) {
+            w.put_words(j, REG_PA, sig[j], 1);
+            w.put_fp(j, REG_PA + 1, fp_neg(ld_fp(sig[j] + NL)));
+        }
+        const bool h_inf = hr[j][(h_hom ? 3 : 2) * NL] != 0;
+        if (!h_inf) w.put_words(j, REG_PB, hr[j], h_hom ? 3 : 2);
+        if (h_inf || !h_hom) w.put_fp(j, REG_PB + 2, k_one());
+        w.put_words(j, REG_QB, arec + (size_t)G2J_WORDS * i, 6);
+    }
+    w.sync();
+    // wave::pairing_check over the k banks
+    w.zero(REG_F, 12);
+    w.sync();
+    w.put_fp(-1, REG_F, k_one());
+    w.copy_slots(REG_TB, REG_QB, 6);
+    w.sync();
+    const char* steps = BLS_WAVE_STEPS_STR;
+    constexpr int LW = 6 * SW;  // words of a step's line
+    // the next step's lines load while this step runs: g2's (every bank) and each item's key lines
+    uint32_t la0 = 0, la1 = 0, lb0[BLS_PACK_MAX], lb1[BLS_PACK_MAX];
+    auto fetch = [&](int st) {
+        const uint32_t* g = &T_G2_LINES[st][0][0];
+        la0 = lane < LW ? g[lane] : 0u;
+        la1 = lane + 64 < LW ? g[lane + 64] : 0u;
+        for (int j = 0; j < BLS_PACK_MAX; j++) {
+            lb0[j] = 0u;
+            lb1[j] = 0u;
+            if (j < k && fixed) {
+                const uint32_t* q = ql[j] + (size_t)st * LW;
+                lb0[j] = lane < LW ? q[lane] : 0u;
+                lb1[j] = lane + 64 < LW ? q[lane + 64] : 0u;
+            }
+        }
+    };
+    fetch(0);
+#pragma unroll 1
+    for (int st = 0; st < NSTEPS; st++) {
+        for (int j = 0; j < k; j++) {
+            uint32_t* b = w.bk(j);
+            if (lane < LW) b[SW * REG_LA + lane] = la0;
+            if (lane + 64 < LW) b[SW * REG_LA + lane + 64] = la1;
+            if (fixed) {
+                if (lane < LW) b[SW * REG_LB + lane] = lb0[j];
+                if (lane + 64 < LW) b[SW * REG_LB + lane + 64] = lb1[j];
+            }
+        }
+        w.sync();
+        if (st + 1 < NSTEPS) fetch(st + 1);
+        const Prog pd = fixed ? P_ML_DBL_FIXED : P_ML_DBL_STEP, pa = fixed ? P_ML_ADD_FIXED : P_ML_ADD_STEP;
+        w.run(steps[st] == 'a' ? pa : pd);
+    }
+    w.run(P_CONJ_F);
+    final_exp(w);
+    const uint32_t ok = w.f_is_one_mask();
+    if (lane == 0)
+        for (int j = 0; j < k; j++) {
+            const uint32_t i = i0 + j;
+            st_pair[i] = (st_dec[i] == ST_OK && st_apk[i] == ST_OK && ((ok >> j) & 1u)) ? ST_OK : ST_VERIFY_FAIL;
+        }
+}
 __global__ __launch_bounds__(64) void k_blsw_pair(uint32_t n, const uint32_t* srec, const int32_t* st_dec,
                                                   const uint32_t* hrec, int h_hom, const uint32_t* arec,
                                                   const int32_t* st_apk, KeyTab kt, const uint32_t* pk_off,
@@ -1271,10 +1369,30 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
         BLS_HIP(hipStreamWaitEvent(s0, L.ev[10], 0));
         BLS_HIP(hipStreamWaitEvent(s0, L.ev[11], 0));
         BLS_HIP(hipEventRecord(L.ev[7], s0));
-        hipLaunchKernelGGL(k_blsw_pair, dim3((unsigned)n), dim3(64), 0, s0, (uint32_t)n, (const uint32_t*)srec,
-                           (const int32_t*)sdec, (const uint32_t*)hrec, 0, (const uint32_t*)ajrec, (const int32_t*)sapk,
-                           kt, reinterpret_cast<const uint32_t*>(in + o_off), reinterpret_cast<const uint32_t*>(in + o_cnt),
-                           reinterpret_cast<const uint32_t*>(in + o_idx), km, spair);
+        // items per pairing wave (env NWV_BLS_PACK, 1..4): one LDS bank of ~15 KB each
+        static const uint32_t pack = [] {
+            const char* e = std::getenv("NWV_BLS_PACK");
+            const long v = e ? std::strtol(e, nullptr, 10) : 2;
+            return (uint32_t)(v < 1 ? 1 : v > BLS_PACK_MAX ? BLS_PACK_MAX : v);
+        }();
+        // diagnostic (occupancy experiments): NWV_BLS_LDS_PAD bytes of extra LDS per pairing wave
+        static const size_t lds_pad = [] {
+            const char* e = std::getenv("NWV_BLS_LDS_PAD");
+            return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)0;
+        }();
+        if (pack > 1)
+            hipLaunchKernelGGL(k_blsw_pair_k, dim3((unsigned)((n + pack - 1) / pack)), dim3(64),
+                               (size_t)4 * pack * (wave::KP_WORDS + wave::SW * wave::NSLOTS_PAIR) + lds_pad, s0,
+                               (uint32_t)n, pack, (const uint32_t*)srec, (const int32_t*)sdec, (const uint32_t*)hrec, 0,
+                               (const uint32_t*)ajrec, (const int32_t*)sapk, kt,
+                               reinterpret_cast<const uint32_t*>(in + o_off), reinterpret_cast<const uint32_t*>(in + o_cnt),
+                               reinterpret_cast<const uint32_t*>(in + o_idx), km, spair);
+        else
+            hipLaunchKernelGGL(k_blsw_pair, dim3((unsigned)n), dim3(64), lds_pad, s0, (uint32_t)n, (const uint32_t*)srec,
+                               (const int32_t*)sdec, (const uint32_t*)hrec, 0, (const uint32_t*)ajrec,
+                               (const int32_t*)sapk, kt, reinterpret_cast<const uint32_t*>(in + o_off),
+                               reinterpret_cast<const uint32_t*>(in + o_cnt), reinterpret_cast<const uint32_t*>(in + o_idx),
+                               km, spair);
         BLS_HIP(hipEventRecord(L.ev[8], s0));
         hipLaunchKernelGGL(k_blsw_status, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n,
                            (const int32_t*)sdec, (const int32_t*)ssub, (const int32_t*)sapk, (const int32_t*)spair, st,

@@ -428,3 +428,20 @@ def test_verify_many_sharded_over_devices():
     assert out["shards"] == 3 and out["items"] > 48 and out["want_nonzero"] >= 7
     assert out["registered_on_shard0"] == 100
     assert out["cached_equal"] and out["uncached_equal"], out
+
+
+@pytest.mark.parametrize("pack", ["1", "2", "3", "4"])
+def test_verify_many_packed_waves(pack):
+    """the throughput path's pairing kernel with `pack` items per wave (k_blsw_pair_k, one LDS bank
+    per item; NWV_BLS_WAVE_MAX=0 sends every call there): the 100-key committee round with every
+    adversarial category, with and without the key cache (precomputed vs computed key lines), equal
+    to the oracle -- including a last wave holding fewer items"""
+    import subprocess
+    import sys
+    env = dict(os.environ, NWV_BLS_WAVE_MAX="0", NWV_BLS_PACK=pack, NWV_BLS_DEVICE_REPLICAS="1")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "bls_shard_gpu_check.py")], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["items"] % 3 != 0 and out["want_nonzero"] >= 7
+    assert out["cached_equal"] and out["uncached_equal"], out
