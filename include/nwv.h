@@ -78,6 +78,11 @@ typedef struct nwv_ctx nwv_ctx;
  * default 8192) run each point's decompression power on a 16-lane row (k_msm_prep's row form,
  * latency-bound batches); this flag keeps every batch on the lane-local decompression */
 #define NWV_FLAG_NO_ROW_PREP 512u
+/* diagnostic / tests: large host-staged batches (>= 16 MB of pk, sig and messages) start the
+ * batch MSM's decompressions -- and, when verdict bits are wanted, the per-signature fallback's
+ * tables -- on a second stream once pk and sig are on the device, under the messages' transfer;
+ * this flag keeps the one-stream order (every kernel after the whole copy) */
+#define NWV_FLAG_NO_EARLY_PREP 1024u
 
 /* ------------------------------------------------------------------ lifecycle ----- */
 /* Process-wide context creation (created once, in Primary::spawn).

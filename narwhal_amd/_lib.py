@@ -32,6 +32,8 @@ NWV_FLAG_NO_MSM_REUSE = 32
 NWV_FLAG_BLS_PER_ITEM = 64
 NWV_FLAG_BLS_BATCH = 128
 NWV_FLAG_NO_SIGCACHE = 256
+NWV_FLAG_NO_ROW_PREP = 512
+NWV_FLAG_NO_EARLY_PREP = 1024
 NWV_RUN_TIMED = 0x100
 
 

@@ -61,10 +61,13 @@ typedef uint64_t wword2;
 // the wave's LDS: P << k (k < 16, the combinations' offsets) just BELOW slot 0, then the slots:
 // a kernel allocates KP_WORDS + SW x (its programs' slots) words and works from wm = base +
 // KP_WORDS, so kernels that run only the pairing and G1-check programs (NSLOTS_PAIR slots) take
-// less LDS -- more resident waves -- than those that also run the hash's isogeny map (NSLOTS)
+// less LDS -- more resident waves -- than those that also run the hash's isogeny map (NSLOTS),
+// and the packed pairing kernel's banks hold only the pairing check's run of NSLOTS_PC slots
+// (tools/gen_bls_wave.py lays its constants, registers and temporaries out first)
 constexpr int KP_WORDS = 16 * NL;
 constexpr int WM_WORDS = KP_WORDS + SW * NSLOTS;
 constexpr int WM_WORDS_PAIR = KP_WORDS + SW * NSLOTS_PAIR;
+constexpr int WM_WORDS_PC = KP_WORDS + SW * NSLOTS_PC;
 
 // A lane's record in registers: REC u16 words (five 16-byte loads).  [0] destination slot, [1]
 // flags (1 product, 2 reduce, 4 A signed, 8 B signed), [2] k+1 of A's 2^k p (0 none), [3] k+1 of
@@ -534,19 +537,24 @@ struct Wave {
 };
 #endif
 
-// slot 0 = 0, then the constant table; P << k past the slots
+// slot 0 = 0, the pairing check's constants at slots 1.., the others at CONST2_SLOT..; P << k
+// below slot 0
 template <class W>
 NWV_HD void init_slots(const W& w) {
     w.zero(0, 1);
-    w.put_words(1, &T_CONSTS[0][0], NCONSTS);
+    w.put_words(1, &T_CONSTS[0][0], NCONSTS_PC);
+    w.put_words(CONST2_SLOT, &T_CONSTS[NCONSTS_PC][0], NCONSTS - NCONSTS_PC);
     w.put_words(-16, &T_KP[0][0], 16);  // below slot 0
     w.sync();
 }
 #ifdef BLS_WAVE_DEV
 // the device form: every lane fetches all its words of both tables before storing any (one memory
-// round trip; put_words' loop waits for each 64-word load in turn)
-__device__ __forceinline__ void init_slots(const Wave& w) {
-    constexpr int NC = SW * NCONSTS, NK = 16 * SW, NT = (NC + NK + 63) / 64;
+// round trip; put_words' loop waits for each 64-word load in turn).  PC_ONLY: a bank of
+// NSLOTS_PC slots (the packed pairing kernel), which the other constants lie beyond.
+template <bool PC_ONLY>
+__device__ __forceinline__ void init_slots_t(const Wave& w) {
+    constexpr int NC = SW * (PC_ONLY ? NCONSTS_PC : NCONSTS), NC1 = SW * NCONSTS_PC, NK = 16 * SW;
+    constexpr int NT = (NC + NK + 63) / 64;
     const uint32_t* c = &T_CONSTS[0][0];
     const uint32_t* k = &T_KP[0][0];
     uint32_t v[NT];
@@ -559,11 +567,14 @@ __device__ __forceinline__ void init_slots(const Wave& w) {
 #pragma unroll
     for (int t = 0; t < NT; t++) {
         const int i = w.lane + 64 * t;
-        if (i < NC) w.wm[SW + i] = v[t];
+        if (i < NC1) w.wm[SW + i] = v[t];
+        else if (i < NC) w.wm[SW * CONST2_SLOT + (i - NC1)] = v[t];
         else if (i < NC + NK) w.wm[(i - NC) - KP_WORDS] = v[t];
     }
     w.sync();
 }
+__device__ __forceinline__ void init_slots(const Wave& w) { init_slots_t<false>(w); }
+__device__ __forceinline__ void init_slots_pc(const Wave& w) { init_slots_t<true>(w); }
 #endif
 
 // the square-and-multiply chain of a 64-bit k (top bit 63) below its top bit: each run of

@@ -88,7 +88,10 @@ template <bool PF>
 __device__ __forceinline__ void ed_straus_body(uint64_t n, const uint8_t* __restrict__ sig,
                                                const uint8_t* __restrict__ kbuf, const uint32_t* __restrict__ tables,
                                                const uint32_t* __restrict__ flags, const uint32_t* __restrict__ btab,
-                                               uint64_t* __restrict__ verdict) {
+                                               uint64_t* __restrict__ verdict, const uint32_t* __restrict__ gate) {
+    // gate: a batch MSM's state words queued just before this pass; it accepted (word 1 == 1) ->
+    // every signature is valid and the host reads no verdict bits (nothing to do)
+    if (gate && gate[1] == 1u) return;
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63;
     bool ok = false;
@@ -105,8 +108,8 @@ __device__ __forceinline__ void ed_straus_body(uint64_t n, const uint8_t* __rest
 extern "C" __global__ void __launch_bounds__(256) k_ed_straus(
     uint64_t n, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ kbuf,
     const uint32_t* __restrict__ tables, const uint32_t* __restrict__ flags,
-    const uint32_t* __restrict__ btab, uint64_t* __restrict__ verdict) {
-    ed_straus_body<false>(n, sig, kbuf, tables, flags, btab, verdict);
+    const uint32_t* __restrict__ btab, uint64_t* __restrict__ verdict, const uint32_t* __restrict__ gate) {
+    ed_straus_body<false>(n, sig, kbuf, tables, flags, btab, verdict, gate);
 }
 // the same with each window's A / R table entries loaded one window ahead (more registers, fewer
 // waves per SIMD): the default (C4 2.34 -> 2.29 ms, tools/gpurun/r4_c4_pf.sh); NWV_STRAUS_PF=0
@@ -114,8 +117,8 @@ extern "C" __global__ void __launch_bounds__(256) k_ed_straus(
 extern "C" __global__ void __launch_bounds__(256) k_ed_straus_pf(
     uint64_t n, const uint8_t* __restrict__ sig, const uint8_t* __restrict__ kbuf,
     const uint32_t* __restrict__ tables, const uint32_t* __restrict__ flags,
-    const uint32_t* __restrict__ btab, uint64_t* __restrict__ verdict) {
-    ed_straus_body<true>(n, sig, kbuf, tables, flags, btab, verdict);
+    const uint32_t* __restrict__ btab, uint64_t* __restrict__ verdict, const uint32_t* __restrict__ gate) {
+    ed_straus_body<true>(n, sig, kbuf, tables, flags, btab, verdict, gate);
 }
 
 // RFC 8032: a = clamp(SHA-512(seed)[0..32]), prefix = [32..64], A = [a]B,

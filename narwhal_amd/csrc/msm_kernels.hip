@@ -92,6 +92,9 @@ struct MsmScalarArgs {
     // (k_ed_hash's outputs, so a rejected batch's exact-bad-set pass skips the hashing), or null
     uint32_t* kout;
     uint32_t* fout;
+    // 1: OR the flag into fout (zeroed at staging; the early form's k_ed_points_msm ORs its decode
+    // flags into the same words concurrently), 0: store it
+    uint32_t fout_or;
 };
 struct MsmPointArgs {
     uint64_t n, na;
@@ -125,7 +128,8 @@ __device__ __forceinline__ void msm_scalars_block(uint32_t blk, const MsmScalarA
         if (f != FLAG_S_OK) atomicOr(fail, 1u);
         if (g.kout) {
             msm_store8(g.kout + 8 * i, k);
-            g.fout[i] = f;
+            if (g.fout_or) atomicOr(g.fout + i, f);
+            else g.fout[i] = f;
         }
         uint32_t sd[8];
 #pragma unroll

@@ -411,7 +411,7 @@ __global__ __launch_bounds__(64) void k_blsw_pair_k(uint32_t n, uint32_t kper, c
     const uint32_t i0 = blockIdx.x * kper;
     if (i0 >= n) return;
     const int k = (int)(n - i0 < kper ? n - i0 : kper);
-    const uint32_t bankw = (uint32_t)(KP_WORDS + SW * NSLOTS_PAIR);
+    const uint32_t bankw = (uint32_t)WM_WORDS_PC;
     const WaveK w{lds_k + KP_WORDS, bankw, k, lane};
     const uint32_t* sig[BLS_PACK_MAX];
     const uint32_t* hr[BLS_PACK_MAX];
@@ -424,8 +424,8 @@ __global__ __launch_bounds__(64) void k_blsw_pair_k(uint32_t n, uint32_t kper, c
         ql[j] = (kt.lines && kmode && kmode[i] && pk_cnt[i] == 1) ? kt.lines + KL_WORDS * pk_idx[pk_off[i]] : nullptr;
         fixed = fixed && ql[j] != nullptr;
     }
-    // every bank: slot 0, the constants, P << k below slot 0; then each item's points
-    for (int j = 0; j < k; j++) init_slots(Wave{w.bk(j), lane});
+    // every bank: slot 0, the pairing check's constants, P << k below slot 0; then each item's points
+    for (int j = 0; j < k; j++) init_slots_pc(Wave{w.bk(j), lane});
     w.zero(REG_PA, 2);
     w.zero(REG_PB, 3);
     w.zero(REG_QB, 6);
@@ -1369,7 +1369,7 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
         BLS_HIP(hipStreamWaitEvent(s0, L.ev[10], 0));
         BLS_HIP(hipStreamWaitEvent(s0, L.ev[11], 0));
         BLS_HIP(hipEventRecord(L.ev[7], s0));
-        // items per pairing wave (env NWV_BLS_PACK, 1..4): one LDS bank of ~15 KB each
+        // items per pairing wave (env NWV_BLS_PACK, 1..4): one LDS bank of ~10.5 KB each
         static const uint32_t pack = [] {
             const char* e = std::getenv("NWV_BLS_PACK");
             const long v = e ? std::strtol(e, nullptr, 10) : 2;
@@ -1382,7 +1382,7 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
         }();
         if (pack > 1)
             hipLaunchKernelGGL(k_blsw_pair_k, dim3((unsigned)((n + pack - 1) / pack)), dim3(64),
-                               (size_t)4 * pack * (wave::KP_WORDS + wave::SW * wave::NSLOTS_PAIR) + lds_pad, s0,
+                               (size_t)4 * pack * wave::WM_WORDS_PC + lds_pad, s0,
                                (uint32_t)n, pack, (const uint32_t*)srec, (const int32_t*)sdec, (const uint32_t*)hrec, 0,
                                (const uint32_t*)ajrec, (const int32_t*)sapk, kt,
                                reinterpret_cast<const uint32_t*>(in + o_off), reinterpret_cast<const uint32_t*>(in + o_cnt),

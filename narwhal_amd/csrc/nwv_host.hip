@@ -136,6 +136,8 @@ struct EdBuffers {
     DevBuf in;  // staging arena: pk, sig, off, len, m_state and msg are views into it
     size_t nkeys_distinct = 0;  // 0: every signature is its own A point
     bool kc_split = false;      // keyed batch whose keys are all in the device's key cache
+    // the last batch MSM already built the per-signature fallback's tables (early form, msm_launch)
+    bool tables_ready = false;
     void release() {
         for (DevBuf* b : {&pk, &sig, &msg, &off, &len, &kbuf, &flags, &tables, &verdict, &m_scal,
                           &m_partial, &m_state, &m_pts, &m_digits, &m_cnt, &m_tiles, &m_entries,
@@ -144,6 +146,7 @@ struct EdBuffers {
             b->release();
         nkeys_distinct = 0;
         kc_split = false;
+        tables_ready = false;
     }
 };
 
@@ -167,6 +170,12 @@ struct Lane {
     PinnedBuf b2stage;             // host side of that arena's single H2D copy
     PinnedBuf b2dig;               // digests of a digest-then-verify call, copied back early
     hipEvent_t b2stage_ev = nullptr;
+    // large stagings (ed_stage's piped form): pksig_ev fires once pk, sig, the offsets and the MSM
+    // state words are on the device, while the messages are still crossing PCIe; the batch MSM's
+    // decompressions then start on `aux` (msm_launch's early form), aux_ev joins them back
+    hipStream_t aux = nullptr;
+    hipEvent_t pksig_ev = nullptr, aux_ev = nullptr;
+    bool pksig_pending = false;
 };
 
 // Committee key cache of a device.  fastcrypto decompresses a public key once, when it is
@@ -237,6 +246,13 @@ void lane_close(Lane& d) {
     d.hstage_ev = nullptr;
     if (d.b2stage_ev) (void)hipEventDestroy(d.b2stage_ev);
     d.b2stage_ev = nullptr;
+    if (d.aux) (void)hipStreamSynchronize(d.aux);
+    for (hipEvent_t* e : {&d.pksig_ev, &d.aux_ev}) {
+        if (*e) (void)hipEventDestroy(*e);
+        *e = nullptr;
+    }
+    if (d.aux) (void)hipStreamDestroy(d.aux);
+    d.aux = nullptr;
     d.b2stage.release();
     d.b2dig.release();
     for (DevBuf* b : {&d.b2_base, &d.b2_off, &d.b2_len, &d.b2_out, &d.b2_packed, &d.b2_plen, &d.b2_err, &d.b2_in})
@@ -257,6 +273,9 @@ int lane_open(Gpu& g, Lane** out) {
     hipError_t e = hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&d->hstage_ev, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&d->b2stage_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&d->aux, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&d->pksig_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&d->aux_ev, hipEventDisableTiming);
     // both events start out complete, so the first wait on them returns at once
     if (e == hipSuccess) e = hipEventRecord(d->hstage_ev, d->stream);
     if (e == hipSuccess) e = hipEventRecord(d->b2stage_ev, d->stream);
@@ -379,20 +398,23 @@ int ed_scratch(EdBuffers& b, size_t n) {
 
 // msm_pts: the point records of a batch MSM that just ran on these buffers over per-signature
 // keys (na = n A points): k_ed_points_msm reuses its decompressions.
+// tables_ready: the batch MSM's early form already built the tables (and k, the flags): only the
+// Straus pass runs, returning at once when the MSM's state words (gate) say it accepted.
 int ed_launch(Lane& d, EdBuffers& b, size_t n, hipStream_t stream, hipEvent_t* ev,
-              const uint32_t* msm_pts = nullptr) {
+              const uint32_t* msm_pts = nullptr, bool tables_ready = false, const uint32_t* gate = nullptr) {
     if (n == 0) return NWV_OK;
     int rc = ed_scratch(b, n);
     if (rc) return rc;
     const size_t waves = (n + 63) / 64;
     const dim3 blk(256), grid((unsigned)((n + 255) / 256)), grid2((unsigned)((2 * 64 * waves + 255) / 256));
     if (ev) NWV_HIP(hipEventRecord(ev[0], stream));
-    if (!msm_pts)  // (after a batch MSM over per-signature keys, k_msm_prep left k and the flags)
+    if (!msm_pts && !tables_ready)  // (after a batch MSM over per-signature keys, k_msm_prep left k and the flags)
         hipLaunchKernelGGL(k_ed_hash, grid, blk, 0, stream, (uint64_t)n, b.pk.as<uint8_t>(),
                            b.sig.as<uint8_t>(), b.msg.as<uint8_t>(), b.off.as<uint64_t>(),
                            b.len.as<uint32_t>(), b.kbuf.as<uint8_t>(), b.flags.as<uint32_t>());
     if (ev) NWV_HIP(hipEventRecord(ev[1], stream));
-    if (msm_pts)
+    if (tables_ready) {
+    } else if (msm_pts)
         hipLaunchKernelGGL(k_ed_points_msm, grid2, blk, 0, stream, (uint64_t)n, (uint64_t)n, msm_pts,
                            b.tables.as<uint32_t>(), b.flags.as<uint32_t>());
     else
@@ -405,7 +427,7 @@ int ed_launch(Lane& d, EdBuffers& b, size_t n, hipStream_t stream, hipEvent_t* e
     }();
     hipLaunchKernelGGL(straus_pf ? k_ed_straus_pf : k_ed_straus, grid, blk, 0, stream, (uint64_t)n, b.sig.as<uint8_t>(),
                        b.kbuf.as<uint8_t>(), b.tables.as<uint32_t>(), b.flags.as<uint32_t>(),
-                       d.btab().as<uint32_t>(), b.verdict.as<uint64_t>());
+                       d.btab().as<uint32_t>(), b.verdict.as<uint64_t>(), gate);
     if (ev) NWV_HIP(hipEventRecord(ev[3], stream));
     NWV_HIP(hipGetLastError());
     return NWV_OK;
@@ -550,8 +572,17 @@ constexpr int MSM_NEVENTS = MSM_NKERNELS + 1;  // one event before each kernel, 
 
 // Launch the batch MSM on resident buffers; the verdict word (1 = batch accepted) is
 // m_state[1] (m_state[0] = failure flags).  ev: MSM_NEVENTS events or null.
+// Early form (a piped staging left pksig_pending: pk and sig landed before the messages): the
+// decompressions (k_msm_points) start on the lane's aux stream as soon as pk and sig are on the
+// device, under the messages' PCIe transfer, and -- spec_tables, the caller wants verdict bits --
+// so does the per-signature fallback's table build from their records (k_ed_points_msm, ~0.13 ms
+// at 65,536 that a rejected batch no longer waits for); the hash role (k_msm_scalars) runs when
+// the messages are in, and the sort waits for both.
 int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStream_t stream,
-               hipEvent_t* ev, bool state_ready) {
+               hipEvent_t* ev, bool state_ready, bool spec_tables = false) {
+    const bool pksig = d.pksig_pending;
+    d.pksig_pending = false;
+    b.tables_ready = false;
     if (n == 0) return NWV_OK;
     const size_t na = msm_na(b, n);
     const MsmPlan p = msm_plan(n, na, b.kc_split, (d.flags & NWV_FLAG_MSM_SORT2) ? 1 : 0);
@@ -571,11 +602,14 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     // per-signature keys: the hash role also leaves k_i and the s < l flag for the fallback
     const bool reuse = !keyed && !(d.flags & NWV_FLAG_NO_MSM_REUSE);
     if (reuse && ((rc = b.kbuf.ensure(32 * n + 16)) || (rc = b.flags.ensure(4 * n + 4)))) return rc;
+    const bool early = pksig && reuse && !b.kc_split && stream == d.stream && !ev && state_ready &&
+                       !(d.flags & NWV_FLAG_NO_EARLY_PREP);
+    if (early && spec_tables && (rc = ed_scratch(b, n))) return rc;
     const MsmScalarArgs gs{(uint64_t)n, (uint64_t)na, keyed, b.pk.as<uint8_t>(), b.sig.as<uint8_t>(),
                            b.msg.as<uint8_t>(), b.off.as<uint64_t>(), b.len.as<uint32_t>(), state + 8,
                            b.m_ascal.as<uint32_t>(), digits, b.m_partial.as<uint32_t>(), state,
                            b.kc_split ? 1u : 0u, b.m_ctr.as<uint32_t>(), reuse ? b.kbuf.as<uint32_t>() : nullptr,
-                           reuse ? b.flags.as<uint32_t>() : nullptr};
+                           reuse ? b.flags.as<uint32_t>() : nullptr, early ? 1u : 0u};
     // decompression on 16-lane rows when the batch is small enough to be latency-bound
     static const uint64_t row_prep_max = [] {
         const char* e = std::getenv("NWV_MSM_ROW_PREP_MAX");
@@ -591,11 +625,24 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     const size_t waves = (n + 63) / 64 + (na + 63) / 64;
     const unsigned sblk = (unsigned)((n + pthr - 1) / pthr);  // hash workgroups (k_msm_tail's partials)
     const unsigned pblk = rows ? (unsigned)((n + ndec + 3) / 4) : (unsigned)((64 * waves + 255) / 256);
-    const bool fused = !(d.flags & NWV_FLAG_MSM_SPLIT_PREP);
-    if (fused)
-        hipLaunchKernelGGL(k_msm_prep, dim3(sblk + pblk), dim3(pthr), 0, stream, gs, p.lay, gp, sblk);
-    else
+    const bool fused = !(d.flags & NWV_FLAG_MSM_SPLIT_PREP) && !early;
+    if (early) {
+        NWV_HIP(hipStreamWaitEvent(d.aux, d.pksig_ev, 0));
+        hipLaunchKernelGGL(k_msm_points, dim3(pblk), dim3(pthr), 0, d.aux, gp);
+        if (spec_tables) {
+            const size_t waves2 = 2 * 64 * ((n + 63) / 64);
+            hipLaunchKernelGGL(k_ed_points_msm, dim3((unsigned)((waves2 + 255) / 256)), dim3(256), 0, d.aux, (uint64_t)n,
+                               (uint64_t)n, b.m_pts.as<uint32_t>(), b.tables.as<uint32_t>(), b.flags.as<uint32_t>());
+            b.tables_ready = true;
+        }
+        NWV_HIP(hipEventRecord(d.aux_ev, d.aux));
         hipLaunchKernelGGL(k_msm_scalars, dim3(sblk), dim3(pthr), 0, stream, gs, p.lay);
+        NWV_HIP(hipStreamWaitEvent(stream, d.aux_ev, 0));
+    } else if (fused) {
+        hipLaunchKernelGGL(k_msm_prep, dim3(sblk + pblk), dim3(pthr), 0, stream, gs, p.lay, gp, sblk);
+    } else {
+        hipLaunchKernelGGL(k_msm_scalars, dim3(sblk), dim3(pthr), 0, stream, gs, p.lay);
+    }
     const uint32_t* kc = b.kc_split ? d.gpu->kc.recs.as<uint32_t>() : nullptr;
     if (keyed)
         hipLaunchKernelGGL(k_msm_keysum, dim3((unsigned)b.nkeys_distinct), dim3(256), 0, stream, (uint64_t)n,
@@ -604,7 +651,7 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
                            state);
     if ((rc = mark(1))) return rc;
     if ((rc = mark(2))) return rc;
-    if (!fused) hipLaunchKernelGGL(k_msm_points, dim3(pblk), dim3(pthr), 0, stream, gp);
+    if (!fused && !early) hipLaunchKernelGGL(k_msm_points, dim3(pblk), dim3(pthr), 0, stream, gp);
     if ((rc = mark(3))) return rc;
     const size_t lds_nb = (size_t)4 << (p.lay.cmax - 1);
     uint32_t* kst = b.m_kstart.as<uint32_t>();
@@ -873,6 +920,8 @@ int ed_stage(Lane& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, con
     NWV_HIP(hipEventSynchronize(d.hstage_ev));
     if ((rc = d.hstage.ensure(total))) return rc;
     uint8_t* h = static_cast<uint8_t*>(d.hstage.p);
+    d.pksig_pending = false;
+    b.tables_ready = false;
     // large stagings: the caller's pk / sig / message bytes are packed piece by piece with each
     // piece's DMA queued at once (pack_copy_h2d); the small computed regions go first
     const bool piped = 96 * (inputs ? n : 0) + mbytes >= ((size_t)16 << 20);
@@ -899,13 +948,20 @@ int ed_stage(Lane& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, con
         // packed, then the padding and keyed tables behind them
         uint8_t* gdev = b.in.as<uint8_t>();
         NWV_HIP(hipMemcpyAsync(gdev + o_off, h + o_off, o_msg - o_off, hipMemcpyHostToDevice, d.stream));
-        std::vector<PackSeg> segs;
-        if (inputs) {
-            segs.push_back(PackSeg{o_pk, pk + 32 * lo, 32 * n});
-            segs.push_back(PackSeg{o_sig, sig + 64 * lo, 64 * n});
+        // pk and sig (and the fallback's zeroed flag words) ahead of the messages: pksig_ev lets the
+        // batch MSM decompress while the messages are still in flight
+        int prc = NWV_OK;
+        if (inputs && !kt) {
+            if ((rc = b.flags.ensure(4 * n + 4))) return rc;
+            NWV_HIP(hipMemsetAsync(b.flags.p, 0, 4 * n + 4, d.stream));
+            prc = pack_copy_h2d(d.ordinal, gdev, h, {PackSeg{o_pk, pk + 32 * lo, 32 * n}, PackSeg{o_sig, sig + 64 * lo, 64 * n}},
+                                d.stream);
+            if (!prc && hipEventRecord(d.pksig_ev, d.stream) == hipSuccess) d.pksig_pending = true;
+        } else if (inputs) {
+            prc = pack_copy_h2d(d.ordinal, gdev, h, {PackSeg{o_pk, pk + 32 * lo, 32 * n}, PackSeg{o_sig, sig + 64 * lo, 64 * n}},
+                                d.stream);
         }
-        if (mbytes) segs.push_back(PackSeg{o_msg, msg_base + mlo, mbytes});
-        int prc = pack_copy_h2d(d.ordinal, gdev, h, segs, d.stream);
+        if (!prc && mbytes) prc = pack_copy_h2d(d.ordinal, gdev, h, {PackSeg{o_msg, msg_base + mlo, mbytes}}, d.stream);
         if (prc) {
             // copies already queued may still read the pinned buffer: the next staging waits
             (void)hipEventRecord(d.hstage_ev, d.stream);
@@ -1330,8 +1386,26 @@ static int batch_on_device(Lane& d, EdBuffers& b, size_t n, const uint8_t seed[3
                          (!(d.flags & NWV_FLAG_MSM_NEVER) && n >= msm_min_n());
     if (use_msm) {
         htrace("batch:msm-launch");
-        if ((rc = msm_launch(d, b, n, seed, stream, nullptr, state_ready))) return rc;
+        if ((rc = msm_launch(d, b, n, seed, stream, nullptr, state_ready, bits != nullptr))) return rc;
         htrace("batch:msm-launched");
+        if (bits && b.tables_ready) {
+            // the early form built the fallback's tables: its Straus pass queues behind the MSM now
+            // (gated on the MSM's verdict word) and one read-back brings both
+            if ((rc = ed_launch(d, b, n, stream, nullptr, nullptr, true, b.m_state.as<uint32_t>()))) return rc;
+            uint32_t st[2] = {0, 0};
+            NWV_HIP(hipMemcpyAsync(st, b.m_state.p, 8, hipMemcpyDeviceToHost, stream));
+            NWV_HIP(hipMemcpyAsync(bits, b.verdict.p, 8 * ((n + 63) / 64), hipMemcpyDeviceToHost, stream));
+            NWV_HIP(hipStreamSynchronize(stream));
+            htrace("batch:gated-done");
+            if (st[1] == 1) {
+                std::memset(bits, 0, 8 * ((n + 63) / 64));
+                set_ones(bits, 0, n);
+                *ok = 1;
+            } else {
+                *ok = verdicts_all_valid(bits, n) ? 1 : 0;
+            }
+            return NWV_OK;
+        }
         uint32_t st[2] = {0, 0};
         NWV_HIP(hipMemcpyAsync(st, b.m_state.p, 8, hipMemcpyDeviceToHost, stream));
         NWV_HIP(hipStreamSynchronize(stream));
@@ -1362,6 +1436,7 @@ static int batch_on_device(Lane& d, EdBuffers& b, size_t n, const uint8_t seed[3
     }
     NWV_HIP(hipMemcpyAsync(out, b.verdict.p, 8 * ((n + 63) / 64), hipMemcpyDeviceToHost, stream));
     NWV_HIP(hipStreamSynchronize(stream));
+    htrace("batch:fallback-done");
     *ok = verdicts_all_valid(out, n) ? 1 : 0;
     return NWV_OK;
 }

@@ -591,6 +591,40 @@ extern "C" {
         c: *const NwvCertificate,
         result: *mut i32,
     ) -> c_int;
+    // the same service over a BLS12-381 committee (nwv_bls_verify_mixed_many per flush)
+    pub fn nwv_service_create_bls(
+        ctx: *mut NwvCtx,
+        committee: *const NwvBlsCommittee,
+        max_batch: usize,
+        max_wait_us: u32,
+        out: *mut *mut NwvService,
+    ) -> c_int;
+    pub fn nwv_service_set_committee_bls(svc: *mut NwvService, committee: *const NwvBlsCommittee) -> c_int;
+    pub fn nwv_service_submit_bls_header(
+        svc: *mut NwvService,
+        h: *const NwvBlsHeader,
+        done: NwvDoneFn,
+        user: *mut c_void,
+    ) -> c_int;
+    pub fn nwv_service_submit_bls_vote(
+        svc: *mut NwvService,
+        v: *const NwvBlsVote,
+        done: NwvDoneFn,
+        user: *mut c_void,
+    ) -> c_int;
+    pub fn nwv_service_submit_bls_certificate(
+        svc: *mut NwvService,
+        c: *const NwvBlsCertificate,
+        done: NwvDoneFn,
+        user: *mut c_void,
+    ) -> c_int;
+    pub fn nwv_service_verify_bls_header(svc: *mut NwvService, h: *const NwvBlsHeader, result: *mut i32) -> c_int;
+    pub fn nwv_service_verify_bls_vote(svc: *mut NwvService, v: *const NwvBlsVote, result: *mut i32) -> c_int;
+    pub fn nwv_service_verify_bls_certificate(
+        svc: *mut NwvService,
+        c: *const NwvBlsCertificate,
+        result: *mut i32,
+    ) -> c_int;
     pub fn nwv_service_flush(svc: *mut NwvService) -> c_int;
     pub fn nwv_service_stats(svc: *mut NwvService, out: *mut u64) -> c_int;
     pub fn nwv_service_free(svc: *mut NwvService);

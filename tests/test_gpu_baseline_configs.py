@@ -220,3 +220,37 @@ def test_c4_adversarial_65536_every_category(eng):
     assert (bits == want).all()
     each = eng.verify_each_arrays(pk, sg, arena, offs, lens)
     assert (each == want).all()
+
+
+@pytest.mark.parametrize("forge", ["equation", "none"])
+def test_early_prep_equals_one_stream_order(eng, forge):
+    """a host-staged 65,536 x 512 B batch takes msm_launch's early form (decompressions and the
+    fallback's tables on the lane's second stream while the messages cross PCIe, the Straus pass
+    gated on the MSM's verdict word).  Forged entries that all decode (message and s bit flips: the
+    MSM rejects at its final sum, not at the prep's early reject) and an all-valid batch: the bits
+    equal the oracle's and those of an engine kept on the one-stream order
+    (NWV_FLAG_NO_EARLY_PREP), call after call on the same buffers"""
+    import narwhal_amd
+    from narwhal_amd import _lib
+    n = 65536
+    pk, sg, msgs, offs, lens = _synth_arrays(eng, n, 512, seed=4242)
+    forged = []
+    if forge == "equation":
+        rng = np.random.default_rng(7)
+        forged = sorted(int(x) for x in rng.choice(n, size=48, replace=False))
+        for j, i in enumerate(forged):
+            if j % 2:
+                msgs[512 * i + 17] ^= 0x04
+            else:
+                sg[64 * i + 40] ^= 0x01  # s bit flip (s stays < l: top byte untouched)
+    want = _oracle_bits(pk, sg, msgs, offs, lens)
+    assert list(np.flatnonzero(~want)) == forged
+    one = narwhal_amd.Engine(device=0, flags=_lib.NWV_FLAG_NO_EARLY_PREP)
+    try:
+        for _ in range(2):
+            ok, bits = _gpu_batch(eng, pk, sg, msgs, offs, lens)
+            assert ok == (not forged) and (bits == want).all()
+            ok1, bits1 = _gpu_batch(one, pk, sg, msgs, offs, lens)
+            assert ok1 == ok and (bits1 == bits).all()
+    finally:
+        one.close()

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """C4 (65,536 x 512 B, 1 % adversarial) host-to-host call time with the per-signature fallback
-building its tables from the MSM's point records (default) and with a second decompression
-(NWV_FLAG_NO_MSM_REUSE); both bad sets must equal the injected one."""
+building its tables from the MSM's point records (default: the early form, decompressions and
+tables under the messages' transfer), on one stream (NWV_FLAG_NO_EARLY_PREP) and with a second
+decompression (NWV_FLAG_NO_MSM_REUSE); every bad set must equal the injected one."""
 import json
 import os
 import sys
@@ -16,7 +17,8 @@ def main():
     from narwhal_amd import _lib
     import config_legs as CL
     out = {}
-    for name, flags in (("reuse", 0), ("no_reuse", _lib.NWV_FLAG_NO_MSM_REUSE)):
+    for name, flags in (("reuse", 0), ("one_stream", _lib.NWV_FLAG_NO_EARLY_PREP),
+                        ("no_reuse", _lib.NWV_FLAG_NO_MSM_REUSE)):
         eng = narwhal_amd.Engine(device=0, flags=flags)
         r, _ = CL.leg_c4(eng, reps=9)
         out[name] = r

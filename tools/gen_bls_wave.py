@@ -208,9 +208,11 @@ class Regs:
     def bound(self, name):
         return self.regs[name][2]
 
-    def layout(self, n_consts):
-        s = 1 + n_consts
-        for name in self.order:
+    def layout(self, start, names):
+        """registers `names` from slot `start` on; the programs compiled next take their
+        temporaries from the slot after them"""
+        s = start
+        for name in names:
             self.regs[name][0] = s
             s += self.regs[name][1]
         self.temp_base = s
@@ -238,6 +240,11 @@ REGS.add("V", 3)
 REGS.add("W", 6)     # G2 homogeneous points (key sums): accumulator (6) and addend (6)
 REGS.add("W2", 6)
 REGS.add("S", 8)     # scratch inputs: hash-to-curve map outputs, subgroup-check inputs
+# the pairing check's registers: the programs that touch no others (the Miller loop, the final
+# exponentiation, the line programs) see slot 0, their own constants, these registers and their
+# temporaries as one run of slots [0, NSLOTS_PC) -- the bank one item takes in the packed pairing
+# kernel -- and every other constant, register and temporary lies above it
+PC_REGS = ("F", "G", "M", "A", "B", "C", "LA", "LB", "PA", "PB", "QB", "TB", "N")
 
 
 # ============================================================== tower over generic elements ===
@@ -1503,7 +1510,7 @@ def emit(compiled, path):
             stages.append((len(st), nap, nan, nbp, nbn, (1 if anymul else 0) | (2 if anyred else 0), rec_len, off))
         progs.append((name, first, len(cp.stages), stages[first][7], stages[first][0]))
         max_slot = max(max_slot, cp.max_slot)
-    consts = sorted(CTX.consts.values(), key=lambda a: a.id)
+    consts = sorted(CTX.consts.values(), key=lambda a: a.slot)
     la = line_table(G2X, G2Y)
     L = []
     L.append("// generated by tools/gen_bls_wave.py -- do not edit")
@@ -1518,6 +1525,20 @@ def emit(compiled, path):
     pair_max = max(compiled[nm].max_slot for nm in names if nm != "iso2_add" and not nm.startswith("g1_sum"))
     L.append(f"constexpr int NSLOTS_PAIR = {pair_max};")
     L.append(f"constexpr int NCONSTS = {len(consts)};")
+    # the pairing check's programs address [0, NSLOTS_PC) only (checked here): slot 0, the first
+    # NCONSTS_PC constants at slots 1.., PC_REGS, their temporaries; the other constants start at
+    # CONST2_SLOT, then the other registers and temporaries
+    for name in names:
+        if _prog_regs(compiled[name].prog) <= set(PC_REGS):
+            for st in compiled[name].stages:
+                for r in st:
+                    tl = [sl for part in (r["a"], r["b"]) if part for side in part for sl, _ in side]
+                    assert r["dst"] < LAYOUT["nslots_pc"] and all(sl < LAYOUT["nslots_pc"] for sl in tl), name
+    assert [a.slot for a in consts] == list(range(1, 1 + LAYOUT["nconsts_pc"])) + \
+        list(range(LAYOUT["const2_slot"], LAYOUT["const2_slot"] + len(consts) - LAYOUT["nconsts_pc"]))
+    L.append(f"constexpr int NCONSTS_PC = {LAYOUT['nconsts_pc']};")
+    L.append(f"constexpr int NSLOTS_PC = {LAYOUT['nslots_pc']};")
+    L.append(f"constexpr int CONST2_SLOT = {LAYOUT['const2_slot']};")
     for r in REGS.order:
         L.append(f"constexpr int REG_{r} = {REGS.regs[r][0]};")
     L.append(f"constexpr int SLOT_ONE = {CTX.consts[mont(1)].slot};  // the Montgomery one (a constant slot)")
@@ -1587,16 +1608,52 @@ def build_all():
         body(TraceIO(prog))
         CTX.prog = None
         traced.append((prog, body))
-    CTX.cst(1)  # the Montgomery one (combination lanes of product stages multiply by it)
-    REGS.layout(len(CTX.consts))
-    for i, a in enumerate(sorted(CTX.consts.values(), key=lambda a: a.id)):
+    one = CTX.cst(1)  # the Montgomery one (combination lanes of product stages multiply by it)
+    pc = [prog for prog, _ in traced if _prog_regs(prog) <= set(PC_REGS)]
+    pc_consts = {a for prog in pc for a in _prog_consts(prog)} | set(one.f)
+    consts = sorted(CTX.consts.values(), key=lambda a: a.id)
+    first = [a for a in consts if a in pc_consts]
+    rest = [a for a in consts if a not in pc_consts]
+    for i, a in enumerate(first):
         a.slot = 1 + i
     compiled = {}
-    for prog, body in traced:
-        cp = compile_prog(prog)
-        cp.prog, cp.body = prog, body
-        compiled[prog.name] = cp
-    return compiled
+
+    def comp(group):
+        for prog, body in traced:
+            if prog in group:
+                cp = compile_prog(prog)
+                cp.prog, cp.body = prog, body
+                compiled[prog.name] = cp
+    # the pairing check's programs first: slot 0, their constants, PC_REGS, their temporaries
+    REGS.layout(1 + len(first), PC_REGS)
+    comp(pc)
+    LAYOUT["nslots_pc"] = max(compiled[p.name].max_slot for p in pc)
+    LAYOUT["nconsts_pc"] = len(first)
+    # then the other constants, the other registers and the other programs' temporaries
+    LAYOUT["const2_slot"] = LAYOUT["nslots_pc"]
+    for i, a in enumerate(rest):
+        a.slot = LAYOUT["const2_slot"] + i
+    REGS.layout(LAYOUT["const2_slot"] + len(rest), [r for r in REGS.order if r not in PC_REGS])
+    comp([prog for prog, _ in traced if prog not in pc])
+    order = [prog.name for prog, _ in traced]
+    return {name: compiled[name] for name in order}
+
+
+LAYOUT = {}
+
+
+def _prog_regs(prog):
+    return {r for r, _ in prog.inputs} | {r for r, _, _ in prog.outputs}
+
+
+def _prog_consts(prog):
+    """the constant atoms a traced program reads (its products', combinations' and outputs' forms)"""
+    out = set()
+    for a in prog.atoms:
+        out |= {d for d in a.deps() if d.kind == "const"}
+    for _, _, x in prog.outputs:
+        out |= {d for d in x.f if d.kind == "const"}
+    return out
 
 
 def check_programs(compiled, trials=2):

@@ -14,7 +14,8 @@ using namespace bls::wave;
 // every slot past the constants holds some value below 2p (1 in Montgomery form, perturbed)
 __device__ void fill(const Wave& w) {
     init_slots(w);
-    for (int s = 1 + NCONSTS + w.lane; s < NSLOTS; s += 64) {
+    for (int s = 1 + NCONSTS_PC + w.lane; s < NSLOTS; s += 64) {
+        if (s >= CONST2_SLOT && s < CONST2_SLOT + NCONSTS - NCONSTS_PC) continue;
         fp a = k_one();
         a.l[0] = (a.l[0] + 7919u * s) & LM;
         for (int j = 0; j < NL; j++) w.wm[SW * s + j] = a.l[j];
