@@ -1372,7 +1372,7 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
         // items per pairing wave (env NWV_BLS_PACK, 1..4): one LDS bank of ~10.5 KB each
         static const uint32_t pack = [] {
             const char* e = std::getenv("NWV_BLS_PACK");
-            const long v = e ? std::strtol(e, nullptr, 10) : 2;
+            const long v = e ? std::strtol(e, nullptr, 10) : 3;
             return (uint32_t)(v < 1 ? 1 : v > BLS_PACK_MAX ? BLS_PACK_MAX : v);
         }();
         // diagnostic (occupancy experiments): NWV_BLS_LDS_PAD bytes of extra LDS per pairing wave
