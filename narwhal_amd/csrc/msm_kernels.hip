@@ -189,6 +189,7 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_keysum(
     uint32_t m, const uint32_t* __restrict__ kslot, const uint32_t* __restrict__ kc, uint32_t* __restrict__ pts,
     uint32_t* __restrict__ fail) {
     __shared__ unsigned long long col[256 * 9];
+    __shared__ unsigned long long part[32 * 8];
     const uint32_t key = blockIdx.x;
     if (kc && threadIdx.x < 2 * MSM_PT_WORDS) {
         const uint32_t* src = kc + (size_t)KC_SLOT_WORDS * kslot[key];
@@ -205,9 +206,21 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_keysum(
 #pragma unroll
     for (int k = 0; k < 8; k++) col[threadIdx.x * 9 + k] = s[k];
     __syncthreads();
+    // column sums over the rows that hold signatures (a committee key signs one or a few of a
+    // call's messages): 32 partial sums a column, then 8 threads add the 32 (< 2^(32+32)); one
+    // thread walking all 256 rows was a 256-long dependent LDS chain (~10 us)
+    const uint32_t cnt = key_off[key + 1] - key_off[key], rows = cnt < 256u ? cnt : 256u;
+    {
+        const uint32_t c = threadIdx.x & 7, p0 = threadIdx.x >> 3;
+        unsigned long long t = 0;
+        for (uint32_t r = p0; r < rows; r += 32) t += col[r * 9 + c];
+        part[p0 * 8 + c] = t;
+    }
+    __syncthreads();
     if (threadIdx.x < 8) {
         unsigned long long t = 0;
-        for (int r = 0; r < 256; r++) t += col[r * 9 + threadIdx.x];  // < 2^(32+32)
+        const uint32_t np = rows < 32u ? rows : 32u;
+        for (uint32_t r = 0; r < np; r++) t += part[r * 8 + threadIdx.x];
         col[threadIdx.x] = t;
     }
     __syncthreads();

@@ -514,6 +514,10 @@ MsmPlan msm_plan(size_t n, size_t na, bool split = false, int sort2 = 0) {
     p.max_entries = (uint64_t)(na + 1) * p.lay.nw + (uint64_t)n * p.lay.nw_z;
     // ~2 waves per SIMD of bucket lanes (256 CUs x 4 SIMDs x 2 x 64), 8..64 entries each
     p.seg = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, p.max_entries / (256 * 4 * 2 * 64)));
+    // tiny batches (a certificate's few signatures): nearly every bucket is empty, and each lane's
+    // segment close walks to the next non-empty bucket by dependent loads; two entries a lane
+    // (C1 Certificate::verify n = 4: p50 0.191 -> 0.184 ms; a 1K batch is slower below 8)
+    if (p.max_entries <= 2048) p.seg = 2;
     if (const char* e = std::getenv("NWV_MSM_SEG")) p.seg = (uint32_t)std::max(1L, std::strtol(e, nullptr, 10));
     p.nseg = (p.max_entries + p.seg - 1) / p.seg;
     // tail: chunks of at most 256 buckets (one per lane of a k_msm_tail workgroup)
@@ -1949,9 +1953,19 @@ static uint64_t b2_quad_min() {
     }();
     return v;
 }
+// few messages (a types-layer call's header / vote / certificate preimages): the quad form too,
+// for latency -- one lane's compression chain is ~4x the quad's, and m quads fill no more of the
+// chip than the call has messages (NWV_B2_QUAD_MAX_M, default 4,096 messages)
+static uint64_t b2_quad_max_m() {
+    static const uint64_t v = [] {
+        const char* e = std::getenv("NWV_B2_QUAD_MAX_M");
+        return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)4096;
+    }();
+    return v;
+}
 static void b2_launch(Lane& d, size_t m, uint64_t maxlen, const uint8_t* base, const uint64_t* off,
                       const uint64_t* len, uint32_t* out) {
-    if (maxlen >= b2_quad_min())
+    if (maxlen >= b2_quad_min() || m <= b2_quad_max_m())
         hipLaunchKernelGGL(k_blake2b_quad, dim3((unsigned)((m + 15) / 16)), dim3(64), 0, d.stream,
                            (uint64_t)m, base, off, len, out);
     else

@@ -33,6 +33,16 @@ def test_many_random_lengths(eng):
     assert eng.blake2b256_many(msgs) == [hashlib.blake2b(m, digest_size=32).digest() for m in msgs]
 
 
+def test_many_short_messages_one_lane_form(eng):
+    """above NWV_B2_QUAD_MAX_M (4,096) short messages take the one-lane kernel (k_blake2b_many),
+    below it the quad kernel: both against hashlib, lengths 0..300 (0, 1, 2 and 3 blocks)"""
+    rnd = random.Random(77)
+    for m in (5000, 3000):
+        msgs = [rnd.randbytes(rnd.randrange(0, 300)) for _ in range(m)]
+        msgs[0], msgs[1], msgs[2] = b"", rnd.randbytes(128), rnd.randbytes(256)
+        assert eng.blake2b256_many(msgs) == [hashlib.blake2b(x, digest_size=32).digest() for x in msgs]
+
+
 def test_serialized_batches_golden(eng):
     g = of.load_golden("worker_batches.json")
     bufs = [bytes.fromhex(b["serialized"]) for b in g["batches"] if "serialized" in b]
