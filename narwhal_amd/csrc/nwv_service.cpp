@@ -296,6 +296,13 @@ void nwv_service::run() {
             rc_call = nwv_verify_mixed_many(ctx, &com_b->view, nh, H.data(), rh.data(), nv, V.data(), rv.data(), nc,
                                             C.data(), rc.data());
         }
+        // the call's statistics before its callbacks: a submitter woken by its verdict sees them
+        lk.lock();
+        stats[0]++;
+        stats[1] += batch.size();
+        stats[2] = std::max<uint64_t>(stats[2], batch.size());
+        stats[reason]++;
+        lk.unlock();
         size_t ih = 0, iv = 0, ic = 0;
         {
             CallbackScope scope(this);
@@ -307,10 +314,6 @@ void nwv_service::run() {
         }
         lk.lock();
         for (auto& it : batch) open.erase(it->seq);
-        stats[0]++;
-        stats[1] += batch.size();
-        stats[2] = std::max<uint64_t>(stats[2], batch.size());
-        stats[reason]++;
         cv_done.notify_all();
     }
 }
