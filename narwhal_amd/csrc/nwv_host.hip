@@ -815,6 +815,25 @@ class StagePool {
     bool open_ = false, started_ = false;
 };
 
+// fn(helper) over the staging pool, or -- the pool busy with another call's staging (batches in
+// flight on several lanes or devices) -- over a few helper threads of this call's own, so that
+// concurrent large stagings do not drop to one copying thread each
+template <class F>
+static void stage_run(F&& work) {
+    if (StagePool::get().run(work)) return;
+    constexpr int kOwn = 3;
+    std::vector<std::thread> th;
+    for (int t = 0; t < kOwn; t++) {
+        try {
+            th.emplace_back([&work] { work(true); });
+        } catch (...) {
+            break;  // no thread: the others (and the caller) take the pieces
+        }
+    }
+    work(false);
+    for (auto& t : th) t.join();
+}
+
 // Host-side packing copy into the pinned staging buffer: a 65,536 x 512 B batch is ~40 MB, which
 // one thread copies at a few GB/s (longer than the PCIe transfer and the batch MSM together), so
 // copies above 4 MiB are split into 2 MiB pieces over the staging pool.
@@ -830,7 +849,7 @@ static void pack_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
         for (size_t k; (k = next.fetch_add(1)) < np;)
             std::memcpy(dst + k * kPiece, src + k * kPiece, std::min(kPiece, bytes - k * kPiece));
     };
-    if (!StagePool::get().run(work)) work(false);
+    stage_run(work);
 }
 
 // Large message regions: packing into pinned memory and the H2D DMA overlap.  The caller and the
@@ -862,7 +881,8 @@ static int pack_copy_h2d(int ordinal, uint8_t* dev_base, uint8_t* host_base, con
                 err.store(1);
         }
     };
-    if (pieces.size() < 2 || !StagePool::get().run(work)) work(false);
+    if (pieces.size() < 2) work(false);
+    else stage_run(work);
     return (err.load() || done.load() != pieces.size()) ? set_err(NWV_ERR_HIP, "pipelined staging copy") : NWV_OK;
 }
 
