@@ -471,15 +471,27 @@ def bls_pmc(n_items, kernel="k_blsw_pair"):
     return None, None
 
 
+def bls_pack():
+    """items per pairing wave of large calls (nwv_bls.hip: NWV_BLS_PACK, default 3, 1..4)"""
+    import os
+    try:
+        v = int(os.environ.get("NWV_BLS_PACK", "3"))
+    except ValueError:
+        v = 3
+    return min(4, max(1, v))
+
+
 def bls_roofline(n_items, pairing_ms, peak, fixed_lines=True):
-    """the dominant BLS kernel (k_blsw_pair: every item's pairing check on its own wave) against
-    the measured v_mad_u64_u32 rate; with a committed PMC pass of HEAD's BLS sources also its VALU
-    issue floor (instructions at the measured rates) and HBM traffic"""
+    """the dominant BLS kernel (k_blsw_pair_k: the pairing checks, bls_pack() items per wave; with
+    NWV_BLS_PACK=1 k_blsw_pair, one per wave) against the measured v_mad_u64_u32 rate; with a
+    committed PMC pass of HEAD's BLS sources also its VALU issue floor (instructions at the
+    measured rates) and HBM traffic"""
     mad_peak_ts = (peak["v_mad_u64_u32_per_s"] / 1e12) if peak else None
     c = bls_pairing_products(fixed_lines)
     mads = c["total"] * c["mads_per_product"] * n_items
     a = mads / (pairing_ms * 1e-3) / 1e12 if pairing_ms > 0 else None
-    pmc, src = bls_pmc(n_items)
+    kernel = "k_blsw_pair_k" if bls_pack() > 1 else "k_blsw_pair"
+    pmc, src = bls_pmc(n_items, kernel)
     floor = traffic = None
     if pmc and peak and "SQ_INSTS_VALU" in pmc and "SQ_INSTS_VALU_INT64" in pmc and pairing_ms > 0:
         v, i64 = pmc["SQ_INSTS_VALU"], pmc["SQ_INSTS_VALU_INT64"]
@@ -488,8 +500,8 @@ def bls_roofline(n_items, pairing_ms, peak, fixed_lines=True):
                  "source": src}
     if pmc and "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
         traffic = 2 * pmc["FETCH_SIZE"] * 1024 + pmc["WRITE_SIZE"] * 1024
-    return {"kernel": "k_blsw_pair", "bound": "valu", "achieved": a, "unit": "T v_mad_u64_u32/s", "peak": mad_peak_ts,
-            "frac": (a / mad_peak_ts) if (a and mad_peak_ts) else None, "kernel_ms": pairing_ms,
+    return {"kernel": kernel, "items_per_wave": bls_pack(), "bound": "valu", "achieved": a, "unit": "T v_mad_u64_u32/s",
+            "peak": mad_peak_ts, "frac": (a / mad_peak_ts) if (a and mad_peak_ts) else None, "kernel_ms": pairing_ms,
             "mads_per_launch": mads, "items": n_items, "issue_floor": floor, "traffic": traffic,
             "pmc_source": src,
             "algorithmic": f"{c['total']} Fp products per pairing check ({c['miller_loop']} Miller loop with "
