@@ -969,14 +969,15 @@ int ed_stage(Lane& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, con
     htrace("stage:packed");
     if (piped) {
         // offsets, lengths and MSM state, then pk / sig / messages piece by piece as they are
-        // packed, then the padding and keyed tables behind them
+        // packed, then the padding and keyed tables behind them (the early form's flag words are
+        // allocated before the first copy: an error return must not leave a copy reading `h`)
+        if (inputs && !kt && (rc = b.flags.ensure(4 * n + 4))) return rc;
         uint8_t* gdev = b.in.as<uint8_t>();
         NWV_HIP(hipMemcpyAsync(gdev + o_off, h + o_off, o_msg - o_off, hipMemcpyHostToDevice, d.stream));
         // pk and sig (and the fallback's zeroed flag words) ahead of the messages: pksig_ev lets the
         // batch MSM decompress while the messages are still in flight
         int prc = NWV_OK;
         if (inputs && !kt) {
-            if ((rc = b.flags.ensure(4 * n + 4))) return rc;
             NWV_HIP(hipMemsetAsync(b.flags.p, 0, 4 * n + 4, d.stream));
             prc = pack_copy_h2d(d.ordinal, gdev, h, {PackSeg{o_pk, pk + 32 * lo, 32 * n}, PackSeg{o_sig, sig + 64 * lo, 64 * n}},
                                 d.stream);
