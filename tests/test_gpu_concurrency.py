@@ -85,3 +85,32 @@ def test_concurrent_contexts_same_device(eng):
                 assert ok is True and all(bits)
     finally:
         other.close()
+
+
+def test_concurrent_large_stagings(eng):
+    """calls large enough for the piped staging (>= 16 MB of pk, sig and messages: msm_launch's
+    early form, the fallback's speculative tables, the gated Straus pass) from four threads at once:
+    all but one find the staging pool busy and copy with helper threads of their own.  Verdict bits
+    of a forged and a valid batch against the oracle, every call"""
+    import numpy as np
+    from narwhal_amd import _lib
+    n, mlen = 40000, 400
+    rnd = random.Random(11)
+    seeds = [rnd.randbytes(32) for _ in range(n)]
+    msgs = [rnd.randbytes(mlen) for _ in range(n)]
+    pk, sg = eng.sign_many(seeds, msgs)
+    good = [(pk[32 * i:32 * i + 32].tobytes(), sg[64 * i:64 * i + 64].tobytes(), msgs[i]) for i in range(n)]
+    bad = _corrupt(good, [3, 17000, 39999])
+    want = {}
+    for name, items in (("good", good), ("bad", bad)):
+        apk, asg, arena, offs, lens = _lib.soa(items)
+        words = of.verify_each_mt(bytes(apk[:32 * n]), bytes(asg[:64 * n]), bytes(arena), offs.copy(), lens.copy(), 8)
+        want[name] = list(np.unpackbits(words.view(np.uint8), bitorder="little")[:n].astype(bool))
+    assert want["good"].count(False) == 0 and want["bad"].count(False) == 3
+    names = ["good", "bad"] * 3
+    with ThreadPoolExecutor(4) as ex:
+        res = list(ex.map(lambda a: (a[1], eng.verify_batch(good if a[1] == "good" else bad,
+                                                            seed=bytes([a[0] + 1]) * 32)), enumerate(names)))
+    for name, (ok, bits) in res:
+        assert ok == (name == "good")
+        assert list(bits) == want[name]
