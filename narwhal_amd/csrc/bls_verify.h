@@ -355,9 +355,10 @@ NWV_HD bool w_g1_in_group(const W& w, const uint32_t* rec) {
 // (h_hom), apk as an affine G2 record or a Jacobian one (X, Y, Z; q_jac: k_blsw_apk's)
 template <class W>
 NWV_HD bool w_pairing_check_g(const W& w, const uint32_t* sig_rec, const uint32_t* h_rec, bool h_hom,
-                              const uint32_t* q_rec, bool q_jac, const uint32_t* qlines) {
+                              const uint32_t* q_rec, bool q_jac, const uint32_t* qlines, bool pc_bank = false) {
     using namespace wave;
-    init_slots(w);
+    if (pc_bank) init_slots_pc(w);  // a bank of NSLOTS_PC slots (the packed kernel's)
+    else init_slots(w);
     w.zero(REG_PA, 2);
     w.zero(REG_PB, 3);
     w.zero(REG_QB, 6);

@@ -547,6 +547,14 @@ NWV_HD void init_slots(const W& w) {
     w.put_words(-16, &T_KP[0][0], 16);  // below slot 0
     w.sync();
 }
+// a packed pairing bank of NSLOTS_PC slots: slot 0, the pairing check's constants, P << k
+template <class W>
+NWV_HD void init_slots_pc(const W& w) {
+    w.zero(0, 1);
+    w.put_words(1, &T_CONSTS[0][0], NCONSTS_PC);
+    w.put_words(-16, &T_KP[0][0], 16);
+    w.sync();
+}
 #ifdef BLS_WAVE_DEV
 // the device form: every lane fetches all its words of both tables before storing any (one memory
 // round trip; put_words' loop waits for each 64-word load in turn).  PC_ONLY: a bank of

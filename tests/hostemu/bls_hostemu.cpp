@@ -316,6 +316,45 @@ int bh_w3_fast_aggregate_verify(const uint8_t* sig, size_t n_pks, const uint8_t*
     return w_pairing_check_h(w, srec, hrec, arec, mode == 2 ? tab.data() : nullptr) ? ST_OK : ST_VERIFY_FAIL;
 }
 
+// the pairing check on a bank of exactly NSLOTS_PC slots (the packed kernel's k_blsw_pair_k bank),
+// with a canary behind it: the pairing check's programs must address nothing past NSLOTS_PC.
+// mode 1 = computed lines, 2 = the key's line table (precomputed on a full-size wave).  Returns
+// the status, or -1000 when the canary was touched.
+int bh_w_pc_fast_aggregate_verify(const uint8_t* sig, size_t n_pks, const uint8_t* pks, const uint8_t* msg, size_t n,
+                                  const uint8_t* dst, size_t dl, int mode) {
+    int32_t st = bh_w_sig_status(sig);
+    if (st != ST_OK) return st;
+    uint32_t srec[G1_REC_WORDS], hrec[G1H_REC_WORDS], arec[G2_REC_WORDS];
+    fp x, y;
+    bool inf;
+    g1_decompress(x, y, inf, sig);
+    st_g1(srec, inf ? fp_zero() : x, inf ? fp_zero() : y, inf);
+    if (n_pks == 0) return ST_AGGR_MISMATCH;
+    std::vector<uint32_t> krec(G2_REC_WORDS * n_pks), idx(n_pks);
+    std::vector<int32_t> kst(n_pks);
+    for (size_t i = 0; i < n_pks; i++) {
+        kst[i] = key_decode(pks + 96 * i, krec.data() + G2_REC_WORDS * i);
+        idx[i] = (uint32_t)i;
+    }
+    st = apk_record(krec.data(), kst.data(), idx.data(), (uint32_t)n_pks, arec);
+    if (st != ST_OK) return st;
+    const wave::Wave full = host_wave();
+    w_hash_to_g1(full, msg, (uint32_t)n, dst, (uint32_t)dl, hrec);
+    std::vector<uint32_t> tab;
+    if (mode == 2) {
+        tab.resize((size_t)wave::NSTEPS * 6 * NL);
+        w_key_lines(full, arec, tab.data());
+    }
+    constexpr uint32_t CANARY = 0xC0FFEE11u, CW = 4096;
+    std::vector<uint32_t> bank(wave::WM_WORDS_PC + CW, CANARY);
+    wave::Wave w;
+    w.wm = bank.data() + wave::KP_WORDS;
+    const bool ok = w_pairing_check_g(w, srec, hrec, true, arec, false, mode == 2 ? tab.data() : nullptr, true);
+    for (uint32_t i = 0; i < CW; i++)
+        if (bank[wave::WM_WORDS_PC + i] != CANARY) return -1000;
+    return ok ? ST_OK : ST_VERIFY_FAIL;
+}
+
 // the variable-time inversion of the wave engine's final exponentiation (plain big-endian in / out)
 void bh_fp_inv_vt(const uint8_t* a, uint8_t* out) {
     fp x;

@@ -41,6 +41,7 @@ def emu():
     L.bh_w_sig_status.argtypes = [c]
     L.bh_w2_fast_aggregate_verify.argtypes = [c, sz, c, c, sz, c, sz]
     L.bh_w3_fast_aggregate_verify.argtypes = [c, sz, c, c, sz, c, sz, ctypes.c_int]
+    L.bh_w_pc_fast_aggregate_verify.argtypes = [c, sz, c, c, sz, c, sz, ctypes.c_int]
     L.bh_fp_inv_vt.argtypes = [c, vp]
     L.bh_w_aggregate.argtypes = [sz, c, vp, ctypes.c_int]
     L.bh_fp_inv_rows.argtypes = [c, vp]
@@ -335,3 +336,24 @@ def test_generated_wave_tables_match_generator():
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-2000:]
     assert "match the generator" in p.stderr
+
+
+def test_wave_pairing_on_pc_bank(emu):
+    """the packed pairing kernel's bank holds only the pairing check's NSLOTS_PC slots (the
+    generator lays them out first): the whole pairing check, computed lines and a key's line
+    table, run on a bank of exactly that size with a canary behind it -- statuses equal the
+    oracle's and nothing past the bank is touched"""
+    rnd = random.Random(59)
+    sks = [rnd.randrange(1, r).to_bytes(32, "big") for _ in range(3)]
+    pks = [B.keygen(k)[1] for k in sks]
+    m = rnd.randbytes(32)
+    _, agg = B.aggregate([B.sign(k, m) for k in sks])
+    one = B.sign(sks[0], m)
+    for sig, ks, msg in [(agg, pks, m), (agg, pks, m + b"?"), (one, pks[:1], m), (one, pks[1:2], m),
+                         (C.IDENTITY_G1, pks, m)]:
+        want = B.fast_aggregate_verify(sig, ks, msg)
+        for mode in (1, 2):
+            got = emu.bh_w_pc_fast_aggregate_verify(sig, len(ks), b"".join(ks), msg, len(msg), B.DST_NUL,
+                                                    len(B.DST_NUL), mode)
+            assert got != -1000, "a pairing-check program addressed a slot past NSLOTS_PC"
+            assert got == want, (mode, len(ks))
