@@ -939,7 +939,14 @@ struct MsmTailArgs {
     uint32_t* runs;  // [2] accepted / rejected runs since staging (never reset by a run), or null
     uint32_t S;
     unsigned long long* stamps;  // diagnostics (NWV_TAIL_STAMPS): [nw][8] s_memrealtime, or null
+    // a word of coherent pinned host memory the host polls instead of copying the verdict back
+    // and waiting for the stream (1 accepted, 2 rejected; the host zeroes it before the launch), or null
+    uint32_t* hverdict;
 };
+// the verdict into the host-polled word: a system-scope release store from a vector lane
+__device__ __forceinline__ void tail_host_verdict(uint32_t* hv, bool ok) {
+    if (hv) __hip_atomic_store(hv, ok ? 1u : 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 static constexpr int TAIL_PART_SLOTS = 9;  // R_s + up to 8 planes (C <= 256)
 
 namespace {
@@ -1221,6 +1228,7 @@ __device__ __forceinline__ void msm_tail_body(const MsmLayout& lay, const MsmTai
         if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
             *a.verdict = 0u;
             if (a.runs) a.runs[1] += 1u;
+            tail_host_verdict(a.hverdict, false);
         }
         return;
     }
@@ -1287,6 +1295,7 @@ __device__ __forceinline__ void msm_tail_body(const MsmLayout& lay, const MsmTai
         *a.verdict = ok ? 1u : 0u;
         // per-run tally (runs of one batch are ordered on its stream: a plain increment)
         if (a.runs) a.runs[ok ? 0 : 1] += 1u;
+        tail_host_verdict(a.hverdict, ok);
     }
     const int w = lay.nw - 1;  // stamp slot
     NWV_TAIL_STAMP(6);

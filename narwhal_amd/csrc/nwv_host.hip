@@ -176,6 +176,9 @@ struct Lane {
     hipStream_t aux = nullptr;
     hipEvent_t pksig_ev = nullptr, aux_ev = nullptr;
     bool pksig_pending = false;
+    // one word of coherent pinned host memory: the batch MSM's tail stores its verdict there and
+    // batch_on_device polls it (no verdict copy, no wait for the stream's completion signal)
+    uint32_t* hword = nullptr;
 };
 
 // Committee key cache of a device.  fastcrypto decompresses a public key once, when it is
@@ -253,6 +256,8 @@ void lane_close(Lane& d) {
     }
     if (d.aux) (void)hipStreamDestroy(d.aux);
     d.aux = nullptr;
+    if (d.hword) (void)hipHostFree(d.hword);
+    d.hword = nullptr;
     d.b2stage.release();
     d.b2dig.release();
     for (DevBuf* b : {&d.b2_base, &d.b2_off, &d.b2_len, &d.b2_out, &d.b2_packed, &d.b2_plen, &d.b2_err, &d.b2_in})
@@ -276,6 +281,9 @@ int lane_open(Gpu& g, Lane** out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&d->aux, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&d->pksig_ev, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&d->aux_ev, hipEventDisableTiming);
+    if (e == hipSuccess &&
+        hipHostMalloc(reinterpret_cast<void**>(&d->hword), 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+        d->hword = nullptr;  // (optional: the verdict is then copied back)
     // both events start out complete, so the first wait on them returns at once
     if (e == hipSuccess) e = hipEventRecord(d->hstage_ev, d->stream);
     if (e == hipSuccess) e = hipEventRecord(d->b2stage_ev, d->stream);
@@ -583,7 +591,7 @@ constexpr int MSM_NEVENTS = MSM_NKERNELS + 1;  // one event before each kernel, 
 // at 65,536 that a rejected batch no longer waits for); the hash role (k_msm_scalars) runs when
 // the messages are in, and the sort waits for both.
 int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStream_t stream,
-               hipEvent_t* ev, bool state_ready, bool spec_tables = false) {
+               hipEvent_t* ev, bool state_ready, bool spec_tables = false, uint32_t* hverdict = nullptr) {
     const bool pksig = d.pksig_pending;
     d.pksig_pending = false;
     b.tables_ready = false;
@@ -725,7 +733,8 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     const MsmTailArgs ta{b.m_bsum.as<uint32_t>(), b.m_hpart.as<uint32_t>(), kst, E, p.nkeys, p.seg,
                          b.m_tpart.as<uint32_t>(), b.m_wsum.as<uint32_t>(),
                          b.m_ctr.as<uint32_t>(), state, b.m_partial.as<uint32_t>(),
-                         d.gpu->comb.as<uint32_t>(), sblk, quad_max_c, state + 1, state + 2, p.tail_S, st_buf};
+                         d.gpu->comb.as<uint32_t>(), sblk, quad_max_c, state + 1, state + 2, p.tail_S, st_buf,
+                         hverdict};
     // combine items per thread: (lg C + 1) x S_w over the windows (C = nb / S_w buckets per chunk)
     int items = 0;
     for (int w = 0; w < p.lay.nw; w++) {
@@ -1411,8 +1420,33 @@ static int batch_on_device(Lane& d, EdBuffers& b, size_t n, const uint8_t seed[3
                          (!(d.flags & NWV_FLAG_MSM_NEVER) && n >= msm_min_n());
     if (use_msm) {
         htrace("batch:msm-launch");
-        if ((rc = msm_launch(d, b, n, seed, stream, nullptr, state_ready, bits != nullptr))) return rc;
+        // batch-verdict calls of up to 65,536 signatures (latency-bound: a spinning host thread
+        // costs little) poll the tail's word in pinned host memory instead of copying the verdict
+        // back and waiting for the stream: 1K p50 0.233 -> 0.227 ms (NWV_NO_HOST_POLL: the copy)
+        static const bool no_poll = std::getenv("NWV_NO_HOST_POLL") != nullptr;
+        uint32_t* hv = (!bits && !no_poll && stream == d.stream && n <= 65536) ? d.hword : nullptr;
+        if (hv) __atomic_store_n(hv, 0u, __ATOMIC_RELEASE);
+        if ((rc = msm_launch(d, b, n, seed, stream, nullptr, state_ready, bits != nullptr, hv))) return rc;
         htrace("batch:msm-launched");
+        if (hv) {
+            // spin on the word (a few hundred us at most for the batches that come this way), then
+            // the stream's own completion; a word that never flips (bounded at ~2 s) falls back
+            // to the copy below
+            uint32_t v = 0;
+            const auto t0 = std::chrono::steady_clock::now();
+            for (uint64_t k = 0; (v = __atomic_load_n(hv, __ATOMIC_ACQUIRE)) == 0u; k++) {
+                if ((k & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+                __builtin_ia32_pause();
+            }
+            // the stream's own completion too (by now the tail has stored its last word: this
+            // returns at once; without it p99 rose by ~10 us while p50 gained ~2 us)
+            NWV_HIP(hipStreamSynchronize(stream));
+            if (v != 0u) {
+                htrace("batch:verdict-polled");
+                *ok = v == 1u ? 1 : 0;
+                return NWV_OK;
+            }
+        }
         if (bits && b.tables_ready) {
             // the early form built the fallback's tables: its Straus pass queues behind the MSM now
             // (gated on the MSM's verdict word) and one read-back brings both
