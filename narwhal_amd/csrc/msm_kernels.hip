@@ -942,7 +942,11 @@ struct MsmTailArgs {
     // a word of coherent pinned host memory the host polls instead of copying the verdict back
     // and waiting for the stream (1 accepted, 2 rejected; the host zeroes it before the launch), or null
     uint32_t* hverdict;
+    // the top TAIL_QUAD_TOP windows (the longest chains) run chunk butterflies of at most this
+    // many buckets on quads whatever quad_max_c says: one quad pass a level at C = 128
+    uint32_t quad_top_c;
 };
+static constexpr int TAIL_QUAD_TOP = 4;
 // the verdict into the host-polled word: a system-scope release store from a vector lane
 __device__ __forceinline__ void tail_host_verdict(uint32_t* hv, bool ok) {
     if (hv) __hip_atomic_store(hv, ok ? 1u : 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1123,7 +1127,8 @@ __device__ __forceinline__ bool msm_tail_window(const MsmLayout& lay, const MsmT
     ge_p3 p = ge_p3_identity();
     if (t < C) p = msm_bucket_join(a, lay.kbase[w] + (uint32_t)(s * C + t));
     if (s == 0) NWV_TAIL_STAMP(7);
-    if ((uint32_t)C <= a.quad_max_c) {
+    const uint32_t qmax = w >= lay.nw - TAIL_QUAD_TOP && a.quad_top_c > a.quad_max_c ? a.quad_top_c : a.quad_max_c;
+    if ((uint32_t)C <= qmax) {
         // on quads (latency-bound small batches): every level's C / 2 additions (lanes i with bit
         // o clear add lane i + o, in place) as 64 quads per pass
         if (t < C) store_p3(mine, p);

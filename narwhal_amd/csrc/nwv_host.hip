@@ -463,18 +463,30 @@ struct MsmPlan {
 // only the z range, nw == nw_z.
 // sort2: 1 forces the two-level counting sort whenever the sort has more than one chunk (tests),
 // 0 lets the size decide (windows of at least NWV_MSM_SORT2_MIN_PTS points, default 2^20)
+// batches of at most this many signatures run the tail's butterflies on lane quads throughout
+// (latency-bound); larger ones keep lane-local additions (fewer instructions while other batches
+// fill the chip) except in the top windows.  NWV_TAIL_QUAD_MAX_N
+uint64_t tail_quad_max_n() {
+    static const uint64_t v = [] {
+        const char* e = std::getenv("NWV_TAIL_QUAD_MAX_N");
+        return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)16384;
+    }();
+    return v;
+}
+
 MsmPlan msm_plan(size_t n, size_t na, bool split = false, int sort2 = 0) {
     MsmPlan p;
     p.na = na;
     p.np = (uint64_t)na + 1 + n;
     double best = 1e300;
+    const bool narrow_top = n > tail_quad_max_n();  // (msm_split)
     // window widths: ~7 field multiplies per bucket entry against ~18 per bucket (running sums),
     // chosen separately for the z range (all na + 1 + n points) and the range above it (na + 1)
     for (int c_lo = 6; c_lo <= 15; c_lo++)
         for (int c_hi = 3; c_hi <= 15; c_hi++) {
             if (split && c_hi > 3) break;
             MsmLayout L;
-            if (!(split ? msm_make_layout_z(c_lo, L) : msm_make_layout2(c_lo, c_hi, L))) continue;
+            if (!(split ? msm_make_layout_z(c_lo, L) : msm_make_layout2(c_lo, c_hi, L, narrow_top))) continue;
             const double entries = (double)(na + 1) * L.nw + (double)n * L.nw_z;
             const double cost = 7.0 * entries + 18.0 * L.kbase[L.nw];
             if (cost < best) {
@@ -723,18 +735,19 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
         st_buf = b.m_stamps.as<unsigned long long>();
         NWV_HIP(hipMemsetAsync(st_buf, 0, 8 * 8 * (size_t)MSM_MAX_WINDOWS, stream));
     }
-    // quad-lane butterflies where the tail is latency-bound (small batches); large batches keep the
-    // lane-local additions (fewer instructions while other batches fill the chip).  NWV_TAIL_QUAD_MAX_N
-    static const uint64_t quad_max_n = [] {
-        const char* e = std::getenv("NWV_TAIL_QUAD_MAX_N");
-        return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)16384;
+    // quad-lane butterflies where the tail is latency-bound (small batches, tail_quad_max_n)
+    const uint32_t quad_max_c = n <= tail_quad_max_n() ? 256u : 0u;
+    // the top windows' butterflies precede the longest chains: on quads at any size where they
+    // take one quad pass a level (NWV_TAIL_QUAD_TOP_C, 0 = never)
+    static const uint32_t quad_top_c = [] {
+        const char* e = std::getenv("NWV_TAIL_QUAD_TOP_C");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 128u;
     }();
-    const uint32_t quad_max_c = n <= quad_max_n ? 256u : 0u;
     const MsmTailArgs ta{b.m_bsum.as<uint32_t>(), b.m_hpart.as<uint32_t>(), kst, E, p.nkeys, p.seg,
                          b.m_tpart.as<uint32_t>(), b.m_wsum.as<uint32_t>(),
                          b.m_ctr.as<uint32_t>(), state, b.m_partial.as<uint32_t>(),
                          d.gpu->comb.as<uint32_t>(), sblk, quad_max_c, state + 1, state + 2, p.tail_S, st_buf,
-                         hverdict};
+                         hverdict, quad_top_c};
     // combine items per thread: (lg C + 1) x S_w over the windows (C = nb / S_w buckets per chunk)
     int items = 0;
     for (int w = 0; w < p.lay.nw; w++) {

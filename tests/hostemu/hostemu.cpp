@@ -380,7 +380,9 @@ static int msm_batch_impl(size_t n, const uint8_t* pk, const uint8_t* sig, const
                           bool split) {
     ensure_btab();
     MsmLayout lay;
-    if (!(split ? msm_make_layout_z(c, lay) : msm_make_layout(c, lay))) return -1;
+    const bool nt = c < 0;  // c < 0: the narrow-top layout of width -c (msm_split)
+    if (nt) c = -c;
+    if (!(split ? msm_make_layout_z(c, lay) : msm_make_layout(c, lay, nt))) return -1;
     uint32_t seed[8];
     std::memcpy(seed, seed32, 32);
     const size_t na = split ? 2 * n + 1 : n;  // points before B
@@ -562,7 +564,7 @@ int he_msm_recode(const uint8_t* s32, int c, int bits, int* out) {
     uint32_t s[8];
     words(s32, s);
     MsmLayout lay;
-    if (!msm_make_layout(c, lay)) return -1;
+    if (!msm_make_layout(c < 0 ? -c : c, lay, c < 0)) return -1;  // c < 0: narrow-top layout
     const int nw = bits == MSM_BITS_Z ? lay.nw_z : lay.nw;
     msm_recode(s, lay, nw, [&](int w, int d) {
         out[2 * w] = lay.pos[w];
@@ -571,10 +573,10 @@ int he_msm_recode(const uint8_t* s32, int c, int bits, int* out) {
     return nw;
 }
 
-// layout(c): nw, nw_z, then widths
+// layout(c): nw, nw_z, then widths (c < 0: the narrow-top layout of width -c)
 int he_msm_layout(int c, int* out) {
     MsmLayout lay;
-    if (!msm_make_layout(c, lay)) return -1;
+    if (!msm_make_layout(c < 0 ? -c : c, lay, c < 0)) return -1;
     out[0] = lay.nw;
     out[1] = lay.nw_z;
     for (int w = 0; w < lay.nw; w++) out[2 + w] = lay.width[w];

@@ -67,26 +67,36 @@ def honest(rnd, n, mlen=32):
     return out
 
 
-@pytest.mark.parametrize("c", [6, 8, 10, 12, 13, 14, 15])
+@pytest.mark.parametrize("c", [6, 8, 10, 12, 13, 14, 15, -8, -12, -13])
 def test_window_layout_full_buckets(he, c):
     """Near-equal widths <= c; the z range ends exactly at 129 bits and the full range at 254,
-    so every window's top digit range equals its bucket range (no skewed top window)."""
+    so every window's top digit range equals its bucket range (no skewed top window).  c < 0:
+    the narrow-top layout of width -c (large batches, msm.h msm_split): the same widths per
+    range, non-increasing from each range's bottom window to its top."""
     out = (ctypes.c_int * 64)()
     nw = he.he_msm_layout(c, out)
     nwz, widths = out[1], [out[2 + w] for w in range(nw)]
     assert sum(widths[:nwz]) == 129 and sum(widths) == 254
-    assert max(widths) <= c and max(widths) - min(widths) <= 1 + (c >= 14)
+    assert max(widths) <= abs(c) and max(widths) - min(widths) <= 1 + (abs(c) >= 14)
+    if c < 0:
+        even = (ctypes.c_int * 64)()
+        assert he.he_msm_layout(-c, even) == nw and even[1] == nwz
+        for lo, hi in ((0, nwz), (nwz, nw)):
+            assert widths[lo:hi] == sorted(widths[lo:hi], reverse=True)
+            assert sorted(widths[lo:hi]) == sorted(even[2 + w] for w in range(lo, hi))
 
 
-@pytest.mark.parametrize("c,bits", [(6, 253), (8, 253), (13, 253), (15, 253), (6, 128), (13, 128)])
+@pytest.mark.parametrize("c,bits", [(6, 253), (8, 253), (13, 253), (15, 253), (6, 128), (13, 128), (-12, 253),
+                                    (-13, 253), (-13, 128)])
 def test_recoding_identity(he, c, bits):
-    rnd = random.Random(c * 1000 + bits)
+    rnd = random.Random(abs(c) * 1000 + bits + (c < 0))
     d = (ctypes.c_int * 128)()
     lay = (ctypes.c_int * 64)()
     he.he_msm_layout(c, lay)
     widths = [lay[2 + w] for w in range(lay[0])]
     hi = L if bits == 253 else 2**128
-    for s in [0, 1, hi - 1, 2**(bits - 1), (1 << (c - 1)), (1 << (c - 1)) - 1] + [rnd.randrange(hi) for _ in range(300)]:
+    for s in [0, 1, hi - 1, 2**(bits - 1), (1 << (abs(c) - 1)), (1 << (abs(c) - 1)) - 1] + \
+            [rnd.randrange(hi) for _ in range(300)]:
         nw = he.he_msm_recode(s.to_bytes(32, "little"), c, bits, d)
         assert nw == (lay[1] if bits == 128 else lay[0])
         assert sum(d[2 * w + 1] << d[2 * w] for w in range(nw)) == s
@@ -179,7 +189,7 @@ def test_z_prf(he):
         assert out.raw == bytes(want) + bytes(16)
 
 
-@pytest.mark.parametrize("c,G", [(6, 1), (6, 8), (8, 128), (13, 256), (13, 64)])
+@pytest.mark.parametrize("c,G", [(6, 1), (6, 8), (8, 128), (13, 256), (13, 64), (-12, 64), (-13, 256)])
 def test_valid_batches_accept(he, c, G):
     rnd = random.Random(c + G)
     items = honest(rnd, 9, mlen=rnd.choice([0, 32, 100]))
@@ -207,9 +217,9 @@ def test_invalid_signature_rejects(he):
             s = int.from_bytes(sg[32:], "little") + L  # s >= l
             sg[32:] = s.to_bytes(32, "little")
         bad[7] = (pk, bytes(sg), m)
-        assert not any(False for _ in [])
         assert of.verify(*bad[7]) is False
         assert not msm_batch(he, bad, 8, 32)
+        assert not msm_batch(he, bad, -9, 32)  # the narrow-top layout
 
 
 def test_golden_and_zip215_batches_match_oracle(he):
