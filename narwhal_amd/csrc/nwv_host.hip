@@ -179,6 +179,9 @@ struct Lane {
     // one word of coherent pinned host memory: the batch MSM's tail stores its verdict there and
     // batch_on_device polls it (no verdict copy, no wait for the stream's completion signal)
     uint32_t* hword = nullptr;
+    // staged runs with prep chaining (NWV_STAGE_CHAIN): k_msm_prep waits for chain_wait (an earlier
+    // staged run's prep on this device) and chain_rec is recorded after it; null otherwise
+    hipEvent_t chain_wait = nullptr, chain_rec = nullptr;
 };
 
 // Committee key cache of a device.  fastcrypto decompresses a public key once, when it is
@@ -232,6 +235,11 @@ struct Gpu {
     std::condition_variable cv;
     std::vector<Lane*> lanes, idle;
     size_t max_lanes = 4;
+    // staged-run prep chain (NWV_STAGE_CHAIN = k): a ring of k events; run r's prep waits for run
+    // r - k's and records into slot r mod k
+    std::mutex chain_mu;
+    std::vector<hipEvent_t> chain_ev;
+    uint64_t chain_runs = 0;
 };
 
 int with_device(Lane& d) {
@@ -380,6 +388,8 @@ void gpu_close(Gpu& g) {
     g.btab.release();
     g.comb.release();
     g.kc.recs.release();
+    for (hipEvent_t e : g.chain_ev) (void)hipEventDestroy(e);
+    g.chain_ev.clear();
 }
 
 // --------------------------------------------------------------- Ed25519 pipeline ------
@@ -663,7 +673,9 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
         hipLaunchKernelGGL(k_msm_scalars, dim3(sblk), dim3(pthr), 0, stream, gs, p.lay);
         NWV_HIP(hipStreamWaitEvent(stream, d.aux_ev, 0));
     } else if (fused) {
+        if (d.chain_wait) NWV_HIP(hipStreamWaitEvent(stream, d.chain_wait, 0));
         hipLaunchKernelGGL(k_msm_prep, dim3(sblk + pblk), dim3(pthr), 0, stream, gs, p.lay, gp, sblk);
+        if (d.chain_rec) NWV_HIP(hipEventRecord(d.chain_rec, stream));
     } else {
         hipLaunchKernelGGL(k_msm_scalars, dim3(sblk), dim3(pthr), 0, stream, gs, p.lay);
     }
@@ -1236,8 +1248,9 @@ struct nwv_staged {
     KernelLog log[2];              // [0] per-signature pipeline, [1] batch MSM
     int last_mode = -1;
     bool pending_timing = false;
-    hipGraphExec_t graph = nullptr;  // captured batch MSM (mode 1)
+    hipGraphExec_t graph = nullptr;  // captured batch MSM (mode 1, unchained replays)
     bool graph_failed = false;
+    bool chain_ready = false;  // first run done: chained replays launch directly
     bool tally_ready = false;  // m_state[2..4) zeroed before the first mode-1 run
     // per-run coefficient seeds go to the device from a ring of pinned slots, so a graph replay is
     // two truly asynchronous calls (a pageable copy may wait for the stream)
@@ -1809,6 +1822,32 @@ static int staged_graph(nwv_staged* st) {
     return NWV_OK;
 }
 
+// Staged runs chain their preps (NWV_STAGE_CHAIN = k, default 3, 0 = off): run r's k_msm_prep
+// starts only once run r - k's has finished on the device.  Batches issued back to back then
+// start staggered, each prep sharing the chip with at most k - 1 others and with the sorts,
+// buckets and tails of the batches ahead, instead of 12 preps running side by side and every
+// batch's latency-bound tail landing at once.  The driver's 20-step headline: 194 -> 201 M
+// sigs/s (k = 3; k = 2: 203 M, steady state -4 %; k = 1: 172 M); the steady state moves by
+// -1.5 % at k = 3 (profiles/round5_stage_chain_experiment.json).
+int stage_chain_depth() {  // read per run: tests switch it between runs
+    const char* e = std::getenv("NWV_STAGE_CHAIN");
+    return e ? std::max(0, std::min(64, std::atoi(e))) : 3;
+}
+
+// a replay's coefficient seed: into the next pinned slot, then one asynchronous copy
+static int staged_seed_copy(nwv_staged* st, const uint8_t seed[32]) {
+    const int slot = (int)(st->seed_runs++ % nwv_staged::SEED_SLOTS);
+    int rc = st->seeds.ensure(32 * nwv_staged::SEED_SLOTS);
+    if (rc) return rc;
+    if (!st->seed_ev[slot]) NWV_HIP(hipEventCreateWithFlags(&st->seed_ev[slot], hipEventDisableTiming));
+    else NWV_HIP(hipEventSynchronize(st->seed_ev[slot]));  // the slot's copy of 64 runs ago
+    uint8_t* hs = static_cast<uint8_t*>(st->seeds.p) + 32 * slot;
+    std::memcpy(hs, seed, 32);
+    NWV_HIP(hipMemcpyAsync(st->buf.m_state.as<uint32_t>() + 8, hs, 32, hipMemcpyHostToDevice, st->stream));
+    NWV_HIP(hipEventRecord(st->seed_ev[slot], st->stream));
+    return NWV_OK;
+}
+
 int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]) {
     const bool timed = (mode & NWV_RUN_TIMED) != 0;
     mode &= ~NWV_RUN_TIMED;
@@ -1829,21 +1868,36 @@ int nwv_staged_run(nwv_staged* st, int mode, const uint8_t seed32[32]) {
             NWV_HIP(hipMemsetAsync(st->buf.m_state.as<uint32_t>() + 2, 0, 8, st->stream));
             st->tally_ready = true;
         }
-        if (!timed && st->graph) {
-            const int slot = (int)(st->seed_runs++ % nwv_staged::SEED_SLOTS);
-            if ((rc = st->seeds.ensure(32 * nwv_staged::SEED_SLOTS))) return rc;
-            if (!st->seed_ev[slot]) NWV_HIP(hipEventCreateWithFlags(&st->seed_ev[slot], hipEventDisableTiming));
-            else NWV_HIP(hipEventSynchronize(st->seed_ev[slot]));  // the slot's copy of 64 runs ago
-            uint8_t* hs = static_cast<uint8_t*>(st->seeds.p) + 32 * slot;
-            std::memcpy(hs, seed, 32);
-            NWV_HIP(hipMemcpyAsync(st->buf.m_state.as<uint32_t>() + 8, hs, 32, hipMemcpyHostToDevice, st->stream));
-            NWV_HIP(hipEventRecord(st->seed_ev[slot], st->stream));
+        const int chain_k = stage_chain_depth();
+        const bool replay = !timed && st->n && (chain_k > 0 ? st->chain_ready : st->graph != nullptr);
+        if (replay && (rc = staged_seed_copy(st, seed))) return rc;
+        if (replay && chain_k > 0) {
+            // run r's k_msm_prep waits for run r - k's on this device (direct launches: the
+            // event pair changes from run to run)
+            Gpu& G = *st->gpu;
+            std::lock_guard<std::mutex> lk(G.chain_mu);
+            if (G.chain_ev.size() != (size_t)chain_k) {
+                for (hipEvent_t e : G.chain_ev) (void)hipEventDestroy(e);  // (released once their records complete)
+                G.chain_ev.assign(chain_k, nullptr);
+                for (auto& e : G.chain_ev) NWV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                G.chain_runs = 0;
+            }
+            hipEvent_t ce = G.chain_ev[G.chain_runs % chain_k];
+            st->own.chain_wait = G.chain_runs >= (uint64_t)chain_k ? ce : nullptr;
+            st->own.chain_rec = ce;
+            G.chain_runs++;
+            rc = msm_launch(st->own, st->buf, st->n, nullptr, st->stream, nullptr, false);
+            st->own.chain_wait = st->own.chain_rec = nullptr;
+        } else if (replay) {
             NWV_HIP(hipGraphLaunch(st->graph, st->stream));
         } else {
             // first run of the batch (allocates its buffers) or a timed run; an untimed first run
-            // also captures the graph the later runs replay
+            // also captures the graph the later runs replay (unchained form)
             rc = msm_launch(st->own, st->buf, st->n, seed, st->stream, timed ? st->ev : nullptr, false);
-            if (!rc && !timed && st->n) rc = staged_graph(st);
+            if (!rc && !timed && st->n) {
+                if (chain_k > 0) st->chain_ready = true;
+                else rc = staged_graph(st);
+            }
         }
     } else {
         rc = ed_launch(st->own, st->buf, st->n, st->stream, timed ? st->ev : nullptr);

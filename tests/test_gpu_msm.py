@@ -210,10 +210,14 @@ def test_staged_msm_runs_and_times(eng, split):
     assert not ok and [i for i in range(len(items)) if not vb[i]] == bad
 
 
-def test_staged_graph_replay_valid_and_invalid(eng):
-    """untimed mode-1 runs replay a captured HIP graph with a fresh seed each time: verdicts stay
-    exact for a valid batch and for one with a forged signature (fallback after fetch)"""
+@pytest.mark.parametrize("chain", ["0", "1", "3"])
+def test_staged_graph_replay_valid_and_invalid(eng, monkeypatch, chain):
+    """untimed mode-1 runs replay with a fresh seed each time -- a captured HIP graph
+    (NWV_STAGE_CHAIN=0) or direct launches whose preps are chained across runs (depth 1, 3 =
+    default): verdicts stay exact for a valid batch and for one with a forged signature
+    (fallback after fetch)"""
     from narwhal_amd import _lib
+    monkeypatch.setenv("NWV_STAGE_CHAIN", chain)
     items = _synthetic(eng, 3000, 64, seed=21)
     pk, sg, arena, offs, lens = _lib.soa(items)
     st = eng.stage(pk, sg, arena, offs, lens)
@@ -235,6 +239,34 @@ def test_staged_graph_replay_valid_and_invalid(eng):
         assert not allv and list(np.flatnonzero(~bits)) == [1234]
     assert st.run_tally() == (0, 4)
     st.free()
+
+
+@pytest.mark.parametrize("chain", ["1", "2", "3"])
+def test_staged_chain_across_batches(eng, monkeypatch, chain):
+    """staged runs issued round-robin over five resident batches (one holding a forged signature)
+    with no host read in between, each prep waiting for the prep `chain` runs earlier on another
+    batch's stream: every run completes and each batch's device tally is exact"""
+    from narwhal_amd import _lib
+    monkeypatch.setenv("NWV_STAGE_CHAIN", chain)
+    stages = []
+    for b in range(5):
+        items = _synthetic(eng, 1500 + 300 * b, 48, seed=40 + b)
+        pk, sg, arena, offs, lens = _lib.soa(items)
+        if b == 2:
+            sg = sg.copy()
+            sg[64 * 777 + 40] ^= 2
+        st = eng.stage(pk, sg, arena, offs, lens)
+        st.run(mode=1)  # first run: buffers (and, unchained, the graph)
+        stages.append(st)
+    for r in range(4):
+        for st in stages:
+            st.run(mode=1, seed=bytes([r + 3]) * 32)
+    for b, st in enumerate(stages):
+        assert st.run_tally() == ((0, 5) if b == 2 else (5, 0)), b
+    allv, bits = stages[2].fetch()
+    assert not allv and list(np.flatnonzero(~bits)) == [777]
+    for st in stages:
+        st.free()
 
 
 def _keyed(items):
