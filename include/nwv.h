@@ -83,6 +83,9 @@ typedef struct nwv_ctx nwv_ctx;
  * tables -- on a second stream once pk and sig are on the device, under the messages' transfer;
  * this flag keeps the one-stream order (every kernel after the whole copy) */
 #define NWV_FLAG_NO_EARLY_PREP 1024u
+/* diagnostic / tests: a keyed batch MSM whose hashes fit one k_msm_prep workgroup sums its keys'
+ * scalars in that workgroup (no k_msm_keysum launch); this flag keeps the separate launch */
+#define NWV_FLAG_NO_FUSED_KEYSUM 2048u
 
 /* ------------------------------------------------------------------ lifecycle ----- */
 /* Process-wide context creation (created once, in Primary::spawn).

@@ -34,6 +34,7 @@ NWV_FLAG_BLS_BATCH = 128
 NWV_FLAG_NO_SIGCACHE = 256
 NWV_FLAG_NO_ROW_PREP = 512
 NWV_FLAG_NO_EARLY_PREP = 1024
+NWV_FLAG_NO_FUSED_KEYSUM = 2048
 NWV_RUN_TIMED = 0x100
 
 

@@ -95,7 +95,58 @@ struct MsmScalarArgs {
     // 1: OR the flag into fout (zeroed at staging; the early form's k_ed_points_msm ORs its decode
     // flags into the same words concurrently), 0: store it
     uint32_t fout_or;
+    // fuse_keysum: a keyed batch whose hashes fit ONE workgroup (n <= its threads, nkeys <= its
+    // threads) sums its keys' scalars in that workgroup after the hashes (k_msm_keysum's work,
+    // thread j = key j), under the decompressions running beside it in the same grid: one launch
+    // and its hand-off fewer on the per-call path (C1 Certificate::verify)
+    uint32_t fuse_keysum;
+    uint32_t nkeys;
+    const uint32_t* key_off;  // CSR of the keys' signatures (k_msm_keysum's key_off / key_sig)
+    const uint32_t* key_sig;
+    const uint32_t* kslot;    // split form: the keys' cache slots, the cache, the point records
+    const uint32_t* kc;
+    uint32_t* pts;
 };
+
+// A key's scalar (8 column sums of 32-bit words, each < 2^64) reduced mod l and recoded into its
+// digit row(s): row `key`, and in the split form (kc) the 2^128 multiple's row m + key
+__device__ __forceinline__ void msm_key_digits(const unsigned long long* colsum, uint32_t key, uint32_t m,
+                                               uint64_t np, bool split, const MsmLayout& lay,
+                                               int16_t* __restrict__ digits) {
+    uint32_t x[16];
+    unsigned long long c = 0;
+    for (int k = 0; k < 16; k++) {
+        if (k < 8) {
+            const unsigned long long v = colsum[k];
+            const unsigned long long lo = (c & 0xffffffffull) + (v & 0xffffffffull);
+            x[k] = (uint32_t)lo;
+            c = (c >> 32) + (v >> 32) + (lo >> 32);
+        } else {
+            x[k] = (uint32_t)c;
+            c >>= 32;
+        }
+    }
+    uint32_t r[8];
+    sc_reduce512(x, r);
+    if (split) {
+        uint32_t lo[8], hi[8];
+        msm_split128(r, lo, hi);
+        msm_recode(lo, lay, lay.nw_z, [&](int w, int d) { digits[(uint64_t)w * np + key] = (int16_t)d; });
+        msm_recode(hi, lay, lay.nw_z, [&](int w, int d) { digits[(uint64_t)w * np + m + key] = (int16_t)d; });
+    } else {
+        msm_recode(r, lay, lay.nw, [&](int w, int d) { digits[(uint64_t)w * np + key] = (int16_t)d; });
+    }
+}
+
+// word t < 2 MSM_PT_WORDS of a cached key's records (A, then 2^128 A) into points key and m + key;
+// the record's last word set = the key did not decode
+__device__ __forceinline__ void msm_key_record_word(const uint32_t* __restrict__ kc, const uint32_t* __restrict__ kslot,
+                                                    uint32_t key, uint32_t m, uint32_t t, uint32_t* __restrict__ pts,
+                                                    uint32_t* fail) {
+    const uint32_t* src = kc + (size_t)KC_SLOT_WORDS * kslot[key];
+    pts[(size_t)MSM_PT_WORDS * (t < MSM_PT_WORDS ? key : m + key) + (t % MSM_PT_WORDS)] = src[t];
+    if (t == MSM_PT_WORDS - 1 && src[t]) atomicOr(fail, 2u);
+}
 struct MsmPointArgs {
     uint64_t n, na;
     uint64_t ndec;  // A points to decompress into [0, ndec): na, or 0 when they come from the key cache
@@ -173,6 +224,23 @@ __device__ __forceinline__ void msm_scalars_block(uint32_t blk, const MsmScalarA
     }
     if (blk == 0)  // (no memset launch)
         for (uint32_t t = threadIdx.x; t < 128; t += nt) g.tail_ctr[t] = 0u;
+    if (g.fuse_keysum) {  // (the host sets it only for a grid with one hash workgroup)
+        __syncthreads();  // every z_i k_i of ascal is written (one workgroup: one CU)
+        const uint32_t m = g.nkeys;
+        if (g.kc)
+            for (uint32_t t = threadIdx.x; t < 2u * MSM_PT_WORDS * m; t += nt)
+                msm_key_record_word(g.kc, g.kslot, t / (2 * MSM_PT_WORDS), m, t % (2 * MSM_PT_WORDS), g.pts, fail);
+        if (threadIdx.x < m) {
+            const uint32_t key = threadIdx.x;
+            unsigned long long cs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            for (uint32_t t = g.key_off[key]; t < g.key_off[key + 1]; t++) {
+                const uint32_t* a = g.ascal + 8 * (size_t)g.key_sig[t];
+#pragma unroll
+                for (int k = 0; k < 8; k++) cs[k] += a[k];
+            }
+            msm_key_digits(cs, key, m, na + 1 + n, g.kc != nullptr, lay, digits);
+        }
+    }
 }
 
 // Keyed batches (ed25519_consensus groups batch entries by verification key): one workgroup per
@@ -191,12 +259,7 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_keysum(
     __shared__ unsigned long long col[256 * 9];
     __shared__ unsigned long long part[32 * 8];
     const uint32_t key = blockIdx.x;
-    if (kc && threadIdx.x < 2 * MSM_PT_WORDS) {
-        const uint32_t* src = kc + (size_t)KC_SLOT_WORDS * kslot[key];
-        const uint32_t t = threadIdx.x;
-        pts[(size_t)MSM_PT_WORDS * (t < MSM_PT_WORDS ? key : m + key) + (t % MSM_PT_WORDS)] = src[t];
-        if (t == MSM_PT_WORDS - 1 && src[t]) atomicOr(fail, 2u);  // the key did not decode
-    }
+    if (kc && threadIdx.x < 2 * MSM_PT_WORDS) msm_key_record_word(kc, kslot, key, m, threadIdx.x, pts, fail);
     unsigned long long s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (uint32_t t = key_off[key] + threadIdx.x; t < key_off[key + 1]; t += 256) {
         const uint32_t* a = ascal + 8 * (size_t)key_sig[t];
@@ -224,32 +287,7 @@ extern "C" __global__ void __launch_bounds__(256) k_msm_keysum(
         col[threadIdx.x] = t;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t x[16];
-        unsigned long long c = 0;
-        for (int k = 0; k < 16; k++) {
-            if (k < 8) {
-                const unsigned long long v = col[k];
-                const unsigned long long lo = (c & 0xffffffffull) + (v & 0xffffffffull);
-                x[k] = (uint32_t)lo;
-                c = (c >> 32) + (v >> 32) + (lo >> 32);
-            } else {
-                x[k] = (uint32_t)c;
-                c >>= 32;
-            }
-        }
-        uint32_t r[8];
-        sc_reduce512(x, r);
-        const uint64_t np = na + 1 + n;
-        if (kc) {
-            uint32_t lo[8], hi[8];
-            msm_split128(r, lo, hi);
-            msm_recode(lo, lay, lay.nw_z, [&](int w, int d) { digits[(uint64_t)w * np + key] = (int16_t)d; });
-            msm_recode(hi, lay, lay.nw_z, [&](int w, int d) { digits[(uint64_t)w * np + m + key] = (int16_t)d; });
-        } else {
-            msm_recode(r, lay, lay.nw, [&](int w, int d) { digits[(uint64_t)w * np + key] = (int16_t)d; });
-        }
-    }
+    if (threadIdx.x == 0) msm_key_digits(col, key, m, na + 1 + n, kc != nullptr, lay, digits);
 }
 
 // One-time per device: the fixed-base comb table, entry 8 j + i - 1 = i 16^j B (msm.h)

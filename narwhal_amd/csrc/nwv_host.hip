@@ -639,7 +639,7 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     const bool early = pksig && reuse && !b.kc_split && stream == d.stream && !ev && state_ready &&
                        !(d.flags & NWV_FLAG_NO_EARLY_PREP);
     if (early && spec_tables && (rc = ed_scratch(b, n))) return rc;
-    const MsmScalarArgs gs{(uint64_t)n, (uint64_t)na, keyed, b.pk.as<uint8_t>(), b.sig.as<uint8_t>(),
+    MsmScalarArgs gs{(uint64_t)n, (uint64_t)na, keyed, b.pk.as<uint8_t>(), b.sig.as<uint8_t>(),
                            b.msg.as<uint8_t>(), b.off.as<uint64_t>(), b.len.as<uint32_t>(), state + 8,
                            b.m_ascal.as<uint32_t>(), digits, b.m_partial.as<uint32_t>(), state,
                            b.kc_split ? 1u : 0u, b.m_ctr.as<uint32_t>(), reuse ? b.kbuf.as<uint32_t>() : nullptr,
@@ -660,6 +660,18 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     const unsigned sblk = (unsigned)((n + pthr - 1) / pthr);  // hash workgroups (k_msm_tail's partials)
     const unsigned pblk = rows ? (unsigned)((n + ndec + 3) / 4) : (unsigned)((64 * waves + 255) / 256);
     const bool fused = !(d.flags & NWV_FLAG_MSM_SPLIT_PREP) && !early;
+    const uint32_t* kc = b.kc_split ? d.gpu->kc.recs.as<uint32_t>() : nullptr;
+    // a keyed batch whose hashes fit one workgroup: its key sums run in that workgroup
+    // (MsmScalarArgs::fuse_keysum) instead of a k_msm_keysum launch
+    if (keyed && fused && sblk == 1 && b.nkeys_distinct <= pthr && !(d.flags & NWV_FLAG_NO_FUSED_KEYSUM)) {
+        gs.fuse_keysum = 1u;
+        gs.nkeys = (uint32_t)b.nkeys_distinct;
+        gs.key_off = b.koff.as<uint32_t>();
+        gs.key_sig = b.ksig.as<uint32_t>();
+        gs.kslot = b.kslot.as<uint32_t>();
+        gs.kc = kc;
+        gs.pts = b.m_pts.as<uint32_t>();
+    }
     if (early) {
         NWV_HIP(hipStreamWaitEvent(d.aux, d.pksig_ev, 0));
         hipLaunchKernelGGL(k_msm_points, dim3(pblk), dim3(pthr), 0, d.aux, gp);
@@ -679,8 +691,7 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
     } else {
         hipLaunchKernelGGL(k_msm_scalars, dim3(sblk), dim3(pthr), 0, stream, gs, p.lay);
     }
-    const uint32_t* kc = b.kc_split ? d.gpu->kc.recs.as<uint32_t>() : nullptr;
-    if (keyed)
+    if (keyed && !gs.fuse_keysum)
         hipLaunchKernelGGL(k_msm_keysum, dim3((unsigned)b.nkeys_distinct), dim3(256), 0, stream, (uint64_t)n,
                            (uint64_t)na, p.lay, b.koff.as<uint32_t>(), b.ksig.as<uint32_t>(), b.m_ascal.as<uint32_t>(),
                            digits, (uint32_t)b.nkeys_distinct, b.kslot.as<uint32_t>(), kc, b.m_pts.as<uint32_t>(),

@@ -309,6 +309,48 @@ def test_keyed_batches_committee(keng, n, m):
     assert ok and all(bits)
 
 
+@pytest.mark.parametrize("fused", [True, False])
+def test_keyed_small_batches_fused_keysum(eng, eng_nokc, fused):
+    """keyed batches whose hashes fit one k_msm_prep workgroup sum their keys' scalars in that
+    workgroup (no k_msm_keysum launch; NWV_FLAG_NO_FUSED_KEYSUM keeps the launch): key cache on
+    and off, one signature per key, several per key, 64 signatures, and a forged signature or a
+    signature over the wrong message pinpointed -- the oracle's verdicts either way"""
+    import narwhal_amd
+    from narwhal_amd import _lib
+    engines = [eng, eng_nokc]
+    if not fused:
+        engines = [narwhal_amd.Engine(device=0, flags=_lib.NWV_FLAG_MSM_ALWAYS | _lib.NWV_FLAG_NO_FUSED_KEYSUM | f)
+                   for f in (0, _lib.NWV_FLAG_NO_KEYCACHE)]
+    try:
+        for e in engines:
+            for n, m in [(1, 1), (4, 4), (7, 3), (17, 17), (64, 5), (64, 64)]:
+                rnd = np.random.default_rng(1000 * n + m)
+                kseeds = [rnd.bytes(32) for _ in range(m)]
+                msgs = [rnd.bytes(32) for _ in range(n)]
+                pk, sg = e.sign_many([kseeds[i % m] for i in range(n)], msgs)
+                items = [(pk[32 * i:32 * i + 32].tobytes(), sg[64 * i:64 * i + 64].tobytes(), msgs[i])
+                         for i in range(n)]
+                keys, kidx = _keyed(items)
+                sigs = [x[1] for x in items]
+                ok, bits = e.verify_batch_keyed(keys, kidx, sigs, msgs, seed=bytes([n]) * 32)
+                assert ok and all(bits), (n, m)
+                bad = n - 1
+                s = bytearray(sigs[bad])
+                s[40] ^= 4
+                sigs2 = list(sigs)
+                sigs2[bad] = bytes(s)
+                ok, bits = e.verify_batch_keyed(keys, kidx, sigs2, msgs)
+                assert not ok and [i for i in range(n) if not bits[i]] == [bad], (n, m)
+                msgs2 = list(msgs)
+                msgs2[0] = msgs2[0][:-1] + bytes([msgs2[0][-1] ^ 1])
+                ok, bits = e.verify_batch_keyed(keys, kidx, sigs, msgs2)
+                assert not ok and [i for i in range(n) if not bits[i]] == [0], (n, m)
+    finally:
+        if not fused:
+            for e in engines:
+                e.close()
+
+
 def test_keyed_many_keys_bypass_cache(eng):
     """a keyed call with more distinct keys than NWV_KEYCACHE_MAX_KEYS (4,096) goes uncached
     (full-width scalars); the same keys in a call of 3,000 distinct keys go through the cache:
