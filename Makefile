@@ -38,8 +38,8 @@ oracle:
 	$(MAKE) -C oracle
 
 hostemu: tests/_build/libhostemu.so tests/_build/libsvcstub.so tests/_build/libblsemu.so tests/_build/libblsshard.so
-# the BLS calls' split over a multi-device context (bls_shard.h) with a stub per-device verifier
-tests/_build/libblsshard.so: tests/hostemu/bls_shard_stub.cpp narwhal_amd/csrc/bls_shard.h
+# the BLS and Ed25519 calls' split over a multi-device context (bls_shard.h, shard.h) with stub per-device work
+tests/_build/libblsshard.so: tests/hostemu/bls_shard_stub.cpp narwhal_amd/csrc/bls_shard.h narwhal_amd/csrc/shard.h
 	@mkdir -p tests/_build
 	g++ -O1 -g -std=c++17 -fPIC -shared -pthread -o $@ tests/hostemu/bls_shard_stub.cpp
 # the gfx950 BLS12-381 code compiled for the host (tests/test_bls_hostemu.py)
@@ -62,12 +62,16 @@ tests/_build/libhostemu.so: tests/hostemu/hostemu.cpp $(CSRC)
 	@mkdir -p tests/_build
 	$(HIPCC) -std=c++17 -O1 --offload-host-only -x hip -DNWV_BOUNDS_CHECK -fPIC -shared -o $@ tests/hostemu/hostemu.cpp
 
-tools: tools/ubench_valu tools/ubench_field tools/ubench_wave
+tools: tools/ubench_valu tools/ubench_field tools/ubench_wave tools/ubench_row tools/ubench_prep
 tools/ubench_valu: tools/ubench_valu.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -o $@ $<
 tools/ubench_field: tools/ubench_field.hip narwhal_amd/csrc/fe25519.h
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 tools/ubench_wave: tools/ubench_wave.hip $(BLS_SRC)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
+tools/ubench_row: tools/ubench_row.hip narwhal_amd/csrc/fe_row.h narwhal_amd/csrc/msm.h
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Wno-unused-value -o $@ $<
+tools/ubench_prep: tools/ubench_prep.hip $(CSRC)
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 
 clean:

@@ -978,16 +978,25 @@ struct MsmTailArgs {
     uint32_t S;
     unsigned long long* stamps;  // diagnostics (NWV_TAIL_STAMPS): [nw][8] s_memrealtime, or null
     // a word of coherent pinned host memory the host polls instead of copying the verdict back
-    // and waiting for the stream (1 accepted, 2 rejected; the host zeroes it before the launch), or null
+    // and waiting for the stream, or null: (hseq << 2) | code, code 1 accepted, 2 rejected,
+    // 3 undetermined (a window never published, below).  hseq is the call's sequence number, so a
+    // store left over from an earlier call on the lane is never taken for this call's verdict.
     uint32_t* hverdict;
     // the top TAIL_QUAD_TOP windows (the longest chains) run chunk butterflies of at most this
     // many buckets on quads whatever quad_max_c says: one quad pass a level at C = 128
     uint32_t quad_top_c;
+    uint32_t hseq;
+    // bound on the final-sum wave's polls of one window's ready flag (each a coherent load plus a
+    // short sleep).  Reaching it ends the kernel with *verdict = 2, "undetermined": the host then
+    // runs the per-signature pass instead of reporting the batch invalid.
+    uint32_t spin_limit;
 };
 static constexpr int TAIL_QUAD_TOP = 4;
+// batch verdict codes in *verdict (state word 1) and the host word's low two bits
+static constexpr uint32_t MSM_REJECTED = 0u, MSM_ACCEPTED = 1u, MSM_UNDETERMINED = 2u;
 // the verdict into the host-polled word: a system-scope release store from a vector lane
-__device__ __forceinline__ void tail_host_verdict(uint32_t* hv, bool ok) {
-    if (hv) __hip_atomic_store(hv, ok ? 1u : 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+__device__ __forceinline__ void tail_host_verdict(const MsmTailArgs& a, uint32_t code) {
+    if (a.hverdict) __hip_atomic_store(a.hverdict, (a.hseq << 2) | code, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 static constexpr int TAIL_PART_SLOTS = 9;  // R_s + up to 8 planes (C <= 256)
 
@@ -1269,9 +1278,9 @@ template <int PER>
 __device__ __forceinline__ void msm_tail_body(const MsmLayout& lay, const MsmTailArgs& a) {
     if (msm_failed(a.fail)) {  // rejected at prep (the sort and bucket kernels skipped their work)
         if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
-            *a.verdict = 0u;
+            *a.verdict = MSM_REJECTED;
             if (a.runs) a.runs[1] += 1u;
-            tail_host_verdict(a.hverdict, false);
+            tail_host_verdict(a, 2u);
         }
         return;
     }
@@ -1311,10 +1320,10 @@ __device__ __forceinline__ void msm_tail_body(const MsmLayout& lay, const MsmTai
     bool timed_out = false;
 #pragma unroll 1
     for (int w = 0; w < lay.nw; w++) {
-        // a bounded wait (~0.5 s): a window that never publishes ends the kernel with a reject
+        // a bounded wait: a window that never publishes ends the kernel with "undetermined"
         uint32_t spins = 0;
-        while (tail_ld_coh(ready + w) == 0u && ++spins < (1u << 24)) __builtin_amdgcn_s_sleep(1);
-        if (spins >= (1u << 24)) {
+        while (tail_ld_coh(ready + w) == 0u && ++spins < a.spin_limit) __builtin_amdgcn_s_sleep(1);
+        if (spins >= a.spin_limit) {
             timed_out = true;
             break;
         }
@@ -1335,10 +1344,11 @@ __device__ __forceinline__ void msm_tail_body(const MsmLayout& lay, const MsmTai
     const unsigned long long bad = __ballot(t < 2 && nz);
     if (t == 0) {
         const bool ok = !timed_out && bad == 0 && *a.fail == 0;
-        *a.verdict = ok ? 1u : 0u;
-        // per-run tally (runs of one batch are ordered on its stream: a plain increment)
+        *a.verdict = timed_out ? MSM_UNDETERMINED : ok ? MSM_ACCEPTED : MSM_REJECTED;
+        // per-run tally (runs of one batch are ordered on its stream: a plain increment); an
+        // undetermined run is not an accepted one
         if (a.runs) a.runs[ok ? 0 : 1] += 1u;
-        tail_host_verdict(a.hverdict, ok);
+        tail_host_verdict(a, timed_out ? 3u : ok ? 1u : 2u);
     }
     const int w = lay.nw - 1;  // stamp slot
     NWV_TAIL_STAMP(6);

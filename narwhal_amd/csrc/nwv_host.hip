@@ -23,6 +23,7 @@
 #include "blake2b_kernels.hip"
 #include "ed25519_kernels.hip"
 #include "msm_kernels.hip"
+#include "shard.h"
 
 #include <random>
 
@@ -179,6 +180,7 @@ struct Lane {
     // one word of coherent pinned host memory: the batch MSM's tail stores its verdict there and
     // batch_on_device polls it (no verdict copy, no wait for the stream's completion signal)
     uint32_t* hword = nullptr;
+    uint32_t hseq = 0;  // sequence number of the lane's last polled call (30 bits, never 0)
     // staged runs with prep chaining (NWV_STAGE_CHAIN): k_msm_prep waits for chain_wait (an earlier
     // staged run's prep on this device) and chain_rec is recorded after it; null otherwise
     hipEvent_t chain_wait = nullptr, chain_rec = nullptr;
@@ -613,7 +615,8 @@ constexpr int MSM_NEVENTS = MSM_NKERNELS + 1;  // one event before each kernel, 
 // at 65,536 that a rejected batch no longer waits for); the hash role (k_msm_scalars) runs when
 // the messages are in, and the sort waits for both.
 int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStream_t stream,
-               hipEvent_t* ev, bool state_ready, bool spec_tables = false, uint32_t* hverdict = nullptr) {
+               hipEvent_t* ev, bool state_ready, bool spec_tables = false, uint32_t* hverdict = nullptr,
+               uint32_t hseq = 0) {
     const bool pksig = d.pksig_pending;
     d.pksig_pending = false;
     b.tables_ready = false;
@@ -766,11 +769,18 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
         const char* e = std::getenv("NWV_TAIL_QUAD_TOP_C");
         return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 128u;
     }();
+    // the final-sum wave's bound on waiting for one window (NWV_TAIL_SPIN_LIMIT: a test hook that
+    // forces the undetermined outcome; the default is seconds of polling)
+    static const uint32_t spin_limit = [] {
+        const char* e = std::getenv("NWV_TAIL_SPIN_LIMIT");
+        const unsigned long v = e ? std::strtoul(e, nullptr, 10) : (1ul << 24);
+        return (uint32_t)std::max(1ul, std::min(v, (unsigned long)UINT32_MAX));
+    }();
     const MsmTailArgs ta{b.m_bsum.as<uint32_t>(), b.m_hpart.as<uint32_t>(), kst, E, p.nkeys, p.seg,
                          b.m_tpart.as<uint32_t>(), b.m_wsum.as<uint32_t>(),
                          b.m_ctr.as<uint32_t>(), state, b.m_partial.as<uint32_t>(),
                          d.gpu->comb.as<uint32_t>(), sblk, quad_max_c, state + 1, state + 2, p.tail_S, st_buf,
-                         hverdict, quad_top_c};
+                         hverdict, quad_top_c, hseq & 0x3FFFFFFFu, spin_limit};
     // combine items per thread: (lg C + 1) x S_w over the windows (C = nb / S_w buckets per chunk)
     int items = 0;
     for (int w = 0; w < p.lay.nw; w++) {
@@ -1227,6 +1237,10 @@ bool verdicts_all_valid(const uint64_t* bits, size_t n) {
 
 struct nwv_ctx {
     std::vector<Gpu*> devs;
+    // a call splits over the devices only into ranges of at least this many signatures
+    // (shard.h; env NWV_SHARD_MIN, read at nwv_init)
+    size_t shard_min = 16384;
+    size_t b2_shard_min = 4096;  // the same for BLAKE2b digest calls (messages; NWV_B2_SHARD_MIN)
 };
 
 // Per-kernel device time of the staged pipelines (HIP events on the batch's own stream).
@@ -1272,37 +1286,17 @@ struct nwv_staged {
     std::vector<hipEvent_t> marks;  // nwv_staged_mark: step-completion timestamps on this stream
 };
 
-// Shard [0, n) into contiguous, 64-aligned ranges over the context's devices and run fn(dev,
-// lo, hi) on one host thread per device.
+// Shard [0, n) into contiguous, 64-aligned ranges of at least ctx->shard_min signatures over the
+// context's devices (shard.h) and run fn(lane, lo, hi) for each: range 0 on the calling thread, the
+// others on one host thread each.  A call below 2 shard_min runs on device 0 alone.
 template <class Fn>
 static int for_shards(nwv_ctx* ctx, size_t n, Fn fn) {
-    const size_t nd = ctx->devs.size();
-    const size_t words = (n + 63) / 64;
-    const size_t per = (words + nd - 1) / nd;
-    std::vector<int> rcs(nd, NWV_OK);
-    std::vector<std::thread> th;
-    for (size_t k = 0; k < nd; k++) {
-        const size_t lo = std::min(n, k * per * 64), hi = std::min(n, (k + 1) * per * 64);
-        if (lo >= hi) continue;
-        auto run = [&, k, lo, hi]() {
-            LaneRef lane(*ctx->devs[k]);
-            const int rc = lane.rc();
-            rcs[k] = rc ? rc : fn(*lane, lo, hi);
-        };
-        if (nd == 1) {
-            run();
-        } else {
-            try {
-                th.emplace_back(run);
-            } catch (...) {  // no host thread: run this shard inline (never throw across the C ABI)
-                run();
-            }
-        }
-    }
-    for (auto& t : th) t.join();
-    for (int rc : rcs)
-        if (rc) return rc;
-    return NWV_OK;
+    const auto ranges = nwv::ed_shard_ranges(n, ctx->devs.size(), ctx->shard_min);
+    return nwv::for_ranges(ranges, [&](size_t k, size_t lo, size_t hi) -> int {
+        LaneRef lane(*ctx->devs[k]);
+        const int rc = lane.rc();
+        return rc ? rc : fn(*lane, lo, hi);
+    });
 }
 
 extern "C" {
@@ -1310,22 +1304,37 @@ extern "C" {
 int nwv_abi_version(void) { return NWV_ABI_VERSION; }
 const char* nwv_last_error(void) { return g_last_error.c_str(); }
 
+static size_t env_size(const char* name, size_t dflt, size_t lo, size_t hi) {
+    const char* e = std::getenv(name);
+    if (!e || !*e) return dflt;
+    const unsigned long long v = std::strtoull(e, nullptr, 10);
+    return (size_t)std::min<unsigned long long>(hi, std::max<unsigned long long>(lo, v));
+}
+
+// Test hook: env NWV_DEVICE_REPLICAS=r (read at nwv_init, 1..8) opens r independent device
+// objects (own lanes, key cache, basepoint tables) per ordinal, so the multi-device split of
+// for_shards -- ranges, per-range seeds, verdict words at lo / 64, the rc merge -- runs on a
+// one-GPU box exactly as it does over r real devices.
 static int init_devices(nwv_ctx** out, std::vector<int> ordinals, uint32_t flags) {
     if (!out) return set_err(NWV_ERR_ARG, "null out");
     *out = nullptr;
     auto* ctx = new (std::nothrow) nwv_ctx;
     if (!ctx) return set_err(NWV_ERR_OOM, "context allocation");
-    for (int o : ordinals) {
-        auto* d = new Gpu;
-        int rc = gpu_open(*d, o, flags);
-        if (rc) {
-            gpu_close(*d);
-            delete d;
-            nwv_free(ctx);
-            return rc;
+    ctx->shard_min = env_size("NWV_SHARD_MIN", ctx->shard_min, 1, SIZE_MAX);
+    ctx->b2_shard_min = env_size("NWV_B2_SHARD_MIN", ctx->b2_shard_min, 1, SIZE_MAX);
+    const size_t replicas = env_size("NWV_DEVICE_REPLICAS", 1, 1, 8);
+    for (int o : ordinals)
+        for (size_t r = 0; r < replicas; r++) {
+            auto* d = new Gpu;
+            int rc = gpu_open(*d, o, flags);
+            if (rc) {
+                gpu_close(*d);
+                delete d;
+                nwv_free(ctx);
+                return rc;
+            }
+            ctx->devs.push_back(d);
         }
-        ctx->devs.push_back(d);
-    }
     *out = ctx;
     return NWV_OK;
 }
@@ -1462,27 +1471,40 @@ static int batch_on_device(Lane& d, EdBuffers& b, size_t n, const uint8_t seed[3
         // back and waiting for the stream: 1K p50 0.233 -> 0.227 ms (NWV_NO_HOST_POLL: the copy)
         static const bool no_poll = std::getenv("NWV_NO_HOST_POLL") != nullptr;
         uint32_t* hv = (!bits && !no_poll && stream == d.stream && n <= 65536) ? d.hword : nullptr;
-        if (hv) __atomic_store_n(hv, 0u, __ATOMIC_RELEASE);
-        if ((rc = msm_launch(d, b, n, seed, stream, nullptr, state_ready, bits != nullptr, hv))) return rc;
+        uint32_t seq = 0;
+        if (hv) {
+            d.hseq = (d.hseq + 1) & 0x3FFFFFFFu;
+            if (d.hseq == 0) d.hseq = 1;
+            seq = d.hseq;
+            __atomic_store_n(hv, 0u, __ATOMIC_RELEASE);
+        }
+        if ((rc = msm_launch(d, b, n, seed, stream, nullptr, state_ready, bits != nullptr, hv, seq))) {
+            // a launch that failed part-way may have queued work that still stores into the word:
+            // drain the stream so the lane's next call starts clean
+            (void)hipStreamSynchronize(stream);
+            return rc;
+        }
         htrace("batch:msm-launched");
         if (hv) {
-            // spin on the word (a few hundred us at most for the batches that come this way), then
-            // the stream's own completion; a word that never flips (bounded at ~2 s) falls back
-            // to the copy below
+            // spin on the word until it carries this call's sequence number (a few hundred us at
+            // most for the batches that come this way), then the stream's own completion; a word
+            // that never flips (bounded at ~2 s) falls back to the copy below
             uint32_t v = 0;
             const auto t0 = std::chrono::steady_clock::now();
-            for (uint64_t k = 0; (v = __atomic_load_n(hv, __ATOMIC_ACQUIRE)) == 0u; k++) {
+            for (uint64_t k = 0; ((v = __atomic_load_n(hv, __ATOMIC_ACQUIRE)) >> 2) != seq; k++) {
                 if ((k & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
                 __builtin_ia32_pause();
             }
             // the stream's own completion too (by now the tail has stored its last word: this
             // returns at once; without it p99 rose by ~10 us while p50 gained ~2 us)
             NWV_HIP(hipStreamSynchronize(stream));
-            if (v != 0u) {
+            const uint32_t code = (v >> 2) == seq ? (v & 3u) : 0u;
+            if (code == 1u || code == 2u) {
                 htrace("batch:verdict-polled");
-                *ok = v == 1u ? 1 : 0;
+                *ok = code == 1u ? 1 : 0;
                 return NWV_OK;
             }
+            // code 3 (the tail could not determine the verdict) or no word: the state copy below
         }
         if (bits && b.tables_ready) {
             // the early form built the fallback's tables: its Straus pass queues behind the MSM now
@@ -1516,8 +1538,10 @@ static int batch_on_device(Lane& d, EdBuffers& b, size_t n, const uint8_t seed[3
         // a batch of valid signatures always passes (the cofactored equation holds for each term
         // whatever z_i), so a rejection means some signature is invalid: callers that only want
         // the batch verdict (fastcrypto's verify_batch / aggregate verify) get it without the
-        // per-signature pass, which only runs to name the bad signatures
-        if (!bits) {
+        // per-signature pass, which only runs to name the bad signatures.  An undetermined MSM
+        // (st[1] == 2: the tail gave up waiting for a window) is never reported as a rejection:
+        // the per-signature pass decides.
+        if (!bits && st[1] == 0) {
             *ok = 0;
             return NWV_OK;
         }
@@ -1549,7 +1573,6 @@ int nwv_ed25519_verify_batch(nwv_ctx* ctx, size_t n, const uint8_t* pk, const ui
         if (msg_len[i] && !msg_base) return set_err(NWV_ERR_ARG, "null msg_base");
     uint8_t seed[32];
     fill_seed(seed32, seed);
-    std::vector<int> oks(ctx->devs.size(), 1);
     std::mutex omu;
     int rc = for_shards(ctx, n, [&](Lane& d, size_t lo, size_t hi) -> int {
         // each shard gets its own coefficient stream: seed' = seed with the shard start mixed in
@@ -2163,47 +2186,26 @@ int nwv_blake2b256_many(nwv_ctx* ctx, size_t n, const uint8_t* base, const uint6
     if (n == 0) return NWV_OK;
     static const uint8_t empty[1] = {0};
     if (!base) base = empty;
-    const size_t nd = ctx->devs.size();
-    const size_t per = (n + nd - 1) / nd;
-    std::vector<int> rcs(nd, NWV_OK);
-    std::vector<std::thread> th;
-    for (size_t k = 0; k < nd; k++) {
-        const size_t lo = std::min(n, k * per), hi = std::min(n, (k + 1) * per);
-        if (lo >= hi) continue;
-        auto run = [&, k, lo, hi]() {
-            LaneRef lane(*ctx->devs[k]);
-            Lane& d = *lane;
-            std::vector<uint64_t> roff;
-            int rc = lane.rc();
-            B2Staged st{};
-            if (!rc) rc = b2_stage(d, n, base, off, len, lo, hi, roff, st);
-            if (!rc) {
-                const size_t m = hi - lo;
-                uint64_t maxlen = 0;
-                for (size_t k2 = lo; k2 < hi; k2++) maxlen = std::max<uint64_t>(maxlen, len[k2]);
-                b2_launch(d, m, maxlen, st.base, st.off, st.len, d.b2_out.as<uint32_t>());
-                hipError_t e = hipGetLastError();
-                if (e == hipSuccess) e = hipMemcpyAsync(out + 32 * lo, d.b2_out.p, 32 * m,
-                                                        hipMemcpyDeviceToHost, d.stream);
-                if (e == hipSuccess) e = hipStreamSynchronize(d.stream);
-                if (e != hipSuccess) rc = set_err(NWV_ERR_HIP, hipGetErrorString(e));
-            }
-            rcs[k] = rc;
-        };
-        if (nd == 1) {
-            run();
-        } else {
-            try {
-                th.emplace_back(run);
-            } catch (...) {  // no host thread: run this shard inline (never throw across the C ABI)
-                run();
-            }
+    const auto ranges = nwv::shard_ranges(n, ctx->devs.size(), ctx->b2_shard_min, 1);
+    return nwv::for_ranges(ranges, [&](size_t k, size_t lo, size_t hi) -> int {
+        LaneRef lane(*ctx->devs[k]);
+        Lane& d = *lane;
+        std::vector<uint64_t> roff;
+        int rc = lane.rc();
+        B2Staged st{};
+        if (!rc) rc = b2_stage(d, n, base, off, len, lo, hi, roff, st);
+        if (!rc) {
+            const size_t m = hi - lo;
+            uint64_t maxlen = 0;
+            for (size_t k2 = lo; k2 < hi; k2++) maxlen = std::max<uint64_t>(maxlen, len[k2]);
+            b2_launch(d, m, maxlen, st.base, st.off, st.len, d.b2_out.as<uint32_t>());
+            hipError_t e = hipGetLastError();
+            if (e == hipSuccess) e = hipMemcpyAsync(out + 32 * lo, d.b2_out.p, 32 * m, hipMemcpyDeviceToHost, d.stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(d.stream);
+            if (e != hipSuccess) rc = set_err(NWV_ERR_HIP, hipGetErrorString(e));
         }
-    }
-    for (auto& t : th) t.join();
-    for (int rc : rcs)
-        if (rc) return rc;
-    return NWV_OK;
+        return rc;
+    });
 }
 
 int nwv_ed25519_verify_batch_keyed_digests(nwv_ctx* ctx, size_t n_pre, const uint8_t* pre_base,
@@ -2224,8 +2226,9 @@ int nwv_ed25519_verify_batch_keyed_digests(nwv_ctx* ctx, size_t n_pre, const uin
     moff.resize(n);
     mlen.assign(n, 32u);
     for (size_t i = 0; i < n; i++) moff[i] = 32ull * digest_idx[i];
-    if (ctx->devs.size() != 1 || n_pre == 0 || n == 0) {
-        // several devices: the digests come back to the host and the signatures are sharded
+    if (nwv::ed_shard_ranges(n, ctx->devs.size(), ctx->shard_min).size() > 1 || n_pre == 0 || n == 0) {
+        // a batch that splits over several devices: the digests come back to the host and the
+        // signatures are sharded (a smaller one stays fused on device 0, below)
         int rc = nwv_blake2b256_many(ctx, n_pre, pre_base, pre_off, pre_len, digests_out);
         if (rc || n == 0) return rc;
         return nwv_ed25519_verify_batch_keyed(ctx, n_keys, keys, n, key_idx, sig, digests_out, moff.data(),

@@ -222,13 +222,15 @@ def test_c4_adversarial_65536_every_category(eng):
     assert (each == want).all()
 
 
-@pytest.mark.parametrize("forge", ["equation", "none"])
+@pytest.mark.parametrize("forge", ["equation", "decode", "none"])
 def test_early_prep_equals_one_stream_order(eng, forge):
     """a host-staged 65,536 x 512 B batch takes msm_launch's early form (decompressions and the
     fallback's tables on the lane's second stream while the messages cross PCIe, the Straus pass
     gated on the MSM's verdict word).  Forged entries that all decode (message and s bit flips: the
-    MSM rejects at its final sum, not at the prep's early reject) and an all-valid batch: the bits
-    equal the oracle's and those of an engine kept on the one-stream order
+    MSM rejects at its final sum, not at the prep's early reject); entries whose R or A does not
+    decode or whose s >= l (the decode-failure and non-canonical-s flags that k_msm_scalars on the
+    main stream and k_ed_points_msm on the aux stream set in the same flag words); and an all-valid
+    batch: the bits equal the oracle's and those of an engine kept on the one-stream order
     (NWV_FLAG_NO_EARLY_PREP), call after call on the same buffers"""
     import narwhal_amd
     from narwhal_amd import _lib
@@ -243,6 +245,21 @@ def test_early_prep_equals_one_stream_order(eng, forge):
                 msgs[512 * i + 17] ^= 0x04
             else:
                 sg[64 * i + 40] ^= 0x01  # s bit flip (s stays < l: top byte untouched)
+    elif forge == "decode":
+        g = of.load_golden("ed25519_vectors.json")["vectors"]
+        r_bad = [bytes.fromhex(v["sig"])[:32] for v in g if v["category"] == "B7_R_undecodable"]
+        a_bad = [bytes.fromhex(v["pk"]) for v in g if v["category"] == "B7_A_undecodable"]
+        L_ORDER = 2**252 + 27742317777372353535851937790883648493
+        rng = np.random.default_rng(8)
+        forged = sorted(int(x) for x in rng.choice(n, size=30, replace=False))
+        for j, i in enumerate(forged):
+            if j % 3 == 0:
+                sg[64 * i:64 * i + 32] = np.frombuffer(r_bad[j % len(r_bad)], dtype=np.uint8)
+            elif j % 3 == 1:
+                pk[32 * i:32 * i + 32] = np.frombuffer(a_bad[j % len(a_bad)], dtype=np.uint8)
+            else:
+                v = int.from_bytes(sg[64 * i + 32:64 * i + 64].tobytes(), "little") + L_ORDER
+                sg[64 * i + 32:64 * i + 64] = np.frombuffer(v.to_bytes(32, "little"), dtype=np.uint8)
     want = _oracle_bits(pk, sg, msgs, offs, lens)
     assert list(np.flatnonzero(~want)) == forged
     one = narwhal_amd.Engine(device=0, flags=_lib.NWV_FLAG_NO_EARLY_PREP)
