@@ -72,7 +72,7 @@ tools/ubench_wave: tools/ubench_wave.hip $(BLS_SRC)
 tools/ubench_row: tools/ubench_row.hip narwhal_amd/csrc/fe_row.h narwhal_amd/csrc/msm.h
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Wno-unused-value -o $@ $<
 tools/ubench_prep: tools/ubench_prep.hip $(CSRC)
-	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Wno-unused-value -o $@ $<
 
 clean:
 	rm -rf narwhal_amd/lib tests/_build
