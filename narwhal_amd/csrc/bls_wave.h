@@ -137,8 +137,21 @@ NWV_HD void acc_n(const wword* wm, const Rec& r, uint64_t* a) {
 #pragma unroll
         for (int j = 0; j < NL / 2; j++) a[j] += x[u][j] << sh[u];
 }
-template <int BASE>
+// at most G terms' reads in flight at once (8: all of a section's; 4 halves the registers they
+// hold, for the packed pairing kernel, which must fit two waves per SIMD)
+template <int BASE, int G = 8>
 NWV_HD void acc_terms(const wword* wm, const Rec& r, int n, uint64_t* a) {
+    if (G < 8 && n > G) {
+        acc_n<BASE, (G < 8 ? G : 1)>(wm, r, a);
+        switch (n - G) {
+            case 1: acc_n<BASE + G, 1>(wm, r, a); break;
+            case 2: acc_n<BASE + G, 2>(wm, r, a); break;
+            case 3: acc_n<BASE + G, 3>(wm, r, a); break;
+            case 4: acc_n<BASE + G, 4>(wm, r, a); break;
+            default: break;
+        }
+        return;
+    }
     switch (n) {
         case 1: acc_n<BASE, 1>(wm, r, a); break;
         case 2: acc_n<BASE, 2>(wm, r, a); break;
@@ -153,23 +166,24 @@ NWV_HD void acc_terms(const wword* wm, const Rec& r, int n, uint64_t* a) {
 }
 // the limb sums of a combination: positive terms + 2^k p - negative terms (the subtraction per
 // 32-bit limb: with the redundant offset no limb below the top goes negative)
-template <int BASE>
-NWV_HD void comb_sums(const wword* wm, const Rec& r, int np, int nn, uint32_t k1, uint32_t* out) {
+// (kpt: the P << k table, KP_WORDS words; a one-item wave keeps it just below slot 0)
+template <int BASE, int G = 8>
+NWV_HD void comb_sums(const wword* wm, const wword* kpt, const Rec& r, int np, int nn, uint32_t k1, uint32_t* out) {
     uint64_t a[NL / 2];
     if (k1) {
-        const wword2* kp = reinterpret_cast<const wword2*>(wm - KP_WORDS + NL * (k1 - 1));
+        const wword2* kp = reinterpret_cast<const wword2*>(kpt + NL * (k1 - 1));
 #pragma unroll
         for (int j = 0; j < NL / 2; j++) a[j] = kp[j];
     } else {
 #pragma unroll
         for (int j = 0; j < NL / 2; j++) a[j] = 0;
     }
-    acc_terms<BASE>(wm, r, np, a);
+    acc_terms<BASE, G>(wm, r, np, a);
     if (nn) {
         uint64_t b[NL / 2];
 #pragma unroll
         for (int j = 0; j < NL / 2; j++) b[j] = 0;
-        acc_terms<BASE + TMAX>(wm, r, nn, b);
+        acc_terms<BASE + TMAX, G>(wm, r, nn, b);
 #pragma unroll
         for (int j = 0; j < NL / 2; j++) {
             out[2 * j] = (uint32_t)a[j] - (uint32_t)b[j];
@@ -182,6 +196,10 @@ NWV_HD void comb_sums(const wword* wm, const Rec& r, int np, int nn, uint32_t k1
             out[2 * j + 1] = (uint32_t)(a[j] >> 32);
         }
     }
+}
+template <int BASE>
+NWV_HD void comb_sums(const wword* wm, const Rec& r, int np, int nn, uint32_t k1, uint32_t* out) {
+    comb_sums<BASE>(wm, wm - KP_WORDS, r, np, nn, k1, out);
 }
 // normalised limbs (< 2^28): one sequential carry pass (the top limb takes the rest)
 NWV_HD fp carry_seq(const uint32_t* a) {
@@ -235,14 +253,15 @@ NWV_HD fp quick_reduce(const fp& x) {
     return r;
 }
 
-NWV_HD fp lane_value(const wword* wm, const Hdr& h, const Rec& r) {
+template <int G = 8>
+NWV_HD fp lane_value(const wword* wm, const wword* kpt, const Hdr& h, const Rec& r) {
     const uint32_t fl = rec_u16(r, 1);
     uint32_t a[NL];
-    comb_sums<4>(wm, r, h.nap, h.nan, rec_u16(r, 2), a);
+    comb_sums<4, G>(wm, kpt, r, h.nap, h.nan, rec_u16(r, 2), a);
     fp v;
     if (fl & 1) {
         uint32_t b[NL];
-        comb_sums<4 + 2 * TMAX>(wm, r, h.nbp, h.nbn, rec_u16(r, 3), b);
+        comb_sums<4 + 2 * TMAX, G>(wm, kpt, r, h.nbp, h.nbn, rec_u16(r, 3), b);
         v = fp_mul(carry_par(a), carry_par(b));
     } else {
         v = carry_seq(a);
@@ -250,6 +269,41 @@ NWV_HD fp lane_value(const wword* wm, const Hdr& h, const Rec& r) {
     }
     return v;
 }
+NWV_HD fp lane_value(const wword* wm, const Hdr& h, const Rec& r) { return lane_value<8>(wm, wm - KP_WORDS, h, r); }
+
+// ---- the pairing check as one flat script ------------------------------------------------------
+// The throughput kernel (k_blsw_pair_k) runs a whole pairing check as ONE loop over a script of
+// ops instead of one interpreter call per program run: an out-of-line interpreter call saves and
+// restores the callee-saved VGPRs it uses (~100 per lane) through scratch memory on every call, and
+// a check makes a few hundred calls -- that was ~616 KB of scratch writes per item and 31 K VMEM
+// instructions per wave (profiles/round5_bls_pmc_n16384.json).  With the stage loop at
+// one call site the kernel makes no calls in the loop.  Ops: RUN a program `reps` times over; LINES,
+// the Miller loop's next step lines into every bank (prefetched one step ahead); INV, each item's
+// Fp inversion (the final exponentiation's one).  next_run links every op to the next RUN op, so
+// the interpreter loads that op's first lane record while the current op runs.  The script is built
+// from the same templates as pairing_check / final_exp (a recording W), so there is one definition
+// of the sequence.
+enum : uint32_t { SOP_RUN = 0, SOP_LINES = 1, SOP_INV = 2 };
+struct SOp {
+    uint32_t a;         // RUN: program offset; LINES: step; INV: destination slot
+    uint32_t b;         // RUN: stages | first stage's lanes << 16; INV: source slot
+    uint32_t c;         // reps | kind << 16
+    int32_t next_run;   // index of the next RUN op, -1 at the end
+};
+constexpr int SCRIPT_MAX = 512;
+struct ScriptRec {
+    SOp* ops;
+    int* n;
+    void sync() const {}
+    void run(Prog p, int reps = 1) const {
+        if (reps <= 0) return;
+        ops[(*n)++] = SOp{p.off, (uint32_t)p.n | ((uint32_t)p.nl0 << 16), (uint32_t)reps | (SOP_RUN << 16), -1};
+    }
+    void invert_slot(int dst, int src) const {
+        ops[(*n)++] = SOp{(uint32_t)dst, (uint32_t)src, 1u | (SOP_INV << 16), -1};
+    }
+};
+inline uint32_t sop_kind(const SOp& o) { return o.c >> 16; }
 
 #ifdef BLS_WAVE_DEV
 // ---- device: one wave, wm = its LDS slots ------------------------------------------------------
@@ -677,6 +731,27 @@ NWV_HD bool pairing_check(const W& w, const uint32_t* qlines) {
     w.run(P_CONJ_F);
     final_exp(w);
     return w.f_is_one();
+}
+
+// the ops of pairing_check after its set-up (F = 1, TB = QB): the Miller loop with precomputed key
+// lines (fixed) or computed ones, the conjugation, the final exponentiation.  Returns the count.
+inline int pairing_script(bool fixed, SOp* ops) {
+    int n = 0;
+    const ScriptRec w{ops, &n};
+    const char* steps = BLS_WAVE_STEPS_STR;
+    const Prog pd = fixed ? P_ML_DBL_FIXED : P_ML_DBL_STEP, pa = fixed ? P_ML_ADD_FIXED : P_ML_ADD_STEP;
+    for (int k = 0; k < NSTEPS; k++) {
+        ops[n++] = SOp{(uint32_t)k, 0u, 1u | (SOP_LINES << 16), -1};
+        w.run(steps[k] == 'a' ? pa : pd);
+    }
+    w.run(P_CONJ_F);
+    final_exp(w);
+    int nxt = -1;
+    for (int i = n - 1; i >= 0; i--) {
+        ops[i].next_run = nxt;
+        if (sop_kind(ops[i]) == SOP_RUN) nxt = i;
+    }
+    return n;
 }
 
 }  // namespace wave

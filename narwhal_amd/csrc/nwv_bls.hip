@@ -399,20 +399,38 @@ __device__ __forceinline__ void blsw_pair_item(uint32_t* wm, uint32_t i, const u
 // item as blsw_pair_item; an item whose signature or keys failed gets VERIFY_FAIL whatever its bank
 // computed.  Precomputed key lines are used only when every item of the wave has them (the Miller
 // loop's program is one for the wave).
+//
+// The whole check is one loop over the flat script of wave::pairing_script (g_pair_script, one per
+// line mode): the stage loop below is the kernel's only copy of the interpreter and the loop makes
+// no calls, so no callee-saved registers go through scratch (round 5's out-of-line wave_run_k
+// wrote ~616 KB of scratch per item).  The banks share one P << k table at the front of the LDS
+// (9.6 KB a bank instead of 10.5 KB).
 constexpr int BLS_PACK_MAX = 4;
-__global__ __launch_bounds__(64) void k_blsw_pair_k(uint32_t n, uint32_t kper, const uint32_t* srec,
-                                                    const int32_t* st_dec, const uint32_t* hrec, int h_hom,
-                                                    const uint32_t* arec, const int32_t* st_apk, KeyTab kt,
-                                                    const uint32_t* pk_off, const uint32_t* pk_cnt,
-                                                    const uint32_t* pk_idx, const uint32_t* kmode, int32_t* st_pair) {
+__device__ wave::SOp g_pair_script[2][wave::SCRIPT_MAX];  // [fixed key lines]
+__device__ int g_pair_script_n[2];
+// two waves per SIMD (<= 256 registers: at most 4 terms' LDS reads in flight, NWV_BLS_PAIR_TERMS)
+// with two items a wave (NWV_BLS_PACK: 2 x 9.6 KB banks + the shared 0.9 KB table = 8 waves per
+// CU): 16,384 checks 23.5 -> 17.8 ms against one wave per SIMD with three items
+// (profiles/round6_bls_pair_sweep.txt)
+#ifndef NWV_BLS_PAIR_WAVES
+#define NWV_BLS_PAIR_WAVES 2
+#endif
+#ifndef NWV_BLS_PAIR_TERMS
+#define NWV_BLS_PAIR_TERMS 4
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NWV_BLS_PAIR_WAVES))) void k_blsw_pair_k(
+    uint32_t n, uint32_t kper, const uint32_t* srec, const int32_t* st_dec, const uint32_t* hrec, int h_hom,
+    const uint32_t* arec, const int32_t* st_apk, KeyTab kt, const uint32_t* pk_off, const uint32_t* pk_cnt,
+    const uint32_t* pk_idx, const uint32_t* kmode, int32_t* st_pair) {
     using namespace wave;
     extern __shared__ uint32_t lds_k[];
     const int lane = (int)threadIdx.x;
     const uint32_t i0 = blockIdx.x * kper;
     if (i0 >= n) return;
     const int k = (int)(n - i0 < kper ? n - i0 : kper);
-    const uint32_t bankw = (uint32_t)WM_WORDS_PC;
+    constexpr uint32_t bankw = (uint32_t)(SW * NSLOTS_PC);
     const WaveK w{lds_k + KP_WORDS, bankw, k, lane};
+    const wword* kpt = (const wword*)lds_k;  // the shared P << k table
     const uint32_t* sig[BLS_PACK_MAX];
     const uint32_t* hr[BLS_PACK_MAX];
     const uint32_t* ql[BLS_PACK_MAX];
@@ -424,8 +442,12 @@ __global__ __launch_bounds__(64) void k_blsw_pair_k(uint32_t n, uint32_t kper, c
         ql[j] = (kt.lines && kmode && kmode[i] && pk_cnt[i] == 1) ? kt.lines + KL_WORDS * pk_idx[pk_off[i]] : nullptr;
         fixed = fixed && ql[j] != nullptr;
     }
-    // every bank: slot 0, the pairing check's constants, P << k below slot 0; then each item's points
-    for (int j = 0; j < k; j++) init_slots_pc(Wave{w.bk(j), lane});
+    // P << k once, then every bank: slot 0 = 0, the pairing check's constants at slots 1..
+    for (int t = lane; t < KP_WORDS; t += 64) lds_k[t] = (&T_KP[0][0])[t];
+    for (int j = 0; j < k; j++) {
+        if (lane < SW) w.bk(j)[lane] = 0u;
+        for (int t = lane; t < SW * NCONSTS_PC; t += 64) w.bk(j)[SW + t] = (&T_CONSTS[0][0])[t];
+    }
     w.zero(REG_PA, 2);
     w.zero(REG_PB, 3);
     w.zero(REG_QB, 6);
@@ -442,13 +464,12 @@ __global__ __launch_bounds__(64) void k_blsw_pair_k(uint32_t n, uint32_t kper, c
         w.put_words(j, REG_QB, arec + (size_t)G2J_WORDS * i, 6);
     }
     w.sync();
-    // wave::pairing_check over the k banks
+    // wave::pairing_check's set-up over the k banks
     w.zero(REG_F, 12);
     w.sync();
     w.put_fp(-1, REG_F, k_one());
     w.copy_slots(REG_TB, REG_QB, 6);
     w.sync();
-    const char* steps = BLS_WAVE_STEPS_STR;
     constexpr int LW = 6 * SW;  // words of a step's line
     // the next step's lines load while this step runs: g2's (every bank) and each item's key lines
     uint32_t la0 = 0, la1 = 0, lb0[BLS_PACK_MAX], lb1[BLS_PACK_MAX];
@@ -467,30 +488,96 @@ __global__ __launch_bounds__(64) void k_blsw_pair_k(uint32_t n, uint32_t kper, c
         }
     };
     fetch(0);
+    const SOp* script = g_pair_script[fixed ? 1 : 0];
+    const int nops = g_pair_script_n[fixed ? 1 : 0];
+    auto first_rec = [&](const SOp& o) { return load_rec(T_DATA + o.a + (uint32_t)(lane % (int)(o.b >> 16)) * REC); };
+    Rec cur = first_rec(script[0].c >> 16 == SOP_RUN ? script[0] : script[script[0].next_run]);
+    int step = 0;
 #pragma unroll 1
-    for (int st = 0; st < NSTEPS; st++) {
-        for (int j = 0; j < k; j++) {
-            uint32_t* b = w.bk(j);
-            if (lane < LW) b[SW * REG_LA + lane] = la0;
-            if (lane + 64 < LW) b[SW * REG_LA + lane + 64] = la1;
-            if (fixed) {
-                if (lane < LW) b[SW * REG_LB + lane] = lb0[j];
-                if (lane + 64 < LW) b[SW * REG_LB + lane + 64] = lb1[j];
+    for (int oi = 0; oi < nops; oi++) {
+        const SOp op = script[oi];
+        const uint32_t kind = op.c >> 16;
+        if (kind == SOP_LINES) {
+            for (int j = 0; j < k; j++) {
+                uint32_t* b = w.bk(j);
+                if (lane < LW) b[SW * REG_LA + lane] = la0;
+                if (lane + 64 < LW) b[SW * REG_LA + lane + 64] = la1;
+                if (fixed) {
+                    if (lane < LW) b[SW * REG_LB + lane] = lb0[j];
+                    if (lane + 64 < LW) b[SW * REG_LB + lane + 64] = lb1[j];
+                }
             }
+            w.sync();
+            if (step + 1 < NSTEPS) fetch(step + 1);
+            step++;
+            continue;
         }
-        w.sync();
-        if (st + 1 < NSTEPS) fetch(st + 1);
-        const Prog pd = fixed ? P_ML_DBL_FIXED : P_ML_DBL_STEP, pa = fixed ? P_ML_ADD_FIXED : P_ML_ADD_STEP;
-        w.run(steps[st] == 'a' ? pa : pd);
+        if (kind == SOP_INV) {
+            w.invert_slot((int)op.a, (int)op.b);
+            w.sync();
+            continue;
+        }
+        // RUN: the program's stages, `reps` times over (wave_run_k's loop, inline: the one copy)
+        const uint16_t* base0 = T_DATA + op.a;
+        const uint16_t* base = base0;
+        const int np = (int)(op.b & 0xffffu), nl0 = (int)(op.b >> 16), total = np * (int)(op.c & 0xffffu);
+        int nl = nl0;
+#pragma unroll 1
+        for (int t = 0, s = 0; t < total; t++) {
+            Hdr h = rec_hdr(cur);
+            h.nap = __builtin_amdgcn_readfirstlane(h.nap);
+            h.nan = __builtin_amdgcn_readfirstlane(h.nan);
+            h.nbp = __builtin_amdgcn_readfirstlane(h.nbp);
+            h.nbn = __builtin_amdgcn_readfirstlane(h.nbn);
+            const bool wrap = s + 1 == np;
+            const int nl_next = wrap ? nl0 : __builtin_amdgcn_readfirstlane(h.nl_next);
+            const uint16_t* nbase = wrap ? base0 : base + (uint32_t)nl * REC;
+            // the next stage's record, or the next RUN op's first one (records are static data)
+            Rec nxt = cur;
+            if (t + 1 < total) nxt = load_rec(nbase + (uint32_t)(lane % nl_next) * REC);
+            else if (op.next_run >= 0) nxt = first_rec(script[op.next_run]);
+            const int ipp = 64 / nl, first = lane / nl;
+            if (first < ipp) {
+                const uint32_t dst = rec_u16(cur, 0);
+#pragma unroll 1
+                for (int item = first; item < k; item += ipp) {
+                    wword* wm = (wword*)w.bk(item);
+                    const fp v = lane_value<NWV_BLS_PAIR_TERMS>(wm, kpt, h, cur);
+#pragma unroll
+                    for (int j = 0; j < NL; j++) wm[SW * dst + j] = v.l[j];
+                }
+            }
+            wsync();
+            base = nbase;
+            nl = nl_next;
+            cur = nxt;
+            s = wrap ? 0 : s + 1;
+        }
     }
-    w.run(P_CONJ_F);
-    final_exp(w);
     const uint32_t ok = w.f_is_one_mask();
     if (lane == 0)
         for (int j = 0; j < k; j++) {
             const uint32_t i = i0 + j;
             st_pair[i] = (st_dec[i] == ST_OK && st_apk[i] == ST_OK && ((ok >> j) & 1u)) ? ST_OK : ST_VERIFY_FAIL;
         }
+}
+// the flat scripts into g_pair_script on the calling thread's device, once per device
+static int ensure_pair_script() {
+    static std::mutex mu;
+    static bool done[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
+        return nwv_internal_set_err(NWV_ERR_HIP, "pair script: no device");
+    std::lock_guard<std::mutex> g(mu);
+    if (done[dev]) return NWV_OK;
+    static wave::SOp ops[2][wave::SCRIPT_MAX];
+    int cnt[2];
+    for (int f = 0; f < 2; f++) cnt[f] = wave::pairing_script(f != 0, ops[f]);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_pair_script), ops, sizeof(ops)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(g_pair_script_n), cnt, sizeof(cnt)) != hipSuccess)
+        return nwv_internal_set_err(NWV_ERR_HIP, "pair script copy");
+    done[dev] = true;
+    return NWV_OK;
 }
 __global__ __launch_bounds__(64) void k_blsw_pair(uint32_t n, const uint32_t* srec, const int32_t* st_dec,
                                                   const uint32_t* hrec, int h_hom, const uint32_t* arec,
@@ -1369,10 +1456,10 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
         BLS_HIP(hipStreamWaitEvent(s0, L.ev[10], 0));
         BLS_HIP(hipStreamWaitEvent(s0, L.ev[11], 0));
         BLS_HIP(hipEventRecord(L.ev[7], s0));
-        // items per pairing wave (env NWV_BLS_PACK, 1..4): one LDS bank of ~10.5 KB each
+        // items per pairing wave (env NWV_BLS_PACK, 1..4): one LDS bank of ~9.6 KB each
         static const uint32_t pack = [] {
             const char* e = std::getenv("NWV_BLS_PACK");
-            const long v = e ? std::strtol(e, nullptr, 10) : 3;
+            const long v = e ? std::strtol(e, nullptr, 10) : 2;
             return (uint32_t)(v < 1 ? 1 : v > BLS_PACK_MAX ? BLS_PACK_MAX : v);
         }();
         // diagnostic (occupancy experiments): NWV_BLS_LDS_PAD bytes of extra LDS per pairing wave
@@ -1380,9 +1467,10 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
             const char* e = std::getenv("NWV_BLS_LDS_PAD");
             return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)0;
         }();
+        if (pack > 1 && ensure_pair_script()) return NWV_ERR_HIP;
         if (pack > 1)
             hipLaunchKernelGGL(k_blsw_pair_k, dim3((unsigned)((n + pack - 1) / pack)), dim3(64),
-                               (size_t)4 * pack * wave::WM_WORDS_PC + lds_pad, s0,
+                               (size_t)4 * (wave::KP_WORDS + pack * wave::SW * wave::NSLOTS_PC) + lds_pad, s0,
                                (uint32_t)n, pack, (const uint32_t*)srec, (const int32_t*)sdec, (const uint32_t*)hrec, 0,
                                (const uint32_t*)ajrec, (const int32_t*)sapk, kt,
                                reinterpret_cast<const uint32_t*>(in + o_off), reinterpret_cast<const uint32_t*>(in + o_cnt),

@@ -355,6 +355,77 @@ int bh_w_pc_fast_aggregate_verify(const uint8_t* sig, size_t n_pks, const uint8_
     return ok ? ST_OK : ST_VERIFY_FAIL;
 }
 
+// the packed kernel's flat script (wave::pairing_script, k_blsw_pair_k): the same set-up as
+// bh_w_pc_fast_aggregate_verify, then the script's ops on the host wave -- RUN a program, LINES
+// the step's lines into LA (g2's) and LB (the key's table, fixed mode), INV the inversion -- and
+// F == 1.  mode 1 = computed lines, 2 = the key's line table.  Returns the status; *n_ops the
+// script's length.
+int bh_w_script_fast_aggregate_verify(const uint8_t* sig, size_t n_pks, const uint8_t* pks, const uint8_t* msg,
+                                      size_t n, const uint8_t* dst, size_t dl, int mode, int* n_ops) {
+    using namespace wave;
+    int32_t st = bh_w_sig_status(sig);
+    if (st != ST_OK) return st;
+    uint32_t srec[G1_REC_WORDS], hrec[G1H_REC_WORDS], arec[G2_REC_WORDS];
+    fp x, y;
+    bool inf;
+    g1_decompress(x, y, inf, sig);
+    st_g1(srec, inf ? fp_zero() : x, inf ? fp_zero() : y, inf);
+    if (n_pks == 0) return ST_AGGR_MISMATCH;
+    std::vector<uint32_t> krec(G2_REC_WORDS * n_pks), idx(n_pks);
+    std::vector<int32_t> kst(n_pks);
+    for (size_t i = 0; i < n_pks; i++) {
+        kst[i] = key_decode(pks + 96 * i, krec.data() + G2_REC_WORDS * i);
+        idx[i] = (uint32_t)i;
+    }
+    st = apk_record(krec.data(), kst.data(), idx.data(), (uint32_t)n_pks, arec);
+    if (st != ST_OK) return st;
+    const Wave full = host_wave();
+    w_hash_to_g1(full, msg, (uint32_t)n, dst, (uint32_t)dl, hrec);
+    std::vector<uint32_t> tab;
+    const bool fixed = mode == 2;
+    if (fixed) {
+        tab.resize((size_t)NSTEPS * 6 * NL);
+        w_key_lines(full, arec, tab.data());
+    }
+    std::vector<uint32_t> bank(WM_WORDS_PC, 0);
+    Wave w;
+    w.wm = bank.data() + KP_WORDS;
+    init_slots_pc(w);
+    w.zero(REG_PA, 2);
+    w.zero(REG_PB, 3);
+    w.zero(REG_QB, 6);
+    if (!srec[2 * NL]) {
+        w.put_words(REG_PA, srec, 1);
+        w.put_fp(REG_PA + 1, fp_neg(ld_fp(srec + NL)));
+    }
+    if (!hrec[3 * NL]) w.put_words(REG_PB, hrec, 3);
+    else w.put_fp(REG_PB + 2, k_one());
+    w.put_words(REG_QB, arec, 4);
+    w.put_fp(REG_QB + 4, k_one());
+    w.zero(REG_F, 12);
+    w.put_fp(REG_F, k_one());
+    w.copy_slots(REG_TB, REG_QB, 6);
+    static SOp ops[SCRIPT_MAX];
+    const int cnt = pairing_script(fixed, ops);
+    *n_ops = cnt;
+    for (int i = 0; i < cnt; i++) {
+        const SOp& o = ops[i];
+        if (sop_kind(o) == SOP_LINES) {
+            w.put_words(REG_LA, &T_G2_LINES[o.a][0][0], 6);
+            if (fixed) w.put_words(REG_LB, tab.data() + (size_t)o.a * 6 * NL, 6);
+        } else if (sop_kind(o) == SOP_INV) {
+            w.invert_slot((int)o.a, (int)o.b);
+        } else {
+            // next_run must name the next RUN op
+            int j = i + 1;
+            while (j < cnt && sop_kind(ops[j]) != SOP_RUN) j++;
+            if (o.next_run != (j < cnt ? j : -1)) return -2000;
+            w.run(Prog{o.a, (uint16_t)(o.b & 0xffffu), (uint16_t)(o.b >> 16)}, (int)(o.c & 0xffffu));
+        }
+    }
+    return w.f_is_one() ? ST_OK : ST_VERIFY_FAIL;
+}
+
 // the variable-time inversion of the wave engine's final exponentiation (plain big-endian in / out)
 void bh_fp_inv_vt(const uint8_t* a, uint8_t* out) {
     fp x;

@@ -357,3 +357,30 @@ def test_wave_pairing_on_pc_bank(emu):
                                                     len(B.DST_NUL), mode)
             assert got != -1000, "a pairing-check program addressed a slot past NSLOTS_PC"
             assert got == want, (mode, len(ks))
+
+
+def test_wave_flat_pairing_script(emu):
+    """the packed pairing kernel runs one flat script (wave::pairing_script: the Miller loop's line
+    loads and programs, the conjugation, the final exponentiation's programs and inversion) in one
+    interpreter loop instead of an out-of-line call per program; the script, replayed op by op on
+    the host wave, gives the oracle's statuses with computed and with precomputed key lines"""
+    import ctypes
+    emu.bh_w_script_fast_aggregate_verify.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                                      ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                                      ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    rnd = random.Random(73)
+    sks = [rnd.randrange(1, r).to_bytes(32, "big") for _ in range(3)]
+    pks = [B.keygen(k)[1] for k in sks]
+    m = rnd.randbytes(32)
+    _, agg = B.aggregate([B.sign(k, m) for k in sks])
+    one = B.sign(sks[0], m)
+    for sig, ks, msg in [(agg, pks, m), (agg, pks, m + b"?"), (one, pks[:1], m), (one, pks[1:2], m),
+                         (C.IDENTITY_G1, pks, m)]:
+        want = B.fast_aggregate_verify(sig, ks, msg)
+        for mode in (1, 2):
+            nops = ctypes.c_int(0)
+            got = emu.bh_w_script_fast_aggregate_verify(sig, len(ks), b"".join(ks), msg, len(msg), B.DST_NUL,
+                                                        len(B.DST_NUL), mode, ctypes.byref(nops))
+            assert got != -2000, "a RUN op's next_run link is wrong"
+            assert got == want, (mode, len(ks))
+            assert 2 * 68 < nops.value <= 512
