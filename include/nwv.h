@@ -86,6 +86,10 @@ typedef struct nwv_ctx nwv_ctx;
 /* diagnostic / tests: a keyed batch MSM whose hashes fit one k_msm_prep workgroup sums its keys'
  * scalars in that workgroup (no k_msm_keysum launch); this flag keeps the separate launch */
 #define NWV_FLAG_NO_FUSED_KEYSUM 2048u
+/* diagnostic / tests: a keyed batch of at most 64 signatures whose keys were all registered
+ * (nwv_keycache_register: each key gets a fixed-base comb table) is checked in one launch,
+ * signature by signature (k_ed_tiny); this flag sends it through the batch MSM instead */
+#define NWV_FLAG_NO_TINY 4096u
 
 /* ------------------------------------------------------------------ lifecycle ----- */
 /* Process-wide context creation (created once, in Primary::spawn).
@@ -95,6 +99,10 @@ int nwv_init(nwv_ctx** out, int n_devices, uint32_t flags);
 int nwv_init_device(nwv_ctx** out, int device_ordinal, uint32_t flags);
 void nwv_free(nwv_ctx* ctx);
 int nwv_device_count(const nwv_ctx* ctx);
+/* Diagnostics: how the context's batch calls ran so far, summed over its devices: out[0] keyed
+ * batches checked by the one-launch path (k_ed_tiny), out[1] batch MSMs, out[2] per-signature
+ * passes (verify_each, or after a rejected MSM when verdict bits were asked for). */
+int nwv_diag_counters(const nwv_ctx* ctx, uint64_t out[3]);
 /* HIP ordinal of the context's i-th device (-1 if out of range) */
 int nwv_device_ordinal(const nwv_ctx* ctx, int i);
 int nwv_abi_version(void);
@@ -151,8 +159,11 @@ int nwv_ed25519_verify_batch_keyed_digests(nwv_ctx* ctx, size_t n_pre, const uin
 /* Fill every device's committee key cache with n_keys keys (n_keys x 32), e.g. at epoch start
  * (Core::change_epoch, primary/src/core.rs:592-611).  Batch calls fill the cache themselves;
  * nwv_ed25519_pubkey_verify only looks its key up (an unseen key runs uncached and takes no
- * slot), so registering the committee gives its members' single verifies the cached form.  A
- * full cache leaves further keys uncached; verdicts never depend on the cache. */
+ * slot), so registering the committee gives its members' single verifies the cached form.  Each
+ * registered key also gets a fixed-base comb table (i 16^j A, 64 KiB), which sends keyed batches
+ * of at most 64 signatures by registered keys -- Certificate::verify, Header::verify,
+ * Vote::verify -- through the one-launch path.  Registering the same key list again is a no-op.
+ * A full cache leaves further keys uncached; verdicts never depend on the cache. */
 int nwv_keycache_register(nwv_ctx* ctx, size_t n_keys, const uint8_t* keys);
 
 /* ---- fastcrypto 0.1.2 trait surface (Ed25519 scheme module; contract of

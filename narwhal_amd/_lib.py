@@ -35,6 +35,7 @@ NWV_FLAG_NO_SIGCACHE = 256
 NWV_FLAG_NO_ROW_PREP = 512
 NWV_FLAG_NO_EARLY_PREP = 1024
 NWV_FLAG_NO_FUSED_KEYSUM = 2048
+NWV_FLAG_NO_TINY = 4096
 NWV_RUN_TIMED = 0x100
 
 
@@ -63,6 +64,7 @@ def load():
         "nwv_init_device": ([ctypes.POINTER(_vp), _i32, ctypes.c_uint32], _i32),
         "nwv_free": ([_vp], None),
         "nwv_device_count": ([_vp], _i32),
+        "nwv_diag_counters": ([_vp, _vp], _i32),
         "nwv_abi_version": ([], _i32),
         "nwv_last_error": ([], ctypes.c_char_p),
         "nwv_ed25519_verify_each": ([_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp], _i32),
@@ -201,6 +203,17 @@ class Engine:
     @property
     def device_count(self):
         return self.lib.nwv_device_count(self._h)
+
+    def diag_counters(self):
+        """{'tiny': one-launch keyed batches, 'msm': batch MSMs, 'each': per-signature passes}"""
+        out = np.zeros(3, dtype=np.uint64)
+        _check(self.lib.nwv_diag_counters(self._h, out.ctypes.data))
+        return {"tiny": int(out[0]), "msm": int(out[1]), "each": int(out[2])}
+
+    def keycache_register(self, keys):
+        """nwv_keycache_register: keys, a list of 32-byte keys (the committee, at epoch start)"""
+        kb = np.frombuffer(b"".join(keys) or b"\0", dtype=np.uint8)
+        _check(self.lib.nwv_keycache_register(self._h, len(keys), _ptr(kb)))
 
     # ---- Ed25519 ---------------------------------------------------------------------
     def verify_each_arrays(self, pk, sig, arena, offs, lens):

@@ -12,9 +12,10 @@
 
 using namespace nwv;
 
+// out2 (optional): a second copy of the digests (coherent pinned host memory: no copy back)
 extern "C" __global__ void __launch_bounds__(256) k_blake2b_many(
     uint64_t n, const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
-    const uint64_t* __restrict__ len, uint32_t* __restrict__ out) {
+    const uint64_t* __restrict__ len, uint32_t* __restrict__ out, uint32_t* __restrict__ out2) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint8_t* p = base + off[i];
@@ -39,6 +40,11 @@ extern "C" __global__ void __launch_bounds__(256) k_blake2b_many(
     uint4* o = reinterpret_cast<uint4*>(out + 8 * i);
     o[0] = make_uint4(d[0], d[1], d[2], d[3]);
     o[1] = make_uint4(d[4], d[5], d[6], d[7]);
+    if (out2) {
+        uint4* o2 = reinterpret_cast<uint4*>(out2 + 8 * i);
+        o2[0] = make_uint4(d[0], d[1], d[2], d[3]);
+        o2[1] = make_uint4(d[4], d[5], d[6], d[7]);
+    }
 }
 
 // ---- long messages: 4 lanes per message --------------------------------------------------
@@ -100,7 +106,7 @@ __device__ __forceinline__ uint64_t iv64(int k) {
 
 extern "C" __global__ void __launch_bounds__(64) k_blake2b_quad(
     uint64_t n, const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
-    const uint64_t* __restrict__ len, uint32_t* __restrict__ out) {
+    const uint64_t* __restrict__ len, uint32_t* __restrict__ out, uint32_t* __restrict__ out2) {
     __shared__ uint64_t blk[16][16];
     const int lane = threadIdx.x, q = lane & 3, slot = lane >> 2;
     const uint64_t i = (uint64_t)blockIdx.x * 16 + slot;
@@ -181,6 +187,10 @@ extern "C" __global__ void __launch_bounds__(64) k_blake2b_quad(
     if (active) {
         out[8 * i + 2 * q] = (uint32_t)h0;
         out[8 * i + 2 * q + 1] = (uint32_t)(h0 >> 32);
+        if (out2) {
+            out2[8 * i + 2 * q] = (uint32_t)h0;
+            out2[8 * i + 2 * q + 1] = (uint32_t)(h0 >> 32);
+        }
     }
 }
 

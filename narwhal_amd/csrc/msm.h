@@ -211,13 +211,9 @@ NWV_HD void msm_split128(const uint32_t s[8], uint32_t lo[8], uint32_t hi[8]) {
 // so [8]([b]B) = [8 b mod l]B.)
 static constexpr int COMB_TABLES = 64, COMB_ENTRIES = 8;
 
-// i 16^j B (1 <= i <= 8) as an MSM point record (affine Niels)
-NWV_HD void comb_entry(int j, int i, uint32_t* e) {
-    uint32_t bw[8];
-    ge_basepoint_words(bw);
-    ge_p3 B;
-    ge_decompress(bw, B);
-    ge_p3 Q = j ? p3_dbl_n(B, 4 * j) : B;
+// i 16^j P (1 <= i <= 8) as an MSM point record (affine Niels)
+NWV_HD void comb_entry_of(const ge_p3& P, int j, int i, uint32_t* e) {
+    ge_p3 Q = j ? p3_dbl_n(P, 4 * j) : P;
     const ge_cached cq = ge_p3_to_cached(Q);
     ge_p3 acc = ge_p3_identity();
     for (int bit = 3; bit >= 0; bit--) {
@@ -229,6 +225,14 @@ NWV_HD void comb_entry(int j, int i, uint32_t* e) {
     store_fe(e + 10, q.ymx);
     store_fe(e + 20, q.xy2d);
     e[30] = e[31] = 0u;
+}
+// i 16^j B
+NWV_HD void comb_entry(int j, int i, uint32_t* e) {
+    uint32_t bw[8];
+    ge_basepoint_words(bw);
+    ge_p3 B;
+    ge_decompress(bw, B);
+    comb_entry_of(B, j, i, e);
 }
 
 // signed radix-16 digits of c < 2^253: c = sum_{j < 64} d_j 16^j, d_j in [-8, 8)  (d_63 <= 2)
@@ -345,6 +349,8 @@ NWV_HD uint32_t msm_unpack2_entry(uint32_t e, int shift) {
 // padded to 32 words = 128 bytes so a bucket lane's random gather touches one cache line; a
 // negative digit swaps y+x / y-x and negates 2dxy on the fly.
 static constexpr int MSM_PT_WORDS = 32;
+// words of one point's comb table (COMB_TABLES x COMB_ENTRIES records: i 16^j P)
+static constexpr int COMB_WORDS = MSM_PT_WORDS * COMB_TABLES * COMB_ENTRIES;
 
 NWV_HD void msm_store_point(uint32_t* e, const ge_p3& p) {
     store_fe(e, fe_carry(fe_add(p.Y, p.X)));

@@ -350,19 +350,12 @@ __device__ __forceinline__ void msm_points_block(uint32_t blk, const MsmPointArg
 // through 48 words of LDS per row.  The call launches k_msm_prep with 64-thread workgroups: four
 // such waves on one CU (one per SIMD) decompressed in 62 us against 52 us for single-wave
 // workgroups spread over the chip (512 waves, tools/ubench_prep.hip, profiles/round5_ubench_prep.jsonl).
-__device__ __forceinline__ void msm_points_rows_block(uint32_t blk, const MsmPointArgs& g) {
 #if defined(__HIP_DEVICE_COMPILE__)  // (rowf's lane type is the host emulation's wave elsewhere)
-    __shared__ uint32_t rl[4 * 192];  // per wave: 4 rows x 48 words
-    const uint64_t n = g.n, na = g.na, tot = n + g.ndec;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, row = lane >> 4, limb = lane & 15;
-    const uint64_t wave = (uint64_t)blk * (blockDim.x >> 6) + wv;  // 4 points per wave
-    if (wave * 4 >= tot) return;                                   // whole wave past the end (wave-uniform)
-    uint32_t* sh = rl + 192 * wv + 48 * row;                       // this row's 48 words
-    const uint64_t j = wave * 4 + row;
-    const bool live = j < tot;
-    // limb `limb` of the encoding; its bit 255 (the sign of x) cleared, kept per row
-    uint32_t y16 = 0u;
-    if (live) y16 = reinterpret_cast<const uint16_t*>(j < n ? g.sig + 64 * j : g.apk + 32 * (j - n))[limb];
+// ge_decompress on the 16-lane row that holds limb `limb` of an encoding in y16 (bit 15 of limb 15
+// is x's sign): leaves the affine Niels record -- y + x, y - x, 2 d x y as 16-limb rows -- in
+// sh[0, 48) (this row's 48 words of LDS) and returns whether the encoding decodes (row-uniform).
+// Every lane of the wave calls it (the products are DPP row operations).
+__device__ __forceinline__ bool row_decompress(uint32_t y16, int lane, int row, int limb, uint32_t* sh) {
     const bool sign = (__shfl(y16, (lane & ~15) + 15) >> 15) != 0u;
     if (limb == 15) y16 &= 0x7FFFu;
     rowf::RowConsts k = rowf::row_consts();
@@ -397,6 +390,24 @@ __device__ __forceinline__ void msm_points_rows_block(uint32_t blk, const MsmPoi
     sh[16 + limb] = ymx;
     sh[32 + limb] = xy2d;
     rowf::lds_order();
+    return ok;
+}
+#endif
+
+__device__ __forceinline__ void msm_points_rows_block(uint32_t blk, const MsmPointArgs& g) {
+#if defined(__HIP_DEVICE_COMPILE__)  // (rowf's lane type is the host emulation's wave elsewhere)
+    __shared__ uint32_t rl[4 * 192];  // per wave: 4 rows x 48 words
+    const uint64_t n = g.n, na = g.na, tot = n + g.ndec;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, row = lane >> 4, limb = lane & 15;
+    const uint64_t wave = (uint64_t)blk * (blockDim.x >> 6) + wv;  // 4 points per wave
+    if (wave * 4 >= tot) return;                                   // whole wave past the end (wave-uniform)
+    uint32_t* sh = rl + 192 * wv + 48 * row;                       // this row's 48 words
+    const uint64_t j = wave * 4 + row;
+    const bool live = j < tot;
+    // limb `limb` of the encoding (bit 255: the sign of x)
+    uint32_t y16 = 0u;
+    if (live) y16 = reinterpret_cast<const uint16_t*>(j < n ? g.sig + 64 * j : g.apk + 32 * (j - n))[limb];
+    const bool ok = row_decompress(y16, lane, row, limb, sh);
     if (live && limb < 3) {
         uint32_t* e = g.pts + (size_t)MSM_PT_WORDS * (j < n ? na + 1 + j : j - n);
         store_fe(e + 10 * limb, fe_from_limbs16(sh + 16 * limb));

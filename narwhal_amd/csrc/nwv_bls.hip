@@ -418,16 +418,23 @@ __device__ int g_pair_script_n[2];
 #ifndef NWV_BLS_PAIR_TERMS
 #define NWV_BLS_PAIR_TERMS 4
 #endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NWV_BLS_PAIR_WAVES))) void k_blsw_pair_k(
-    uint32_t n, uint32_t kper, const uint32_t* srec, const int32_t* st_dec, const uint32_t* hrec, int h_hom,
-    const uint32_t* arec, const int32_t* st_apk, KeyTab kt, const uint32_t* pk_off, const uint32_t* pk_cnt,
-    const uint32_t* pk_idx, const uint32_t* kmode, int32_t* st_pair) {
+// x / d and x % d for 0 <= x <= 64 and a wave-uniform 1 <= d <= 64 without a division sequence:
+// x ceil(2^16 / d) >> 16 is exact there (the error x (ceil(2^16/d) - 2^16/d) / 2^16 < 1/1024 < 1/d)
+__constant__ const uint32_t k_div_magic[65] = {0, 65536, 32768, 21846, 16384, 13108, 10923, 9363, 8192, 7282, 6554, 5958, 5462, 5042, 4682, 4370, 4096, 3856, 3641, 3450, 3277, 3121, 2979, 2850, 2731, 2622, 2521, 2428, 2341, 2260, 2185, 2115, 2048, 1986, 1928, 1873, 1821, 1772, 1725, 1681, 1639, 1599, 1561, 1525, 1490, 1457, 1425, 1395, 1366, 1338, 1311, 1286, 1261, 1237, 1214, 1192, 1171, 1150, 1130, 1111, 1093, 1075, 1058, 1041, 1024};  // ceil(2^16 / d)
+__device__ __forceinline__ int lane_div(int x, int d) {
+    const uint32_t m = k_div_magic[__builtin_amdgcn_readfirstlane(d)];
+    return (int)(((uint32_t)x * m) >> 16);
+}
+__device__ __forceinline__ int lane_mod(int x, int d) { return x - lane_div(x, d) * d; }
+// items [i0, i0 + k) on this wave: lds_k = the P << k table, then k banks; G: term reads in flight
+template <int G>
+__device__ __forceinline__ void pair_flat(uint32_t* lds_k, uint32_t i0, int k, const uint32_t* srec,
+                                          const int32_t* st_dec, const uint32_t* hrec, int h_hom,
+                                          const uint32_t* arec, const int32_t* st_apk, const KeyTab& kt,
+                                          const uint32_t* pk_off, const uint32_t* pk_cnt, const uint32_t* pk_idx,
+                                          const uint32_t* kmode, int32_t* st_pair) {
     using namespace wave;
-    extern __shared__ uint32_t lds_k[];
     const int lane = (int)threadIdx.x;
-    const uint32_t i0 = blockIdx.x * kper;
-    if (i0 >= n) return;
-    const int k = (int)(n - i0 < kper ? n - i0 : kper);
     constexpr uint32_t bankw = (uint32_t)(SW * NSLOTS_PC);
     const WaveK w{lds_k + KP_WORDS, bankw, k, lane};
     const wword* kpt = (const wword*)lds_k;  // the shared P << k table
@@ -490,7 +497,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NWV_BLS_PAIR
     fetch(0);
     const SOp* script = g_pair_script[fixed ? 1 : 0];
     const int nops = g_pair_script_n[fixed ? 1 : 0];
-    auto first_rec = [&](const SOp& o) { return load_rec(T_DATA + o.a + (uint32_t)(lane % (int)(o.b >> 16)) * REC); };
+    auto first_rec = [&](const SOp& o) { return load_rec(T_DATA + o.a + (uint32_t)lane_mod(lane, (int)(o.b >> 16)) * REC); };
     Rec cur = first_rec(script[0].c >> 16 == SOP_RUN ? script[0] : script[script[0].next_run]);
     int step = 0;
 #pragma unroll 1
@@ -534,15 +541,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NWV_BLS_PAIR
             const uint16_t* nbase = wrap ? base0 : base + (uint32_t)nl * REC;
             // the next stage's record, or the next RUN op's first one (records are static data)
             Rec nxt = cur;
-            if (t + 1 < total) nxt = load_rec(nbase + (uint32_t)(lane % nl_next) * REC);
+            if (t + 1 < total) nxt = load_rec(nbase + (uint32_t)lane_mod(lane, nl_next) * REC);
             else if (op.next_run >= 0) nxt = first_rec(script[op.next_run]);
-            const int ipp = 64 / nl, first = lane / nl;
+            const int ipp = lane_div(64, nl), first = lane_div(lane, nl);
             if (first < ipp) {
                 const uint32_t dst = rec_u16(cur, 0);
 #pragma unroll 1
                 for (int item = first; item < k; item += ipp) {
                     wword* wm = (wword*)w.bk(item);
-                    const fp v = lane_value<NWV_BLS_PAIR_TERMS>(wm, kpt, h, cur);
+                    const fp v = lane_value<G>(wm, kpt, h, cur);
 #pragma unroll
                     for (int j = 0; j < NL; j++) wm[SW * dst + j] = v.l[j];
                 }
@@ -560,6 +567,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NWV_BLS_PAIR
             const uint32_t i = i0 + j;
             st_pair[i] = (st_dec[i] == ST_OK && st_apk[i] == ST_OK && ((ok >> j) & 1u)) ? ST_OK : ST_VERIFY_FAIL;
         }
+}
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NWV_BLS_PAIR_WAVES))) void k_blsw_pair_k(
+    uint32_t n, uint32_t kper, const uint32_t* srec, const int32_t* st_dec, const uint32_t* hrec, int h_hom,
+    const uint32_t* arec, const int32_t* st_apk, KeyTab kt, const uint32_t* pk_off, const uint32_t* pk_cnt,
+    const uint32_t* pk_idx, const uint32_t* kmode, int32_t* st_pair) {
+    extern __shared__ uint32_t lds_k[];
+    const uint32_t i0 = blockIdx.x * kper;
+    if (i0 >= n) return;
+    pair_flat<NWV_BLS_PAIR_TERMS>(lds_k, i0, (int)(n - i0 < kper ? n - i0 : kper), srec, st_dec, hrec, h_hom, arec,
+                                  st_apk, kt, pk_off, pk_cnt, pk_idx, kmode, st_pair);
 }
 // the flat scripts into g_pair_script on the calling thread's device, once per device
 static int ensure_pair_script() {
@@ -598,6 +615,19 @@ __global__ __launch_bounds__(64) void k_blsw_pair_sub(uint32_t n, const uint32_t
     const uint32_t b = blockIdx.x;
     if (b < n)
         blsw_pair_item(wm, b, srec, st_dec, hrec, h_hom, arec, st_apk, kt, pk_off, pk_cnt, pk_idx, kmode, st_pair);
+    else if (b < 2 * n)
+        blsw_sub_item(wm, b - n, srec, st_dec, st_sub);
+}
+// the same with the pairing on the flat script (pair_flat, one item on the wave); NWV_BLS_SUB_FLAT=1
+__global__ __launch_bounds__(64) void k_blsw_pair_sub_f(uint32_t n, const uint32_t* srec, const int32_t* st_dec,
+                                                        const uint32_t* hrec, int h_hom, const uint32_t* arec,
+                                                        const int32_t* st_apk, KeyTab kt, const uint32_t* pk_off,
+                                                        const uint32_t* pk_cnt, const uint32_t* pk_idx,
+                                                        const uint32_t* kmode, int32_t* st_pair, int32_t* st_sub) {
+    BLSW_LDS(wave::NSLOTS_PAIR);
+    const uint32_t b = blockIdx.x;
+    if (b < n)
+        pair_flat<8>(wm_lds, b, 1, srec, st_dec, hrec, h_hom, arec, st_apk, kt, pk_off, pk_cnt, pk_idx, kmode, st_pair);
     else if (b < 2 * n)
         blsw_sub_item(wm, b - n, srec, st_dec, st_sub);
 }
@@ -1398,7 +1428,13 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
         BLS_HIP(hipEventRecord(L.ev[4], s0));
         BLS_HIP(hipStreamWaitEvent(s0, L.ev[10], 0));
         BLS_HIP(hipEventRecord(L.ev[7], s0));
-        hipLaunchKernelGGL(k_blsw_pair_sub, dim3((unsigned)(2 * n)), dim3(64), 0, s0, (uint32_t)n,
+        static const bool sub_flat = [] {
+            const char* e = std::getenv("NWV_BLS_SUB_FLAT");
+            return e && std::atoi(e) != 0;
+        }();
+        if (sub_flat && ensure_pair_script()) return NWV_ERR_HIP;
+        hipLaunchKernelGGL(sub_flat ? k_blsw_pair_sub_f : k_blsw_pair_sub, dim3((unsigned)(2 * n)), dim3(64), 0, s0,
+                           (uint32_t)n,
                            (const uint32_t*)srec, (const int32_t*)sdec, (const uint32_t*)hh, 1, (const uint32_t*)ajrec,
                            (const int32_t*)sapk, kt, reinterpret_cast<const uint32_t*>(in + o_off),
                            reinterpret_cast<const uint32_t*>(in + o_cnt), reinterpret_cast<const uint32_t*>(in + o_idx),

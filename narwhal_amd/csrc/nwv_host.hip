@@ -23,6 +23,7 @@
 #include "blake2b_kernels.hip"
 #include "ed25519_kernels.hip"
 #include "msm_kernels.hip"
+#include "tiny_kernels.hip"
 #include "shard.h"
 
 #include <random>
@@ -105,13 +106,13 @@ struct DevBuf {
 struct PinnedBuf {
     void* p = nullptr;
     size_t cap = 0;
-    int ensure(size_t bytes) {
+    int ensure(size_t bytes, unsigned flags = hipHostMallocDefault) {
         if (bytes <= cap) return NWV_OK;
         if (p) (void)hipHostFree(p);
         p = nullptr;
         cap = 0;
         const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 16);
-        if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) {
+        if (hipHostMalloc(&p, want, flags) != hipSuccess) {
             p = nullptr;
             return set_err(NWV_ERR_OOM, "hipHostMalloc");
         }
@@ -139,6 +140,10 @@ struct EdBuffers {
     bool kc_split = false;      // keyed batch whose keys are all in the device's key cache
     // the last batch MSM already built the per-signature fallback's tables (early form, msm_launch)
     bool tables_ready = false;
+    // a keyed batch of at most TINY_MAX signatures by registered keys (ed_stage_keyed): the
+    // one-launch path (k_ed_tiny) with each signature's key cache slot and comb table
+    bool tiny = false;
+    uint32_t tiny_slot[TINY_MAX], tiny_cidx[TINY_MAX];
     void release() {
         for (DevBuf* b : {&pk, &sig, &msg, &off, &len, &kbuf, &flags, &tables, &verdict, &m_scal,
                           &m_partial, &m_state, &m_pts, &m_digits, &m_cnt, &m_tiles, &m_entries,
@@ -148,6 +153,7 @@ struct EdBuffers {
         nkeys_distinct = 0;
         kc_split = false;
         tables_ready = false;
+        tiny = false;
     }
 };
 
@@ -179,11 +185,12 @@ struct Lane {
     bool pksig_pending = false;
     // one word of coherent pinned host memory: the batch MSM's tail stores its verdict there and
     // batch_on_device polls it (no verdict copy, no wait for the stream's completion signal)
-    uint32_t* hword = nullptr;
+    uint32_t* hword = nullptr;  // 64 bytes: [0] the verdict code, [2, 4) k_ed_tiny's verdict bits
     uint32_t hseq = 0;  // sequence number of the lane's last polled call (30 bits, never 0)
     // staged runs with prep chaining (NWV_STAGE_CHAIN): k_msm_prep waits for chain_wait (an earlier
     // staged run's prep on this device) and chain_rec is recorded after it; null otherwise
     hipEvent_t chain_wait = nullptr, chain_rec = nullptr;
+    DevBuf tiny_ws;  // k_ed_tiny's workspace (zeroed once; the kernel leaves it zeroed)
 };
 
 // Committee key cache of a device.  fastcrypto decompresses a public key once, when it is
@@ -223,6 +230,12 @@ struct KeyCache {
     uint32_t used = 0, cap = 0;
     bool broken = false;  // allocation or fill failed once: stay uncached
     bool b_ready = false;  // slot 0 (B) filled
+    // registered keys' fixed-base comb tables (k_key_comb_fill, COMB_WORDS words each; allocated
+    // once at full size, NWV_COMB_KEYS tables, default 1,024 = 64 MiB); comb_of[slot] = table
+    DevBuf combs;
+    uint32_t comb_cap = 0, comb_used = 0;
+    std::vector<uint32_t> comb_of;
+    uint64_t reg_fp = 0;  // fingerprint of the last key list registered with every key combed
 };
 
 // One device of a context: the basepoint table, the key cache and the pool of lanes (created on
@@ -242,6 +255,8 @@ struct Gpu {
     std::mutex chain_mu;
     std::vector<hipEvent_t> chain_ev;
     uint64_t chain_runs = 0;
+    // diagnostics (nwv_diag_counters): one-launch tiny batches, batch MSMs, per-signature passes
+    std::atomic<uint64_t> n_tiny{0}, n_msm{0}, n_each{0};
 };
 
 int with_device(Lane& d) {
@@ -270,6 +285,7 @@ void lane_close(Lane& d) {
     d.hword = nullptr;
     d.b2stage.release();
     d.b2dig.release();
+    d.tiny_ws.release();
     for (DevBuf* b : {&d.b2_base, &d.b2_off, &d.b2_len, &d.b2_out, &d.b2_packed, &d.b2_plen, &d.b2_err, &d.b2_in})
         b->release();
     if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -390,6 +406,7 @@ void gpu_close(Gpu& g) {
     g.btab.release();
     g.comb.release();
     g.kc.recs.release();
+    g.kc.combs.release();
     for (hipEvent_t e : g.chain_ev) (void)hipEventDestroy(e);
     g.chain_ev.clear();
 }
@@ -1001,6 +1018,7 @@ int ed_stage(Lane& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, con
     uint8_t* h = static_cast<uint8_t*>(d.hstage.p);
     d.pksig_pending = false;
     b.tables_ready = false;
+    b.tiny = false;
     // large stagings: the caller's pk / sig / message bytes are packed piece by piece with each
     // piece's DMA queued at once (pack_copy_h2d); the small computed regions go first
     const bool piped = 96 * (inputs ? n : 0) + mbytes >= ((size_t)16 << 20);
@@ -1219,8 +1237,23 @@ int ed_stage_keyed(Lane& d, EdBuffers& b, size_t lo, size_t hi, size_t n_keys, c
     int rc = keycache_slots(d, klist.data(), m, kslot, kc_lookup_only);
     if (rc) return rc;
     const KeyedTail kt{klist.data(), m, koff.data(), ksig.data(), kslot.empty() ? nullptr : kslot.data()};
-    return ed_stage(d, b, 0, n, pk.data(), sig + 64 * lo, msg_base, msg_off + lo, msg_len + lo, seed32, &kt,
-                    dev_msg);
+    rc = ed_stage(d, b, 0, n, pk.data(), sig + 64 * lo, msg_base, msg_off + lo, msg_len + lo, seed32, &kt, dev_msg);
+    if (rc) return rc;
+    // the one-launch path: few signatures, every key registered (comb table present)
+    if (n && n <= (size_t)TINY_MAX && !kslot.empty() && !(d.flags & (NWV_FLAG_NO_TINY | NWV_FLAG_MSM_NEVER))) {
+        KeyCache& kc = d.gpu->kc;
+        std::lock_guard<std::mutex> g(kc.mu);
+        bool all = !kc.comb_of.empty();
+        for (size_t i = 0; i < n && all; i++) {
+            const uint32_t sl = kslot[kid[i]];
+            const uint32_t c = sl < kc.comb_of.size() ? kc.comb_of[sl] : UINT32_MAX;
+            all = c != UINT32_MAX;
+            b.tiny_slot[i] = sl;
+            b.tiny_cidx[i] = c;
+        }
+        b.tiny = all;
+    }
+    return NWV_OK;
 }
 
 bool verdicts_all_valid(const uint64_t* bits, size_t n) {
@@ -1369,6 +1402,16 @@ void nwv_free(nwv_ctx* ctx) {
 }
 
 int nwv_device_count(const nwv_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+int nwv_diag_counters(const nwv_ctx* ctx, uint64_t out[3]) {
+    if (!ctx || !out) return set_err(NWV_ERR_ARG, "null argument");
+    out[0] = out[1] = out[2] = 0;
+    for (const Gpu* g : ctx->devs) {
+        out[0] += g->n_tiny.load();
+        out[1] += g->n_msm.load();
+        out[2] += g->n_each.load();
+    }
+    return NWV_OK;
+}
 int nwv_device_ordinal(const nwv_ctx* ctx, int i) {
     return (ctx && i >= 0 && i < (int)ctx->devs.size()) ? ctx->devs[i]->ordinal : -1;
 }
@@ -1457,14 +1500,98 @@ static void set_ones(uint64_t* bits, size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; i++) bits[i >> 6] |= 1ULL << (i & 63);
 }
 
+// k_ed_tiny over a staged tiny keyed batch (b.tiny): every signature's verdict in one launch,
+// read back through the lane's polled host word (or the workspace when the lane has none)
+static int tiny_on_device(Lane& d, EdBuffers& b, size_t n, hipStream_t stream, int* ok, uint64_t* bits) {
+    int rc;
+    if (!d.tiny_ws.p) {
+        if ((rc = d.tiny_ws.ensure(64))) return rc;
+        NWV_HIP(hipMemsetAsync(d.tiny_ws.p, 0, 64, stream));
+    }
+    static const bool no_poll = std::getenv("NWV_NO_HOST_POLL") != nullptr;
+    uint32_t* hv = (!no_poll && stream == d.stream) ? d.hword : nullptr;
+    TinyArgs a{};
+    a.pk = b.pk.as<uint8_t>();
+    a.sig = b.sig.as<uint8_t>();
+    a.msg = b.msg.as<uint8_t>();
+    a.off = b.off.as<uint64_t>();
+    a.len = b.len.as<uint32_t>();
+    a.kc = d.gpu->kc.recs.as<uint32_t>();
+    a.combs = d.gpu->kc.combs.as<uint32_t>();
+    a.bcomb = d.gpu->comb.as<uint32_t>();
+    a.ws = d.tiny_ws.as<uint32_t>();
+    a.hword = hv;
+    a.n = (uint32_t)n;
+    if (hv) {
+        d.hseq = (d.hseq + 1) & 0x3FFFFFFFu;
+        if (d.hseq == 0) d.hseq = 1;
+        a.hseq = d.hseq;
+        __atomic_store_n(hv, 0u, __ATOMIC_RELEASE);
+    }
+    std::memcpy(a.kslot, b.tiny_slot, 4 * n);
+    std::memcpy(a.cidx, b.tiny_cidx, 4 * n);
+    static const bool stamps = std::getenv("NWV_TINY_STAMPS") != nullptr;  // diagnostics only
+    if (stamps) {
+        if ((rc = b.m_stamps.ensure(8 * 8))) return rc;
+        NWV_HIP(hipMemsetAsync(b.m_stamps.p, 0, 64, stream));
+        a.stamps = b.m_stamps.as<unsigned long long>();
+    }
+    hipLaunchKernelGGL(k_ed_tiny, dim3((unsigned)n), dim3(64 * TINY_WAVES), 0, stream, a);
+    if (hipGetLastError() != hipSuccess) {
+        (void)hipStreamSynchronize(stream);
+        return set_err(NWV_ERR_HIP, "k_ed_tiny launch");
+    }
+    uint64_t vb = 0;
+    uint32_t all = 0;
+    bool got = false;
+    if (hv) {
+        uint32_t v = 0;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint64_t k = 0; ((v = __atomic_load_n(hv, __ATOMIC_ACQUIRE)) >> 2) != a.hseq; k++) {
+            if ((k & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+            __builtin_ia32_pause();
+        }
+        NWV_HIP(hipStreamSynchronize(stream));
+        if ((v >> 2) == a.hseq) {
+            vb = (uint64_t)hv[2] | ((uint64_t)hv[3] << 32);
+            all = (v & 3u) == 1u;
+            got = true;
+        }
+    }
+    if (!got) {
+        uint32_t r[4] = {0, 0, 0, 0};
+        NWV_HIP(hipMemcpyAsync(r, a.ws + 4, 16, hipMemcpyDeviceToHost, stream));
+        NWV_HIP(hipStreamSynchronize(stream));
+        vb = (uint64_t)r[0] | ((uint64_t)r[1] << 32);
+        all = r[2];
+    }
+    htrace("batch:tiny-done");
+    if (stamps) {  // phase times of workgroup 0 in us from its start (s_memrealtime: 100 MHz)
+        unsigned long long t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpy(t, b.m_stamps.p, 64, hipMemcpyDeviceToHost) == hipSuccess)
+            std::fprintf(stderr, "tiny n=%zu: R %.1f hash %.1f comb-done %.1f barrier %.1f final %.1f us\n", n,
+                         (t[1] - t[0]) / 100.0, (t[2] - t[0]) / 100.0, (t[4] - t[0]) / 100.0, (t[5] - t[0]) / 100.0,
+                         (t[6] - t[0]) / 100.0);
+    }
+    *ok = all ? 1 : 0;
+    if (bits) bits[0] = vb;
+    return NWV_OK;
+}
+
 // Batch verdict of resident buffers: MSM, then (only if it rejects) the per-signature fallback
-// for the exact bad set.  bits: the shard's verdict words (may be null).
+// for the exact bad set.  bits: the shard's verdict words (may be null).  A tiny keyed batch by
+// registered keys takes the one-launch per-signature path instead (exact bits, no fallback).
 static int batch_on_device(Lane& d, EdBuffers& b, size_t n, const uint8_t seed[32], hipStream_t stream,
                            int* ok, uint64_t* bits, bool state_ready = false) {
     int rc;
+    if (b.tiny && n <= (size_t)TINY_MAX) {
+        d.gpu->n_tiny++;
+        return tiny_on_device(d, b, n, stream, ok, bits);
+    }
     const bool use_msm = (d.flags & NWV_FLAG_MSM_ALWAYS) ||
                          (!(d.flags & NWV_FLAG_MSM_NEVER) && n >= msm_min_n());
     if (use_msm) {
+        d.gpu->n_msm++;
         htrace("batch:msm-launch");
         // batch-verdict calls of up to 65,536 signatures (latency-bound: a spinning host thread
         // costs little) poll the tail's word in pinned host memory instead of copying the verdict
@@ -1547,6 +1674,7 @@ static int batch_on_device(Lane& d, EdBuffers& b, size_t n, const uint8_t seed[3
         }
     }
     htrace("batch:fallback");
+    d.gpu->n_each++;
     if ((rc = ed_launch(d, b, n, stream, nullptr, msm_reusable(d, b, use_msm)))) return rc;
     std::vector<uint64_t> tmp;
     uint64_t* out = bits;
@@ -1636,13 +1764,71 @@ int nwv_ed25519_verify_batch_keyed(nwv_ctx* ctx, size_t n_keys, const uint8_t* k
 // (nwv_ed25519_pubkey_verify, which only looks keys up) take the 128-bit-scalar form.
 int nwv_keycache_register(nwv_ctx* ctx, size_t n_keys, const uint8_t* keys) {
     if (!ctx || (n_keys && !keys)) return set_err(NWV_ERR_ARG, "null argument");
+    // the same key list as the last registration (the types layer registers its committee on
+    // every call): nothing to do
+    uint64_t fp = 0x9E3779B97F4A7C15ull ^ (uint64_t)n_keys;
+    for (size_t i = 0; i < 4 * n_keys; i++) {
+        uint64_t w;
+        std::memcpy(&w, keys + 8 * i, 8);
+        fp = (fp ^ w) * 0xFF51AFD7ED558CCDull;
+        fp ^= fp >> 29;
+    }
+    if (fp == 0) fp = 1;
+    static const uint32_t comb_keys = (uint32_t)env_size("NWV_COMB_KEYS", 1024, 0, 1u << 16);
     for (Gpu* g : ctx->devs) {
+        {
+            std::lock_guard<std::mutex> lk(g->kc.mu);
+            if (g->kc.reg_fp == fp) continue;
+        }
         LaneRef lane(*g);
         int rc = lane.rc();
-        std::vector<uint32_t> slots;
-        for (size_t a = 0; a < n_keys && !rc; a += 4096)
+        std::vector<uint32_t> slots, all;
+        for (size_t a = 0; a < n_keys && !rc; a += 4096) {
             rc = keycache_slots(*lane, keys + 32 * a, std::min<size_t>(4096, n_keys - a), slots);
+            all.insert(all.end(), slots.begin(), slots.end());
+        }
         if (rc) return rc;
+        if (all.size() != n_keys || comb_keys == 0 || (g->flags & NWV_FLAG_NO_KEYCACHE)) continue;  // uncached
+        // fixed-base comb tables for the keys that have none yet (the one-launch path, k_ed_tiny)
+        KeyCache& kc = g->kc;
+        std::lock_guard<std::mutex> lk(kc.mu);
+        if (!kc.comb_cap) {
+            if (kc.combs.ensure((size_t)4 * COMB_WORDS * comb_keys)) continue;  // no room: batches use the MSM
+            kc.comb_cap = comb_keys;
+            kc.comb_of.assign(kc.cap ? kc.cap : (1u << 16), UINT32_MAX);
+        }
+        std::vector<uint8_t> nk;
+        std::vector<uint32_t> ni, nslot;
+        for (size_t j = 0; j < n_keys; j++) {
+            const uint32_t sl = all[j];
+            if (sl >= kc.comb_of.size() || kc.comb_of[sl] != UINT32_MAX) continue;
+            bool dup = false;
+            for (uint32_t q : nslot) dup = dup || q == sl;
+            if (dup) continue;
+            if (kc.comb_used + ni.size() >= kc.comb_cap) break;  // full: later keys take the MSM path
+            nk.insert(nk.end(), keys + 32 * j, keys + 32 * j + 32);
+            ni.push_back(kc.comb_used + (uint32_t)ni.size());
+            nslot.push_back(sl);
+        }
+        if (!ni.empty()) {
+            Lane& d = *lane;
+            DevBuf tmp;
+            if ((rc = tmp.ensure(36 * ni.size() + 64))) return rc;
+            uint8_t* tk = tmp.as<uint8_t>();
+            uint32_t* ti = reinterpret_cast<uint32_t*>(tk + 32 * ni.size());
+            NWV_HIP(hipMemcpyAsync(tk, nk.data(), nk.size(), hipMemcpyHostToDevice, d.stream));
+            NWV_HIP(hipMemcpyAsync(ti, ni.data(), 4 * ni.size(), hipMemcpyHostToDevice, d.stream));
+            const size_t lanes = ni.size() * COMB_TABLES * COMB_ENTRIES;
+            hipLaunchKernelGGL(k_key_comb_fill, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, d.stream,
+                               (uint32_t)ni.size(), tk, ti, kc.combs.as<uint32_t>());
+            NWV_HIP(hipGetLastError());
+            NWV_HIP(hipStreamSynchronize(d.stream));  // published only once the tables are written
+            for (size_t q = 0; q < ni.size(); q++) kc.comb_of[nslot[q]] = ni[q];
+            kc.comb_used += (uint32_t)ni.size();
+        }
+        bool every = true;
+        for (size_t j = 0; j < n_keys && every; j++) every = all[j] < kc.comb_of.size() && kc.comb_of[all[j]] != UINT32_MAX;
+        if (every) kc.reg_fp = fp;
     }
     return NWV_OK;
 }
@@ -2119,14 +2305,15 @@ static uint64_t b2_quad_max_m() {
     }();
     return v;
 }
+// out2 (optional): a second copy of the digests, e.g. straight into coherent pinned host memory
 static void b2_launch(Lane& d, size_t m, uint64_t maxlen, const uint8_t* base, const uint64_t* off,
-                      const uint64_t* len, uint32_t* out) {
+                      const uint64_t* len, uint32_t* out, uint32_t* out2 = nullptr) {
     if (maxlen >= b2_quad_min() || m <= b2_quad_max_m())
         hipLaunchKernelGGL(k_blake2b_quad, dim3((unsigned)((m + 15) / 16)), dim3(64), 0, d.stream,
-                           (uint64_t)m, base, off, len, out);
+                           (uint64_t)m, base, off, len, out, out2);
     else
         hipLaunchKernelGGL(k_blake2b_many, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, d.stream,
-                           (uint64_t)m, base, off, len, out);
+                           (uint64_t)m, base, off, len, out, out2);
 }
 
 // device pointers of a staged digest batch (views into b2_in, or the b2_base/off/len buffers)
@@ -2245,21 +2432,20 @@ int nwv_ed25519_verify_batch_keyed_digests(nwv_ctx* ctx, size_t n_pre, const uin
     B2Staged st{};
     if (!rc) rc = b2_stage(d, n_pre, pre_base, pre_off, pre_len, 0, n_pre, roff, st);
     if (rc) return rc;
-    // the digests stay on the device as the message arena of the batch (over-read slack included)
+    // the digests stay on the device as the message arena of the batch; the over-read slack past
+    // them needs no particular contents (SHA-512 and BLAKE2b mask the bytes past a message)
     if ((rc = d.b2_out.ensure(32 * n_pre + 4 * MSG_PAD))) return rc;
     uint64_t maxlen = 0;
     for (size_t k = 0; k < n_pre; k++) maxlen = std::max<uint64_t>(maxlen, pre_len[k]);
-    NWV_HIP(hipMemsetAsync(d.b2_out.as<uint8_t>() + 32 * n_pre, 0, 4 * MSG_PAD, d.stream));
-    b2_launch(d, n_pre, maxlen, st.base, st.off, st.len, d.b2_out.as<uint32_t>());
-    NWV_HIP(hipGetLastError());
-    // the digests head back to pinned memory right behind the hash (stream order), so the only
-    // wait left is the verdict's
-    if ((rc = d.b2dig.ensure(32 * n_pre))) return rc;
-    NWV_HIP(hipMemcpyAsync(d.b2dig.p, d.b2_out.p, 32 * n_pre, hipMemcpyDeviceToHost, d.stream));
-    // no host round trip: the batch is staged behind the hash on the same stream
+    // the batch is staged before the hash launch (its copy does not depend on the digests), so
+    // hash and verification run back to back; no host round trip between them
     rc = ed_stage_keyed(d, d.ed, 0, n, n_keys, keys, key_idx, sig, nullptr, moff.data(), mlen.data(), seed,
                         &d.b2_out);
     if (rc) return rc;
+    // the hash also writes the digests straight into coherent pinned host memory (no copy back)
+    if ((rc = d.b2dig.ensure(32 * n_pre, hipHostMallocCoherent | hipHostMallocMapped))) return rc;
+    b2_launch(d, n_pre, maxlen, st.base, st.off, st.len, d.b2_out.as<uint32_t>(), static_cast<uint32_t*>(d.b2dig.p));
+    NWV_HIP(hipGetLastError());
     int ok = 1;
     rc = batch_on_device(d, d.ed, n, seed, d.stream, &ok, verdict_bits_or_null, true);
     if (rc) return rc;

@@ -273,7 +273,12 @@ struct DigestSigBatch {
         db.arena.resize(db.arena.size() + 16);
         bits.assign((n + 63) / 64 + 1, 0);
         int all = 0;
-        int rc = nwv_ed25519_verify_batch_keyed_digests(ctx, m, db.arena.data(), db.off.data(), db.len.data(),
+        // the committee registered on the devices (a no-op after an epoch's first call): a call of
+        // at most 64 signatures by its members -- a certificate, a header, a vote -- then takes
+        // the one-launch path (k_ed_tiny) inside the engine call below
+        int rc = (c && c->n) ? nwv_keycache_register(ctx, c->n, c->keys) : NWV_OK;
+        if (rc) return rc;
+        rc = nwv_ed25519_verify_batch_keyed_digests(ctx, m, db.arena.data(), db.off.data(), db.len.data(),
                                                         dig.data(), keys.size() / 32, keys.data(), n, kidx.data(),
                                                         sig.data(), didx.data(), nullptr, &all, bits.data());
         if (rc) return rc;

@@ -43,6 +43,8 @@ pub const NWV_FLAG_BLS_PER_ITEM: u32 = 64;
 pub const NWV_FLAG_BLS_BATCH: u32 = 128;
 /// BLS12-381: no verified-signature ring (every aggregate decodes and G1-checks its signatures)
 pub const NWV_FLAG_NO_SIGCACHE: u32 = 256;
+/// Keyed batches of <= 64 signatures by registered keys go through the batch MSM, not k_ed_tiny.
+pub const NWV_FLAG_NO_TINY: u32 = 4096;
 
 // per-item BLS12-381 statuses (include/nwv_bls.h)
 pub const NWV_BLS_OK: i32 = 0;
@@ -173,6 +175,7 @@ extern "C" {
     pub fn nwv_init_device(out: *mut *mut NwvCtx, device_ordinal: c_int, flags: u32) -> c_int;
     pub fn nwv_free(ctx: *mut NwvCtx);
     pub fn nwv_device_count(ctx: *const NwvCtx) -> c_int;
+    pub fn nwv_diag_counters(ctx: *const NwvCtx, out: *mut u64) -> c_int;
     pub fn nwv_device_ordinal(ctx: *const NwvCtx, i: c_int) -> c_int;
     pub fn nwv_abi_version() -> c_int;
     pub fn nwv_last_error() -> *const c_char;

@@ -558,6 +558,50 @@ int he_comb_check(const uint8_t* b32) {
     return std::memcmp(w1, w2, 32) == 0 ? 1 : 0;
 }
 
+// The one-launch path's per-signature check (tiny_kernels.hip k_ed_tiny), sequentially: the key's
+// comb table i 16^j A (k_key_comb_fill: an undecodable key gets the identity's table), the
+// signed radix-16 digits of s (zeroed when s >= l) and of k, [s]B - [k]A as the sum of one entry
+// of each table per digit position (the kernel's lane j), minus R, times 8, the identity test,
+// and the decode / canonicity flags.  Returns the verdict (1 accept).
+int he_tiny_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint32_t len) {
+    uint32_t Aw[8], Rw[8], Sw[8], k[8];
+    words(pk, Aw);
+    words(sig, Rw);
+    words(sig + 32, Sw);
+    std::vector<uint8_t> m(len + 64, 0);
+    if (len) std::memcpy(m.data(), msg, len);
+    const bool sok = lane_hash(Aw, Rw, Sw, m.data(), len, k) == FLAG_S_OK;
+    if (!sok)
+        for (int q = 0; q < 8; q++) Sw[q] = 0u;
+    ge_p3 A, R;
+    const bool aok = ge_decompress(Aw, A);
+    if (!aok) A = ge_p3_identity();
+    const bool rok = ge_decompress(Rw, R);
+    int ds[COMB_TABLES], dk[COMB_TABLES];
+    comb_digits(Sw, ds);
+    comb_digits(k, dk);
+    std::vector<uint32_t> e(MSM_PT_WORDS);
+    ge_p3 P = ge_p3_identity();
+    for (int j = 0; j < COMB_TABLES; j++) {
+        ge_p3 Pj = ge_p3_identity();
+        if (ds[j] < -8 || ds[j] > 8 || dk[j] < -8 || dk[j] > 8) return -1;  // past the tables
+        if (ds[j]) {
+            comb_entry(j, ds[j] < 0 ? -ds[j] : ds[j], e.data());
+            Pj = ge_p1p1_to_p3(ge_madd(Pj, msm_load_point(e.data(), ds[j] < 0)));
+        }
+        if (dk[j]) {
+            comb_entry_of(A, j, dk[j] < 0 ? -dk[j] : dk[j], e.data());
+            Pj = ge_p1p1_to_p3(ge_madd(Pj, msm_load_point(e.data(), dk[j] > 0)));
+        }
+        P = p3_add(P, Pj);
+    }
+    // -R as the kernel adds it: R's affine Niels record, negated
+    uint32_t rrec[MSM_PT_WORDS];
+    msm_store_point(rrec, R);
+    P = ge_p1p1_to_p3(ge_madd(P, msm_load_point(rrec, true)));
+    return (p3_mul8_is_identity(P) && aok && rok && sok) ? 1 : 0;
+}
+
 // signed digits of a 256-bit scalar over layout(c): z range (bits = 128) or full range (253);
 // out: nw, then (pos, digit) pairs
 int he_msm_recode(const uint8_t* s32, int c, int bits, int* out) {

@@ -285,3 +285,22 @@ def test_point_kernel_op_count_matches_bench(he):
     for seed in (b"\x01" * 32, b"\x77" * 32):
         he.he_msm_point_counts(of.pubkey(seed), of.sign(seed, b"m"), c)
         assert (c[0], c[1]) == bench.OPS_MSM_POINTS
+
+
+def test_tiny_path_per_signature_check(he):
+    """the one-launch path for tiny keyed batches (k_ed_tiny): [8](R - ([s]B - [k]A)) = 0 with both
+    multiples summed from fixed-base combs (B's and the key's i 16^j A), run on the host, equals the
+    oracle's ZIP-215 verdict on every golden vector (every Appendix-B category) and on the 196-case
+    small-order table -- including undecodable keys (the identity's table) and s >= l"""
+    he.he_tiny_verify.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32]
+    vecs = [(bytes.fromhex(v["pk"]), bytes.fromhex(v["sig"]), bytes.fromhex(v["msg"]))
+            for v in of.load_golden("ed25519_vectors.json")["vectors"]]
+    vecs += [(bytes.fromhex(v["pk"]), bytes.fromhex(v["sig"]), bytes.fromhex(v["msg"]))
+             for v in of.load_golden("zip215_small_order.json")["vectors"]]
+    seen = set()
+    for pk, sig, msg in vecs:
+        got = he.he_tiny_verify(pk, sig, msg, len(msg))
+        want = int(of.verify(pk, sig, msg))
+        assert got == want, (pk.hex(), sig.hex())
+        seen.add(want)
+    assert seen == {0, 1} and len(vecs) > 300

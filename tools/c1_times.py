@@ -15,8 +15,11 @@ def main():
     import narwhal_amd
     import config_legs as CL
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 300
-    eng = narwhal_amd.Engine(device=0)
+    flags = int(sys.argv[2], 0) if len(sys.argv) > 2 else 0  # e.g. 4096 = NWV_FLAG_NO_TINY
+    eng = narwhal_amd.Engine(device=0, flags=flags)
     r, _ = CL.leg_c1(eng, reps=reps)
+    r["flags"] = flags
+    r["diag_counters"] = eng.diag_counters()
     eng.close()
     print(json.dumps(r), flush=True)
 

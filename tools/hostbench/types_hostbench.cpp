@@ -37,6 +37,7 @@ extern "C" int nwv_ed25519_verify_batch_keyed_digests(nwv_ctx* ctx, size_t n_pre
 
 // the BLS12-381 layer's engine calls (nwv_types.cpp links them; this bench times the Ed25519 path)
 extern "C" int nwv_bls_keycache_register(nwv_ctx*, size_t, const uint8_t*) { return NWV_OK; }
+extern "C" int nwv_keycache_register(nwv_ctx*, size_t, const uint8_t*) { return NWV_OK; }
 extern "C" int nwv_bls_verify_many(nwv_ctx*, size_t, const uint8_t*, size_t n, const uint8_t*, const uint32_t*,
                                    const uint32_t*, const uint32_t*, const uint8_t*, const uint64_t*, const uint32_t*,
                                    const uint8_t*, size_t, int32_t* status) {
