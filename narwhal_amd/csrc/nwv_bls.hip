@@ -409,8 +409,9 @@ constexpr int BLS_PACK_MAX = 4;
 __device__ wave::SOp g_pair_script[2][wave::SCRIPT_MAX];  // [fixed key lines]
 __device__ int g_pair_script_n[2];
 // two waves per SIMD (<= 256 registers: at most 4 terms' LDS reads in flight, NWV_BLS_PAIR_TERMS)
-// with two items a wave (NWV_BLS_PACK: 2 x 9.6 KB banks + the shared 0.9 KB table = 8 waves per
-// CU): 16,384 checks 23.5 -> 17.8 ms against one wave per SIMD with three items
+// with three items a wave (NWV_BLS_PACK: 3 x 6.5 KB banks -- registers never live together share
+// slots, tools/gen_bls_wave.py PC_ALIAS -- + the shared 0.9 KB table = 8 waves per CU): 16,384
+// checks 23.5 -> 16.0 ms against one wave per SIMD with three 10.5 KB banks
 // (profiles/round6_bls_pair_sweep.txt)
 #ifndef NWV_BLS_PAIR_WAVES
 #define NWV_BLS_PAIR_WAVES 2
@@ -1492,10 +1493,10 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
         BLS_HIP(hipStreamWaitEvent(s0, L.ev[10], 0));
         BLS_HIP(hipStreamWaitEvent(s0, L.ev[11], 0));
         BLS_HIP(hipEventRecord(L.ev[7], s0));
-        // items per pairing wave (env NWV_BLS_PACK, 1..4): one LDS bank of ~9.6 KB each
+        // items per pairing wave (env NWV_BLS_PACK, 1..4): one LDS bank of ~6.5 KB each
         static const uint32_t pack = [] {
             const char* e = std::getenv("NWV_BLS_PACK");
-            const long v = e ? std::strtol(e, nullptr, 10) : 2;
+            const long v = e ? std::strtol(e, nullptr, 10) : 3;
             return (uint32_t)(v < 1 ? 1 : v > BLS_PACK_MAX ? BLS_PACK_MAX : v);
         }();
         // diagnostic (occupancy experiments): NWV_BLS_LDS_PAD bytes of extra LDS per pairing wave

@@ -645,7 +645,10 @@ def leg_bls(eng, threads=1, certs=100, quorum=67, committee=100, reps=20, throug
         out["roofline"] = bls_roofline(n, out["throughput"]["kernel_ms"]["pairing_check"], peak)
         sample = sorted(rnd.choice(n, 48, replace=False).tolist())
         tp_check = ([sigs[k] for k in sample], [[kidx[k]] for k in sample], [msgs[k] for k in sample])
-    out["dag_round"] = leg_bls_dag(eng, b, sks, pks, rnd, dag_rounds)
+    out["dag_round"], arrs = leg_bls_dag(eng, b, sks, pks, rnd, dag_rounds)
+    # the same round through the batching service with concurrent submitters (SURVEY §8 f1 + f4)
+    out["service"] = leg_bls_service(eng, *arrs[:4])
+    del arrs
     # the oracle: statuses of the round (and a throughput sample) + the CPU baseline
     import bls_ffi as B  # checker / CPU baseline only
     t0 = time.perf_counter()
@@ -679,7 +682,7 @@ def leg_bls(eng, threads=1, certs=100, quorum=67, committee=100, reps=20, throug
             "sample": f"{rounds} x the same {certs}-certificate round ({quorum} of {committee} signers each), "
                       f"items split over {threads} threads; oracle/bls_oracle.c (plain C restatement of blst "
                       "fast_aggregate_verify), each key decoded and validated once per call"}
-        out["round"]["gpu_over_cpu"] = out["round"]["certs_per_s"] / out["cpu_baseline"]["value"]
+        out["round"]["gpu_speedup_over_cpu"] = out["round"]["certs_per_s"] / out["cpu_baseline"]["value"]
     out["note"] = ("BLS12-381 min_sig (48 B G1 signatures, 96 B G2 keys), fastcrypto's DST, committee keys "
                    "registered in the device key cache; item = sig decode + G1 check, key sum, hash to G1, "
                    "pairing check")
@@ -723,7 +726,125 @@ def leg_bls_dag(eng, b, sks, pks, rnd, rounds=20):
         assert rc == 0 and not any(hres) and not any(vres) and not any(cres)
         if r >= 2:
             ts.append(dt)
-    return dict(_pcts(ts), headers=n, votes=len(vsample), certificates=n, quorum=q,
-                items_per_round=2 * n + len(vsample),
-                note="one nwv_bls_verify_mixed_many call per round: every digest in one BLAKE2b launch, every "
-                     "signature check (200 single-key, 100 aggregates of 67) in one BLS verification call")
+    out = dict(_pcts(ts), headers=n, votes=len(vsample), certificates=n, quorum=q,
+               items_per_round=2 * n + len(vsample),
+               note="one nwv_bls_verify_mixed_many call per round: every digest in one BLAKE2b launch, every "
+                    "signature check (200 single-key, 100 aggregates of 67) in one BLS verification call")
+    return out, (cc, harr, varr, carr, keep)
+
+
+def leg_bls_service(eng, cc, harr, varr, carr, rounds=10, submitters=8):
+    """The BLS round through the in-library batching service (nwv_service_create_bls), the way the
+    Core loop's producers feed it (primary/src/core.rs:614-714): `submitters` threads each hand
+    their share of a round's 299 headers, votes and certificates to the service asynchronously
+    (nwv_service_submit_bls_*); each message's completion callback records its latency (submit ->
+    own DagError code).  Reports the round time, p50 / p99 per message and the engine calls the
+    service made (each flush = one nwv_bls_verify_mixed_many).  Then the same with blocking
+    submitters (nwv_service_verify_bls_*: each thread waits for its message's code before the next)."""
+    import threading
+    from narwhal_amd import service as S
+    lib = S.bind(T.lib())
+    fns = [lib.nwv_service_submit_bls_header] * len(harr) + [lib.nwv_service_submit_bls_vote] * len(varr) + \
+        [lib.nwv_service_submit_bls_certificate] * len(carr)
+    vfns = [lib.nwv_service_verify_bls_header] * len(harr) + [lib.nwv_service_verify_bls_vote] * len(varr) + \
+        [lib.nwv_service_verify_bls_certificate] * len(carr)
+    structs = [harr[i] for i in range(len(harr))] + [varr[i] for i in range(len(varr))] + \
+        [carr[i] for i in range(len(carr))]
+    m = len(structs)
+    out = {"messages_per_round": m, "rounds": rounds, "submitters": submitters}
+    h = ctypes.c_void_p()
+    _lib._check(lib.nwv_service_create_bls(eng._h, ctypes.byref(cc), 512, 1000, ctypes.byref(h)))
+    t_sub, t_done = np.zeros(m), np.zeros(m)
+    codes = np.zeros(m, dtype=np.int32)
+    ev, lk, left = threading.Event(), threading.Lock(), [0]
+
+    def on_done(user, code):
+        i = user or 0
+        t_done[i] = time.perf_counter()
+        codes[i] = code
+        with lk:
+            left[0] -= 1
+            if left[0] == 0:
+                ev.set()
+
+    cb = S.DONE_FN(on_done)
+    try:
+        # asynchronous submitters
+        lat, rtimes, calls = [], [], []
+        for r in range(rounds + 1):
+            ev.clear()
+            left[0] = m
+            st0 = np.zeros(6, dtype=np.uint64)
+            lib.nwv_service_stats(h, st0.ctypes.data)
+            go = threading.Barrier(submitters + 1)
+
+            def submit(lo):
+                go.wait()
+                for i in range(lo, m, submitters):
+                    t_sub[i] = time.perf_counter()
+                    _lib._check(fns[i](h, ctypes.byref(structs[i]), cb, ctypes.c_void_p(i)))
+
+            th = [threading.Thread(target=submit, args=(lo,)) for lo in range(submitters)]
+            for t in th:
+                t.start()
+            go.wait()
+            t0 = time.perf_counter()
+            for t in th:
+                t.join()
+            assert ev.wait(60), "service round timed out"
+            dt = time.perf_counter() - t0
+            assert not codes.any(), [int(c) for c in codes if c][:8]
+            st1 = np.zeros(6, dtype=np.uint64)
+            lib.nwv_service_stats(h, st1.ctypes.data)
+            if r:  # the first round warms up
+                rtimes.append(dt)
+                lat.append(t_done - t_sub)
+                calls.append(int(st1[0] - st0[0]))
+        a = np.concatenate(lat) * 1e3
+        out["async_submitters"] = {"ms_per_round": float(np.median(rtimes)) * 1e3,
+                                   "latency_ms_p50": float(np.percentile(a, 50)),
+                                   "latency_ms_p99": float(np.percentile(a, 99)),
+                                   "engine_calls_per_round": float(np.mean(calls)),
+                                   "max_engine_calls_per_round": int(max(calls))}
+        # blocking submitters: each thread has one message outstanding at a time
+        blat, brt, bcalls = [], [], []
+        for r in range(3):
+            st0 = np.zeros(6, dtype=np.uint64)
+            lib.nwv_service_stats(h, st0.ctypes.data)
+            per = [[] for _ in range(submitters)]
+            bad = []
+
+            def blocking(lo):
+                res = ctypes.c_int32(0)
+                for i in range(lo, m, submitters):
+                    t1 = time.perf_counter()
+                    rc = vfns[i](h, ctypes.byref(structs[i]), ctypes.byref(res))
+                    per[lo].append(time.perf_counter() - t1)
+                    if rc or res.value:
+                        bad.append((i, rc, res.value))
+
+            th = [threading.Thread(target=blocking, args=(lo,)) for lo in range(submitters)]
+            t0 = time.perf_counter()
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            dt = time.perf_counter() - t0
+            assert not bad, bad[:4]
+            st1 = np.zeros(6, dtype=np.uint64)
+            lib.nwv_service_stats(h, st1.ctypes.data)
+            if r:
+                brt.append(dt)
+                blat += [x for p in per for x in p]
+                bcalls.append(int(st1[0] - st0[0]))
+        b = np.array(blat) * 1e3
+        out["blocking_submitters"] = {"ms_per_round": float(np.median(brt)) * 1e3,
+                                      "latency_ms_p50": float(np.percentile(b, 50)),
+                                      "latency_ms_p99": float(np.percentile(b, 99)),
+                                      "engine_calls_per_round": float(np.mean(bcalls))}
+    finally:
+        lib.nwv_service_free(h)
+    out["note"] = ("nwv_service_create_bls(max_batch 512, max_wait 1000 us); async: each submitter thread "
+                   "submits its share of the round at once and the callbacks record each message's latency; "
+                   "blocking: one message outstanding per thread")
+    return out

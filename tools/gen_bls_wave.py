@@ -245,6 +245,37 @@ REGS.add("S", 8)     # scratch inputs: hash-to-curve map outputs, subgroup-check
 # temporaries as one run of slots [0, NSLOTS_PC) -- the bank one item takes in the packed pairing
 # kernel -- and every other constant, register and temporary lies above it
 PC_REGS = ("F", "G", "M", "A", "B", "C", "LA", "LB", "PA", "PB", "QB", "TB", "N")
+# Registers that are never live at the same time share slots (pc_layout), so a packed pairing
+# bank is small enough for three items a wave at two waves per SIMD (8 waves x 3 banks <= the
+# CU's 160 KB of LDS): the Miller loop's registers (LA .. TB) are dead once the final
+# exponentiation starts, which only then writes M, A, B, C, G.  Inside it (wave::final_exp's
+# order): N (the inversion's exchange) is dead before M is first written; C holds the inversion's
+# cofactors, then is dead until its x-power, which starts after A's last use; G holds the
+# inverse (inversion, easy part), then is dead until the end, after B's last use.  So N = M,
+# C = A, G = B.  No program reads or writes two registers that share a slot (checked in build_all).
+PC_ALIAS = {"M": ("LA", 0), "N": ("M", 0), "B": ("LA", 12), "G": ("LA", 12), "A": ("LA", 24), "C": ("LA", 24)}
+
+
+def pc_layout(start):
+    """the pairing check's registers from slot `start`: F, then the Miller loop's run LA .. TB with
+    the final exponentiation's M, B and A = C = G over it (PC_ALIAS); returns the first free slot"""
+    s = start
+    for name in ("F", "LA", "LB", "PA", "PB", "QB", "TB"):
+        REGS.regs[name][0] = s
+        s += REGS.regs[name][1]
+    end = s
+    for name in ("M", "B", "A", "C", "G", "N"):
+        ref, off = PC_ALIAS[name]
+        REGS.regs[name][0] = REGS.regs[ref][0] + off
+        end = max(end, REGS.regs[name][0] + REGS.regs[name][1])
+    REGS.temp_base = end
+    return end
+
+
+def _overlap(r1, r2):
+    b1, c1, _ = REGS.regs[r1]
+    b2, c2, _ = REGS.regs[r2]
+    return b1 < b2 + c2 and b2 < b1 + c1
 
 
 # ============================================================== tower over generic elements ===
@@ -1381,7 +1412,7 @@ def _p_phi(io):
 # registers (unused outside the pairing), a four-level tree of complete additions -> U.  Sixteen,
 # not more: a 32-point tree needs 349 slots against the pairing programs' 307, and every wave
 # kernel's LDS (hence the pairing kernel's occupancy) follows the largest program.
-SUM_IN = [(r, i) for r in ("F", "G", "M", "A") for i in range(12)]
+SUM_IN = [(r, i) for r in ("F", "M", "G", "A") for i in range(12)]  # one run of slots (pc_layout)
 SUM_N = len(SUM_IN) // 3
 
 
@@ -1625,7 +1656,13 @@ def build_all():
                 cp.prog, cp.body = prog, body
                 compiled[prog.name] = cp
     # the pairing check's programs first: slot 0, their constants, PC_REGS, their temporaries
-    REGS.layout(1 + len(first), PC_REGS)
+    pc_layout(1 + len(first))
+    for prog, _ in traced:  # no program touches two registers that share slots
+        regs = sorted(_prog_regs(prog))
+        for i, r1 in enumerate(regs):
+            for r2 in regs[i + 1:]:
+                if r1 in PC_REGS and r2 in PC_REGS and _overlap(r1, r2):
+                    raise SystemExit(f"{prog.name}: registers {r1} and {r2} share slots (PC_ALIAS)")
     comp(pc)
     LAYOUT["nslots_pc"] = max(compiled[p.name].max_slot for p in pc)
     LAYOUT["nconsts_pc"] = len(first)
