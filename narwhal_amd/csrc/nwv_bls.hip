@@ -202,6 +202,31 @@ __global__ __launch_bounds__(BLS_LANES) void k_bls_h2c_g(uint32_t n, const uint8
     if (!h.inf) g1_to_affine_vt(x, y, h);
     st_g1(rec + (size_t)G1_REC_WORDS * i, x, y, h.inf);
 }
+// The same on a lane pair: lane 2 j maps u_0 and lane 2 j + 1 u_1 of item 32 b + j; the odd lane
+// hands its point over through LDS.  32 items a wave instead of 8: a 16,384-item call is 512 waves
+// (one per SIMD at most) instead of 2,048 (two per SIMD, six of every group's eight lanes
+// repeating the pair's work), so each lane's dependent chain runs with its SIMD to itself.
+constexpr int G1J_WORDS = 3 * NL + 1;
+__global__ __launch_bounds__(BLS_LANES) void k_bls_h2c_2(uint32_t n, const uint8_t* msg, const uint64_t* off,
+                                                         const uint32_t* len, const uint8_t* dst, uint32_t dl,
+                                                         uint32_t* rec, const uint32_t* kmode) {
+    __shared__ uint32_t xa[(BLS_LANES / 2) * G1J_WORDS];
+    const int pr = (int)threadIdx.x >> 1, u = (int)threadIdx.x & 1;
+    const uint32_t i = blockIdx.x * (BLS_LANES / 2) + (uint32_t)pr;
+    jac<fp> q;
+    if (i < n) {
+        q = h2c_map(msg + off[i], len[i], dst, dl, u);
+        if (u) st_g1j(xa + G1J_WORDS * pr, q);
+    }
+    __syncthreads();
+    if (i >= n || u) return;
+    const jac<fp> q1 = ld_g1j(xa + G1J_WORDS * pr);
+    const jac<fp> h0 = jac_add(q, q1);
+    const jac<fp> h = kmode && kmode[i] ? h0 : jac_mul64(h0, BLS_H_EFF);
+    fp x = fp_zero(), y = fp_zero();
+    if (!h.inf) g1_to_affine_vt(x, y, h);
+    st_g1(rec + (size_t)G1_REC_WORDS * i, x, y, h.inf);
+}
 // the item's status in the oracle's order: the signature's, then the keys'
 __global__ __launch_bounds__(BLS_LANES) void k_bls_status(uint32_t n, const int32_t* st_sig, const int32_t* st_apk,
                                                           int32_t* st) {
@@ -1478,6 +1503,16 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     BLS_HIP(hipEventRecord(L.ev[10], s1));
     // side 1: hash to G1 (every item: the statuses are not known yet)
     BLS_HIP(hipEventRecord(L.ev[5], s2));
+    // hash to G1: lane pairs (NWV_BLS_H2C_GROUP=1: the 8-lane group form)
+    static const bool h2c_group = [] {
+        const char* e = std::getenv("NWV_BLS_H2C_GROUP");
+        return e && std::atoi(e) != 0;
+    }();
+    if (!h2c_group)
+        hipLaunchKernelGGL(k_bls_h2c_2, dim3((unsigned)((n + BLS_LANES / 2 - 1) / (BLS_LANES / 2))), dim3(BLS_LANES), 0,
+                           s2, (uint32_t)n, in + o_msg, reinterpret_cast<const uint64_t*>(in + o_moff),
+                           reinterpret_cast<const uint32_t*>(in + o_mlen), in + o_dst, (uint32_t)dl, hrec, km);
+    else
     hipLaunchKernelGGL(k_bls_h2c_g, dim3(gBlocks(n)), dim3(BLS_LANES), 0, s2, (uint32_t)n, in + o_msg,
                        reinterpret_cast<const uint64_t*>(in + o_moff), reinterpret_cast<const uint32_t*>(in + o_mlen),
                        in + o_dst, (uint32_t)dl, hrec, km);
