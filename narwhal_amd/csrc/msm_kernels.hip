@@ -997,11 +997,14 @@ struct MsmTailArgs {
     // many buckets on quads whatever quad_max_c says: one quad pass a level at C = 128
     uint32_t quad_top_c;
     uint32_t hseq;
-    // bound on the final-sum wave's polls of one window's ready flag (each a coherent load plus a
-    // short sleep).  Reaching it ends the kernel with *verdict = 2, "undetermined": the host then
-    // runs the per-signature pass instead of reporting the batch invalid.
-    uint32_t spin_limit;
 };
+// bound on the final-sum wave's polls of one window's ready flag (each a coherent load plus a
+// short sleep; seconds in all).  Reaching it ends the kernel with *verdict = 2, "undetermined":
+// the host then runs the per-signature pass instead of reporting the batch invalid.  A compile-time
+// constant: read from the kernel's arguments instead, it cost the tail 10 us at 65,536 signatures
+// (same-box A/B, profiles/round6_tail_spin_ab.json).  The _spin1 kernels (bound 1) are the test
+// hook that forces the undetermined outcome (NWV_TAIL_SPIN_LIMIT).
+static constexpr uint32_t TAIL_SPIN = 1u << 24;
 static constexpr int TAIL_QUAD_TOP = 4;
 // batch verdict codes in *verdict (state word 1) and the host word's low two bits
 static constexpr uint32_t MSM_REJECTED = 0u, MSM_ACCEPTED = 1u, MSM_UNDETERMINED = 2u;
@@ -1183,9 +1186,12 @@ __device__ __forceinline__ bool msm_tail_window(const MsmLayout& lay, const MsmT
     // ---- chunk butterfly: lane 0 -> R_s, lane 2^k -> T_{s,k}
     uint32_t* mine = lds + P3_WORDS * t;
     ge_p3 p = ge_p3_identity();
+    const uint32_t qmax = w >= lay.nw - TAIL_QUAD_TOP && a.quad_top_c > a.quad_max_c ? a.quad_top_c : a.quad_max_c;
+    // (bucket joins stay lane-local: joining on quads, each continuation piece loaded into LDS and
+    // added by quad_p3_add, made the tail at 65,536 slower, 152 -> 168 us, same-box A/B,
+    // profiles/round6_tail_quad_join_ab.json: each piece's global load sat on the quad's chain)
     if (t < C) p = msm_bucket_join(a, lay.kbase[w] + (uint32_t)(s * C + t));
     if (s == 0) NWV_TAIL_STAMP(7);
-    const uint32_t qmax = w >= lay.nw - TAIL_QUAD_TOP && a.quad_top_c > a.quad_max_c ? a.quad_top_c : a.quad_max_c;
     if ((uint32_t)C <= qmax) {
         // on quads (latency-bound small batches): every level's C / 2 additions (lanes i with bit
         // o clear add lane i + o, in place) as 64 quads per pass
@@ -1285,7 +1291,7 @@ __device__ __forceinline__ bool msm_tail_window(const MsmLayout& lay, const MsmT
     return true;
 }
 
-template <int PER>
+template <int PER, uint32_t SPIN>
 __device__ __forceinline__ void msm_tail_body(const MsmLayout& lay, const MsmTailArgs& a) {
     if (msm_failed(a.fail)) {  // rejected at prep (the sort and bucket kernels skipped their work)
         if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
@@ -1333,8 +1339,8 @@ __device__ __forceinline__ void msm_tail_body(const MsmLayout& lay, const MsmTai
     for (int w = 0; w < lay.nw; w++) {
         // a bounded wait: a window that never publishes ends the kernel with "undetermined"
         uint32_t spins = 0;
-        while (tail_ld_coh(ready + w) == 0u && ++spins < a.spin_limit) __builtin_amdgcn_s_sleep(1);
-        if (spins >= a.spin_limit) {
+        while (tail_ld_coh(ready + w) == 0u && ++spins < SPIN) __builtin_amdgcn_s_sleep(1);
+        if (spins >= SPIN) {
             timed_out = true;
             break;
         }
@@ -1366,7 +1372,15 @@ __device__ __forceinline__ void msm_tail_body(const MsmLayout& lay, const MsmTai
 #endif
 }
 
-extern "C" __global__ void __launch_bounds__(256) k_msm_tail(MsmLayout lay, MsmTailArgs a) { msm_tail_body<1>(lay, a); }
+extern "C" __global__ void __launch_bounds__(256) k_msm_tail(MsmLayout lay, MsmTailArgs a) {
+    msm_tail_body<1, TAIL_SPIN>(lay, a);
+}
 extern "C" __global__ void __launch_bounds__(256) k_msm_tail_wide(MsmLayout lay, MsmTailArgs a) {
-    msm_tail_body<3>(lay, a);
+    msm_tail_body<3, TAIL_SPIN>(lay, a);
+}
+extern "C" __global__ void __launch_bounds__(256) k_msm_tail_spin1(MsmLayout lay, MsmTailArgs a) {
+    msm_tail_body<1, 1u>(lay, a);
+}
+extern "C" __global__ void __launch_bounds__(256) k_msm_tail_wide_spin1(MsmLayout lay, MsmTailArgs a) {
+    msm_tail_body<3, 1u>(lay, a);
 }

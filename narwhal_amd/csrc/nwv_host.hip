@@ -786,18 +786,14 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
         const char* e = std::getenv("NWV_TAIL_QUAD_TOP_C");
         return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 128u;
     }();
-    // the final-sum wave's bound on waiting for one window (NWV_TAIL_SPIN_LIMIT: a test hook that
-    // forces the undetermined outcome; the default is seconds of polling)
-    static const uint32_t spin_limit = [] {
-        const char* e = std::getenv("NWV_TAIL_SPIN_LIMIT");
-        const unsigned long v = e ? std::strtoul(e, nullptr, 10) : (1ul << 24);
-        return (uint32_t)std::max(1ul, std::min(v, (unsigned long)UINT32_MAX));
-    }();
+    // NWV_TAIL_SPIN_LIMIT (test hook): the _spin1 kernels, whose final-sum wave gives up on a window
+    // at its first poll -- the undetermined outcome
+    static const bool spin1 = std::getenv("NWV_TAIL_SPIN_LIMIT") != nullptr;
     const MsmTailArgs ta{b.m_bsum.as<uint32_t>(), b.m_hpart.as<uint32_t>(), kst, E, p.nkeys, p.seg,
                          b.m_tpart.as<uint32_t>(), b.m_wsum.as<uint32_t>(),
                          b.m_ctr.as<uint32_t>(), state, b.m_partial.as<uint32_t>(),
                          d.gpu->comb.as<uint32_t>(), sblk, quad_max_c, state + 1, state + 2, p.tail_S, st_buf,
-                         hverdict, quad_top_c, hseq & 0x3FFFFFFFu, spin_limit};
+                         hverdict, quad_top_c, hseq & 0x3FFFFFFFu};
     // combine items per thread: (lg C + 1) x S_w over the windows (C = nb / S_w buckets per chunk)
     int items = 0;
     for (int w = 0; w < p.lay.nw; w++) {
@@ -807,11 +803,11 @@ int msm_launch(Lane& d, EdBuffers& b, size_t n, const uint8_t seed32[32], hipStr
         items = std::max(items, (lgC + 1) * Sw);
     }
     if (items <= 256)
-        hipLaunchKernelGGL(k_msm_tail, dim3(p.tail_S, (unsigned)p.lay.nw + 1), dim3(256), (size_t)4 * (256 * P3_WORDS + 4),
-                           stream, p.lay, ta);
-    else
-        hipLaunchKernelGGL(k_msm_tail_wide, dim3(p.tail_S, (unsigned)p.lay.nw + 1), dim3(256),
+        hipLaunchKernelGGL(spin1 ? k_msm_tail_spin1 : k_msm_tail, dim3(p.tail_S, (unsigned)p.lay.nw + 1), dim3(256),
                            (size_t)4 * (256 * P3_WORDS + 4), stream, p.lay, ta);
+    else
+        hipLaunchKernelGGL(spin1 ? k_msm_tail_wide_spin1 : k_msm_tail_wide, dim3(p.tail_S, (unsigned)p.lay.nw + 1),
+                           dim3(256), (size_t)4 * (256 * P3_WORDS + 4), stream, p.lay, ta);
     if ((rc = mark(8))) return rc;
     if ((rc = mark(9))) return rc;
     NWV_HIP(hipGetLastError());
