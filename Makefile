@@ -62,7 +62,10 @@ tests/_build/libhostemu.so: tests/hostemu/hostemu.cpp $(CSRC)
 	@mkdir -p tests/_build
 	$(HIPCC) -std=c++17 -O1 --offload-host-only -x hip -DNWV_BOUNDS_CHECK -fPIC -shared -o $@ tests/hostemu/hostemu.cpp
 
-tools: tools/ubench_valu tools/ubench_field tools/ubench_wave tools/ubench_row tools/ubench_prep
+tools: tools/ubench_valu tools/ubench_field tools/ubench_wave tools/ubench_row tools/ubench_prep tools/libsvcbench.so
+# native drivers of the C5 service leg (bench tooling): the service and the Core drain timed from C++ threads
+tools/libsvcbench.so: tools/svcbench.cpp narwhal_amd/lib/libnwv.so include/nwv.h include/nwv_types.h include/nwv_service.h
+	g++ -O2 -std=c++17 -fPIC -shared -pthread -Wall -o $@ $< -Lnarwhal_amd/lib -lnwv -Wl,-rpath,'$$ORIGIN/../narwhal_amd/lib'
 tools/ubench_valu: tools/ubench_valu.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -o $@ $<
 tools/ubench_field: tools/ubench_field.hip narwhal_amd/csrc/fe25519.h

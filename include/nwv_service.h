@@ -44,6 +44,11 @@ typedef void (*nwv_done_fn)(void* user, int32_t result);
  * oldest pending item has waited this long (0: flush whatever is pending at once). */
 int nwv_service_create(nwv_ctx* ctx, const nwv_committee* committee, size_t max_batch, uint32_t max_wait_us,
                        nwv_service** out);
+/* burst flush (default off): also flush once no item has been submitted for idle_us, so a burst
+ * of submissions (a round of headers, votes and certificates delivered together) goes out as one
+ * call as soon as it ends instead of waiting out max_wait_us, or being cut by it; max_batch and
+ * max_wait_us still apply.  0 turns it off. */
+int nwv_service_set_idle(nwv_service* svc, uint32_t idle_us);
 /* later submissions are verified against this committee; pending items are completed first */
 int nwv_service_set_committee(nwv_service* svc, const nwv_committee* committee);
 
@@ -78,7 +83,7 @@ int nwv_service_verify_bls_certificate(nwv_service* svc, const nwv_bls_certifica
 int nwv_service_flush(nwv_service* svc);
 
 /* out[0] engine calls, [1] items verified, [2] largest batch, [3] flushes triggered by
- * max_batch, [4] by max_wait_us, [5] by nwv_service_flush / set_committee / free */
+ * max_batch, [4] by max_wait_us or the idle gap, [5] by nwv_service_flush / set_committee / free */
 int nwv_service_stats(nwv_service* svc, uint64_t out[6]);
 
 /* completes every pending item, then stops the service threads */

@@ -56,11 +56,20 @@ struct OwnedCommittee {
 
 enum Kind { HEADER = 0, VOTE = 1, CERT = 2 };
 
+// an uninitialised buffer (every byte of an item's copy is written by the copy itself: a vector's
+// zero fill doubled the memory traffic of a submission)
+template <class T>
+struct RawBuf {
+    std::unique_ptr<T[]> p;
+    void resize(size_t n) { p.reset(n ? new T[n] : nullptr); }
+    T* data() { return p.get(); }
+};
+
 // one submitted message, deep-copied: the views point into bytes / words
 struct Item {
     Kind kind;
-    std::vector<uint8_t> bytes;
-    std::vector<uint32_t> words;
+    RawBuf<uint8_t> bytes;
+    RawBuf<uint32_t> words;
     nwv_header h{};
     nwv_vote v{};
     nwv_certificate c{};
@@ -227,6 +236,8 @@ struct nwv_service {
     bool bls = false;  // BLS12-381 service (nwv_service_create_bls): one nwv_bls_verify_mixed_many per flush
     size_t max_batch = 1;
     std::chrono::microseconds max_wait{0};
+    std::chrono::microseconds idle{0};  // nwv_service_set_idle: flush once no item arrived for this long (0: off)
+    Clock::time_point last_submit{};
     std::mutex mu;
     std::condition_variable cv_work, cv_done;
     std::deque<std::unique_ptr<Item>> pending;
@@ -255,9 +266,17 @@ void nwv_service::run() {
         int reason = -1;
         if (pending.size() >= max_batch) reason = 3;
         else if (stop || flush_upto > front.seq) reason = 5;
-        else if (Clock::now() >= front.t + max_wait) reason = 4;
+        else {
+            // a burst has ended (no arrival for `idle`) or the oldest item has waited max_wait
+            const auto now = Clock::now();
+            auto due = front.t + max_wait;
+            if (idle.count() > 0) due = std::min(due, last_submit + idle);
+            if (now >= due) reason = 4;
+        }
         if (reason < 0) {
-            cv_work.wait_until(lk, front.t + max_wait);
+            auto due = front.t + max_wait;
+            if (idle.count() > 0) due = std::min(due, last_submit + idle);
+            cv_work.wait_until(lk, due);
             continue;
         }
         // take up to 8 batches' worth: under a backlog one larger call beats several small ones
@@ -326,6 +345,7 @@ int nwv_service::submit(std::unique_ptr<Item> it, nwv_done_fn done, void* user) 
     it->com = com;
     it->seq = next_seq++;
     it->t = Clock::now();
+    last_submit = it->t;
     open.insert(it->seq);
     pending.push_back(std::move(it));
     if (pending.size() == 1 || pending.size() >= max_batch) cv_work.notify_one();
@@ -546,6 +566,16 @@ int nwv_service_flush(nwv_service* svc) {
     svc->flush_upto = std::max(svc->flush_upto, upto);
     svc->cv_work.notify_all();
     svc->cv_done.wait(lk, [&] { return svc->open.empty() || *svc->open.begin() >= upto; });
+    return NWV_OK;
+}
+
+int nwv_service_set_idle(nwv_service* svc, uint32_t idle_us) {
+    if (!svc) return NWV_ERR_ARG;
+    {
+        std::lock_guard<std::mutex> g(svc->mu);
+        svc->idle = std::chrono::microseconds(idle_us);
+    }
+    svc->cv_work.notify_all();
     return NWV_OK;
 }
 

@@ -40,6 +40,7 @@ _SIGS = {
     "nwv_service_verify_bls_vote": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "nwv_service_verify_bls_certificate": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)],
                                            ctypes.c_int),
+    "nwv_service_set_idle": ([ctypes.c_void_p, ctypes.c_uint32], ctypes.c_int),
     "nwv_service_flush": ([ctypes.c_void_p], ctypes.c_int),
     "nwv_service_stats": ([ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     "nwv_service_free": ([ctypes.c_void_p], None),
@@ -64,7 +65,8 @@ class Service:
     types.Header / Vote with 96-byte keys and 48-byte signatures and types.BlsCertificate; each
     flush is one nwv_bls_verify_mixed_many call (nwv_service_create_bls)."""
 
-    def __init__(self, engine, committee, max_batch=256, max_wait_us=200, lib=None, ctx=None, scheme="ed25519"):
+    def __init__(self, engine, committee, max_batch=256, max_wait_us=200, lib=None, ctx=None, scheme="ed25519",
+                 idle_us=0):
         if scheme not in ("ed25519", "bls"):
             raise ValueError("scheme must be 'ed25519' or 'bls'")
         self.lib = bind(lib if lib is not None else _lib.load())
@@ -78,6 +80,8 @@ class Service:
         if rc:
             raise _lib.NwvError(rc, "nwv_service_create")
         self._h = h
+        if idle_us:
+            _lib._check(self.lib.nwv_service_set_idle(h, idle_us))
         self._callbacks = {}
         self._keys = itertools.count()
 
@@ -181,7 +185,8 @@ class CoreDrain:
     _CLS = {"header": T._Header, "vote": T._Vote, "certificate": T._Certificate}
     _CLS_BLS = {"header": T._Header, "vote": T._Vote, "certificate": T._BlsCertificate}
 
-    def __init__(self, engine, committee, max_items=512, max_wait_us=1000, min_items=64, scheme="ed25519"):
+    def __init__(self, engine, committee, max_items=512, max_wait_us=1000, min_items=64, scheme="ed25519",
+                 idle_us=50):
         if max_items < 1:
             raise ValueError("max_items must be >= 1")
         if scheme not in ("ed25519", "bls"):
@@ -191,6 +196,7 @@ class CoreDrain:
         self.max_items = max_items
         self.max_wait_us = max_wait_us
         self.min_items = min_items
+        self.idle_us = idle_us
         self.set_committee(committee)
         self.calls = self.items = self.largest = 0
 
@@ -201,9 +207,10 @@ class CoreDrain:
 
     def drain(self, q, first=None):
         """`first` (or a blocking q.get()) plus whatever q holds, at most max_items messages; when
-        q runs dry it waits for more until the deadline only while fewer than min_items are taken
-        (a big enough batch goes at once: waiting would only add latency; q: a queue.Queue
-        standing in for Core's channels)"""
+        q runs dry it waits for more until the deadline while fewer than min_items are taken, and
+        (idle_us > 0) for at most idle_us more once min_items are in: a burst still arriving is
+        taken whole, while a big enough batch with nothing behind it goes at once (q: a
+        queue.Queue standing in for Core's channels)"""
         import queue
         import time
         out = [q.get() if first is None else first]
@@ -215,7 +222,9 @@ class CoreDrain:
             except queue.Empty:
                 pass
             left = deadline - time.perf_counter()
-            if left <= 0 or len(out) >= self.min_items:
+            if len(out) >= self.min_items:
+                left = min(left, self.idle_us * 1e-6)
+            if left <= 0:
                 break
             try:
                 out.append(q.get(timeout=left))

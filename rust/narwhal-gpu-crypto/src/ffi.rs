@@ -628,6 +628,7 @@ extern "C" {
         c: *const NwvBlsCertificate,
         result: *mut i32,
     ) -> c_int;
+    pub fn nwv_service_set_idle(svc: *mut NwvService, idle_us: u32) -> c_int;
     pub fn nwv_service_flush(svc: *mut NwvService) -> c_int;
     pub fn nwv_service_stats(svc: *mut NwvService, out: *mut u64) -> c_int;
     pub fn nwv_service_free(svc: *mut NwvService);

@@ -494,6 +494,10 @@ impl VerificationService {
     pub fn set_committee(&self, committee: &ffi::NwvCommittee) -> bool {
         unsafe { ffi::nwv_service_set_committee(self.0, committee) == ffi::NWV_OK }
     }
+    /// burst flush: also flush once nothing was submitted for `idle_us` (0: off)
+    pub fn set_idle(&self, idle_us: u32) -> bool {
+        unsafe { ffi::nwv_service_set_idle(self.0, idle_us) == ffi::NWV_OK }
+    }
     fn code(rc: i32, r: i32) -> Result<DagCode, String> {
         if rc == ffi::NWV_OK {
             Ok(r)

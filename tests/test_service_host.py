@@ -135,6 +135,46 @@ def test_max_batch_and_deadline_triggers(lib):
         svc.close()
 
 
+def test_idle_gap_flushes_a_burst_as_one_call(lib):
+    """nwv_service_set_idle: a burst of submissions goes out as ONE engine call once nothing has
+    arrived for idle_us -- long before max_wait_us -- and a second burst after a pause is a second
+    call; with the gap off the same burst waits out max_wait_us"""
+    lib.stub_reset(0, 0)
+    rnd = random.Random(12)
+    svc = S.Service(None, _committee(0), max_batch=1000, max_wait_us=3_000_000, lib=lib, ctx=ctypes.c_void_p(1),
+                    idle_us=40_000)
+    try:
+        for burst in range(2):
+            items = [_vote(rnd, 0, k == 5) for k in range(40)]
+            codes, ev = [], threading.Event()
+
+            def cb(code, codes=codes, ev=ev):
+                codes.append(code)
+                if len(codes) == 40:
+                    ev.set()
+            t0 = time.perf_counter()
+            for it in items:
+                svc.submit_vote(it, cb)
+            assert ev.wait(5)
+            waited = time.perf_counter() - t0
+            assert 0.04 <= waited < 1.5, waited  # the idle gap, not the 3 s deadline
+            assert sorted(codes) == [0] * 39 + [T.InvalidSignature.code]
+            st = svc.stats()
+            assert st["calls"] == burst + 1 and st["by_deadline"] == burst + 1 and st["max_batch"] == 40, st
+            time.sleep(0.1)
+    finally:
+        svc.close()
+    svc = S.Service(None, _committee(0), max_batch=1000, max_wait_us=300_000, lib=lib, ctx=ctypes.c_void_p(1))
+    try:
+        ev = threading.Event()
+        t0 = time.perf_counter()
+        for k in range(10):
+            svc.submit_vote(_vote(rnd, 0, False), lambda c, k=k: ev.set() if k == 9 else None)
+        assert ev.wait(5) and time.perf_counter() - t0 >= 0.29  # no gap: the deadline
+    finally:
+        svc.close()
+
+
 def test_flush_completes_everything_submitted_before(lib):
     lib.stub_reset(0, 0)
     rnd = random.Random(3)
@@ -265,6 +305,14 @@ def test_core_drain_policy():
     t0 = time.perf_counter()
     assert d2.drain(q) == [0, 1]  # a late message within the deadline joins the flush
     assert 0.15 < time.perf_counter() - t0 < 2.0  # then the deadline ends the drain
+    # idle_us: past min_items, a message arriving within the gap still joins; then the gap ends it
+    d4 = S.CoreDrain(None, com, max_items=100, max_wait_us=2_000_000, min_items=2, idle_us=150_000)
+    for i in range(3):
+        q.put(i)
+    threading.Timer(0.03, lambda: q.put(3)).start()
+    t0 = time.perf_counter()
+    assert d4.drain(q) == [0, 1, 2, 3]
+    assert 0.15 < time.perf_counter() - t0 < 1.5  # the gap after the last arrival, not the 2 s deadline
 
 
 def test_blocking_wait_that_closes_a_cycle_is_refused(lib):

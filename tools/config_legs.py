@@ -11,6 +11,7 @@
 Fixtures are built with the product only (GPU signer, GPU digests, nwv_certificate_new); the CPU
 legs that time the oracle live in bench.py (cpu_baseline_configs)."""
 import ctypes
+import os
 import hashlib
 import time
 
@@ -273,7 +274,7 @@ def leg_c5_service(eng, com, cc, harr, varr, carr, nsig, rounds=20):
         go.set()
         th.join()
     a = np.array(lat) * 1e3
-    out.update({"consumer": "one thread, CoreDrain(max_items=512, max_wait_us=1000, min_items=64)",
+    out.update({"consumer": "one thread, CoreDrain(max_items=512, max_wait_us=1000, min_items=64, idle_us=50)",
                 "ms_per_round": float(np.median(rtimes)) * 1e3, "sigs_per_s": nsig / float(np.median(rtimes)),
                 "latency_ms_p50": float(np.percentile(a, 50)), "latency_ms_p99": float(np.percentile(a, 99)),
                 "engine_calls": len(sizes), "largest_flush": int(max(sizes)),
@@ -327,6 +328,7 @@ def leg_c5_service(eng, com, cc, harr, varr, carr, nsig, rounds=20):
                            "ms_per_round": float(np.median(rtimes)) * 1e3,
                            "sigs_per_s": nsig / float(np.median(rtimes)),
                            "engine_calls": int(stats2[0]), "items": int(stats2[1]), "largest_batch": int(stats2[2])}
+    out["native"] = leg_c5_service_native(eng, cc, harr, varr, carr, nsig, rounds)
     # the same messages, one engine call per message, serially (the reference's Core loop shape)
     tl = T.lib()
     one = []
@@ -339,6 +341,56 @@ def leg_c5_service(eng, com, cc, harr, varr, carr, nsig, rounds=20):
             one.append(time.perf_counter() - t1)
     out["one_call_per_message"] = {"latency_ms_p50": float(np.median(one)) * 1e3,
                                    "ms_per_round": float(np.sum(one)) * 1e3}
+    return out
+
+
+def _svcbench():
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "libsvcbench.so")
+    lib = ctypes.CDLL(path)
+    vp, sz, i32, u32, dp = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p
+    lib.svcbench_service.argtypes = [vp, vp, sz, vp, sz, vp, sz, vp, i32, i32, sz, u32, u32, dp, dp, dp, dp]
+    lib.svcbench_drain.argtypes = [vp, vp, sz, vp, sz, vp, sz, vp, i32, sz, u32, sz, u32, dp, dp, dp, dp]
+    return lib
+
+
+def leg_c5_service_native(eng, cc, harr, varr, carr, nsig, rounds=20):
+    """The C5 service leg driven from C++ threads (tools/svcbench.cpp), as a Rust Core would run it
+    (rust/narwhal-gpu-crypto/src/core_drain.rs): no Python queue, no ctypes call per message.
+    'drain_idle*': a producer thread delivers the round's 299 messages one at a time into a channel
+    and ONE consumer drains and verifies (CoreDrain's pattern, max_items 512, max_wait 1000 us,
+    min_items 64; idle_us 50: past min_items wait up to 50 us for each next message);
+    'service_k_idle*': k threads submit the round to nwv_service asynchronously (idle 50: the
+    burst flush, nwv_service_set_idle)."""
+    sb = _svcbench()
+    n = len(harr) + len(varr) + len(carr)
+    args = (eng._h, ctypes.byref(cc), len(harr), ctypes.cast(harr, ctypes.c_void_p), len(varr),
+            ctypes.cast(varr, ctypes.c_void_p), len(carr), ctypes.cast(carr, ctypes.c_void_p))
+    out = {"messages_per_round": n, "rounds": rounds}
+    rt = np.zeros(rounds)
+    lat = np.zeros(rounds * n)
+    calls = np.zeros(rounds, dtype=np.uint32)
+    big = np.zeros(rounds, dtype=np.uint32)
+    for idle in (0, 50):
+        rc = sb.svcbench_drain(*args, rounds, 512, 1000, 64, idle, rt.ctypes.data, lat.ctypes.data, calls.ctypes.data,
+                               big.ctypes.data)
+        assert rc == 0, rc
+        out[f"drain_idle{idle}"] = {
+            "max_items": 512, "max_wait_us": 1000, "min_items": 64, "idle_us": idle,
+            "ms_per_round": float(np.median(rt)), "sigs_per_s": nsig / (float(np.median(rt)) * 1e-3),
+            "latency_ms_p50": float(np.percentile(lat, 50)), "latency_ms_p99": float(np.percentile(lat, 99)),
+            "engine_calls_per_round": float(np.mean(calls)), "largest_flush": int(big.max())}
+    for k, wait, idle in ((1, 200, 0), (8, 200, 0), (1, 1000, 50), (8, 1000, 50)):
+        st = np.zeros(6, dtype=np.uint64)
+        sub = np.zeros(rounds)
+        rc = sb.svcbench_service(*args, k, rounds, 512, wait, idle, rt.ctypes.data, sub.ctypes.data, lat.ctypes.data,
+                                 st.ctypes.data)
+        assert rc == 0, rc
+        out[f"service_{k}_idle{idle}"] = {
+            "submitter_threads": k, "max_batch": 512, "max_wait_us": wait, "idle_us": idle,
+            "ms_per_round": float(np.median(rt)), "sigs_per_s": nsig / (float(np.median(rt)) * 1e-3),
+            "submit_ms_per_round": float(np.median(sub)),
+            "latency_ms_p50": float(np.percentile(lat, 50)), "latency_ms_p99": float(np.percentile(lat, 99)),
+            "engine_calls_per_round": float(st[0]) / (rounds + 1), "largest_batch": int(st[2])}
     return out
 
 
