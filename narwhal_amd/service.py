@@ -186,7 +186,7 @@ class CoreDrain:
     _CLS_BLS = {"header": T._Header, "vote": T._Vote, "certificate": T._BlsCertificate}
 
     def __init__(self, engine, committee, max_items=512, max_wait_us=1000, min_items=64, scheme="ed25519",
-                 idle_us=50):
+                 idle_us=0):
         if max_items < 1:
             raise ValueError("max_items must be >= 1")
         if scheme not in ("ed25519", "bls"):

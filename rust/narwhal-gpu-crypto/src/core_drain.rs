@@ -40,11 +40,13 @@ pub struct DrainPolicy {
 }
 
 impl Default for DrainPolicy {
-    /// 512 messages, 64, 1 ms, 50 us: a 100-node round (100 headers, 100 certificates, 99 votes)
-    /// fits one flush and a burst still arriving is taken whole (a gap of 50 us ends it), while a
-    /// trickle waits at most 1 ms (about two coalesced verifications of such a round)
+    /// 512 messages, 64, 1 ms, no idle wait: a 100-node round (100 headers, 100 certificates, 99
+    /// votes) fits one flush, a burst of 64+ goes at once, and a trickle waits at most 1 ms (about
+    /// two coalesced verifications of such a round).  `idle` of 50 us takes a fast burst whole
+    /// (one call instead of two: 0.79 -> 0.69 ms a round from native threads) but costs the
+    /// overlap with a slow producer
     fn default() -> Self {
-        DrainPolicy { max_items: 512, min_items: 64, max_wait: Duration::from_micros(1000), idle: Duration::from_micros(50) }
+        DrainPolicy { max_items: 512, min_items: 64, max_wait: Duration::from_micros(1000), idle: Duration::ZERO }
     }
 }
 

@@ -274,7 +274,7 @@ def leg_c5_service(eng, com, cc, harr, varr, carr, nsig, rounds=20):
         go.set()
         th.join()
     a = np.array(lat) * 1e3
-    out.update({"consumer": "one thread, CoreDrain(max_items=512, max_wait_us=1000, min_items=64, idle_us=50)",
+    out.update({"consumer": "one thread, CoreDrain(max_items=512, max_wait_us=1000, min_items=64)",
                 "ms_per_round": float(np.median(rtimes)) * 1e3, "sigs_per_s": nsig / float(np.median(rtimes)),
                 "latency_ms_p50": float(np.percentile(a, 50)), "latency_ms_p99": float(np.percentile(a, 99)),
                 "engine_calls": len(sizes), "largest_flush": int(max(sizes)),
