@@ -373,7 +373,7 @@ NWV_HD bool w_pairing_check_g(const W& w, const uint32_t* sig_rec, const uint32_
     w.put_words(REG_QB, q_rec, q_jac ? 6 : 4);
     if (!q_jac) w.put_fp(REG_QB + 4, k_one());
     w.sync();
-    return wave::pairing_check(w, qlines);
+    return wave::pairing_check(w, qlines, !pc_bank);  // a PC bank holds the one-step programs only
 }
 // w_pairing_check with H in homogeneous coordinates (w_hash_to_g1's record)
 template <class W>

@@ -703,10 +703,12 @@ NWV_HD void final_exp(const W& w) {
 //   sig: affine x, y (identity -> x = y = 0: pair A then contributes only its lines' l0 in Fp2,
 //        which the final exponentiation maps to 1);
 //   H:   homogeneous X, Y, Z (x = X / Z);  Q: Jacobian X, Y, Z (Fp2 each; affine -> Z = 1);
-//   qlines: Q's precomputed line table (NSTEPS x 6 slots) or null (computed from T in the loop).
+//   qlines: Q's precomputed line table (NSTEPS x 6 slots) or null (computed from T in the loop);
+//   two_step: with qlines, the one- to three-step programs of BLS_WAVE_GROUPS_STR (NSLOTS_PAIR2
+//   slots), else one program a step (NSLOTS_PC slots suffice).
 // The caller has run init_slots and filled PA (x, -y), PB, QB; this sets F = 1, TB = QB.
 template <class W>
-NWV_HD bool pairing_check(const W& w, const uint32_t* qlines) {
+NWV_HD bool pairing_check(const W& w, const uint32_t* qlines, bool two_step = true) {
     w.zero(REG_F, 12);
     w.sync();
     w.put_fp(REG_F, k_one());
@@ -714,6 +716,63 @@ NWV_HD bool pairing_check(const W& w, const uint32_t* qlines) {
     w.sync();
     const char* steps = BLS_WAVE_STEPS_STR;
     constexpr int LW = 6 * SW;  // words of a step's line
+    if (qlines && two_step) {
+        // both pairs' lines precomputed: programs of one to three steps (BLS_WAVE_GROUPS_STR: a
+        // multi-step program folds each step's output combinations into the next one's operands
+        // and schedules the later steps' line products beside the first's work: 308 stages
+        // against 408), the lines of the group's steps in LA / LB, LA2 / LB2, LA3 / LB3, the next
+        // group's fetched while this one runs (LDS of NSLOTS_PAIR2 slots)
+        const char* groups = BLS_WAVE_GROUPS_STR;
+        auto la = w.fetch(&T_G2_LINES[0][0][0], LW), lb = w.fetch(qlines, LW);
+        auto la2 = w.fetch(&T_G2_LINES[1][0][0], LW), lb2 = w.fetch(qlines + LW, LW);
+        auto la3 = w.fetch(&T_G2_LINES[2][0][0], LW), lb3 = w.fetch(qlines + 2 * LW, LW);
+        int k = 0;
+#pragma unroll 1
+        for (int g = 0; g < NGROUPS; g++) {
+            const char c = groups[g];
+            const int ns = (c == 'd' || c == 'a') ? 1 : (c == 'D' || c == 'E' || c == 'A') ? 2 : 3;
+            w.put_pre(REG_LA, la, LW);
+            w.put_pre(REG_LB, lb, LW);
+            if (ns > 1) {
+                w.put_pre(REG_LA2, la2, LW);
+                w.put_pre(REG_LB2, lb2, LW);
+            }
+            if (ns > 2) {
+                w.put_pre(REG_LA3, la3, LW);
+                w.put_pre(REG_LB3, lb3, LW);
+            }
+            w.sync();
+            k += ns;
+            if (k < NSTEPS) {
+                la = w.fetch(&T_G2_LINES[k][0][0], LW);
+                lb = w.fetch(qlines + (size_t)k * LW, LW);
+            }
+            if (k + 1 < NSTEPS) {
+                la2 = w.fetch(&T_G2_LINES[k + 1][0][0], LW);
+                lb2 = w.fetch(qlines + (size_t)(k + 1) * LW, LW);
+            }
+            if (k + 2 < NSTEPS) {
+                la3 = w.fetch(&T_G2_LINES[k + 2][0][0], LW);
+                lb3 = w.fetch(qlines + (size_t)(k + 2) * LW, LW);
+            }
+            Prog p = P_ML_DBL_FIXED;
+            switch (c) {
+                case 'a': p = P_ML_ADD_FIXED; break;
+                case 'D': p = P_ML2_DD_FIXED; break;
+                case 'E': p = P_ML2_DA_FIXED; break;
+                case 'A': p = P_ML2_AD_FIXED; break;
+                case 'T': p = P_ML3_DDD_FIXED; break;
+                case 'U': p = P_ML3_DDA_FIXED; break;
+                case 'V': p = P_ML3_DAD_FIXED; break;
+                case 'W': p = P_ML3_ADD_FIXED; break;
+                default: break;
+            }
+            w.run(p);
+        }
+        w.run(P_CONJ_F);
+        final_exp(w);
+        return w.f_is_one();
+    }
     auto la = w.fetch(&T_G2_LINES[0][0][0], LW);
     auto lb = w.fetch(qlines ? qlines : &T_G2_LINES[0][0][0], qlines ? LW : 0);
 #pragma unroll 1

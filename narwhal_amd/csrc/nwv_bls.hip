@@ -35,6 +35,7 @@
 #include "../../include/nwv_bls.h"
 #include "bls_verify.h"
 #include "bls_shard.h"
+#include "stage_args.h"
 
 using namespace bls;
 using nwv::bls_for_ranges;
@@ -627,7 +628,9 @@ __global__ __launch_bounds__(64) void k_blsw_pair(uint32_t n, const uint32_t* sr
                                                   const int32_t* st_apk, KeyTab kt, const uint32_t* pk_off,
                                                   const uint32_t* pk_cnt, const uint32_t* pk_idx, const uint32_t* kmode,
                                                   int32_t* st_pair) {
-    BLSW_IDX();
+    BLSW_LDS(wave::NSLOTS_PAIR2);  // the two-step Miller-loop programs (a key's line table)
+    const uint32_t i = blockIdx.x;
+    if (i >= n) return;
     blsw_pair_item(wm, i, srec, st_dec, hrec, h_hom, arec, st_apk, kt, pk_off, pk_cnt, pk_idx, kmode, st_pair);
 }
 // the pairing checks (blocks [0, n)) and the signatures' G1 checks (blocks [n, 2n)) as one launch:
@@ -637,7 +640,7 @@ __global__ __launch_bounds__(64) void k_blsw_pair_sub(uint32_t n, const uint32_t
                                                       const int32_t* st_apk, KeyTab kt, const uint32_t* pk_off,
                                                       const uint32_t* pk_cnt, const uint32_t* pk_idx,
                                                       const uint32_t* kmode, int32_t* st_pair, int32_t* st_sub) {
-    BLSW_LDS(wave::NSLOTS_PAIR);
+    BLSW_LDS(wave::NSLOTS_PAIR2);
     const uint32_t b = blockIdx.x;
     if (b < n)
         blsw_pair_item(wm, b, srec, st_dec, hrec, h_hom, arec, st_apk, kt, pk_off, pk_cnt, pk_idx, kmode, st_pair);
@@ -650,7 +653,7 @@ __global__ __launch_bounds__(64) void k_blsw_pair_sub_f(uint32_t n, const uint32
                                                         const int32_t* st_apk, KeyTab kt, const uint32_t* pk_off,
                                                         const uint32_t* pk_cnt, const uint32_t* pk_idx,
                                                         const uint32_t* kmode, int32_t* st_pair, int32_t* st_sub) {
-    BLSW_LDS(wave::NSLOTS_PAIR);
+    BLSW_LDS(wave::NSLOTS_PAIR2);
     const uint32_t b = blockIdx.x;
     if (b < n)
         pair_flat<8>(wm_lds, b, 1, srec, st_dec, hrec, h_hom, arec, st_apk, kt, pk_off, pk_cnt, pk_idx, kmode, st_pair);
@@ -1425,7 +1428,7 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
         d.last_keys[1] = n_dec;
         return NWV_OK;
     };
-    BLS_HIP(hipMemcpyAsync(in, h, a.total, hipMemcpyHostToDevice, s0));
+    BLS_HIP(nwv_stage::stage_h2d(in, h, a.total, s0));  // small calls: through kernel arguments
     BLS_HIP(hipEventRecord(L.ev[9], s0));
     BLS_HIP(hipStreamWaitEvent(s1, L.ev[9], 0));
     if (wave_small) {
@@ -1447,33 +1450,36 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
                            km, ajrec, sapk);
         BLS_HIP(hipEventRecord(L.ev[2], s1));
         BLS_HIP(hipEventRecord(L.ev[6], s1));
-        BLS_HIP(hipEventRecord(L.ev[10], s1));
         BLS_HIP(hipEventRecord(L.ev[3], s0));
         hipLaunchKernelGGL(k_blsw_sigdec, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, in + o_sigs, srec,
                            sdec);
         BLS_HIP(hipEventRecord(L.ev[4], s0));
-        BLS_HIP(hipStreamWaitEvent(s0, L.ev[10], 0));
-        BLS_HIP(hipEventRecord(L.ev[7], s0));
+        kept.stream = s1;  // k_blsw_status writes the ring slots there
+        // the rest runs on side 0 behind the hash, which ends after the signatures' decode (one
+        // lane each, ~0.45 ms against ~0.57 ms): its wait on the decode is already met, so the
+        // cross-queue hand-off (~25 us in the single-verify trace) is off the critical path
+        BLS_HIP(hipStreamWaitEvent(s1, L.ev[4], 0));
+        BLS_HIP(hipEventRecord(L.ev[7], s1));
         static const bool sub_flat = [] {
             const char* e = std::getenv("NWV_BLS_SUB_FLAT");
             return e && std::atoi(e) != 0;
         }();
         if (sub_flat && ensure_pair_script()) return NWV_ERR_HIP;
-        hipLaunchKernelGGL(sub_flat ? k_blsw_pair_sub_f : k_blsw_pair_sub, dim3((unsigned)(2 * n)), dim3(64), 0, s0,
+        hipLaunchKernelGGL(sub_flat ? k_blsw_pair_sub_f : k_blsw_pair_sub, dim3((unsigned)(2 * n)), dim3(64), 0, s1,
                            (uint32_t)n,
                            (const uint32_t*)srec, (const int32_t*)sdec, (const uint32_t*)hh, 1, (const uint32_t*)ajrec,
                            (const int32_t*)sapk, kt, reinterpret_cast<const uint32_t*>(in + o_off),
                            reinterpret_cast<const uint32_t*>(in + o_cnt), reinterpret_cast<const uint32_t*>(in + o_idx),
                            km, spair, ssub);
-        BLS_HIP(hipEventRecord(L.ev[8], s0));
+        BLS_HIP(hipEventRecord(L.ev[8], s1));
         // (the verified records into the ring slots this call reserved)
-        hipLaunchKernelGGL(k_blsw_status, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n,
+        hipLaunchKernelGGL(k_blsw_status, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s1, (uint32_t)n,
                            (const int32_t*)sdec, (const int32_t*)ssub, (const int32_t*)sapk, (const int32_t*)spair, st,
                            (const uint32_t*)srec, keep ? static_cast<uint32_t*>(d.sc.rec.p) : nullptr,
                            reinterpret_cast<const uint32_t*>(in + o_scs));
         BLS_HIP(hipGetLastError());
-        BLS_HIP(hipMemcpyAsync(status, st, 4 * n, hipMemcpyDeviceToHost, s0));
-        BLS_HIP(hipStreamSynchronize(s0));
+        BLS_HIP(hipMemcpyAsync(status, st, 4 * n, hipMemcpyDeviceToHost, s1));
+        BLS_HIP(hipStreamSynchronize(s1));
         if (keep) {
             d.sc.publish(n, sigs, status, kept.slots);
             kept.sc = nullptr;
@@ -1821,13 +1827,13 @@ int nwv_bls_aggregate(nwv_ctx* ctx, size_t n, const uint8_t* sigs48, uint8_t out
                 else pos[i] = it->second;
             }
             if (all) {
-                BLS_HIP(hipMemcpyAsync(L.in.p, pos.data(), 4 * n, hipMemcpyHostToDevice, L.stream));
+                BLS_HIP(nwv_stage::stage_h2d(L.in.p, pos.data(), 4 * n, L.stream));
                 sum_tree(static_cast<const uint32_t*>(d->sc.rec.p), static_cast<const uint32_t*>(L.in.p), nullptr);
                 return fetch();
             }
         }
     }
-    BLS_HIP(hipMemcpyAsync(L.in.p, sigs48, 48 * n, hipMemcpyHostToDevice, L.stream));
+    BLS_HIP(nwv_stage::stage_h2d(L.in.p, sigs48, 48 * n, L.stream));
     if (n <= 1024) {  // decode on one lane each, the G1 checks on a wave each
         auto* sdec = reinterpret_cast<int32_t*>(w + w_st2);
         hipLaunchKernelGGL(k_blsw_sigdec, dim3(kBlocks(n)), dim3(BLS_LANES), 0, L.stream, (uint32_t)n,

@@ -25,6 +25,7 @@
 #include "msm_kernels.hip"
 #include "tiny_kernels.hip"
 #include "shard.h"
+#include "stage_args.h"
 
 #include <random>
 
@@ -1064,7 +1065,7 @@ int ed_stage(Lane& d, EdBuffers& b, size_t lo, size_t hi, const uint8_t* pk, con
         NWV_HIP(hipMemcpyAsync(gdev + o_msg + mbytes, h + o_msg + mbytes, total - o_msg - mbytes,
                                hipMemcpyHostToDevice, d.stream));
     } else {
-        NWV_HIP(hipMemcpyAsync(b.in.p, h, total, hipMemcpyHostToDevice, d.stream));
+        NWV_HIP(nwv_stage::stage_h2d(b.in.p, h, total, d.stream));  // small calls: through kernel arguments
     }
     NWV_HIP(hipEventRecord(d.hstage_ev, d.stream));
     htrace("stage:copy-issued");
@@ -2346,7 +2347,7 @@ static int b2_stage(Lane& d, size_t n, const uint8_t* base, const uint64_t* off,
         std::memcpy(h + o_len, len + lo, 8 * m);
         if (bytes) std::memcpy(h + o_bytes, base + mlo, bytes);
         std::memset(h + o_bytes + bytes, 0, MSG_PAD);
-        NWV_HIP(hipMemcpyAsync(d.b2_in.p, h, total, hipMemcpyHostToDevice, d.stream));
+        NWV_HIP(nwv_stage::stage_h2d(d.b2_in.p, h, total, d.stream));  // small calls: through kernel arguments
         NWV_HIP(hipEventRecord(d.b2stage_ev, d.stream));
         const uint8_t* g = d.b2_in.as<uint8_t>();
         st = B2Staged{g + o_bytes, reinterpret_cast<const uint64_t*>(g), reinterpret_cast<const uint64_t*>(g + o_len)};

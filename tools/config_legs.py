@@ -328,7 +328,10 @@ def leg_c5_service(eng, com, cc, harr, varr, carr, nsig, rounds=20):
                            "ms_per_round": float(np.median(rtimes)) * 1e3,
                            "sigs_per_s": nsig / float(np.median(rtimes)),
                            "engine_calls": int(stats2[0]), "items": int(stats2[1]), "largest_batch": int(stats2[2])}
-    out["native"] = leg_c5_service_native(eng, cc, harr, varr, carr, nsig, rounds)
+    try:  # bench tooling (tools/libsvcbench.so, built by `make tools`): its absence costs only this field
+        out["native"] = leg_c5_service_native(eng, cc, harr, varr, carr, nsig, rounds)
+    except OSError as e:
+        out["native"] = {"error": str(e)}
     # the same messages, one engine call per message, serially (the reference's Core loop shape)
     tl = T.lib()
     one = []

@@ -237,9 +237,12 @@ REGS.add("TB", 6)    # the Miller loop's running point T = [k] Q (Jacobian)
 REGS.add("N", 2)     # norm / inverse exchange (Fp2) of the final exponentiation's inversion
 REGS.add("U", 6)     # G1 points, homogeneous (X, Y, Z): accumulator and base of scalar chains
 REGS.add("V", 3)
-REGS.add("W", 6)     # G2 homogeneous points (key sums): accumulator (6) and addend (6)
-REGS.add("W2", 6)
+REGS.add("LA2", 6)   # the next step's lines (LA, LB) for the two-step Miller-loop programs (ml2_*);
+REGS.add("LB2", 6)   # outside the pairing check's bank: only the one-item kernels run those programs
 REGS.add("S", 8)     # scratch inputs: hash-to-curve map outputs, subgroup-check inputs
+REGS.add("LA3", 6)   # the third step's lines of a three-step program; these two share slots with U and
+REGS.add("LB3", 6)   # S (UP_ALIAS), which no Miller-loop program touches
+UP_ALIAS = {"LA3": ("U", 0), "LB3": ("S", 0)}
 # the pairing check's registers: the programs that touch no others (the Miller loop, the final
 # exponentiation, the line programs) see slot 0, their own constants, these registers and their
 # temporaries as one run of slots [0, NSLOTS_PC) -- the bank one item takes in the packed pairing
@@ -1123,6 +1126,42 @@ program("ml_dbl_fixed")(lambda io: _mlstep(io, False, True, True))
 program("ml_add_fixed")(lambda io: _mlstep(io, True, True, True))
 
 
+def _mlsteps(io, adds):
+    """consecutive steps with precomputed lines for both pairs (step j's in LA / LB, LA2 / LB2,
+    LA3 / LB3) as one program: the later steps' line products are scheduled beside the first
+    step's work and each step's output combinations fold into the next one's operands -- 10
+    stages for two doublings, 14 for three, against 6 per step"""
+    o = _Overlay(io)
+    for j, add in enumerate(adds):
+        o.rename = {} if j == 0 else {"LA": f"LA{j + 1}", "LB": f"LB{j + 1}"}
+        _mlstep(o, add, True, True)
+    for (reg, i), x in o.w.items():
+        io.put(reg, i, x)
+
+
+class _Overlay:
+    """an io for composing program bodies: writes are kept and read back by later reads; reads of
+    the registers in `rename` go to others"""
+
+    def __init__(self, io):
+        self.io, self.w, self.rename = io, {}, {}
+
+    def fp(self, reg, i):
+        if (reg, i) in self.w:
+            return self.w[(reg, i)]
+        return self.io.fp(self.rename.get(reg, reg), i)
+
+    def put(self, reg, i, x):
+        self.w[(reg, i)] = x
+
+
+# one-item kernels only (wave::pairing_check with a key's line table): not part of the packed bank
+ML2 = {"ml2_dd_fixed": "dd", "ml2_da_fixed": "da", "ml2_ad_fixed": "ad",
+       "ml3_ddd_fixed": "ddd", "ml3_dda_fixed": "dda", "ml3_dad_fixed": "dad", "ml3_add_fixed": "add"}
+for _n, _a in ML2.items():
+    program(_n)((lambda a: lambda io: _mlsteps(io, [c == "a" for c in a]))(_a))
+
+
 def _lines(io, add):
     """a key's line table (precomputed once per cached key): T <- 2T or T + Q, the line -> LB"""
     T = (f2_of(io, "TB", 0), f2_of(io, "TB", 1), f2_of(io, "TB", 2))
@@ -1137,6 +1176,29 @@ def _lines(io, add):
 
 program("lines_dbl")(lambda io: _lines(io, False))
 program("lines_add")(lambda io: _lines(io, True))
+
+
+# the Miller loop with precomputed lines for both pairs as a sequence of programs: one character
+# per program, 'd' / 'a' one step (ml_dbl_fixed / ml_add_fixed), D E A two steps (dd da ad), T U V W
+# three (ddd dda dad add; ML2); chosen to minimise the stages
+GROUP_STEPS = {"d": "d", "a": "a", "D": "dd", "E": "da", "A": "ad", "T": "ddd", "U": "dda", "V": "dad", "W": "add"}
+GROUP_PROG = {"d": "ml_dbl_fixed", "a": "ml_add_fixed", "D": "ml2_dd_fixed", "E": "ml2_da_fixed", "A": "ml2_ad_fixed",
+              "T": "ml3_ddd_fixed", "U": "ml3_dda_fixed", "V": "ml3_dad_fixed", "W": "ml3_add_fixed"}
+GROUP_STAGES = {}  # program -> stages, filled by build_all (the compiled counts)
+
+
+def miller_groups():
+    steps = "".join(miller_steps())
+    cost = {g: GROUP_STAGES.get(GROUP_PROG[g], 6 * len(GROUP_STEPS[g])) for g in GROUP_STEPS}
+    best = [(0, "")] + [None] * len(steps)
+    for i in range(1, len(steps) + 1):
+        for g, st in GROUP_STEPS.items():
+            j = i - len(st)
+            if j >= 0 and steps[j:i] == st and best[j] is not None:
+                c = (best[j][0] + cost[g], best[j][1] + g)
+                if best[i] is None or c[0] < best[i][0]:
+                    best[i] = c
+    return best[-1][1]
 
 
 def miller_steps():
@@ -1225,8 +1287,9 @@ def final_exp_seq(vals, run=_run_int, inv=None):
     run("mul_F_G", vals)
 
 
-def pairing_check_int(sig_xy, h_xyz, q_xy, fixed_b=False):
-    """e(-sig, g2) e(H, Q) == 1 through the programs (plain integers): sig affine, H homogeneous"""
+def pairing_check_int(sig_xy, h_xyz, q_xy, fixed_b=False, groups=None):
+    """e(-sig, g2) e(H, Q) == 1 through the programs (plain integers): sig affine, H homogeneous;
+    groups (fixed_b only): the Miller loop by the one- and two-step programs of miller_groups"""
     la = line_table(G2X, G2Y)
     lb = line_table(*q_xy) if fixed_b else None
     vals = _f12_vals("F", (((1, 0), (0, 0), (0, 0)), ((0, 0), (0, 0), (0, 0))))
@@ -1237,7 +1300,19 @@ def pairing_check_int(sig_xy, h_xyz, q_xy, fixed_b=False):
     for i, c in enumerate((qx[0], qx[1], qy[0], qy[1], 1, 0)):
         vals[("QB", i)] = c
         vals[("TB", i)] = c
-    for k, st in enumerate(miller_steps()):
+    if groups is not None:
+        assert fixed_b
+        k = 0
+        for g in groups:
+            for j, (ra, rb) in enumerate((("LA", "LB"), ("LA2", "LB2"), ("LA3", "LB3"))[:len(GROUP_STEPS[g])]):
+                for i, c in enumerate([c for two in la[k + j] for c in two]):
+                    vals[(ra, i)] = c
+                for i, c in enumerate([c for two in lb[k + j] for c in two]):
+                    vals[(rb, i)] = c
+            _run_int(GROUP_PROG[g], vals)
+            k += len(GROUP_STEPS[g])
+        assert k == len(miller_steps())
+    for k, st in enumerate(miller_steps() if groups is None else []):
         for i, c in enumerate([c for two in la[k] for c in two]):
             vals[("LA", i)] = c
         if fixed_b:
@@ -1299,9 +1374,14 @@ def check_pairing_formulas():
     qb = _aff_mul(G2X, G2Y, b, 2)
     ok1, _ = pairing_check_int(pa, (pa[0], pa[1], 1), (G2X, G2Y))
     ok2, _ = pairing_check_int(pab, (pa[0] * 5 % P, pa[1] * 5 % P, 5), qb)
-    ok3, _ = pairing_check_int(pab, (pa[0], pa[1], 1), qb, fixed_b=True)
+    ok3, f3 = pairing_check_int(pab, (pa[0], pa[1], 1), qb, fixed_b=True)
     bad, _ = pairing_check_int(_aff_mul(G1X, G1Y, a * b + 1, 1), (pa[0], pa[1], 1), qb)
     assert ok1 and ok2 and ok3 and not bad, (ok1, ok2, ok3, bad)
+    # the two-step programs' schedule: the same verdicts, the same Fp12 before the comparison
+    grp = miller_groups()
+    ok4, f4 = pairing_check_int(pab, (pa[0], pa[1], 1), qb, fixed_b=True, groups=grp)
+    bad4, _ = pairing_check_int(_aff_mul(G1X, G1Y, a * b + 1, 1), (pa[0], pa[1], 1), qb, fixed_b=True, groups=grp)
+    assert ok4 and f4 == f3 and not bad4, (ok4, bad4)
 
 
 # ---- G1: hash to curve (the isogeny map and h_eff) and the subgroup check ---------------------
@@ -1553,8 +1633,11 @@ def emit(compiled, path):
     L.append(f"constexpr int NSLOTS = {max_slot};")
     # the pairing check's and the G1 check's programs (every program but the hash's isogeny map and
     # the aggregate's sums): the pairing kernels give a wave this many slots
-    pair_max = max(compiled[nm].max_slot for nm in names if nm != "iso2_add" and not nm.startswith("g1_sum"))
+    pair_max = max(compiled[nm].max_slot for nm in names
+                   if nm != "iso2_add" and not nm.startswith("g1_sum") and nm not in ML2)
     L.append(f"constexpr int NSLOTS_PAIR = {pair_max};")
+    # ... and with the two-step Miller-loop programs (the one-item pairing kernels: a key's lines)
+    L.append(f"constexpr int NSLOTS_PAIR2 = {max(pair_max, max(compiled[nm].max_slot for nm in ML2))};")
     L.append(f"constexpr int NCONSTS = {len(consts)};")
     # the pairing check's programs address [0, NSLOTS_PC) only (checked here): slot 0, the first
     # NCONSTS_PC constants at slots 1.., PC_REGS, their temporaries; the other constants start at
@@ -1587,6 +1670,13 @@ def emit(compiled, path):
     for name, first, n, off, nl0 in progs:
         L.append(f"constexpr Prog P_{name.upper()} = {{{off}u, {n}, {nl0}}};")
     L.append("#define BLS_WAVE_STEPS_STR \"" + "".join(miller_steps()) + "\"")
+    grp = miller_groups()
+    L.append("// the Miller loop with a key's line table by programs of one to three steps: d / a one step,")
+    L.append("// D E A = dd da ad, T U V W = ddd dda dad add (ml2_* / ml3_*; " +
+             str(sum(GROUP_STAGES[GROUP_PROG[g]] for g in grp)) +
+             " stages against " + str(sum(GROUP_STAGES[GROUP_PROG[c]] for c in miller_steps())) + ")")
+    L.append("#define BLS_WAVE_GROUPS_STR \"" + grp + "\"")
+    L.append(f"constexpr int NGROUPS = {len(grp)};")
     L.append("BLS_WAVE_TABLE uint32_t T_CONSTS[NCONSTS][14] = {")
     for a in consts:
         L.append("    {" + ", ".join(f"0x{x:07x}u" for x in _limbs(a.value)) + "},")
@@ -1670,9 +1760,19 @@ def build_all():
     LAYOUT["const2_slot"] = LAYOUT["nslots_pc"]
     for i, a in enumerate(rest):
         a.slot = LAYOUT["const2_slot"] + i
-    REGS.layout(LAYOUT["const2_slot"] + len(rest), [r for r in REGS.order if r not in PC_REGS])
+    REGS.layout(LAYOUT["const2_slot"] + len(rest), [r for r in REGS.order if r not in PC_REGS and r not in UP_ALIAS])
+    for name, (ref, off) in UP_ALIAS.items():
+        REGS.regs[name][0] = REGS.regs[ref][0] + off
+    for prog, _ in traced:  # no program touches two registers that share slots
+        regs = sorted(_prog_regs(prog))
+        for i, r1 in enumerate(regs):
+            for r2 in regs[i + 1:]:
+                if r1 not in PC_REGS and r2 not in PC_REGS and _overlap(r1, r2):
+                    raise SystemExit(f"{prog.name}: registers {r1} and {r2} share slots (UP_ALIAS)")
     comp([prog for prog, _ in traced if prog not in pc])
     order = [prog.name for prog, _ in traced]
+    for g, name in GROUP_PROG.items():
+        GROUP_STAGES[name] = len(compiled[name].stages)
     return {name: compiled[name] for name in order}
 
 
