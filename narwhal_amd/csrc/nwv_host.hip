@@ -1566,9 +1566,9 @@ static int tiny_on_device(Lane& d, EdBuffers& b, size_t n, hipStream_t stream, i
     if (stamps) {  // phase times of workgroup 0 in us from its start (s_memrealtime: 100 MHz)
         unsigned long long t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (hipMemcpy(t, b.m_stamps.p, 64, hipMemcpyDeviceToHost) == hipSuccess)
-            std::fprintf(stderr, "tiny n=%zu: R %.1f hash %.1f comb-done %.1f barrier %.1f final %.1f us\n", n,
-                         (t[1] - t[0]) / 100.0, (t[2] - t[0]) / 100.0, (t[4] - t[0]) / 100.0, (t[5] - t[0]) / 100.0,
-                         (t[6] - t[0]) / 100.0);
+            std::fprintf(stderr, "tiny n=%zu: R %.1f 8R %.1f hash %.1f 8P %.1f barrier %.1f final %.1f us\n", n,
+                         (t[1] - t[0]) / 100.0, (t[3] - t[0]) / 100.0, (t[2] - t[0]) / 100.0, (t[4] - t[0]) / 100.0,
+                         (t[5] - t[0]) / 100.0, (t[6] - t[0]) / 100.0);
     }
     *ok = all ? 1 : 0;
     if (bits) bits[0] = vb;

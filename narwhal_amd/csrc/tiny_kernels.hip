@@ -11,7 +11,8 @@
 //            then, while R still decompresses, [s]B - [k]A from two fixed-base combs -- B's (per
 //            device) and the key's (i 16^j A, built once at key registration, k_key_comb_fill) --
 //            one table entry of each per lane and a six-level tree of quad-lane additions in LDS:
-//            no doubling chain at all; then -R, [8] (three quad-lane doublings), the identity test
+//            no doubling chain at all; then [8] of that sum (three quad-lane doublings), while
+//            wave 0 doubles R three times on its rows; [8] R = [8]([s]B - [k]A) tested projectively
 //   last     the last workgroup to arrive (one per signature, grid <= 64) collects the verdict bits,
 //            writes the batch verdict and stores both into the lane's polled host word
 // Against the batch MSM path for these sizes (five launches: prep, sort, bucket, tail's 128-
@@ -58,10 +59,12 @@ __device__ __forceinline__ void tiny_digits(const uint32_t c[8], int* out) {
 }  // namespace
 
 // One workgroup of two waves per signature (a CU each: nothing else competes for their SIMDs).
-// Wave 0 decompresses R on a row -- the critical chain; wave 1 hashes on one lane, then sums the
-// signature's comb terms on all 64 lanes while R is still decompressing, then, once R is in,
-// subtracts it, multiplies by 8 and tests the identity.  Phase stamps of workgroup 0 with
-// NWV_TINY_STAMPS: [1] R decoded, [2] hashed, [4] comb summed, [5] barrier, [6] verdict.
+// Wave 0 decompresses R on a row -- the critical chain -- and doubles it three times there; wave 1
+// hashes on one lane, then sums the signature's comb terms on all 64 lanes and multiplies the sum
+// by 8 while R is still decompressing; after the barrier lane 0 compares the two projectively
+// (was: subtract R, three doublings, identity test, all after the barrier: 50.5 us to the verdict).
+// Phase stamps of workgroup 0 with NWV_TINY_STAMPS: [1] R decoded, [3] [8] R, [2] hashed, [4]
+// [8] of the comb sum, [5] barrier, [6] verdict.
 static constexpr int TINY_WAVES = 2;
 // s_memrealtime (100 MHz) into stamp slot k, by lane 0 of a wave of workgroup 0
 #define NWV_TINY_STAMP(k)                                                                       \
@@ -71,7 +74,7 @@ static constexpr int TINY_WAVES = 2;
 extern "C" __global__ void __launch_bounds__(64 * TINY_WAVES) k_ed_tiny(TinyArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
     __shared__ uint32_t rsh[4 * 48];     // wave 0's rows (48 words each; row 0 is R)
-    __shared__ uint32_t rrec[32];        // R's affine Niels record; word 31: 1 = does not decode
+    __shared__ uint32_t rrec[32];        // [8] R: X | Y | Z (10 limbs each); word 31: 1 = R does not decode
     __shared__ int dg[2][COMB_TABLES];   // digits of s and of k
     __shared__ uint32_t hok;             // s < l
     __shared__ uint32_t pts[64 * P3_WORDS];  // the 64 comb terms, summed in place
@@ -84,12 +87,24 @@ extern "C" __global__ void __launch_bounds__(64 * TINY_WAVES) k_ed_tiny(TinyArgs
         const uint32_t y16 = reinterpret_cast<const uint16_t*>(a.sig + 64 * (size_t)i)[limb];
         uint32_t* sh = rsh + 48 * row;
         const bool ok = row_decompress(y16, lane, row, limb, sh);
-        if (row == 0 && limb < 3) store_fe(&rrec[10 * limb], fe_from_limbs16(sh + 16 * limb));
-        if (lane == 0) {
-            rrec[30] = 0u;
-            rrec[31] = ok ? 0u : 1u;
-        }
         NWV_TINY_STAMP(1);
+        // [8] R on the rows while wave 1 finishes [8]([s]B - [k]A): three row doublings (one
+        // multiply latency each) from (2x : 2y : 2) = ((y+x) - (y-x) : (y+x) + (y-x) : 2)
+        rowf::RowConsts k = rowf::row_consts();
+        k.rot = 1;
+        const uint32_t ypx = sh[limb], ymx = sh[16 + limb];
+        rowf::RowP3 d{rowf::carry32(rowf::sub(ypx, ymx, k), k), rowf::carry32(ypx + ymx, k),
+                      rowf::sel(rowf::limb_is(0), 0u, 2u), 0u};
+#pragma unroll 1
+        for (int r = 0; r < 3; r++) d = rowf::row_dbl(d, k);
+        rowf::lds_order();
+        sh[limb] = d.X;
+        sh[16 + limb] = d.Y;
+        sh[32 + limb] = d.Z;
+        rowf::lds_order();
+        if (row == 0 && limb < 3) store_fe(&rrec[10 * limb], fe_from_limbs16(sh + 16 * limb));  // X | Y | Z
+        if (lane == 0) rrec[31] = ok ? 0u : 1u;
+        NWV_TINY_STAMP(3);
     } else {
         if (lane == 0) {
             uint32_t Aw[8], Rw[8], Sw[8], k[8];
@@ -129,26 +144,31 @@ extern "C" __global__ void __launch_bounds__(64 * TINY_WAVES) k_ed_tiny(TinyArgs
             for (int g = lane >> 2; g < 32 / o; g += 16) quad_p3_add(pts, 2 * o * g, o, q);
             rowf::lds_order();
         }
-        NWV_TINY_STAMP(4);
-    }
-    __syncthreads();  // R decompressed, the comb sum done
-    if (wv == 1) {
-        NWV_TINY_STAMP(5);
-        if (lane == 0) {
-            const ge_p3 P = load_p3(pts);
-            store_p3(pts, ge_p1p1_to_p3(ge_madd(P, msm_load_point(rrec, true))));  // [s]B - [k]A - R
-        }
-        rowf::lds_order();
-        // [8] as three doublings on the first quad (an addition of the slot to itself)
+        // [8] P as three doublings on the first quad (an addition of the slot to itself)
         if (lane < 4)
 #pragma unroll 1
             for (int r = 0; r < 3; r++) {
                 quad_p3_add(pts, 0, 0, lane);
                 rowf::lds_order();
             }
+        NWV_TINY_STAMP(4);
+    }
+    __syncthreads();  // [8] R and [8]([s]B - [k]A) done
+    if (wv == 1) {
+        NWV_TINY_STAMP(5);
+        // the cofactored equation [8](R - ([s]B - [k]A)) = 0 as [8] R = [8] P, projectively: the four
+        // cross products on lanes 0..3 (P.X RZ, RX P.Z, P.Y RZ, RY P.Z), canonical words into LDS
+        // (wave 0's rows, free after the barrier), compared by lane 0
+        if (lane < 4) {
+            const uint32_t* u = ((lane & 1) ? rrec : pts) + (lane < 2 ? 0 : 10);
+            const uint32_t* v = ((lane & 1) ? pts : rrec) + 20;
+            fe_freeze(fe_mul(load_fe(u), load_fe(v)), rsh + 8 * lane);
+        }
+        rowf::lds_order();
         if (lane == 0) {
-            const ge_p3 P = load_p3(pts);
-            const bool id = fe_is_zero(P.X) && fe_eq(P.Y, P.Z);
+            bool id = true;
+#pragma unroll
+            for (int q = 0; q < 8; q++) id = id && rsh[q] == rsh[8 + q] && rsh[16 + q] == rsh[24 + q];
             const bool aok = a.kc[(size_t)KC_SLOT_WORDS * a.kslot[i] + MSM_PT_WORDS - 1] == 0u;
             const bool ok = id && aok && hok && rrec[31] == 0u;
             NWV_TINY_STAMP(6);

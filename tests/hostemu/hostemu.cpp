@@ -595,11 +595,37 @@ int he_tiny_verify(const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, ui
         }
         P = p3_add(P, Pj);
     }
-    // -R as the kernel adds it: R's affine Niels record, negated
-    uint32_t rrec[MSM_PT_WORDS];
+    // [8] R as the kernel computes it: three row doublings (fe_row.h row_dbl, every row holding R)
+    // from (2x : 2y : 2) = ((y+x) - (y-x) : (y+x) + (y-x) : 2), R's record as row limbs
+    if (!rok) R = ge_p3_identity();
+    uint32_t rrec[MSM_PT_WORDS], yp[16], ym[16];
     msm_store_point(rrec, R);
-    P = ge_p1p1_to_p3(ge_madd(P, msm_load_point(rrec, true)));
-    return (p3_mul8_is_identity(P) && aok && rok && sok) ? 1 : 0;
+    fe_to_limbs16(load_fe(rrec), yp);
+    fe_to_limbs16(load_fe(rrec + 10), ym);
+    rowf::RowConsts rk = rowf::row_consts();
+    rk.rot = 1;
+    rowf::V ypx, ymx, two;
+    for (int l = 0; l < 64; l++) {
+        ypx.l[l] = yp[l & 15];
+        ymx.l[l] = ym[l & 15];
+        two.l[l] = (l & 15) == 0 ? 2u : 0u;
+    }
+    rowf::RowP3 d{rowf::carry32(rowf::sub(ypx, ymx, rk), rk), rowf::carry32(ypx + ymx, rk), two, rowf::bc(0)};
+    for (int r = 0; r < 3; r++) d = rowf::row_dbl(d, rk);
+    uint32_t xl[16], yl[16], zl[16];
+    for (int i = 0; i < 16; i++) {
+        xl[i] = d.X.l[i];
+        yl[i] = d.Y.l[i];
+        zl[i] = d.Z.l[i];
+    }
+    const fe RX = fe_from_limbs16(xl), RY = fe_from_limbs16(yl), RZ = fe_from_limbs16(zl);
+    // the round-5 form of the same equation, [8](P - R) = O, must agree with the kernel's
+    const ge_p3 Q = ge_p1p1_to_p3(ge_madd(P, msm_load_point(rrec, true)));
+    // [8] P, then [8] R = [8] P projectively (the cofactored equation [8](R - P) = 0)
+    for (int r = 0; r < 3; r++) P = p3_add(P, P);
+    const bool eq = fe_eq(fe_mul(P.X, RZ), fe_mul(RX, P.Z)) && fe_eq(fe_mul(P.Y, RZ), fe_mul(RY, P.Z));
+    if (rok && eq != p3_mul8_is_identity(Q)) return -2;
+    return (eq && aok && rok && sok) ? 1 : 0;
 }
 
 // signed digits of a 256-bit scalar over layout(c): z range (bits = 128) or full range (253);
