@@ -90,6 +90,10 @@ typedef struct nwv_ctx nwv_ctx;
  * (nwv_keycache_register: each key gets a fixed-base comb table) is checked in one launch,
  * signature by signature (k_ed_tiny); this flag sends it through the batch MSM instead */
 #define NWV_FLAG_NO_TINY 4096u
+/* BLS12-381 calls of at most 1,024 items (the per-call paths) record the per-stage timing events
+ * that nwv_bls_last_kernel_ms reports only with this flag: the events cost a single verification
+ * ~0.1 ms (larger calls always record them) */
+#define NWV_FLAG_BLS_STAGE_TIMES 8192u
 
 /* ------------------------------------------------------------------ lifecycle ----- */
 /* Process-wide context creation (created once, in Primary::spawn).

@@ -61,7 +61,8 @@ int nwv_bls_verify_many(nwv_ctx* ctx, size_t n_keys, const uint8_t* keys, size_t
 /* device time of the last nwv_bls_verify_many call on this context, per stage (HIP events; the
  * first four run on three concurrent streams): [0] keys new to the device's key cache, [1]
  * signature decode + G1 checks, [2] hash to G1, [3] key sums, [4] the pairing check (the batch
- * check k_bls_rlc + k_bls_fold + k_bls_final, plus k_bls_pair when it ran) */
+ * check k_bls_rlc + k_bls_fold + k_bls_final, plus k_bls_pair when it ran).  Calls of at most
+ * 1,024 items record these only on a context opened with NWV_FLAG_BLS_STAGE_TIMES (else zeros). */
 int nwv_bls_last_kernel_ms(nwv_ctx* ctx, double out_ms[5]);
 /* how the last nwv_bls_verify_many call checked its pairings: 0 per item on the 8-lane group
  * kernels (NWV_FLAG_BLS_PER_ITEM), 1 one batch check that accepted every item and 2 a batch check

@@ -36,6 +36,7 @@ NWV_FLAG_NO_ROW_PREP = 512
 NWV_FLAG_NO_EARLY_PREP = 1024
 NWV_FLAG_NO_FUSED_KEYSUM = 2048
 NWV_FLAG_NO_TINY = 4096
+NWV_FLAG_BLS_STAGE_TIMES = 8192  # per-stage timing events on small BLS calls (nwv_bls_last_kernel_ms)
 NWV_RUN_TIMED = 0x100
 
 
@@ -188,6 +189,7 @@ class Engine:
             _check(lib.nwv_init_device(ctypes.byref(h), device, flags))
         self._h = h
         self.lib = lib
+        self.device = device  # the HIP ordinal (None: a context over the first n_devices)
 
     def close(self):
         if self._h:

@@ -940,8 +940,12 @@ struct BlsLane {
     // [11] side 1 done.  side[1] is created by the first call that needs it: a lane of small wave
     // calls holds two streams, so eight lanes map one to one onto 16 hardware queues
     hipEvent_t ev[12] = {};
+    // ordering only (no timestamps): [0] inputs resident, [1] signatures decoded (small wave calls)
+    hipEvent_t sev[2] = {};
     ~BlsLane() {
         for (auto& e : ev)
+            if (e) (void)hipEventDestroy(e);
+        for (auto& e : sev)
             if (e) (void)hipEventDestroy(e);
         for (auto& t : side)
             if (t) (void)hipStreamDestroy(t);
@@ -1142,6 +1146,11 @@ class LaneLease {
                 }
                 for (auto& e : l->ev)
                     if (hipEventCreate(&e) != hipSuccess) {
+                        rc_ = nwv_internal_set_err(NWV_ERR_HIP, "bls event");
+                        return;
+                    }
+                for (auto& e : l->sev)
+                    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
                         rc_ = nwv_internal_set_err(NWV_ERR_HIP, "bls event");
                         return;
                     }
@@ -1412,11 +1421,16 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     auto* ajrec = reinterpret_cast<uint32_t*>(w + w_aj);
     hipStream_t s0 = L.stream, s1 = L.side[0], s2 = L.side[1];
     kept.stream = s0;
+    // the per-stage timing events of a small call only on a NWV_FLAG_BLS_STAGE_TIMES context: else
+    // just the two that order the streams (the others cost a single verification ~0.1 ms:
+    // 2.85 -> 2.72-2.81 ms, profiles/round6_bls_stage_timing_ab.json)
+    const bool no_timing = !(d.flags & NWV_FLAG_BLS_STAGE_TIMES);
+    auto trec = [&](int k, hipStream_t s) { return no_timing ? hipSuccess : hipEventRecord(L.ev[k], s); };
     // stage times of the completed call, its path and key counts -> the device's "last call"
     auto finish = [&](int path_done) -> int {
         const int pairs[5][2] = {{0, 1}, {3, 4}, {5, 6}, {1, 2}, {7, 8}};  // keys, sigs, h2c, apk, pairing
-        double ms5[5];
-        for (int k = 0; k < 5; k++) {
+        double ms5[5] = {0, 0, 0, 0, 0};
+        for (int k = 0; k < 5 && !(no_timing && path_done == 3); k++) {
             float ms = 0;
             BLS_HIP(hipEventElapsedTime(&ms, L.ev[pairs[k][0]], L.ev[pairs[k][1]]));
             ms5[k] = ms;
@@ -1429,37 +1443,38 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
         return NWV_OK;
     };
     BLS_HIP(nwv_stage::stage_h2d(in, h, a.total, s0));  // small calls: through kernel arguments
-    BLS_HIP(hipEventRecord(L.ev[9], s0));
-    BLS_HIP(hipStreamWaitEvent(s1, L.ev[9], 0));
+    BLS_HIP(hipEventRecord(L.sev[0], s0));
+    BLS_HIP(hipStreamWaitEvent(s1, L.sev[0], 0));
     if (wave_small) {
         // a call of up to wave_max items on two streams (8 concurrent calls then fit 16 hardware
         // queues one to one): side 0 decodes the keys the cache does not hold, then hashes to G1
         // and sums the keys in one launch (k_blsw_pre); main decodes the signatures, then runs
         // the pairing checks and the signatures' G1 checks in one launch (k_blsw_pair_sub)
-        BLS_HIP(hipEventRecord(L.ev[0], s1));
+        BLS_HIP(trec(0, s1));
         if (n_dec)
             hipLaunchKernelGGL(k_bls_keys_fill, dim3(kBlocks(n_dec)), dim3(BLS_LANES), 0, s1, (uint32_t)n_dec,
                                in + o_keys, reinterpret_cast<const uint32_t*>(in + o_kslot),
                                const_cast<uint32_t*>(kt.rs), const_cast<int32_t*>(kt.ss));
-        BLS_HIP(hipEventRecord(L.ev[1], s1));
-        BLS_HIP(hipEventRecord(L.ev[5], s1));
+        BLS_HIP(trec(1, s1));
+        BLS_HIP(trec(5, s1));
         hipLaunchKernelGGL(k_blsw_pre, dim3((unsigned)(2 * n)), dim3(64), 0, s1, (uint32_t)n, in + o_msg,
                            reinterpret_cast<const uint64_t*>(in + o_moff), reinterpret_cast<const uint32_t*>(in + o_mlen),
                            in + o_dst, (uint32_t)dl, hh, kt, reinterpret_cast<const uint32_t*>(in + o_off),
                            reinterpret_cast<const uint32_t*>(in + o_cnt), reinterpret_cast<const uint32_t*>(in + o_idx),
                            km, ajrec, sapk);
-        BLS_HIP(hipEventRecord(L.ev[2], s1));
-        BLS_HIP(hipEventRecord(L.ev[6], s1));
-        BLS_HIP(hipEventRecord(L.ev[3], s0));
+        BLS_HIP(trec(2, s1));
+        BLS_HIP(trec(6, s1));
+        BLS_HIP(trec(3, s0));
         hipLaunchKernelGGL(k_blsw_sigdec, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s0, (uint32_t)n, in + o_sigs, srec,
                            sdec);
-        BLS_HIP(hipEventRecord(L.ev[4], s0));
+        BLS_HIP(trec(4, s0));
+        BLS_HIP(hipEventRecord(L.sev[1], s0));
         kept.stream = s1;  // k_blsw_status writes the ring slots there
         // the rest runs on side 0 behind the hash, which ends after the signatures' decode (one
         // lane each, ~0.45 ms against ~0.57 ms): its wait on the decode is already met, so the
         // cross-queue hand-off (~25 us in the single-verify trace) is off the critical path
-        BLS_HIP(hipStreamWaitEvent(s1, L.ev[4], 0));
-        BLS_HIP(hipEventRecord(L.ev[7], s1));
+        BLS_HIP(hipStreamWaitEvent(s1, L.sev[1], 0));
+        BLS_HIP(trec(7, s1));
         static const bool sub_flat = [] {
             const char* e = std::getenv("NWV_BLS_SUB_FLAT");
             return e && std::atoi(e) != 0;
@@ -1471,7 +1486,7 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
                            (const int32_t*)sapk, kt, reinterpret_cast<const uint32_t*>(in + o_off),
                            reinterpret_cast<const uint32_t*>(in + o_cnt), reinterpret_cast<const uint32_t*>(in + o_idx),
                            km, spair, ssub);
-        BLS_HIP(hipEventRecord(L.ev[8], s1));
+        BLS_HIP(trec(8, s1));
         // (the verified records into the ring slots this call reserved)
         hipLaunchKernelGGL(k_blsw_status, dim3(kBlocks(n)), dim3(BLS_LANES), 0, s1, (uint32_t)n,
                            (const int32_t*)sdec, (const int32_t*)ssub, (const int32_t*)sapk, (const int32_t*)spair, st,
@@ -1489,7 +1504,7 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     if (!L.side[1] && hipStreamCreateWithFlags(&L.side[1], hipStreamNonBlocking) != hipSuccess)
         return nwv_internal_set_err(NWV_ERR_HIP, "bls stream");
     s2 = L.side[1];
-    BLS_HIP(hipStreamWaitEvent(s2, L.ev[9], 0));
+    BLS_HIP(hipStreamWaitEvent(s2, L.sev[0], 0));
     // side 0: keys, key sums
     BLS_HIP(hipEventRecord(L.ev[0], s1));
     if (n_dec)

@@ -45,6 +45,8 @@ pub const NWV_FLAG_BLS_BATCH: u32 = 128;
 pub const NWV_FLAG_NO_SIGCACHE: u32 = 256;
 /// Keyed batches of <= 64 signatures by registered keys go through the batch MSM, not k_ed_tiny.
 pub const NWV_FLAG_NO_TINY: u32 = 4096;
+/// BLS12-381 calls of <= 1,024 items record the per-stage timing events (nwv_bls_last_kernel_ms).
+pub const NWV_FLAG_BLS_STAGE_TIMES: u32 = 8192;
 
 // per-item BLS12-381 statuses (include/nwv_bls.h)
 pub const NWV_BLS_OK: i32 = 0;
