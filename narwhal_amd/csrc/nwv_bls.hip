@@ -1425,12 +1425,13 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     // just the two that order the streams (the others cost a single verification ~0.1 ms:
     // 2.85 -> 2.72-2.81 ms, profiles/round6_bls_stage_timing_ab.json)
     const bool no_timing = !(d.flags & NWV_FLAG_BLS_STAGE_TIMES);
+    bool untimed = false;  // a small call that recorded no stage events (set on that path only)
     auto trec = [&](int k, hipStream_t s) { return no_timing ? hipSuccess : hipEventRecord(L.ev[k], s); };
     // stage times of the completed call, its path and key counts -> the device's "last call"
     auto finish = [&](int path_done) -> int {
         const int pairs[5][2] = {{0, 1}, {3, 4}, {5, 6}, {1, 2}, {7, 8}};  // keys, sigs, h2c, apk, pairing
         double ms5[5] = {0, 0, 0, 0, 0};
-        for (int k = 0; k < 5 && !(no_timing && path_done == 3); k++) {
+        for (int k = 0; k < 5 && !untimed; k++) {
             float ms = 0;
             BLS_HIP(hipEventElapsedTime(&ms, L.ev[pairs[k][0]], L.ev[pairs[k][1]]));
             ms5[k] = ms;
@@ -1446,6 +1447,7 @@ int verify_on(BlsDev& d, size_t n_keys, const uint8_t* keys, size_t n, const uin
     BLS_HIP(hipEventRecord(L.sev[0], s0));
     BLS_HIP(hipStreamWaitEvent(s1, L.sev[0], 0));
     if (wave_small) {
+        untimed = no_timing;
         // a call of up to wave_max items on two streams (8 concurrent calls then fit 16 hardware
         // queues one to one): side 0 decodes the keys the cache does not hold, then hashes to G1
         // and sums the keys in one launch (k_blsw_pre); main decodes the signatures, then runs

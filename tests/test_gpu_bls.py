@@ -234,6 +234,32 @@ def test_batch_sizes(bls, bls_batch, n, engine):
     assert list(got) == [0] * n and bls.last_path() == ("wave" if engine == "wave" else "batch_accepted")
 
 
+def test_stage_times_small_and_large_calls(bls):
+    """nwv_bls_last_kernel_ms: a call of at most 1,024 items records its per-stage timing events
+    only on a NWV_FLAG_BLS_STAGE_TIMES context (zeros otherwise: the events cost a single
+    verification ~0.1 ms); a larger call always records them.  Statuses are the same either way."""
+    import narwhal_amd
+    from narwhal_amd import _lib
+    from narwhal_amd.bls import Bls
+    sks, pks = _committee(bls, 4, 16)
+    rnd = random.Random(5)
+    msgs = [rnd.randbytes(32) for _ in range(1100)]
+    sigs = bls.sign([sks[i % 4] for i in range(1100)], msgs)
+    keys = [[i % 4] for i in range(1100)]
+    assert not bls.verify_many(pks, sigs[:2], keys[:2], msgs[:2]).any()
+    assert all(v == 0.0 for v in bls.last_kernel_ms().values())
+    assert not bls.verify_many(pks, sigs, keys, msgs).any()  # > 1,024 items
+    assert bls.last_kernel_ms()["pairing_check"] > 0.0
+    e = narwhal_amd.Engine(device=0, flags=_lib.NWV_FLAG_BLS_STAGE_TIMES)
+    try:
+        bt = Bls(e)
+        assert not bt.verify_many(pks, sigs[:2], keys[:2], msgs[:2]).any()
+        km = bt.last_kernel_ms()
+        assert km["pairing_check"] > 0.0 and km["hash_to_g1"] > 0.0 and km["sig_decode"] > 0.0
+    finally:
+        e.close()
+
+
 def test_keycache_register_only(bls):
     """the key cache takes only registered (committee) keys that validate: 70,000 stray keys named
     by verify calls (undecodable, off-curve, outside G2, and valid keys of outsiders) never take a
