@@ -798,7 +798,10 @@ inline int pairing_script(bool fixed, SOp* ops) {
     int n = 0;
     const ScriptRec w{ops, &n};
     const char* steps = BLS_WAVE_STEPS_STR;
-    const Prog pd = fixed ? P_ML_DBL_FIXED : P_ML_DBL_STEP, pa = fixed ? P_ML_ADD_FIXED : P_ML_ADD_STEP;
+    // with both lines precomputed, the steps scheduled into stages of at most 21 lanes (mlp_*:
+    // three items of a packed wave share every pass; a doubling takes 9 passes for three items
+    // against 11 for ml_dbl_fixed's 46- and 51-lane stages)
+    const Prog pd = fixed ? P_MLP_DBL_FIXED : P_ML_DBL_STEP, pa = fixed ? P_MLP_ADD_FIXED : P_ML_ADD_STEP;
     for (int k = 0; k < NSTEPS; k++) {
         ops[n++] = SOp{(uint32_t)k, 0u, 1u | (SOP_LINES << 16), -1};
         w.run(steps[k] == 'a' ? pa : pd);

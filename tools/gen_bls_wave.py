@@ -609,6 +609,13 @@ def _mul_bound(ba, bb):
     return (ba * bb - 1) // R + P + 1
 
 
+# per-program scheduling options: a lane cap (the packed pairing kernel's Miller-loop programs:
+# stages of at most 21 lanes run three items a pass) and registers the program never touches
+# whose slots its temporaries may take (QB / TB: unused when both pairs' lines are precomputed)
+PROG_LANES = {}
+PROG_SPARE_REGS = {}
+
+
 def compile_prog(prog):
     # 1. outputs become atoms in their register slots
     outs = []
@@ -722,7 +729,7 @@ def compile_prog(prog):
         ready = [a for a in remaining if all(d.kind in ("in", "const") or (d.stage is not None and d.stage < s)
                                             for d in a.deps())]
         ready.sort(key=lambda a: (-height[a.id], a.kind != "mul", a.id))
-        take = ready[:LANES]
+        take = ready[:PROG_LANES.get(prog.name, LANES)]
         for a in take:
             a.stage = s
         stages.append(take)
@@ -763,6 +770,9 @@ def compile_prog(prog):
         stages.append(st)
         nst += 1
     free, live = [], []  # free temporaries; (last use stage, slot) in use
+    for r in PROG_SPARE_REGS.get(prog.name, ()):
+        assert r not in _prog_regs(prog), (prog.name, r)
+        free += [REGS.slot(r, i) for i in range(REGS.regs[r][1] - 1, -1, -1)]
     nxt = REGS.temp_base
     for si, st in enumerate(stages, start=1):
         # slots whose value was last read before this stage become free
@@ -1118,6 +1128,14 @@ def line_mul(a, b):
     z = a0[0] * 0
     return ((c00, c01, t11), ((z, z), c11, c12))
 
+
+# the packed pairing kernel's steps with both lines precomputed: the same formulas scheduled into
+# stages of at most 21 lanes, so three items share every pass (a doubling: 9 passes for three
+# items against 11), temporaries also in QB / TB
+for _n, _add in (("mlp_dbl_fixed", False), ("mlp_add_fixed", True)):
+    PROG_LANES[_n] = 21
+    PROG_SPARE_REGS[_n] = ("QB", "TB")
+    program(_n)((lambda a: lambda io: _mlstep(io, a, True, True))(_add))
 
 # the fused form (f^2 (lA lB)) where it has fewer stages: every step but the computed addition
 program("ml_dbl_step")(lambda io: _mlstep(io, False, False, True))
